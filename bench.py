@@ -1,0 +1,247 @@
+#!/usr/bin/env python3
+"""clipgpu benchmark — BASELINE.json metric:
+"images/sec + texts/sec embedding, ViT-B/32-224, batch 256, 1/2/4/8 MI355X".
+
+One step = one pass of the hot path over one batch of synthetic input resident in
+HBM: ViT-B/32-224 vision tower on 256 normalised f32 images per GPU
+(BASELINE.json configs[1]) -> L2-normalised [256, 512], then (N > 1) the RCCL
+all-gather of the embedding matrix over xGMI (weak scaling).
+Weights are seeded synthetic (no checkpoint can be fetched); arithmetic in bf16
+with f32 accumulation / residual stream / LayerNorm / softmax.
+
+Also reported: texts/s for configs[2] (text tower, batch 1024 x 77 tokens);
+roofline of the dominant kernel (c_fc GEMM) from HIP events on the launch stream;
+CPU baseline = the numpy oracle (fp32 port) on a bounded sample on rank 0.
+
+Launch: python bench.py [--gpus 1 --steps K --warmup W]   (N > 1: torch.distributed.run)
+"""
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+import torch  # noqa: E402  (import torch before the native lib: one HIP runtime per process)
+import torch.distributed as dist
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "clip-embedder-rs_amd"))
+
+from open_clip_inference import _lib  # noqa: E402
+from open_clip_inference.engine import Engine, profile_enable, profile_read  # noqa: E402
+
+# ViT-B/32 (open_clip timm/vit_base_patch32_clip_224.openai)
+CFG = {
+    "model_cfg": {"embed_dim": 512, "quick_gelu": True,
+                  "vision_cfg": {"image_size": 224, "layers": 12, "width": 768, "patch_size": 32},
+                  "text_cfg": {"context_length": 77, "vocab_size": 49408, "width": 512, "heads": 8,
+                               "layers": 12}},
+    "preprocess_cfg": {"mean": [0.48145466, 0.4578275, 0.40821073],
+                       "std": [0.26862954, 0.26130258, 0.27577711]},
+}
+MODEL_CONFIG = {"logit_scale": 100.0, "logit_bias": 0.0, "activation_function": "softmax",
+                "tokenizer_needs_lowercase": False, "pad_id": 0, "vocab_size": 49408}
+
+# Algorithmic work per unit: 2 x MAC over all matmuls.
+def vit_flops(B):
+    S, P, D, L, M, E = 224, 32, 768, 12, 3072, 512
+    g2 = (S // P) ** 2
+    N = g2 + 1
+    patch = 2 * B * g2 * D * 3 * P * P
+    per_layer = 2 * B * N * (3 * D * D + D * D + 2 * D * M) + 2 * 2 * B * N * N * D
+    return patch + L * per_layer + 2 * B * D * E
+
+
+def text_flops(B, T=77):
+    D, L, M, E = 512, 12, 2048, 512
+    return L * (2 * B * T * (3 * D * D + D * D + 2 * D * M) + 2 * 2 * B * T * T * D) + 2 * B * D * E
+
+
+PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md chip table)
+B_VISION = 256
+B_TEXT = 1024
+
+
+def make_model_dir():
+    d = tempfile.mkdtemp(prefix="clipgpu_bench_")
+    for name, obj in (("open_clip_config.json", CFG), ("model_config.json", MODEL_CONFIG),
+                      ("clipgpu_synthetic.json", {"seed": 1234})):
+        with open(os.path.join(d, name), "w") as f:
+            json.dump(obj, f)
+    return d
+
+
+def synth_inputs(rank, device):
+    g = torch.Generator(device="cpu").manual_seed(1000 + rank)
+    u8 = torch.randint(0, 256, (B_VISION, 224, 224, 3), dtype=torch.uint8, generator=g)
+    mean = torch.tensor(CFG["preprocess_cfg"]["mean"], dtype=torch.float32)
+    std = torch.tensor(CFG["preprocess_cfg"]["std"], dtype=torch.float32)
+    px = ((u8.float() / 255.0 - mean) / std).permute(0, 3, 1, 2).contiguous()
+    ids = torch.randint(0, 49406, (B_TEXT, 77), dtype=torch.int64, generator=g)
+    ids[:, 0] = 49406
+    ids[:, 76] = 49407
+    return px.to(device), ids.to(device)
+
+
+def cpu_baseline(target_s=12.0):
+    """Numpy oracle (fp32 port of the reference graph) on a bounded sample."""
+    from oracle import clip_ref, weights
+    from oracle.model_spec import vision_spec_from_cfg
+    try:
+        from threadpoolctl import threadpool_info
+        cores = max([int(i.get("num_threads", 1)) for i in threadpool_info()] or [1])
+    except Exception:
+        cores = os.cpu_count() or 1
+    v = vision_spec_from_cfg(CFG["model_cfg"])
+    P = {k: a.astype(np.float32) for k, a in weights.vision_weights(v, 1234).items()}
+    rng = np.random.default_rng(0)
+    px = rng.standard_normal((4, 3, 224, 224)).astype(np.float32)
+    clip_ref.encode_image(P, v, px[:1], dtype=np.float32)  # warm
+    t0 = time.perf_counter()
+    clip_ref.encode_image(P, v, px, dtype=np.float32)
+    per_img = (time.perf_counter() - t0) / 4
+    n = int(max(4, min(256, target_s / max(per_img, 1e-6))))
+    px = rng.standard_normal((n, 3, 224, 224)).astype(np.float32)
+    t0 = time.perf_counter()
+    for i in range(0, n, 16):
+        clip_ref.encode_image(P, v, px[i:i + 16], dtype=np.float32)
+    dt = time.perf_counter() - t0
+    return {"value": round(n / dt, 2), "unit": "images/s", "cores": cores, "kind": "port",
+            "sample": f"{n} synthetic 224x224 images, ViT-B/32 vision tower, numpy fp32 oracle "
+                      f"(oracle/clip_ref.py), batches of 16, {dt:.1f} s"}
+
+
+def load_traffic():
+    p = os.path.join(ROOT, "profiles", "pmc_c_fc.json")
+    if os.path.exists(p):
+        with open(p) as f:
+            return json.load(f).get("hbm_bytes_per_launch")
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--no-text", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dtype", default="bf16")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    mdir = make_model_dir()
+    ve = Engine(mdir, _lib.TOWER_VISION, [local], args.dtype, B_VISION)
+    px, ids = synth_inputs(rank, dev)
+    out = torch.empty((B_VISION, 512), device=dev, dtype=torch.float32)
+    gathered = torch.empty((world * B_VISION, 512), device=dev, dtype=torch.float32)
+    stream = torch.cuda.current_stream(dev)
+
+    def vision_step():
+        ve.embed_pixels_device(px.data_ptr(), B_VISION, out.data_ptr(), stream.cuda_stream)
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, out)
+
+    def timed(step, steps, warmup, prof_engine=None, prof_cat=None):
+        for _ in range(warmup):
+            step()
+        if prof_engine is not None:
+            profile_enable(prof_engine, [prof_cat])
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        dt = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([dt], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t.item())
+        prof = None
+        if prof_engine is not None:
+            prof = profile_read(prof_engine, prof_cat)
+            profile_enable(prof_engine, [])
+        return dt, prof
+
+    dt, (fc_ms, fc_n) = timed(vision_step, args.steps, args.warmup, ve, "c_fc")
+    images = world * B_VISION * args.steps
+    value = images / dt
+    ms_per_step = dt * 1e3 / args.steps
+
+    # roofline of the dominant kernel: c_fc GEMM (+QuickGELU epilogue), M=256*50, N=3072, K=768
+    fc_flops = 2.0 * B_VISION * 50 * 3072 * 768
+    fc_avg_s = (fc_ms / 1e3) / max(fc_n, 1)
+    achieved = fc_flops / fc_avg_s / 1e12
+    whole_tflops = vit_flops(B_VISION) * args.steps / dt / 1e12 / 1.0
+
+    text = None
+    if not args.no_text:
+        te = Engine(mdir, _lib.TOWER_TEXT, [local], args.dtype, B_TEXT)
+        tout = torch.empty((B_TEXT, 512), device=dev, dtype=torch.float32)
+        tgathered = torch.empty((world * B_TEXT, 512), device=dev, dtype=torch.float32)
+
+        def text_step():
+            te.embed_tokens_device(ids.data_ptr(), B_TEXT, tout.data_ptr(), stream.cuda_stream)
+            if world > 1:
+                dist.all_gather_into_tensor(tgathered, tout)
+
+        tsteps = max(3, args.steps // 2)
+        tdt, _ = timed(text_step, tsteps, max(1, args.warmup // 2))
+        text = {"metric": "texts/sec embedding, ViT-B/32 text tower, batch 1024 x 77 tokens",
+                "value": round(world * B_TEXT * tsteps / tdt, 1), "unit": "texts/s",
+                "ms_per_step": round(tdt * 1e3 / tsteps, 3),
+                "mfma_tflops": round(text_flops(B_TEXT) * world * tsteps / tdt / 1e12 / world, 1)}
+        te.close()
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline()
+
+    if rank == 0:
+        line = {
+            "metric": "images/sec embedding, ViT-B/32-224 vision tower, batch 256 per GPU",
+            "value": round(value, 1),
+            "unit": "images/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": args.dtype,
+            "data": "synthetic (seeded u8 images normalised with OpenAI mean/std; seeded weights)",
+            "config": {"workload": "BASELINE.json configs[1]: ViT-B/32-224 VisionEmbedder, batch 256 "
+                                   "synthetic 224x224 per GPU, device-resident input",
+                       "global_batch": world * B_VISION, "seq_len": 50,
+                       "parallelism": f"dp{world}" + (" + RCCL all-gather of [B,512] embeddings" if world > 1 else "")},
+            "roofline": {"bound": "mfma", "kernel": "gemm_bt_kernel c_fc (12800x3072x768, +QuickGELU)",
+                         "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": load_traffic(),
+                         "launches_timed": fc_n, "avg_launch_us": round(fc_avg_s * 1e6, 2)},
+            "whole_forward_mfma_tflops_per_gpu": round(whole_tflops, 1),
+            "text": text,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    ve.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

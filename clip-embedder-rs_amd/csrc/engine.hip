@@ -1,0 +1,675 @@
+// clipgpu engine: one tower (vision or text) replicated on one or more GPUs.
+//
+// Replaces the ONNX Runtime session (src/onnx.rs:7-47) that the reference builds
+// per tower and runs in VisionEmbedder::embed_images (src/vision.rs:100-117) and
+// TextEmbedder::embed_texts (src/text.rs:148-169).  Weights are uploaded once per
+// device (16-bit matrices for MFMA, f32 for LayerNorm/bias/embeddings) into one
+// arena; activations live in a persistent per-device workspace sized for
+// max_batch, so a forward performs no allocation and can be captured in a
+// hipGraph.  Multi-device handles shard the batch into contiguous row blocks,
+// one host worker thread and one stream per device.
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <cstring>
+#include <fstream>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <sys/stat.h>
+#include <thread>
+#include <vector>
+
+#include "../../include/clipgpu.h"
+#include "host/api_util.hpp"
+#include "host/json.hpp"
+#include "host/model.hpp"
+#include "kernels/common.hpp"
+#include "kernels/kernels.hpp"
+
+namespace clipgpu {
+
+#define HIP_CHECK(expr)                                                                             \
+  do {                                                                                              \
+    hipError_t _e = (expr);                                                                         \
+    if (_e != hipSuccess)                                                                           \
+      throw ClipErr(CLIPGPU_ERR_DEVICE, std::string("HIP error: ") + hipGetErrorString(_e) + " (" #expr \
+                                            ")");                                                   \
+  } while (0)
+
+struct LayerW {
+  float *ln1_w, *ln1_b, *bqkv, *bo, *ln2_w, *ln2_b, *b1, *b2;
+  void *wqkv, *wo, *w1, *w2;
+};
+
+struct DevWeights {
+  void* conv_w = nullptr;  // [D][3*P*P] 16-bit
+  float *cls = nullptr, *pos = nullptr, *lnpre_w = nullptr, *lnpre_b = nullptr;
+  float* tok = nullptr;  // text token table [V][D] f32
+  std::vector<LayerW> layers;
+  float *lnpost_w = nullptr, *lnpost_b = nullptr;
+  void* proj_t = nullptr;  // [E][D] 16-bit (transposed visual.proj / text_projection)
+};
+
+struct Replica {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  char* arena = nullptr;  // weights
+  char* work = nullptr;   // activations
+  DevWeights w;
+  float* x = nullptr;     // [rows][D] f32 residual stream
+  void* h = nullptr;      // [rows][D] 16-bit (LN output / attention output)
+  void* big = nullptr;    // [rows][max(3D, MLP)] 16-bit (qkv / MLP hidden)
+  void* pooled = nullptr; // [B][D] 16-bit
+  float* emb = nullptr;   // [B][E] f32 (pre-normalisation)
+  float* out = nullptr;   // [B][E] f32
+  void* in = nullptr;     // device input staging (pixels f32 / u8 / ids)
+  void* pin_in = nullptr; // pinned host staging
+  float* pin_out = nullptr;
+};
+
+}  // namespace clipgpu
+
+namespace clipgpu {
+// Live per-kernel-class timing with HIP events recorded on the launch stream
+// (clipgpu_profile_*; bench.py's roofline.achieved).  Off by default.
+enum ProfCat { PC_PATCH = 0, PC_STEM, PC_QKV, PC_ATTN, PC_OUT_PROJ, PC_LN, PC_C_FC, PC_C_PROJ, PC_HEAD, PC_N };
+static const char* kProfNames[PC_N] = {"patch_embed", "stem_ln", "qkv", "attention", "out_proj",
+                                       "layernorm", "c_fc", "c_proj", "head"};
+struct Profiler {
+  unsigned mask = 0;
+  std::vector<hipEvent_t> pool;
+  size_t used = 0;
+  struct Rec { int cat; hipEvent_t a, b; };
+  std::vector<Rec> pending;
+  double total_ms[PC_N] = {0};
+  long long count[PC_N] = {0};
+  hipEvent_t get() {
+    if (used == pool.size()) {
+      hipEvent_t ev;
+      if (hipEventCreate(&ev) != hipSuccess) return nullptr;
+      pool.push_back(ev);
+    }
+    return pool[used++];
+  }
+};
+}  // namespace clipgpu
+
+struct clipgpu_engine {
+  clipgpu::Profiler prof;
+  clipgpu::TowerSpec spec;
+  clipgpu::PreprocessCfg pre;
+  clipgpu::DType dt = clipgpu::DT_BF16;
+  int max_batch = 0;
+  size_t in_bytes_per_row = 0;
+  std::vector<clipgpu::Replica> reps;
+  std::mutex mu;  // one call per handle at a time (src/vision.rs:107 write lock)
+};
+
+namespace clipgpu {
+
+namespace {
+
+inline size_t align256(size_t n) { return (n + 255) & ~size_t(255); }
+
+bool file_exists(const std::string& p) {
+  struct stat st;
+  return ::stat(p.c_str(), &st) == 0 && S_ISREG(st.st_mode);
+}
+
+const HostTensor& need(const TensorMap& m, const std::string& k) {
+  auto it = m.find(k);
+  if (it == m.end()) throw ClipErr(CLIPGPU_ERR_CONFIG, "Configuration error: missing tensor " + k);
+  return it->second;
+}
+
+// Bump allocator over a device arena.
+struct Bump {
+  char* base;
+  size_t off = 0;
+  size_t cap;
+  void* take(size_t n) {
+    void* p = base + off;
+    off += align256(n);
+    if (off > cap) throw ClipErr(CLIPGPU_ERR_DEVICE, "internal: arena overflow");
+    return p;
+  }
+};
+
+size_t weight_bytes(const TowerSpec& s, const TensorMap& m) {
+  size_t total = 0;
+  for (const ParamDesc& p : tower_params(s)) total += align256((size_t)need(m, p.name).numel() * 4);
+  return total + 4096;
+}
+
+void upload_f32(const HostTensor& t, float* dst) {
+  HIP_CHECK(hipMemcpy(dst, t.data.data(), t.data.size() * 4, hipMemcpyHostToDevice));
+}
+
+void upload_16(DType dt, const float* src, size_t n, void* dst, float* staging, hipStream_t s) {
+  HIP_CHECK(hipMemcpy(staging, src, n * 4, hipMemcpyHostToDevice));
+  HIP_CHECK(launch_cast_f32(dt, staging, dst, (long)n, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+}
+
+void upload_weights(clipgpu_engine& e, Replica& r, const TensorMap& m) {
+  const TowerSpec& s = e.spec;
+  const size_t bytes = weight_bytes(s, m);
+  HIP_CHECK(hipMalloc(&r.arena, bytes));
+  Bump a{r.arena, 0, bytes};
+  const int D = s.width, E = s.embed_dim;
+  size_t max16 = 0;
+  for (const ParamDesc& p : tower_params(s)) max16 = std::max(max16, (size_t)need(m, p.name).numel());
+  float* staging = nullptr;
+  HIP_CHECK(hipMalloc(&staging, max16 * 4));
+  auto f32 = [&](const std::string& k) {
+    const HostTensor& t = need(m, k);
+    float* p = (float*)a.take(t.data.size() * 4);
+    upload_f32(t, p);
+    return p;
+  };
+  auto w16 = [&](const std::string& k) {
+    const HostTensor& t = need(m, k);
+    void* p = a.take(t.data.size() * 2);
+    upload_16(e.dt, t.data.data(), t.data.size(), p, staging, r.stream);
+    return p;
+  };
+  auto w16_transposed = [&](const std::string& k) {  // [D][E] -> [E][D]
+    const HostTensor& t = need(m, k);
+    const int64_t R = t.shape[0], C = t.shape[1];
+    std::vector<float> tr((size_t)(R * C));
+    for (int64_t i = 0; i < R; ++i)
+      for (int64_t j = 0; j < C; ++j) tr[(size_t)(j * R + i)] = t.data[(size_t)(i * C + j)];
+    void* p = a.take(tr.size() * 2);
+    upload_16(e.dt, tr.data(), tr.size(), p, staging, r.stream);
+    return p;
+  };
+  DevWeights& w = r.w;
+  std::string pre;
+  if (s.tower == TOWER_VISION) {
+    w.conv_w = w16("visual.conv1.weight");
+    w.cls = f32("visual.class_embedding");
+    w.pos = f32("visual.positional_embedding");
+    w.lnpre_w = f32("visual.ln_pre.weight");
+    w.lnpre_b = f32("visual.ln_pre.bias");
+    pre = "visual.transformer.resblocks.";
+  } else {
+    w.tok = f32("token_embedding.weight");
+    w.pos = f32("positional_embedding");
+    pre = "transformer.resblocks.";
+  }
+  for (int l = 0; l < s.layers; ++l) {
+    const std::string p = pre + std::to_string(l) + ".";
+    LayerW L;
+    L.ln1_w = f32(p + "ln_1.weight");
+    L.ln1_b = f32(p + "ln_1.bias");
+    L.wqkv = w16(p + "attn.in_proj_weight");
+    L.bqkv = f32(p + "attn.in_proj_bias");
+    L.wo = w16(p + "attn.out_proj.weight");
+    L.bo = f32(p + "attn.out_proj.bias");
+    L.ln2_w = f32(p + "ln_2.weight");
+    L.ln2_b = f32(p + "ln_2.bias");
+    L.w1 = w16(p + "mlp.c_fc.weight");
+    L.b1 = f32(p + "mlp.c_fc.bias");
+    L.w2 = w16(p + "mlp.c_proj.weight");
+    L.b2 = f32(p + "mlp.c_proj.bias");
+    w.layers.push_back(L);
+  }
+  if (s.tower == TOWER_VISION) {
+    w.lnpost_w = f32("visual.ln_post.weight");
+    w.lnpost_b = f32("visual.ln_post.bias");
+    w.proj_t = w16_transposed("visual.proj");
+  } else {
+    w.lnpost_w = f32("ln_final.weight");
+    w.lnpost_b = f32("ln_final.bias");
+    w.proj_t = w16_transposed("text_projection");
+  }
+  (void)D;
+  (void)E;
+  HIP_CHECK(hipFree(staging));
+}
+
+void alloc_workspace(clipgpu_engine& e, Replica& r) {
+  const TowerSpec& s = e.spec;
+  const size_t B = (size_t)e.max_batch, rows = B * (size_t)s.tokens(), D = s.width;
+  const size_t wide = std::max((size_t)3 * D, (size_t)s.mlp_width);
+  const size_t E = s.embed_dim;
+  const size_t sizes[] = {rows * D * 4, rows * D * 2, rows * wide * 2, B * D * 2, B * E * 4, B * E * 4,
+                          B * e.in_bytes_per_row};
+  size_t total = 0;
+  for (size_t z : sizes) total += align256(z);
+  HIP_CHECK(hipMalloc(&r.work, total));
+  HIP_CHECK(hipMemset(r.work, 0, total));
+  Bump a{r.work, 0, total};
+  r.x = (float*)a.take(sizes[0]);
+  r.h = a.take(sizes[1]);
+  r.big = a.take(sizes[2]);
+  r.pooled = a.take(sizes[3]);
+  r.emb = (float*)a.take(sizes[4]);
+  r.out = (float*)a.take(sizes[5]);
+  r.in = a.take(sizes[6]);
+  HIP_CHECK(hipHostMalloc(&r.pin_in, B * e.in_bytes_per_row, hipHostMallocDefault));
+  HIP_CHECK(hipHostMalloc((void**)&r.pin_out, B * E * 4, hipHostMallocDefault));
+}
+
+void check(hipError_t err, const char* what) {
+  if (err != hipSuccess)
+    throw ClipErr(CLIPGPU_ERR_DEVICE, std::string("HIP error in ") + what + ": " + hipGetErrorString(err));
+}
+
+// Records [start, stop] events around one launch when its category is enabled.
+struct ProfScope {
+  Profiler* p;
+  int cat;
+  hipStream_t st;
+  hipEvent_t a = nullptr;
+  ProfScope(const clipgpu_engine& e, int c, hipStream_t s) : p(const_cast<Profiler*>(&e.prof)), cat(c), st(s) {
+    if (p->mask & (1u << cat)) {
+      a = p->get();
+      if (a) (void)hipEventRecord(a, st);
+    }
+  }
+  ~ProfScope() {
+    if (a) {
+      hipEvent_t b = p->get();
+      if (b) {
+        (void)hipEventRecord(b, st);
+        p->pending.push_back({cat, a, b});
+      }
+    }
+  }
+};
+
+GemmParams rows_gemm(const void* A, long lda, const void* W, const float* bias, void* out, long ldo, int M, int N,
+                     int K) {
+  GemmParams g{};
+  g.A = A;
+  g.lda = lda;
+  g.W = W;
+  g.ldw = K;
+  g.bias = bias;
+  g.out = out;
+  g.ldo = ldo;
+  g.M = M;
+  g.N = N;
+  g.K = K;
+  return g;
+}
+
+// The transformer trunk shared by both towers: L x [LN1 -> QKV -> MHA -> out+res ->
+// LN2 -> fc1+act -> fc2+res], with h already holding ln_1(x) of layer 0.
+void trunk(const clipgpu_engine& e, const Replica& r, int B, int causal, hipStream_t st) {
+  const TowerSpec& s = e.spec;
+  const int T = s.tokens(), rows = B * T, D = s.width, MLP = s.mlp_width;
+  for (int l = 0; l < s.layers; ++l) {
+    const LayerW& L = r.w.layers[l];
+    { ProfScope ps(e, PC_QKV, st);
+    check(launch_gemm(e.dt, A_ROWS, EPI_STORE16, ACT_NONE, rows_gemm(r.h, D, L.wqkv, L.bqkv, r.big, 3 * D, rows, 3 * D, D), st), "qkv gemm"); }
+    { ProfScope ps(e, PC_ATTN, st);
+      check(launch_attention(e.dt, r.big, r.h, B, T, s.heads, D, causal, st), "attention"); }
+    { ProfScope ps(e, PC_OUT_PROJ, st);
+      check(launch_gemm(e.dt, A_ROWS, EPI_RESID, ACT_NONE, rows_gemm(r.h, D, L.wo, L.bo, r.x, D, rows, D, D), st), "out_proj gemm"); }
+    { ProfScope ps(e, PC_LN, st);
+      check(launch_ln_rows(e.dt, r.x, L.ln2_w, L.ln2_b, s.ln_eps, r.h, rows, D, st), "ln_2"); }
+    { ProfScope ps(e, PC_C_FC, st);
+      check(launch_gemm(e.dt, A_ROWS, EPI_STORE16, s.act, rows_gemm(r.h, D, L.w1, L.b1, r.big, MLP, rows, MLP, D), st), "c_fc gemm"); }
+    { ProfScope ps(e, PC_C_PROJ, st);
+      check(launch_gemm(e.dt, A_ROWS, EPI_RESID, ACT_NONE, rows_gemm(r.big, MLP, L.w2, L.b2, r.x, D, rows, D, MLP), st), "c_proj gemm"); }
+    if (l + 1 < s.layers) {
+      ProfScope ps(e, PC_LN, st);
+      check(launch_ln_rows(e.dt, r.x, r.w.layers[l + 1].ln1_w, r.w.layers[l + 1].ln1_b, s.ln_eps, r.h, rows, D, st), "ln_1");
+    }
+  }
+}
+
+void head(const clipgpu_engine& e, const Replica& r, int B, const int64_t* ids, float* d_out, hipStream_t st) {
+  const TowerSpec& s = e.spec;
+  const int D = s.width, E = s.embed_dim;
+  ProfScope ps(e, PC_HEAD, st);
+  check(launch_pool_ln(e.dt, r.x, ids, s.tokens(), r.w.lnpost_w, r.w.lnpost_b, s.ln_eps, r.pooled, B, D, st), "pool+ln");
+  check(launch_gemm(e.dt, A_ROWS, EPI_STORE32, ACT_NONE, rows_gemm(r.pooled, D, r.w.proj_t, nullptr, r.emb, E, B, E, D), st), "proj gemm");
+  check(launch_l2norm(r.emb, d_out, B, E, st), "l2norm");
+}
+
+// asrc: A_IMG_F32 (pixels = normalised f32 NCHW) or A_IMG_U8 (NHWC u8 + mean/std)
+void vision_forward(const clipgpu_engine& e, const Replica& r, const void* pixels, int asrc, const float* mean,
+                    const float* stdv, int B, float* d_out, hipStream_t st) {
+  const TowerSpec& s = e.spec;
+  const int D = s.width, G = s.grid(), P = s.patch_size;
+  GemmParams g{};
+  g.W = r.w.conv_w;
+  g.ldw = 3 * P * P;
+  g.bias = nullptr;  // OpenAI-style conv1 has no bias
+  g.out = r.x;
+  g.ldo = D;
+  g.M = B * G * G;
+  g.N = D;
+  g.K = 3 * P * P;
+  g.img = pixels;
+  g.S = s.image_size;
+  g.P = P;
+  g.G = G;
+  g.pos = r.w.pos;
+  for (int c = 0; c < 3; ++c) {
+    g.mean[c] = mean ? mean[c] : 0.f;
+    g.stdv[c] = stdv ? stdv[c] : 1.f;
+  }
+  { ProfScope ps(e, PC_PATCH, st);
+    check(launch_gemm(e.dt, asrc, EPI_PATCH, ACT_NONE, g, st), "patch gemm"); }
+  {
+  ProfScope ps(e, PC_STEM, st);
+  check(launch_vision_embed_ln(e.dt, r.x, r.w.cls, r.w.pos, r.w.lnpre_w, r.w.lnpre_b, r.w.layers[0].ln1_w,
+                               r.w.layers[0].ln1_b, s.ln_eps, r.h, B, s.tokens(), D, st),
+        "embed+ln_pre");
+  }
+  trunk(e, r, B, 0, st);
+  head(e, r, B, nullptr, d_out, st);
+}
+
+void text_forward(const clipgpu_engine& e, const Replica& r, const int64_t* d_ids, int B, float* d_out,
+                  hipStream_t st) {
+  const TowerSpec& s = e.spec;
+  {
+  ProfScope ps(e, PC_STEM, st);
+  check(launch_text_embed_ln(e.dt, d_ids, r.w.tok, r.w.pos, r.w.layers[0].ln1_w, r.w.layers[0].ln1_b, s.ln_eps,
+                             r.x, r.h, B, s.context_length, s.width, s.vocab_size, st),
+        "token embed+ln_1");
+  }
+  trunk(e, r, B, 1, st);
+  head(e, r, B, d_ids, d_out, st);
+}
+
+enum InKind { IN_F32 = 0, IN_U8 = 1, IN_IDS = 2 };
+
+// Host-buffer forward over a row range of one replica, chunked by max_batch.
+void run_host_shard(clipgpu_engine& e, Replica& r, InKind kind, const void* in, size_t in_row_bytes, int64_t b0,
+                    int64_t b1, const float* mean, const float* stdv, float* out) {
+  HIP_CHECK(hipSetDevice(r.device));
+  const int E = e.spec.embed_dim;
+  for (int64_t c0 = b0; c0 < b1; c0 += e.max_batch) {
+    const int n = (int)std::min<int64_t>(e.max_batch, b1 - c0);
+    std::memcpy(r.pin_in, (const char*)in + c0 * in_row_bytes, (size_t)n * in_row_bytes);
+    HIP_CHECK(hipMemcpyAsync(r.in, r.pin_in, (size_t)n * in_row_bytes, hipMemcpyHostToDevice, r.stream));
+    if (kind == IN_IDS)
+      text_forward(e, r, (const int64_t*)r.in, n, r.out, r.stream);
+    else
+      vision_forward(e, r, r.in, kind == IN_F32 ? A_IMG_F32 : A_IMG_U8, mean, stdv, n, r.out, r.stream);
+    HIP_CHECK(hipMemcpyAsync(r.pin_out, r.out, (size_t)n * E * 4, hipMemcpyDeviceToHost, r.stream));
+    HIP_CHECK(hipStreamSynchronize(r.stream));
+    std::memcpy(out + c0 * E, r.pin_out, (size_t)n * E * 4);
+  }
+}
+
+void run_host(clipgpu_engine& e, InKind kind, const void* in, size_t in_row_bytes, int64_t B, const float* mean,
+              const float* stdv, float* out) {
+  const int G = (int)e.reps.size();
+  if (G == 1) {
+    run_host_shard(e, e.reps[0], kind, in, in_row_bytes, 0, B, mean, stdv, out);
+    return;
+  }
+  // Contiguous row blocks, rank order == input order.
+  std::vector<std::thread> th;
+  std::vector<std::string> errs(G);
+  std::vector<int> codes(G, 0);
+  for (int g = 0; g < G; ++g) {
+    const int64_t b0 = B * g / G, b1 = B * (g + 1) / G;
+    if (b0 == b1) continue;
+    th.emplace_back([&, g, b0, b1]() {
+      try {
+        run_host_shard(e, e.reps[g], kind, in, in_row_bytes, b0, b1, mean, stdv, out);
+      } catch (const ClipErr& ex) {
+        codes[g] = ex.code;
+        errs[g] = ex.what();
+      } catch (const std::exception& ex) {
+        codes[g] = CLIPGPU_ERR_DEVICE;
+        errs[g] = ex.what();
+      }
+    });
+  }
+  for (auto& t : th) t.join();
+  for (int g = 0; g < G; ++g)
+    if (codes[g]) throw ClipErr(codes[g], "device " + std::to_string(e.reps[g].device) + ": " + errs[g]);
+}
+
+void destroy_replica(Replica& r) {
+  (void)hipSetDevice(r.device);
+  if (r.stream) (void)hipStreamSynchronize(r.stream);
+  if (r.arena) (void)hipFree(r.arena);
+  if (r.work) (void)hipFree(r.work);
+  if (r.pin_in) (void)hipHostFree(r.pin_in);
+  if (r.pin_out) (void)hipHostFree(r.pin_out);
+  if (r.stream) (void)hipStreamDestroy(r.stream);
+  r = Replica();
+}
+
+}  // namespace
+}  // namespace clipgpu
+
+using namespace clipgpu;
+
+extern "C" {
+
+int clipgpu_abi_version(void) { return CLIPGPU_ABI_VERSION; }
+
+int clipgpu_create(const char* model_dir, int tower, const int* device_ids, int n_devices, int dtype, int max_batch,
+                   clipgpu_engine** out) {
+  return guarded([&]() {
+    if (!out) throw ClipErr(CLIPGPU_ERR_INVALID, "out is NULL");
+    *out = nullptr;
+    if (!model_dir) throw ClipErr(CLIPGPU_ERR_INVALID, "model_dir is NULL");
+    if (tower != CLIPGPU_TOWER_VISION && tower != CLIPGPU_TOWER_TEXT) throw ClipErr(CLIPGPU_ERR_INVALID, "bad tower");
+    if (dtype != CLIPGPU_DTYPE_BF16 && dtype != CLIPGPU_DTYPE_F16) throw ClipErr(CLIPGPU_ERR_INVALID, "bad dtype");
+    if (max_batch <= 0) throw ClipErr(CLIPGPU_ERR_INVALID, "max_batch must be > 0");
+    const std::string dir(model_dir);
+    struct stat st;
+    if (::stat(dir.c_str(), &st) != 0 || !S_ISDIR(st.st_mode))
+      throw ClipErr(CLIPGPU_ERR_CONFIG, "Model folder not found: '" + dir + "'");  // ClipError::ModelFolderNotFound
+    for (const char* f : {"open_clip_config.json", "model_config.json"})
+      if (!file_exists(dir + "/" + f))
+        throw ClipErr(CLIPGPU_ERR_CONFIG, std::string("Missing model file '") + f + "' in folder '" + dir + "'");
+    OpenClipConfig oc;
+    try {
+      oc = load_open_clip_config(dir + "/open_clip_config.json");
+    } catch (const std::runtime_error& ex) {
+      throw ClipErr(CLIPGPU_ERR_CONFIG, ex.what());
+    }
+    std::unique_ptr<clipgpu_engine> e(new clipgpu_engine());
+    e->spec = tower == CLIPGPU_TOWER_VISION ? oc.vision : oc.text;
+    e->pre = oc.pre;
+    e->dt = dtype == CLIPGPU_DTYPE_BF16 ? DT_BF16 : DT_F16;
+    e->max_batch = max_batch;
+    const TowerSpec& s = e->spec;
+    if (s.width % 64 || s.width / s.heads != 64)
+      throw ClipErr(CLIPGPU_ERR_CONFIG, "Configuration error: head_dim must be 64 and width a multiple of 64");
+    if (s.mlp_width % 64) throw ClipErr(CLIPGPU_ERR_CONFIG, "Configuration error: mlp width must be a multiple of 64");
+    if (s.width > 1280) throw ClipErr(CLIPGPU_ERR_CONFIG, "Configuration error: width > 1280 not supported yet");
+    if (s.tokens() > 256) throw ClipErr(CLIPGPU_ERR_CONFIG, "Configuration error: > 256 tokens not supported yet");
+    if (s.tower == TOWER_VISION) {
+      if (s.patch_size % 8 || (3 * s.patch_size * s.patch_size) % 64 || s.image_size % s.patch_size)
+        throw ClipErr(CLIPGPU_ERR_CONFIG, "Configuration error: unsupported patch geometry");
+      e->in_bytes_per_row = (size_t)3 * s.image_size * s.image_size * 4;  // f32 (u8 path uses a quarter)
+    } else {
+      e->in_bytes_per_row = (size_t)s.context_length * 8;
+    }
+    // weights
+    TensorMap m;
+    const std::string st_path = dir + "/open_clip_model.safetensors";
+    const std::string syn_path = dir + "/clipgpu_synthetic.json";
+    try {
+      if (file_exists(st_path)) {
+        m = load_safetensors(st_path, s);
+      } else if (file_exists(syn_path)) {
+        json::ValuePtr j = json::parse_file(syn_path);
+        const json::Value* sd = j->get("seed");
+        if (!sd) throw std::runtime_error("Configuration error: clipgpu_synthetic.json has no seed");
+        m = synth_weights(s, (uint64_t)sd->as_num(0));
+      } else {
+        throw ClipErr(CLIPGPU_ERR_CONFIG, "Missing model file 'open_clip_model.safetensors' in folder '" + dir + "'");
+      }
+    } catch (const ClipErr&) {
+      throw;
+    } catch (const std::runtime_error& ex) {
+      throw ClipErr(CLIPGPU_ERR_CONFIG, ex.what());
+    }
+    int ndev = 0;
+    HIP_CHECK(hipGetDeviceCount(&ndev));
+    std::vector<int> devs;
+    if (device_ids && n_devices > 0) devs.assign(device_ids, device_ids + n_devices);
+    else devs.push_back(0);
+    for (int d : devs)
+      if (d < 0 || d >= ndev) throw ClipErr(CLIPGPU_ERR_DEVICE, "device id " + std::to_string(d) + " not available");
+    e->reps.resize(devs.size());
+    for (size_t i = 0; i < devs.size(); ++i) {
+      Replica& r = e->reps[i];
+      r.device = devs[i];
+      HIP_CHECK(hipSetDevice(r.device));
+      HIP_CHECK(hipStreamCreateWithFlags(&r.stream, hipStreamNonBlocking));
+      upload_weights(*e, r, m);
+      alloc_workspace(*e, r);
+    }
+    *out = e.release();
+  });
+}
+
+void clipgpu_destroy(clipgpu_engine* e) {
+  if (!e) return;
+  for (hipEvent_t ev : e->prof.pool) (void)hipEventDestroy(ev);
+  for (auto& r : e->reps) destroy_replica(r);
+  delete e;
+}
+
+int clipgpu_embed_dim(const clipgpu_engine* e) { return e ? e->spec.embed_dim : -1; }
+int clipgpu_input_size(const clipgpu_engine* e) {
+  return e ? (e->spec.tower == TOWER_VISION ? e->spec.image_size : e->spec.context_length) : -1;
+}
+int clipgpu_num_devices(const clipgpu_engine* e) { return e ? (int)e->reps.size() : -1; }
+
+static void need_tower(const clipgpu_engine* e, int tower) {
+  if (!e) throw ClipErr(CLIPGPU_ERR_INVALID, "engine is NULL");
+  if (e->spec.tower != tower)
+    throw ClipErr(CLIPGPU_ERR_INVALID, tower == TOWER_VISION ? "engine is not a vision tower" : "engine is not a text tower");
+}
+
+int clipgpu_embed_pixels(clipgpu_engine* e, const float* nchw, int64_t B, int64_t S, float* out) {
+  return guarded([&]() {
+    need_tower(e, TOWER_VISION);
+    if (B <= 0) throw ClipErr(CLIPGPU_ERR_INVALID, "Empty batch");
+    if (!nchw || !out) throw ClipErr(CLIPGPU_ERR_INVALID, "NULL buffer");
+    if (S != e->spec.image_size)
+      throw ClipErr(CLIPGPU_ERR_INVALID, "Shape error: expected image size " + std::to_string(e->spec.image_size));
+    std::lock_guard<std::mutex> lk(e->mu);
+    run_host(*e, IN_F32, nchw, (size_t)3 * S * S * 4, B, nullptr, nullptr, out);
+  });
+}
+
+int clipgpu_embed_u8(clipgpu_engine* e, const uint8_t* nhwc, int64_t B, int64_t S, const float mean[3],
+                     const float stdv[3], float* out) {
+  return guarded([&]() {
+    need_tower(e, TOWER_VISION);
+    if (B <= 0) throw ClipErr(CLIPGPU_ERR_INVALID, "Empty batch");
+    if (!nhwc || !out || !mean || !stdv) throw ClipErr(CLIPGPU_ERR_INVALID, "NULL buffer");
+    if (S != e->spec.image_size)
+      throw ClipErr(CLIPGPU_ERR_INVALID, "Shape error: expected image size " + std::to_string(e->spec.image_size));
+    std::lock_guard<std::mutex> lk(e->mu);
+    run_host(*e, IN_U8, nhwc, (size_t)3 * S * S, B, mean, stdv, out);
+  });
+}
+
+int clipgpu_embed_tokens(clipgpu_engine* e, const int64_t* ids, const int64_t* mask, int64_t B, int64_t T,
+                         float* out) {
+  (void)mask;
+  return guarded([&]() {
+    need_tower(e, TOWER_TEXT);
+    if (B <= 0) throw ClipErr(CLIPGPU_ERR_INVALID, "Empty batch");
+    if (!ids || !out) throw ClipErr(CLIPGPU_ERR_INVALID, "NULL buffer");
+    if (T != e->spec.context_length)
+      throw ClipErr(CLIPGPU_ERR_INVALID,
+                    "Shape error: expected context length " + std::to_string(e->spec.context_length));
+    for (int64_t i = 0; i < B * T; ++i)
+      if (ids[i] < 0 || ids[i] >= e->spec.vocab_size)
+        throw ClipErr(CLIPGPU_ERR_INVALID, "Inference error: token id " + std::to_string(ids[i]) + " out of range");
+    std::lock_guard<std::mutex> lk(e->mu);
+    run_host(*e, IN_IDS, ids, (size_t)T * 8, B, nullptr, nullptr, out);
+  });
+}
+
+int clipgpu_embed_pixels_device(clipgpu_engine* e, const float* d_nchw, int64_t B, float* d_out, void* stream) {
+  return guarded([&]() {
+    need_tower(e, TOWER_VISION);
+    if (B <= 0) throw ClipErr(CLIPGPU_ERR_INVALID, "Empty batch");
+    if (B > e->max_batch) throw ClipErr(CLIPGPU_ERR_INVALID, "B exceeds max_batch");
+    Replica& r = e->reps[0];
+    HIP_CHECK(hipSetDevice(r.device));
+    vision_forward(*e, r, d_nchw, A_IMG_F32, nullptr, nullptr, (int)B, d_out, stream ? (hipStream_t)stream : r.stream);
+  });
+}
+
+int clipgpu_embed_u8_device(clipgpu_engine* e, const uint8_t* d_nhwc, int64_t B, const float mean[3],
+                            const float stdv[3], float* d_out, void* stream) {
+  return guarded([&]() {
+    need_tower(e, TOWER_VISION);
+    if (B <= 0) throw ClipErr(CLIPGPU_ERR_INVALID, "Empty batch");
+    if (B > e->max_batch) throw ClipErr(CLIPGPU_ERR_INVALID, "B exceeds max_batch");
+    if (!mean || !stdv) throw ClipErr(CLIPGPU_ERR_INVALID, "NULL mean/std");
+    Replica& r = e->reps[0];
+    HIP_CHECK(hipSetDevice(r.device));
+    vision_forward(*e, r, d_nhwc, A_IMG_U8, mean, stdv, (int)B, d_out, stream ? (hipStream_t)stream : r.stream);
+  });
+}
+
+int clipgpu_embed_tokens_device(clipgpu_engine* e, const int64_t* d_ids, int64_t B, float* d_out, void* stream) {
+  return guarded([&]() {
+    need_tower(e, TOWER_TEXT);
+    if (B <= 0) throw ClipErr(CLIPGPU_ERR_INVALID, "Empty batch");
+    if (B > e->max_batch) throw ClipErr(CLIPGPU_ERR_INVALID, "B exceeds max_batch");
+    Replica& r = e->reps[0];
+    HIP_CHECK(hipSetDevice(r.device));
+    text_forward(*e, r, d_ids, (int)B, d_out, stream ? (hipStream_t)stream : r.stream);
+  });
+}
+
+int clipgpu_profile_enable(clipgpu_engine* e, unsigned mask) {
+  return guarded([&]() {
+    if (!e) throw ClipErr(CLIPGPU_ERR_INVALID, "engine is NULL");
+    std::lock_guard<std::mutex> lk(e->mu);
+    Profiler& p = e->prof;
+    for (auto& rec : p.pending) { (void)hipEventSynchronize(rec.b); }
+    p.pending.clear();
+    p.used = 0;
+    for (int i = 0; i < PC_N; ++i) { p.total_ms[i] = 0; p.count[i] = 0; }
+    p.mask = mask;
+  });
+}
+
+int clipgpu_profile_read(clipgpu_engine* e, int category, double* total_ms, int64_t* launches) {
+  return guarded([&]() {
+    if (!e || category < 0 || category >= PC_N) throw ClipErr(CLIPGPU_ERR_INVALID, "bad profile query");
+    std::lock_guard<std::mutex> lk(e->mu);
+    Profiler& p = e->prof;
+    for (auto& rec : p.pending) {
+      HIP_CHECK(hipEventSynchronize(rec.b));
+      float ms = 0.f;
+      HIP_CHECK(hipEventElapsedTime(&ms, rec.a, rec.b));
+      p.total_ms[rec.cat] += ms;
+      p.count[rec.cat] += 1;
+    }
+    p.pending.clear();
+    p.used = 0;
+    if (total_ms) *total_ms = p.total_ms[category];
+    if (launches) *launches = p.count[category];
+  });
+}
+
+const char* clipgpu_profile_category_name(int category) {
+  return (category >= 0 && category < PC_N) ? kProfNames[category] : "";
+}
+
+int clipgpu_synth_tensor(uint64_t seed, const char* name, double std_, double offset, float* out, int64_t n) {
+  return guarded([&]() {
+    if (!name || !out || n < 0) throw ClipErr(CLIPGPU_ERR_INVALID, "bad arguments");
+    synth_fill(seed, name, std_, offset, out, n);
+  });
+}
+
+}  // extern "C"

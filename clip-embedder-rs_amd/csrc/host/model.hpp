@@ -1,0 +1,85 @@
+// Host-side model description: configs from the model dir, tower specs, and
+// host weight sources (seeded synthetic generator, open_clip safetensors).
+#pragma once
+#include <cstdint>
+#include <map>
+#include <string>
+#include <vector>
+
+namespace clipgpu {
+
+// src/config.rs:49-64 (PreprocessCfg, defaults "bicubic" / "shortest").
+struct PreprocessCfg {
+  float mean[3] = {0.48145466f, 0.4578275f, 0.40821073f};
+  float stdv[3] = {0.26862954f, 0.26130258f, 0.27577711f};
+  std::string interpolation = "bicubic";
+  std::string resize_mode = "shortest";
+};
+
+// src/config.rs:6-14 (ModelConfig), written by pull_onnx.py:128-150.
+struct ModelConfig {
+  bool tokenizer_needs_lowercase = false;
+  std::string activation_function;  // empty == None
+  bool has_logit_scale = false, has_logit_bias = false;
+  float logit_scale = 1.0f, logit_bias = 0.0f;
+  long pad_id = -1;  // -1 == None
+};
+
+enum Tower { TOWER_VISION = 0, TOWER_TEXT = 1 };
+
+// Architecture of one tower.  The reference never parses most of these
+// (src/config.rs:36-47) because they are baked into the ONNX graphs; we derive
+// them from open_clip's model_cfg with open_clip's defaults.
+struct TowerSpec {
+  int tower = TOWER_VISION;
+  int width = 0, layers = 0, heads = 0, mlp_width = 0, embed_dim = 0;
+  int act = 1;          // Act enum (common.hpp)
+  float ln_eps = 1e-5f;
+  // vision
+  int image_size = 0, patch_size = 0;
+  int grid() const { return patch_size ? image_size / patch_size : 0; }
+  int tokens() const { return tower == TOWER_VISION ? grid() * grid() + 1 : context_length; }
+  // text
+  int context_length = 0, vocab_size = 0;
+};
+
+struct OpenClipConfig {
+  int embed_dim = 0;
+  TowerSpec vision, text;
+  PreprocessCfg pre;
+};
+
+OpenClipConfig load_open_clip_config(const std::string& path);  // throws std::runtime_error
+ModelConfig load_model_config(const std::string& path);
+
+struct HostTensor {
+  std::vector<int64_t> shape;
+  std::vector<float> data;
+  int64_t numel() const {
+    int64_t n = 1;
+    for (auto d : shape) n *= d;
+    return n;
+  }
+};
+typedef std::map<std::string, HostTensor> TensorMap;
+
+// Parameter inventory (open_clip state-dict names) of one tower: name, shape,
+// init std, offset.  Mirrors oracle/weights.py exactly.
+struct ParamDesc {
+  std::string name;
+  std::vector<int64_t> shape;
+  double std;
+  double offset;
+};
+std::vector<ParamDesc> tower_params(const TowerSpec& spec);
+
+// splitmix64 counter generator (oracle/weights.py).
+uint64_t fnv1a64(const std::string& s);
+uint64_t mix64(uint64_t z);
+void synth_fill(uint64_t seed, const std::string& name, double std, double offset, float* out, int64_t n);
+TensorMap synth_weights(const TowerSpec& spec, uint64_t seed);
+
+// open_clip_model.safetensors (F32 / F16 / BF16) -> f32 host tensors of one tower.
+TensorMap load_safetensors(const std::string& path, const TowerSpec& spec);
+
+}  // namespace clipgpu

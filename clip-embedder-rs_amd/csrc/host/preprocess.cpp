@@ -1,0 +1,262 @@
+// Host image preprocessing: centre-crop + resize + normalise.
+//
+// Restates VisionEmbedder::preprocess_batch / preprocess_into /
+// resize_with_fast_image_resize / normalize_pixels (src/vision.rs:119-259):
+//   * crop box (f64, source pixels) unless resize_mode == "squash":
+//       scale = S / min(W,H); crop_w = crop_h = S / scale;
+//       crop_x = (W - crop_w) / 2; crop_y = (H - crop_h) / 2      (src/vision.rs:184-192)
+//   * resampling: "bicubic" -> CatmullRom (Keys cubic, a = -0.5, support 2),
+//     "bilinear" -> triangle (support 1), anything else -> nearest   (src/vision.rs:176-180)
+//     as a separable convolution with the filter support scaled by the
+//     downscale factor, horizontal pass then vertical pass, fixed-point
+//     coefficients and a u8 intermediate (the convolution scheme
+//     fast_image_resize 6.0.0 shares with Pillow's Resample.c; this file
+//     follows Pillow's rounding: 22-bit coefficients, round-half-up).
+//   * normalize_pixels: out[c][i] = (px[i*3+c] / 255 - mean[c]) / std[c]   in f32
+//     (src/vision.rs:235-259; divide, not reciprocal-multiply).
+// Parity: bit-exact vs oracle/preprocess_ref.py; vs Pillow 12.2 within 1 u8 level
+// (Pillow rounds the crop box to f32); vs fast_image_resize's 16-bit
+// coefficients ±1 level, unpinned (no Rust toolchain here).
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../../include/clipgpu.h"
+#include "api_util.hpp"
+
+namespace clipgpu {
+
+namespace {
+
+constexpr int PRECISION_BITS = 32 - 8 - 2;
+
+double bicubic_filter(double x) {  // Keys cubic, a = -0.5 (CatmullRom)
+  const double a = -0.5;
+  if (x < 0.0) x = -x;
+  if (x < 1.0) return ((a + 2.0) * x - (a + 3.0)) * x * x + 1;
+  if (x < 2.0) return (((x - 5) * x + 8) * x - 4) * a;
+  return 0.0;
+}
+double bilinear_filter(double x) {
+  if (x < 0.0) x = -x;
+  if (x < 1.0) return 1.0 - x;
+  return 0.0;
+}
+
+struct Coeffs {
+  int ksize = 0;
+  std::vector<int> bounds;  // [out][2] = xmin, count
+  std::vector<int32_t> k;   // [out][ksize] fixed point
+};
+
+Coeffs precompute(int in_size, double in0, double in1, int out_size, double (*filter)(double), double support0) {
+  Coeffs c;
+  const double scale = (in1 - in0) / out_size;
+  const double filterscale = scale < 1.0 ? 1.0 : scale;
+  const double support = support0 * filterscale;
+  c.ksize = (int)std::ceil(support) * 2 + 1;
+  c.bounds.resize((size_t)out_size * 2);
+  c.k.assign((size_t)out_size * c.ksize, 0);
+  std::vector<double> w((size_t)c.ksize);
+  for (int xx = 0; xx < out_size; ++xx) {
+    const double center = in0 + (xx + 0.5) * scale;
+    const double ss = 1.0 / filterscale;
+    int xmin = (int)(center - support + 0.5);
+    if (xmin < 0) xmin = 0;
+    int xmax = (int)(center + support + 0.5);
+    if (xmax > in_size) xmax = in_size;
+    xmax -= xmin;
+    double ww = 0.0;
+    for (int x = 0; x < xmax; ++x) {
+      w[x] = filter((x + xmin - center + 0.5) * ss);
+      ww += w[x];
+    }
+    for (int x = 0; x < xmax; ++x) {
+      const double v = ww != 0.0 ? w[x] / ww : w[x];
+      c.k[(size_t)xx * c.ksize + x] =
+          v < 0 ? (int32_t)(-0.5 + v * (1 << PRECISION_BITS)) : (int32_t)(0.5 + v * (1 << PRECISION_BITS));
+    }
+    c.bounds[(size_t)xx * 2] = xmin;
+    c.bounds[(size_t)xx * 2 + 1] = xmax;
+  }
+  return c;
+}
+
+inline uint8_t clip8(int64_t in) {
+  if (in >= ((int64_t)1 << PRECISION_BITS << 8)) return 255;
+  if (in <= 0) return 0;
+  return (uint8_t)(in >> PRECISION_BITS);
+}
+
+// Separable convolution resize of an RGB8 image restricted to box.
+void resize_conv(const uint8_t* src, int W, int H, double x0, double y0, double x1, double y1, int S,
+                 double (*filter)(double), double support, uint8_t* dst) {
+  const Coeffs ch = precompute(W, x0, x1, S, filter, support);
+  Coeffs cv = precompute(H, y0, y1, S, filter, support);
+  const bool need_h = S != W || x0 != 0.0 || x1 != (double)S;
+  const bool need_v = S != H || y0 != 0.0 || y1 != (double)S;
+  const int yfirst = cv.bounds[0];
+  const int ylast = cv.bounds[(size_t)(S - 1) * 2] + cv.bounds[(size_t)(S - 1) * 2 + 1];
+  std::vector<uint8_t> tmp;
+  const uint8_t* vin = src;
+  int vin_w = W;
+  if (need_h) {
+    for (int i = 0; i < S; ++i) cv.bounds[(size_t)i * 2] -= yfirst;
+    const int th = ylast - yfirst;
+    tmp.resize((size_t)S * th * 3);
+    for (int yy = 0; yy < th; ++yy) {
+      const uint8_t* row = src + (size_t)(yy + yfirst) * W * 3;
+      for (int xx = 0; xx < S; ++xx) {
+        const int xmin = ch.bounds[(size_t)xx * 2], cnt = ch.bounds[(size_t)xx * 2 + 1];
+        const int32_t* k = &ch.k[(size_t)xx * ch.ksize];
+        int64_t s0 = 1 << (PRECISION_BITS - 1), s1 = s0, s2 = s0;
+        for (int x = 0; x < cnt; ++x) {
+          const uint8_t* p = row + (size_t)(x + xmin) * 3;
+          s0 += (int64_t)p[0] * k[x];
+          s1 += (int64_t)p[1] * k[x];
+          s2 += (int64_t)p[2] * k[x];
+        }
+        uint8_t* o = &tmp[((size_t)yy * S + xx) * 3];
+        o[0] = clip8(s0);
+        o[1] = clip8(s1);
+        o[2] = clip8(s2);
+      }
+    }
+    vin = tmp.data();
+    vin_w = S;
+  } else if (yfirst != 0) {
+    // no horizontal pass: vertical bounds refer to source rows directly
+  }
+  if (need_v) {
+    for (int yy = 0; yy < S; ++yy) {
+      const int ymin = cv.bounds[(size_t)yy * 2], cnt = cv.bounds[(size_t)yy * 2 + 1];
+      const int32_t* k = &cv.k[(size_t)yy * cv.ksize];
+      for (int xx = 0; xx < S; ++xx) {
+        int64_t s0 = 1 << (PRECISION_BITS - 1), s1 = s0, s2 = s0;
+        for (int y = 0; y < cnt; ++y) {
+          const uint8_t* p = vin + ((size_t)(y + ymin) * vin_w + xx) * 3;
+          s0 += (int64_t)p[0] * k[y];
+          s1 += (int64_t)p[1] * k[y];
+          s2 += (int64_t)p[2] * k[y];
+        }
+        uint8_t* o = dst + ((size_t)yy * S + xx) * 3;
+        o[0] = clip8(s0);
+        o[1] = clip8(s1);
+        o[2] = clip8(s2);
+      }
+    }
+  } else {
+    for (int yy = 0; yy < S; ++yy) std::memcpy(dst + (size_t)yy * S * 3, vin + (size_t)yy * vin_w * 3, (size_t)S * 3);
+  }
+}
+
+void resize_nearest(const uint8_t* src, int W, int H, double x0, double y0, double x1, double y1, int S,
+                    uint8_t* dst) {
+  const double sx = (x1 - x0) / S, sy = (y1 - y0) / S;
+  for (int yy = 0; yy < S; ++yy) {
+    int y = (int)(y0 + (yy + 0.5) * sy);
+    y = std::min(std::max(y, 0), H - 1);
+    for (int xx = 0; xx < S; ++xx) {
+      int x = (int)(x0 + (xx + 0.5) * sx);
+      x = std::min(std::max(x, 0), W - 1);
+      std::memcpy(dst + ((size_t)yy * S + xx) * 3, src + ((size_t)y * W + x) * 3, 3);
+    }
+  }
+}
+
+void resize_rgb8(const uint8_t* rgb, int W, int H, int S, const std::string& interp, const std::string& mode,
+                 uint8_t* out) {
+  if (!rgb || !out) throw ClipErr(CLIPGPU_ERR_INVALID, "NULL buffer");
+  if (W <= 0 || H <= 0 || S <= 0) throw ClipErr(CLIPGPU_ERR_INVALID, "Resize error: empty image");
+  double x0 = 0, y0 = 0, x1 = W, y1 = H;
+  if (mode != "squash") {  // src/vision.rs:184-192
+    const double scale = (double)S / (double)std::min(W, H);
+    const double cw = (double)S / scale, chh = (double)S / scale;
+    x0 = ((double)W - cw) / 2.0;
+    y0 = ((double)H - chh) / 2.0;
+    x1 = x0 + cw;
+    y1 = y0 + chh;
+  }
+  if (interp == "bicubic") resize_conv(rgb, W, H, x0, y0, x1, y1, S, bicubic_filter, 2.0, out);
+  else if (interp == "bilinear") resize_conv(rgb, W, H, x0, y0, x1, y1, S, bilinear_filter, 1.0, out);
+  else resize_nearest(rgb, W, H, x0, y0, x1, y1, S, out);
+}
+
+void normalize_pixels(const uint8_t* px, int S, const float* mean, const float* stdv, float* out) {
+  const size_t n = (size_t)S * S;
+  for (int c = 0; c < 3; ++c) {
+    float* o = out + c * n;
+    for (size_t i = 0; i < n; ++i) {
+      const float val = (float)px[i * 3 + c] / 255.0f;
+      o[i] = (val - mean[c]) / stdv[c];
+    }
+  }
+}
+
+void preprocess_one(const uint8_t* rgb, int W, int H, int S, const std::string& interp, const std::string& mode,
+                    const float* mean, const float* stdv, float* out) {
+  std::vector<uint8_t> resized((size_t)S * S * 3);
+  resize_rgb8(rgb, W, H, S, interp, mode, resized.data());
+  normalize_pixels(resized.data(), S, mean, stdv, out);
+}
+
+}  // namespace
+}  // namespace clipgpu
+
+using namespace clipgpu;
+
+extern "C" {
+
+int clipgpu_resize_rgb8(const uint8_t* rgb, int width, int height, int size, const char* interpolation,
+                        const char* resize_mode, uint8_t* out_rgb) {
+  return guarded([&]() {
+    resize_rgb8(rgb, width, height, size, interpolation ? interpolation : "bicubic",
+                resize_mode ? resize_mode : "shortest", out_rgb);
+  });
+}
+
+int clipgpu_preprocess_rgb8(const uint8_t* rgb, int width, int height, int size, const char* interpolation,
+                            const char* resize_mode, const float mean[3], const float stdv[3], float* out_chw) {
+  return guarded([&]() {
+    if (!mean || !stdv || !out_chw) throw ClipErr(CLIPGPU_ERR_INVALID, "NULL buffer");
+    preprocess_one(rgb, width, height, size, interpolation ? interpolation : "bicubic",
+                   resize_mode ? resize_mode : "shortest", mean, stdv, out_chw);
+  });
+}
+
+int clipgpu_preprocess_batch(const uint8_t* const* images, const int* widths, const int* heights, int64_t n,
+                             int size, const char* interpolation, const char* resize_mode, const float mean[3],
+                             const float stdv[3], float* out) {
+  return guarded([&]() {
+    if (n <= 0) throw ClipErr(CLIPGPU_ERR_INVALID, "Empty batch");  // src/vision.rs:121-123
+    if (!images || !widths || !heights || !mean || !stdv || !out) throw ClipErr(CLIPGPU_ERR_INVALID, "NULL buffer");
+    const std::string interp = interpolation ? interpolation : "bicubic";
+    const std::string mode = resize_mode ? resize_mode : "shortest";
+    const size_t per = (size_t)3 * size * size;
+    unsigned nt = std::thread::hardware_concurrency();
+    if (nt == 0) nt = 1;
+    nt = (unsigned)std::min<int64_t>(nt, 16);
+    nt = (unsigned)std::min<int64_t>(nt, n);
+    std::vector<std::thread> th;
+    std::vector<std::string> errs(nt);
+    for (unsigned t = 0; t < nt; ++t) {
+      th.emplace_back([&, t]() {
+        try {
+          for (int64_t i = t; i < n; i += nt)
+            preprocess_one(images[i], widths[i], heights[i], size, interp, mode, mean, stdv, out + i * per);
+        } catch (const std::exception& ex) {
+          errs[t] = ex.what();
+        }
+      });
+    }
+    for (auto& x : th) x.join();
+    for (auto& e : errs)
+      if (!e.empty()) throw ClipErr(CLIPGPU_ERR_INVALID, e);
+  });
+}
+
+}  // extern "C"

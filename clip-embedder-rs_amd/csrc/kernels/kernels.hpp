@@ -1,0 +1,72 @@
+// Host-visible launchers for the clipgpu gfx950 kernels.  All launchers are
+// asynchronous on `stream` and never allocate, copy or synchronise (so a
+// forward can be captured into a hipGraph).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace clipgpu {
+
+enum DType { DT_BF16 = 0, DT_F16 = 1 };
+
+// Source of the GEMM A operand.
+enum ASrc {
+  A_ROWS = 0,     // T16 [M][lda], staged by global_load_lds
+  A_IMG_F32 = 1,  // im2col-free patch rows from normalised f32 NCHW pixels
+  A_IMG_U8 = 2,   // im2col-free patch rows from u8 NHWC pixels, normalised on load
+};
+// GEMM epilogue.
+enum Epi {
+  EPI_STORE16 = 0,  // out16[m][n] = act(acc + bias[n])
+  EPI_RESID = 1,    // out32[m][n] += acc + bias[n]        (residual stream, in place)
+  EPI_STORE32 = 2,  // out32[m][n] = acc + bias[n]
+  EPI_PATCH = 3,    // x[b*(G^2+1) + 1 + p][n] = acc + bias[n] + pos[1 + p][n]
+};
+
+struct GemmParams {
+  const void* A; long lda;   // A_ROWS source
+  const void* W; long ldw;   // [N][K] 16-bit weights
+  const float* bias;         // [N] or nullptr
+  void* out; long ldo;
+  int M, N, K;
+  // image sources (A_IMG_*)
+  const void* img; int S, P, G;
+  float mean[3], stdv[3];
+  const float* pos;          // EPI_PATCH positional embedding [G^2+1][N]
+};
+
+// act: Act enum from common.hpp (only used with EPI_STORE16)
+hipError_t launch_gemm(DType dt, int asrc, int epi, int act, const GemmParams& p, hipStream_t s);
+
+// Multi-head self-attention over packed qkv rows [B*N][3*D] -> out [B*N][D];
+// head_dim must be 64; N <= 256.
+hipError_t launch_attention(DType dt, const void* qkv, void* out, int B, int N, int H, int D,
+                            int causal, hipStream_t s);
+
+// out16[r] = LN(x[r]) for r < rows.
+hipError_t launch_ln_rows(DType dt, const float* x, const float* w, const float* b, float eps,
+                          void* out16, int rows, int D, hipStream_t s);
+
+// Vision stem tail: CLS row = cls + pos[0]; x = ln_pre(x) (in place); h = ln_1(x).
+hipError_t launch_vision_embed_ln(DType dt, float* x, const float* cls, const float* pos,
+                                  const float* lnpre_w, const float* lnpre_b,
+                                  const float* ln1_w, const float* ln1_b, float eps,
+                                  void* h, int B, int tokens, int D, hipStream_t s);
+
+// Text stem: x = tok[ids] + pos; h = ln_1(x).
+hipError_t launch_text_embed_ln(DType dt, const int64_t* ids, const float* tok, const float* pos,
+                                const float* ln1_w, const float* ln1_b, float eps, float* x,
+                                void* h, int B, int T, int D, int vocab, hipStream_t s);
+
+// Pool one row per sequence (CLS: ids == nullptr; else first argmax of ids) and LN it.
+hipError_t launch_pool_ln(DType dt, const float* x, const int64_t* ids, int tokens,
+                          const float* w, const float* b, float eps, void* out16, int B, int D,
+                          hipStream_t s);
+
+// out[r] = in[r] / max(||in[r]||_2, 1e-12)
+hipError_t launch_l2norm(const float* in, float* out, int B, int E, hipStream_t s);
+
+// f32 -> T16 conversion (weight upload).
+hipError_t launch_cast_f32(DType dt, const float* in, void* out, long n, hipStream_t s);
+
+}  // namespace clipgpu

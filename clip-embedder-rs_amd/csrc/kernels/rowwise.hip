@@ -1,0 +1,270 @@
+// Row-wise (one wave per row) kernels: LayerNorm variants, token / patch
+// stems, pooling and L2 normalisation.  All HBM-bound: float4 loads, the row
+// held in registers, two-pass mean/variance in f32 (torch LayerNorm:
+// (x - mean) / sqrt(var + eps) * w + b, biased variance).
+//
+// Reference semantics (graph content from pull_onnx.py:53-68, open_clip):
+//   vision stem: x = [cls; conv1(x)] + pos; x = ln_pre(x)          (a10)
+//   text stem:   x = token_embedding[ids] + positional_embedding    (a16)
+//   tails:       ln_post(x[:,0]) / ln_final(x[b, argmax(ids[b])])    (a13, a18)
+//   F.normalize: x / max(||x||_2, 1e-12)
+#include "common.hpp"
+#include "kernels.hpp"
+
+namespace clipgpu {
+
+namespace {
+
+constexpr int MAXV = 5;  // float4 per lane -> D <= 1280
+
+struct RowRegs {
+  float4 v[MAXV];
+};
+
+__device__ __forceinline__ void load_row(const float* src, int D4, int lane, RowRegs& r) {
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    const int c = i * 64 + lane;
+    r.v[i] = c < D4 ? ((const float4*)src)[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
+__device__ __forceinline__ void layer_norm_regs(const RowRegs& in, RowRegs& out, const float* w, const float* b,
+                                                float eps, int D, int lane) {
+  const int D4 = D >> 2;
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i)
+    if (i * 64 + lane < D4) s += in.v[i].x + in.v[i].y + in.v[i].z + in.v[i].w;
+  const float mean = wave_sum(s) / (float)D;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    const int c = i * 64 + lane;
+    if (c < D4) {
+      const float a = in.v[i].x - mean, bb = in.v[i].y - mean, cc = in.v[i].z - mean, d = in.v[i].w - mean;
+      q += a * a + bb * bb + cc * cc + d * d;
+    }
+  }
+  const float var = wave_sum(q) / (float)D;
+  const float rstd = 1.0f / sqrtf(var + eps);
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    const int c = i * 64 + lane;
+    if (c < D4) {
+      const float4 g = ((const float4*)w)[c];
+      const float4 o = ((const float4*)b)[c];
+      out.v[i].x = (in.v[i].x - mean) * rstd * g.x + o.x;
+      out.v[i].y = (in.v[i].y - mean) * rstd * g.y + o.y;
+      out.v[i].z = (in.v[i].z - mean) * rstd * g.z + o.z;
+      out.v[i].w = (in.v[i].w - mean) * rstd * g.w + o.w;
+    } else {
+      out.v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void store_row16(T* dst, const RowRegs& r, int D4, int lane) {
+  typedef typename Vec4<T>::type V4;
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    const int c = i * 64 + lane;
+    if (c < D4) {
+      V4 o;
+      o[0] = (T)r.v[i].x; o[1] = (T)r.v[i].y; o[2] = (T)r.v[i].z; o[3] = (T)r.v[i].w;
+      ((V4*)dst)[c] = o;
+    }
+  }
+}
+
+__device__ __forceinline__ void store_row32(float* dst, const RowRegs& r, int D4, int lane) {
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    const int c = i * 64 + lane;
+    if (c < D4) ((float4*)dst)[c] = r.v[i];
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void ln_rows_kernel(const float* __restrict__ x, const float* w, const float* b,
+                                                      float eps, T* __restrict__ out, int rows, int D) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  RowRegs r, o;
+  load_row(x + (long)row * D, D >> 2, lane, r);
+  layer_norm_regs(r, o, w, b, eps, D, lane);
+  store_row16(out + (long)row * D, o, D >> 2, lane);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void vision_embed_ln_kernel(float* __restrict__ x, const float* cls,
+                                                              const float* pos, const float* lnpre_w,
+                                                              const float* lnpre_b, const float* ln1_w,
+                                                              const float* ln1_b, float eps, T* __restrict__ h,
+                                                              int rows, int tokens, int D) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const int D4 = D >> 2;
+  RowRegs r, y, z;
+  if (row % tokens == 0) {  // CLS token: class_embedding + positional_embedding[0]
+    RowRegs c, p;
+    load_row(cls, D4, lane, c);
+    load_row(pos, D4, lane, p);
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) {
+      r.v[i].x = c.v[i].x + p.v[i].x; r.v[i].y = c.v[i].y + p.v[i].y;
+      r.v[i].z = c.v[i].z + p.v[i].z; r.v[i].w = c.v[i].w + p.v[i].w;
+    }
+  } else {  // patch rows: conv1 + pos already written by the patch GEMM epilogue
+    load_row(x + (long)row * D, D4, lane, r);
+  }
+  layer_norm_regs(r, y, lnpre_w, lnpre_b, eps, D, lane);
+  store_row32(x + (long)row * D, y, D4, lane);
+  layer_norm_regs(y, z, ln1_w, ln1_b, eps, D, lane);
+  store_row16(h + (long)row * D, z, D4, lane);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void text_embed_ln_kernel(const int64_t* __restrict__ ids, const float* tok,
+                                                            const float* pos, const float* ln1_w,
+                                                            const float* ln1_b, float eps, float* __restrict__ x,
+                                                            T* __restrict__ h, int rows, int Tctx, int D,
+                                                            int vocab) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const int D4 = D >> 2;
+  long id = ids[row];
+  id = id < 0 ? 0 : (id >= vocab ? vocab - 1 : id);  // host validates; clamp keeps the gather in bounds
+  RowRegs e, p, y;
+  load_row(tok + id * D, D4, lane, e);
+  load_row(pos + (long)(row % Tctx) * D, D4, lane, p);
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    e.v[i].x += p.v[i].x; e.v[i].y += p.v[i].y; e.v[i].z += p.v[i].z; e.v[i].w += p.v[i].w;
+  }
+  store_row32(x + (long)row * D, e, D4, lane);
+  layer_norm_regs(e, y, ln1_w, ln1_b, eps, D, lane);
+  store_row16(h + (long)row * D, y, D4, lane);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void pool_ln_kernel(const float* __restrict__ x, const int64_t* __restrict__ ids,
+                                                      int tokens, const float* w, const float* b, float eps,
+                                                      T* __restrict__ out, int B, int D) {
+  const int bi = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (bi >= B) return;
+  int src = 0;
+  if (ids != nullptr) {  // first index of the maximum id (torch argmax; EOT is the largest id)
+    long best = -1;
+    int bidx = 0x7fffffff;
+    for (int t = lane; t < tokens; t += 64) {
+      const long v = ids[(long)bi * tokens + t];
+      if (v > best) { best = v; bidx = t; }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const long ov = __shfl_xor(best, o, 64);
+      const int oi = __shfl_xor(bidx, o, 64);
+      if (ov > best || (ov == best && oi < bidx)) { best = ov; bidx = oi; }
+    }
+    src = bidx;
+  }
+  RowRegs r, y;
+  load_row(x + ((long)bi * tokens + src) * D, D >> 2, lane, r);
+  layer_norm_regs(r, y, w, b, eps, D, lane);
+  store_row16(out + (long)bi * D, y, D >> 2, lane);
+}
+
+__global__ __launch_bounds__(256) void l2norm_kernel(const float* __restrict__ in, float* __restrict__ out, int B,
+                                                     int E) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= B) return;
+  const float* src = in + (long)row * E;
+  float s = 0.f;
+  for (int c = lane; c < E; c += 64) s += src[c] * src[c];
+  const float n = fmaxf(sqrtf(wave_sum(s)), 1e-12f);
+  for (int c = lane; c < E; c += 64) out[(long)row * E + c] = src[c] / n;
+}
+
+template <typename T>
+__global__ void cast_kernel(const float* __restrict__ in, T* __restrict__ out, long n) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    out[i] = (T)in[i];
+}
+
+inline dim3 rows_grid(int rows) { return dim3((rows + 3) / 4); }
+
+}  // namespace
+
+#define CLIPGPU_DISPATCH(dt, KERNEL, GRID, ...)                                              \
+  do {                                                                                        \
+    if ((dt) == DT_BF16) hipLaunchKernelGGL(KERNEL<__bf16>, GRID, dim3(256), 0, s, __VA_ARGS__); \
+    else hipLaunchKernelGGL(KERNEL<_Float16>, GRID, dim3(256), 0, s, __VA_ARGS__);              \
+  } while (0)
+
+hipError_t launch_ln_rows(DType dt, const float* x, const float* w, const float* b, float eps, void* out16,
+                          int rows, int D, hipStream_t s) {
+  if (D % 4 || D > 256 * MAXV) return hipErrorInvalidValue;
+  if (dt == DT_BF16)
+    hipLaunchKernelGGL(ln_rows_kernel<__bf16>, rows_grid(rows), dim3(256), 0, s, x, w, b, eps, (__bf16*)out16, rows, D);
+  else
+    hipLaunchKernelGGL(ln_rows_kernel<_Float16>, rows_grid(rows), dim3(256), 0, s, x, w, b, eps, (_Float16*)out16, rows, D);
+  return hipGetLastError();
+}
+
+hipError_t launch_vision_embed_ln(DType dt, float* x, const float* cls, const float* pos, const float* lnpre_w,
+                                  const float* lnpre_b, const float* ln1_w, const float* ln1_b, float eps,
+                                  void* h, int B, int tokens, int D, hipStream_t s) {
+  if (D % 4 || D > 256 * MAXV) return hipErrorInvalidValue;
+  const int rows = B * tokens;
+  if (dt == DT_BF16)
+    hipLaunchKernelGGL(vision_embed_ln_kernel<__bf16>, rows_grid(rows), dim3(256), 0, s, x, cls, pos, lnpre_w,
+                       lnpre_b, ln1_w, ln1_b, eps, (__bf16*)h, rows, tokens, D);
+  else
+    hipLaunchKernelGGL(vision_embed_ln_kernel<_Float16>, rows_grid(rows), dim3(256), 0, s, x, cls, pos, lnpre_w,
+                       lnpre_b, ln1_w, ln1_b, eps, (_Float16*)h, rows, tokens, D);
+  return hipGetLastError();
+}
+
+hipError_t launch_text_embed_ln(DType dt, const int64_t* ids, const float* tok, const float* pos,
+                                const float* ln1_w, const float* ln1_b, float eps, float* x, void* h, int B,
+                                int T, int D, int vocab, hipStream_t s) {
+  if (D % 4 || D > 256 * MAXV) return hipErrorInvalidValue;
+  const int rows = B * T;
+  if (dt == DT_BF16)
+    hipLaunchKernelGGL(text_embed_ln_kernel<__bf16>, rows_grid(rows), dim3(256), 0, s, ids, tok, pos, ln1_w,
+                       ln1_b, eps, x, (__bf16*)h, rows, T, D, vocab);
+  else
+    hipLaunchKernelGGL(text_embed_ln_kernel<_Float16>, rows_grid(rows), dim3(256), 0, s, ids, tok, pos, ln1_w,
+                       ln1_b, eps, x, (_Float16*)h, rows, T, D, vocab);
+  return hipGetLastError();
+}
+
+hipError_t launch_pool_ln(DType dt, const float* x, const int64_t* ids, int tokens, const float* w,
+                          const float* b, float eps, void* out16, int B, int D, hipStream_t s) {
+  if (D % 4 || D > 256 * MAXV) return hipErrorInvalidValue;
+  if (dt == DT_BF16)
+    hipLaunchKernelGGL(pool_ln_kernel<__bf16>, rows_grid(B), dim3(256), 0, s, x, ids, tokens, w, b, eps,
+                       (__bf16*)out16, B, D);
+  else
+    hipLaunchKernelGGL(pool_ln_kernel<_Float16>, rows_grid(B), dim3(256), 0, s, x, ids, tokens, w, b, eps,
+                       (_Float16*)out16, B, D);
+  return hipGetLastError();
+}
+
+hipError_t launch_l2norm(const float* in, float* out, int B, int E, hipStream_t s) {
+  hipLaunchKernelGGL(l2norm_kernel, rows_grid(B), dim3(256), 0, s, in, out, B, E);
+  return hipGetLastError();
+}
+
+hipError_t launch_cast_f32(DType dt, const float* in, void* out, long n, hipStream_t s) {
+  const long blocks = (n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096;
+  if (dt == DT_BF16)
+    hipLaunchKernelGGL(cast_kernel<__bf16>, dim3((unsigned)blocks), dim3(256), 0, s, in, (__bf16*)out, n);
+  else
+    hipLaunchKernelGGL(cast_kernel<_Float16>, dim3((unsigned)blocks), dim3(256), 0, s, in, (_Float16*)out, n);
+  return hipGetLastError();
+}
+
+}  // namespace clipgpu

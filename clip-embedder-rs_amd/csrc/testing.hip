@@ -1,0 +1,144 @@
+// Kernel-level test hooks (include/clipgpu_testing.h): each runs one kernel on
+// device 0 over host f32 buffers so tests/ can check it against numpy.
+#include <hip/hip_runtime.h>
+
+#include <vector>
+
+#include "../../include/clipgpu.h"
+#include "../../include/clipgpu_testing.h"
+#include "host/api_util.hpp"
+#include "kernels/common.hpp"
+#include "kernels/kernels.hpp"
+
+using namespace clipgpu;
+
+namespace {
+
+#define TCHECK(expr)                                                                                  \
+  do {                                                                                                \
+    hipError_t _e = (expr);                                                                           \
+    if (_e != hipSuccess) throw ClipErr(CLIPGPU_ERR_DEVICE, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+  } while (0)
+
+struct DevBuf {
+  void* p = nullptr;
+  explicit DevBuf(size_t n) {
+    TCHECK(hipMalloc(&p, n ? n : 16));
+    TCHECK(hipMemset(p, 0, n ? n : 16));
+  }
+  ~DevBuf() { (void)hipFree(p); }
+  template <typename T> T* as() const { return (T*)p; }
+};
+
+DType dt_of(int dtype) {
+  if (dtype != CLIPGPU_DTYPE_BF16 && dtype != CLIPGPU_DTYPE_F16) throw ClipErr(CLIPGPU_ERR_INVALID, "bad dtype");
+  return dtype == CLIPGPU_DTYPE_BF16 ? DT_BF16 : DT_F16;
+}
+
+void up(void* d, const void* h, size_t n) { TCHECK(hipMemcpy(d, h, n, hipMemcpyHostToDevice)); }
+void down(void* h, const void* d, size_t n) { TCHECK(hipMemcpy(h, d, n, hipMemcpyDeviceToHost)); }
+
+// f32 host -> 16-bit device
+void up16(DType dt, void* d16, const float* h, size_t n) {
+  DevBuf tmp(n * 4);
+  up(tmp.p, h, n * 4);
+  TCHECK(launch_cast_f32(dt, tmp.as<float>(), d16, (long)n, nullptr));
+  TCHECK(hipDeviceSynchronize());
+}
+
+template <typename T>
+__global__ void widen(const T* in, float* out, long n) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    out[i] = (float)in[i];
+}
+
+void down16(DType dt, float* h, const void* d16, size_t n) {
+  DevBuf tmp(n * 4);
+  if (dt == DT_BF16) hipLaunchKernelGGL(widen<__bf16>, dim3(1024), dim3(256), 0, nullptr, (const __bf16*)d16, tmp.as<float>(), (long)n);
+  else hipLaunchKernelGGL(widen<_Float16>, dim3(1024), dim3(256), 0, nullptr, (const _Float16*)d16, tmp.as<float>(), (long)n);
+  TCHECK(hipGetLastError());
+  TCHECK(hipDeviceSynchronize());
+  down(h, tmp.p, n * 4);
+}
+
+}  // namespace
+
+extern "C" {
+
+int clipgpu_test_gemm(int dtype, int mode, int act, int64_t M, int64_t N, int64_t K, const float* A, const float* W,
+                      const float* bias, const float* resid, float* out) {
+  return guarded([&]() {
+    const DType dt = dt_of(dtype);
+    if (M <= 0 || N <= 0 || K <= 0 || K % 64) throw ClipErr(CLIPGPU_ERR_INVALID, "bad GEMM shape (K % 64 == 0)");
+    DevBuf dA(M * K * 2), dW(N * K * 2), dB(N * 4), dO(M * N * 4);
+    up16(dt, dA.p, A, M * K);
+    up16(dt, dW.p, W, N * K);
+    if (bias) up(dB.p, bias, N * 4);
+    GemmParams g{};
+    g.A = dA.p; g.lda = K; g.W = dW.p; g.ldw = K; g.bias = bias ? dB.as<float>() : nullptr;
+    g.out = dO.p; g.ldo = N; g.M = (int)M; g.N = (int)N; g.K = (int)K;
+    int epi = EPI_STORE16;
+    if (mode == 1) {
+      epi = EPI_RESID;
+      if (resid) up(dO.p, resid, M * N * 4);
+    } else if (mode == 2) {
+      epi = EPI_STORE32;
+    }
+    TCHECK(launch_gemm(dt, A_ROWS, epi, mode == 0 ? act : 0, g, nullptr));
+    TCHECK(hipDeviceSynchronize());
+    if (mode == 0) down16(dt, out, dO.p, M * N);
+    else down(out, dO.p, M * N * 4);
+  });
+}
+
+int clipgpu_test_attention(int dtype, int64_t B, int64_t N, int64_t H, int causal, const float* qkv, float* out) {
+  return guarded([&]() {
+    const DType dt = dt_of(dtype);
+    const int64_t D = H * 64;
+    DevBuf dq(B * N * 3 * D * 2), dO(B * N * D * 2);
+    up16(dt, dq.p, qkv, B * N * 3 * D);
+    TCHECK(launch_attention(dt, dq.p, dO.p, (int)B, (int)N, (int)H, (int)D, causal, nullptr));
+    TCHECK(hipDeviceSynchronize());
+    down16(dt, out, dO.p, B * N * D);
+  });
+}
+
+int clipgpu_test_layernorm(int dtype, int64_t rows, int64_t D, float eps, const float* x, const float* w,
+                           const float* b, float* out) {
+  return guarded([&]() {
+    const DType dt = dt_of(dtype);
+    DevBuf dx(rows * D * 4), dw(D * 4), db(D * 4), dO(rows * D * 2);
+    up(dx.p, x, rows * D * 4);
+    up(dw.p, w, D * 4);
+    up(db.p, b, D * 4);
+    TCHECK(launch_ln_rows(dt, dx.as<float>(), dw.as<float>(), db.as<float>(), eps, dO.p, (int)rows, (int)D, nullptr));
+    TCHECK(hipDeviceSynchronize());
+    down16(dt, out, dO.p, rows * D);
+  });
+}
+
+int clipgpu_test_patch_embed(int dtype, int mode, int64_t B, int64_t S, int64_t P, int64_t D, const void* pixels,
+                             const float mean[3], const float stdv[3], const float* conv_w, const float* pos,
+                             float* x_out) {
+  return guarded([&]() {
+    const DType dt = dt_of(dtype);
+    const int64_t G = S / P, K = 3 * P * P, tokens = G * G + 1;
+    const size_t pix_bytes = mode == 0 ? (size_t)B * 3 * S * S * 4 : (size_t)B * S * S * 3;
+    DevBuf dpix(pix_bytes), dw(D * K * 2), dpos(tokens * D * 4), dx(B * tokens * D * 4);
+    up(dpix.p, pixels, pix_bytes);
+    up16(dt, dw.p, conv_w, D * K);
+    up(dpos.p, pos, tokens * D * 4);
+    GemmParams g{};
+    g.W = dw.p; g.ldw = K; g.out = dx.p; g.ldo = D; g.M = (int)(B * G * G); g.N = (int)D; g.K = (int)K;
+    g.img = dpix.p; g.S = (int)S; g.P = (int)P; g.G = (int)G; g.pos = dpos.as<float>();
+    for (int c = 0; c < 3; ++c) {
+      g.mean[c] = mean ? mean[c] : 0.f;
+      g.stdv[c] = stdv ? stdv[c] : 1.f;
+    }
+    TCHECK(launch_gemm(dt, mode == 0 ? A_IMG_F32 : A_IMG_U8, EPI_PATCH, 0, g, nullptr));
+    TCHECK(hipDeviceSynchronize());
+    down(x_out, dx.p, B * tokens * D * 4);
+  });
+}
+
+}  // extern "C"

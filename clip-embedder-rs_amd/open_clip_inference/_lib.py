@@ -1,0 +1,85 @@
+"""ctypes binding of ``include/clipgpu.h`` (the C ABI of ``lib/libclipgpu.so``).
+
+The shared library is the product: HIP/gfx950 kernels + C++ host runtime.  There
+is no fallback — if the library is missing or fails to load, every entry point
+raises, loudly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_double, c_float, c_int, c_int64, c_uint64, c_void_p
+
+from .error import ClipError, error_for_status
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("CLIPGPU_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libclipgpu.so"))
+
+TOWER_VISION = 0
+TOWER_TEXT = 1
+DTYPE_BF16 = 0
+DTYPE_F16 = 1
+
+# (name, restype, argtypes) — every symbol declared in include/clipgpu.h.
+_PROTOS = [
+    ("clipgpu_last_error", c_char_p, []),
+    ("clipgpu_abi_version", c_int, []),
+    ("clipgpu_create", c_int, [c_char_p, c_int, POINTER(c_int), c_int, c_int, c_int, POINTER(c_void_p)]),
+    ("clipgpu_destroy", None, [c_void_p]),
+    ("clipgpu_embed_dim", c_int, [c_void_p]),
+    ("clipgpu_input_size", c_int, [c_void_p]),
+    ("clipgpu_num_devices", c_int, [c_void_p]),
+    ("clipgpu_embed_pixels", c_int, [c_void_p, c_void_p, c_int64, c_int64, c_void_p]),
+    ("clipgpu_embed_u8", c_int, [c_void_p, c_void_p, c_int64, c_int64, POINTER(c_float), POINTER(c_float), c_void_p]),
+    ("clipgpu_embed_tokens", c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_void_p]),
+    ("clipgpu_embed_pixels_device", c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
+    ("clipgpu_embed_u8_device", c_int, [c_void_p, c_void_p, c_int64, POINTER(c_float), POINTER(c_float), c_void_p, c_void_p]),
+    ("clipgpu_embed_tokens_device", c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
+    ("clipgpu_preprocess_rgb8", c_int, [c_void_p, c_int, c_int, c_int, c_char_p, c_char_p, POINTER(c_float), POINTER(c_float), c_void_p]),
+    ("clipgpu_resize_rgb8", c_int, [c_void_p, c_int, c_int, c_int, c_char_p, c_char_p, c_void_p]),
+    ("clipgpu_preprocess_batch", c_int, [POINTER(c_void_p), POINTER(c_int), POINTER(c_int), c_int64, c_int, c_char_p, c_char_p, POINTER(c_float), POINTER(c_float), c_void_p]),
+    ("clipgpu_tokenizer_create", c_int, [c_char_p, c_int, c_int64, POINTER(c_void_p)]),
+    ("clipgpu_tokenizer_destroy", None, [c_void_p]),
+    ("clipgpu_tokenize", c_int, [c_void_p, POINTER(c_char_p), c_int64, c_int, c_void_p, c_void_p]),
+    ("clipgpu_tokenizer_token_id", c_int64, [c_void_p, c_char_p]),
+    ("clipgpu_tokenizer_vocab_size", c_int64, [c_void_p]),
+    ("clipgpu_profile_enable", c_int, [c_void_p, ctypes.c_uint]),
+    ("clipgpu_profile_read", c_int, [c_void_p, c_int, POINTER(c_double), POINTER(c_int64)]),
+    ("clipgpu_profile_category_name", c_char_p, [c_int]),
+    ("clipgpu_synth_tensor", c_int, [c_uint64, c_char_p, c_double, c_double, c_void_p, c_int64]),
+    # include/clipgpu_testing.h
+    ("clipgpu_test_gemm", c_int, [c_int, c_int, c_int, c_int64, c_int64, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    ("clipgpu_test_attention", c_int, [c_int, c_int64, c_int64, c_int64, c_int, c_void_p, c_void_p]),
+    ("clipgpu_test_layernorm", c_int, [c_int, c_int64, c_int64, c_float, c_void_p, c_void_p, c_void_p, c_void_p]),
+    ("clipgpu_test_patch_embed", c_int, [c_int, c_int, c_int64, c_int64, c_int64, c_int64, c_void_p, POINTER(c_float), POINTER(c_float), c_void_p, c_void_p, c_void_p]),
+]
+
+SYMBOLS = [p[0] for p in _PROTOS]
+
+_lib = None
+
+
+def lib():
+    """Load libclipgpu.so once.  Raises ClipError if it is absent (no fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ClipError(f"clipgpu native library not found at {LIB_PATH}; "
+                            "run `make -C clip-embedder-rs_amd` (or __graft_entry__.build())")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, res, args in _PROTOS:
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc: int) -> None:
+    if rc != 0:
+        msg = lib().clipgpu_last_error().decode("utf-8", "replace")
+        raise error_for_status(rc, msg)
+
+
+def f3(vals):
+    return (c_float * 3)(*[float(v) for v in vals])

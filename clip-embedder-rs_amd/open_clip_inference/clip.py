@@ -1,0 +1,94 @@
+"""``Clip`` facade — mirror of src/clip.rs (kept as-is in the north star; restated
+here because the reference's Rust cannot be compiled in this image).  The math is
+the reference's: dot -> ``mul_add(logit_scale, logit_bias)`` (defaults 1.0 / 0.0)
+-> sigmoid or max-subtracted softmax -> sort descending."""
+from __future__ import annotations
+
+import math
+import os
+from typing import List, Sequence, Tuple
+
+import numpy as np
+
+from .config import ModelConfig
+from .model_manager import verify_model_dir
+from .text import TextEmbedder
+from .vision import VisionEmbedder, _Builder
+
+
+class Clip:
+    def __init__(self, vision: VisionEmbedder, text: TextEmbedder, model_dir: str):
+        self.vision = vision
+        self.text = text
+        self.model_dir = model_dir
+
+    @classmethod
+    def from_local_dir(cls, model_dir: str) -> _Builder:  # src/clip.rs:48-66
+        return _Builder(cls, model_dir=model_dir)
+
+    @classmethod
+    def from_local_id(cls, model_id: str) -> _Builder:  # src/clip.rs:35-46
+        return _Builder(cls, model_id=model_id)
+
+    @classmethod
+    def _build(cls, model_dir, devices, dtype, max_batch):
+        verify_model_dir(model_dir, need_tokenizer=True)
+        v = VisionEmbedder._build(model_dir, devices, dtype, max_batch)
+        t = TextEmbedder._build(model_dir, devices, dtype, max_batch)
+        return cls(v, t, model_dir)
+
+    def duplicate(self) -> "Clip":  # src/clip.rs:68-73
+        return Clip(self.vision.duplicate(), self.text.duplicate(), self.model_dir)
+
+    def get_model_config(self) -> ModelConfig:  # src/clip.rs:75-77
+        return self.text.model_config
+
+    def _scale_bias(self):
+        mc = self.text.model_config
+        scale = 1.0 if mc.logit_scale is None else mc.logit_scale
+        bias = 0.0 if mc.logit_bias is None else mc.logit_bias
+        return np.float32(scale), np.float32(bias)
+
+    def _probs(self, logits: np.ndarray) -> np.ndarray:
+        act = self.text.model_config.activation_function or "softmax"
+        if act == "sigmoid":
+            return np.array([self.sigmoid(float(l)) for l in logits], np.float32)
+        return self.softmax(logits)
+
+    def compare(self, image, text: str) -> float:  # src/clip.rs:79-90
+        v = self.vision.embed_image(image)
+        t = self.text.embed_text(text)
+        sim = np.float32(np.dot(v, t))
+        scale, bias = self._scale_bias()
+        return float(np.float32(sim * scale + bias))
+
+    def classify(self, image, labels: Sequence[str]) -> List[Tuple[str, float]]:  # src/clip.rs:92-132
+        v = self.vision.embed_image(image)
+        t = self.text.embed_texts(labels)
+        scale, bias = self._scale_bias()
+        logits = (t @ v).astype(np.float32) * scale + bias
+        probs = self._probs(logits)
+        res = [(str(l), float(p)) for l, p in zip(labels, probs)]
+        res.sort(key=lambda x: -x[1])  # stable, descending (sort_by partial_cmp)
+        return res
+
+    def rank_images(self, images, text: str) -> List[Tuple[int, float]]:  # src/clip.rs:134-170
+        v = self.vision.embed_images(images)
+        t = self.text.embed_text(text)
+        scale, bias = self._scale_bias()
+        logits = (v @ t).astype(np.float32) * scale + bias
+        probs = self._probs(logits)
+        res = [(i, float(p)) for i, p in enumerate(probs)]
+        res.sort(key=lambda x: -x[1])
+        return res
+
+    @staticmethod
+    def softmax(logits) -> np.ndarray:  # src/clip.rs:172-179
+        x = np.asarray(logits, np.float32)
+        m = np.float32(-np.inf) if x.size == 0 else x.max()
+        e = np.exp(x - m).astype(np.float32)
+        return (e / e.sum(dtype=np.float32)).astype(np.float32)
+
+    @staticmethod
+    def sigmoid(logit: float) -> float:  # src/clip.rs:181-185
+        return float(np.float32(1.0) / (np.float32(1.0) + np.exp(np.float32(-logit))))

@@ -1,0 +1,167 @@
+"""Thin owners of the native handles: ``Engine`` (one tower on N GPUs, replaces
+``OnnxSession``, src/onnx.rs:7-47) and ``Tokenizer`` (replaces
+``tokenizers::Tokenizer`` as configured in src/text.rs:62-85)."""
+from __future__ import annotations
+
+import ctypes
+from ctypes import POINTER, c_char_p, c_int, c_void_p
+from typing import Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, f3, lib
+
+
+class Engine:
+    def __init__(self, model_dir: str, tower: int, devices: Optional[Sequence[int]] = None,
+                 dtype: str = "bf16", max_batch: int = 256):
+        self.model_dir = model_dir
+        self.tower = tower
+        self.devices = list(devices) if devices else [0]
+        self.dtype = dtype
+        self.max_batch = int(max_batch)
+        dt = {"bf16": _lib.DTYPE_BF16, "f16": _lib.DTYPE_F16, "fp16": _lib.DTYPE_F16}[dtype]
+        devs = (c_int * len(self.devices))(*self.devices)
+        h = c_void_p()
+        check(lib().clipgpu_create(model_dir.encode(), tower, devs, len(self.devices), dt, self.max_batch,
+                                   ctypes.byref(h)))
+        self._h = h
+
+    @property
+    def handle(self):
+        if self._h is None:
+            raise RuntimeError("engine destroyed")
+        return self._h
+
+    def close(self):
+        if getattr(self, "_h", None) is not None:
+            lib().clipgpu_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def embed_dim(self) -> int:
+        return lib().clipgpu_embed_dim(self.handle)
+
+    @property
+    def input_size(self) -> int:
+        return lib().clipgpu_input_size(self.handle)
+
+    def embed_pixels(self, nchw: np.ndarray) -> np.ndarray:
+        x = np.ascontiguousarray(nchw, dtype=np.float32)
+        if x.ndim != 4 or x.shape[1] != 3 or x.shape[2] != x.shape[3]:
+            from .error import ShapeError
+            raise ShapeError(f"Shape error: expected [B,3,S,S], got {x.shape}")
+        out = np.empty((x.shape[0], self.embed_dim), np.float32)
+        check(lib().clipgpu_embed_pixels(self.handle, x.ctypes.data, x.shape[0], x.shape[2], out.ctypes.data))
+        return out
+
+    def embed_u8(self, nhwc: np.ndarray, mean, std) -> np.ndarray:
+        x = np.ascontiguousarray(nhwc, dtype=np.uint8)
+        out = np.empty((x.shape[0], self.embed_dim), np.float32)
+        check(lib().clipgpu_embed_u8(self.handle, x.ctypes.data, x.shape[0], x.shape[1], f3(mean), f3(std),
+                                     out.ctypes.data))
+        return out
+
+    def embed_tokens(self, ids: np.ndarray, mask: Optional[np.ndarray] = None) -> np.ndarray:
+        x = np.ascontiguousarray(ids, dtype=np.int64)
+        m = None if mask is None else np.ascontiguousarray(mask, dtype=np.int64)
+        out = np.empty((x.shape[0], self.embed_dim), np.float32)
+        check(lib().clipgpu_embed_tokens(self.handle, x.ctypes.data, None if m is None else m.ctypes.data,
+                                         x.shape[0], x.shape[1], out.ctypes.data))
+        return out
+
+    # Device-resident variants: raw device pointers (ints), stream = hipStream_t or 0.
+    def embed_pixels_device(self, d_in: int, B: int, d_out: int, stream: int = 0) -> None:
+        check(lib().clipgpu_embed_pixels_device(self.handle, c_void_p(d_in), B, c_void_p(d_out),
+                                                c_void_p(stream or None)))
+
+    def embed_u8_device(self, d_in: int, B: int, mean, std, d_out: int, stream: int = 0) -> None:
+        check(lib().clipgpu_embed_u8_device(self.handle, c_void_p(d_in), B, f3(mean), f3(std), c_void_p(d_out),
+                                            c_void_p(stream or None)))
+
+    def embed_tokens_device(self, d_ids: int, B: int, d_out: int, stream: int = 0) -> None:
+        check(lib().clipgpu_embed_tokens_device(self.handle, c_void_p(d_ids), B, c_void_p(d_out),
+                                                c_void_p(stream or None)))
+
+
+PROFILE_CATEGORIES = ["patch_embed", "stem_ln", "qkv", "attention", "out_proj", "layernorm", "c_fc",
+                      "c_proj", "head"]
+
+
+def profile_enable(engine: "Engine", categories) -> None:
+    mask = 0
+    for c in categories:
+        mask |= 1 << PROFILE_CATEGORIES.index(c)
+    check(lib().clipgpu_profile_enable(engine.handle, mask))
+
+
+def profile_read(engine: "Engine", category: str):
+    ms = ctypes.c_double()
+    n = ctypes.c_int64()
+    check(lib().clipgpu_profile_read(engine.handle, PROFILE_CATEGORIES.index(category), ctypes.byref(ms),
+                                     ctypes.byref(n)))
+    return ms.value, n.value
+
+
+class Tokenizer:
+    def __init__(self, tokenizer_json: str, context_length: int, pad_id: Optional[int] = None):
+        h = c_void_p()
+        check(lib().clipgpu_tokenizer_create(tokenizer_json.encode(), int(context_length),
+                                             -1 if pad_id is None else int(pad_id), ctypes.byref(h)))
+        self._h = h
+        self.context_length = int(context_length)
+
+    def close(self):
+        if getattr(self, "_h", None) is not None:
+            lib().clipgpu_tokenizer_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def token_id(self, tok: str) -> Optional[int]:
+        v = lib().clipgpu_tokenizer_token_id(self._h, tok.encode("utf-8"))
+        return None if v < 0 else int(v)
+
+    @property
+    def vocab_size(self) -> int:
+        return int(lib().clipgpu_tokenizer_vocab_size(self._h))
+
+    def encode_batch(self, texts: Sequence[str], lowercase: bool = False):
+        n = len(texts)
+        enc = [t.encode("utf-8") for t in texts]
+        arr = (c_char_p * max(n, 1))(*enc)
+        ids = np.empty((n, self.context_length), np.int64)
+        mask = np.empty((n, self.context_length), np.int64)
+        check(lib().clipgpu_tokenize(self._h, arr, n, 1 if lowercase else 0, ids.ctypes.data, mask.ctypes.data))
+        return ids, mask
+
+
+def resize_rgb8(rgb: np.ndarray, size: int, interpolation: str = "bicubic", resize_mode: str = "shortest"):
+    x = np.ascontiguousarray(rgb, dtype=np.uint8)
+    out = np.empty((size, size, 3), np.uint8)
+    check(lib().clipgpu_resize_rgb8(x.ctypes.data, x.shape[1], x.shape[0], size, interpolation.encode(),
+                                    resize_mode.encode(), out.ctypes.data))
+    return out
+
+
+def preprocess_batch_rgb8(images, size: int, interpolation: str, resize_mode: str, mean, std) -> np.ndarray:
+    arrs = [np.ascontiguousarray(a, dtype=np.uint8) for a in images]
+    n = len(arrs)
+    out = np.empty((n, 3, size, size), np.float32)
+    ptrs = (c_void_p * max(n, 1))(*[a.ctypes.data for a in arrs])
+    ws = (c_int * max(n, 1))(*[a.shape[1] for a in arrs])
+    hs = (c_int * max(n, 1))(*[a.shape[0] for a in arrs])
+    check(lib().clipgpu_preprocess_batch(ptrs, ws, hs, n, size, interpolation.encode(), resize_mode.encode(),
+                                         f3(mean), f3(std), out.ctypes.data))
+    return out

@@ -1,0 +1,145 @@
+/*
+ * clipgpu — MI355X-native CLIP embedding engine, C ABI.
+ *
+ * This is the drop-in boundary for the hot path of RuurdBijlsma/clip-embedder-rs
+ * (crate open_clip_inference v0.4.0):
+ *
+ *     image/text -> preprocess/tokenize -> ViT / text transformer -> L2-normalised [B, E]
+ *
+ * Each entry point names the reference interface it replaces (file:line under the
+ * reference tree).  Conventions mirror the reference:
+ *   - caller owns every input/output buffer; the engine copies in and out
+ *     (Value::from_array + .to_owned(), src/vision.rs:105-113, src/text.rs:153-166);
+ *   - return 0 on success, non-zero on error; clipgpu_last_error() gives the
+ *     thread-local message (maps to ClipError::Inference / ::Config / ::Io, src/error.rs:9-41);
+ *   - an empty batch is an error "Empty batch" (src/vision.rs:121-123);
+ *   - one call per handle at a time: each handle serialises its callers with an internal
+ *     mutex (the reference's RwLock write lock, src/vision.rs:107, src/text.rs:155);
+ *     separate handles are independent (duplicate(), src/vision.rs:86-91).
+ * No torch / ndarray / ort types cross this boundary: plain pointers and sizes only.
+ */
+#ifndef CLIPGPU_H
+#define CLIPGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CLIPGPU_ABI_VERSION 1
+
+enum clipgpu_status {
+  CLIPGPU_OK = 0,
+  CLIPGPU_ERR_INVALID = 1,   /* bad argument / shape          -> ClipError::Inference / Shape */
+  CLIPGPU_ERR_CONFIG = 2,    /* model dir / config problem    -> ClipError::Config / MissingModelFile */
+  CLIPGPU_ERR_IO = 3,        /* file system                   -> ClipError::Io */
+  CLIPGPU_ERR_DEVICE = 4,    /* HIP / RCCL failure            -> ClipError::Inference */
+  CLIPGPU_ERR_TOKENIZER = 5  /* tokenizer failure             -> ClipError::Tokenizer */
+};
+
+enum clipgpu_tower { CLIPGPU_TOWER_VISION = 0, CLIPGPU_TOWER_TEXT = 1 };
+enum clipgpu_dtype { CLIPGPU_DTYPE_BF16 = 0, CLIPGPU_DTYPE_F16 = 1 };
+
+typedef struct clipgpu_engine clipgpu_engine;       /* one tower on one or more GPUs (== one OnnxSession) */
+typedef struct clipgpu_tokenizer clipgpu_tokenizer; /* CLIP BPE tokenizer (== tokenizers::Tokenizer) */
+
+/* Thread-local message for the last failed call on this thread ("" if none). */
+const char* clipgpu_last_error(void);
+int clipgpu_abi_version(void);
+
+/* ---- engine lifecycle ----------------------------------------------------------------
+ * Replaces OnnxSession::new (src/onnx.rs:13-30) as called by VisionEmbedder::from_local_dir
+ * (src/vision.rs:58-84) / TextEmbedder::from_local_dir (src/text.rs:54-101).
+ * model_dir must hold open_clip_config.json and model_config.json plus a weight source:
+ * open_clip_model.safetensors, or clipgpu_synthetic.json {"seed": N} (seeded weights).
+ * device_ids/n_devices: the GPUs this handle replicates the weights onto (data-parallel
+ * batch sharding across them); NULL/0 = device 0.  max_batch: rows per device per launch
+ * (larger batches are processed in chunks). */
+int clipgpu_create(const char* model_dir, int tower, const int* device_ids, int n_devices, int dtype,
+                   int max_batch, clipgpu_engine** out);
+void clipgpu_destroy(clipgpu_engine* e);
+
+int clipgpu_embed_dim(const clipgpu_engine* e);      /* E */
+int clipgpu_input_size(const clipgpu_engine* e);     /* vision: image_size S; text: context length T */
+int clipgpu_num_devices(const clipgpu_engine* e);
+
+/* ---- vision forward ------------------------------------------------------------------
+ * Replaces session.run(pixel_values) + extract in VisionEmbedder::embed_images
+ * (src/vision.rs:100-117).  nchw: [B,3,S,S] f32, already normalised (preprocess_batch
+ * output, src/vision.rs:119-135).  out: [B,E] f32 row-major, L2-normalised. */
+int clipgpu_embed_pixels(clipgpu_engine* e, const float* nchw, int64_t B, int64_t S, float* out);
+
+/* Device-side-normalise variant: nhwc u8 [B,S,S,3] (already resized/cropped), mean/std
+ * applied on the GPU exactly as normalize_pixels (src/vision.rs:235-259). */
+int clipgpu_embed_u8(clipgpu_engine* e, const uint8_t* nhwc, int64_t B, int64_t S, const float mean[3],
+                     const float std[3], float* out);
+
+/* ---- text forward ---------------------------------------------------------------------
+ * Replaces session.run(input_ids [, attention_mask]) in TextEmbedder::embed_texts
+ * (src/text.rs:148-169).  ids: [B,T] int64; mask may be NULL (the exported text graph has
+ * no mask input, pull_onnx.py:296-302; it is accepted and ignored, as the reference does
+ * when the graph lacks "attention_mask", src/text.rs:156-161). */
+int clipgpu_embed_tokens(clipgpu_engine* e, const int64_t* ids, const int64_t* mask, int64_t B, int64_t T,
+                         float* out);
+
+/* ---- device-resident entry points (benchmarks, zero-copy pipelines) ----------------------
+ * Inputs/outputs are device pointers on the handle's first device; work is enqueued on
+ * `stream` (a hipStream_t; NULL = the handle's own stream) and the call returns without
+ * synchronising.  B <= max_batch. */
+int clipgpu_embed_pixels_device(clipgpu_engine* e, const float* d_nchw, int64_t B, float* d_out, void* stream);
+int clipgpu_embed_u8_device(clipgpu_engine* e, const uint8_t* d_nhwc, int64_t B, const float mean[3],
+                            const float std[3], float* d_out, void* stream);
+int clipgpu_embed_tokens_device(clipgpu_engine* e, const int64_t* d_ids, int64_t B, float* d_out, void* stream);
+
+/* ---- host preprocessing (src/vision.rs:119-259) ----------------------------------------
+ * rgb: [h][w][3] u8 (DynamicImage::to_rgb8 layout).  Resize with the crop box of
+ * resize_with_fast_image_resize (src/vision.rs:164-198): unless resize_mode == "squash",
+ * the centred min(w,h) square; interpolation "bicubic" (CatmullRom) / "bilinear" / other
+ * (nearest).  Then normalize_pixels (src/vision.rs:235-259) into out_chw [3][size][size]. */
+int clipgpu_preprocess_rgb8(const uint8_t* rgb, int width, int height, int size, const char* interpolation,
+                            const char* resize_mode, const float mean[3], const float std[3], float* out_chw);
+/* Resize/crop only: out_rgb [size][size][3] u8. */
+int clipgpu_resize_rgb8(const uint8_t* rgb, int width, int height, int size, const char* interpolation,
+                        const char* resize_mode, uint8_t* out_rgb);
+/* Batch preprocess with a host thread pool (preprocess_batch's rayon loop, src/vision.rs:128-132):
+ * images[i] is [heights[i]][widths[i]][3] u8; out: [n][3][size][size]. */
+int clipgpu_preprocess_batch(const uint8_t* const* images, const int* widths, const int* heights, int64_t n,
+                             int size, const char* interpolation, const char* resize_mode, const float mean[3],
+                             const float std[3], float* out);
+
+/* ---- tokenizer (src/text.rs:62-139) ----------------------------------------------------
+ * Loads a HF tokenizers CLIP tokenizer.json (BPE + ByteLevel, </w> suffix) and applies
+ * with_padding(Fixed(context_length), pad_id) + with_truncation(max_length=context_length)
+ * as TextEmbedder::from_local_dir does (src/text.rs:70-85).  pad_id < 0: look up "<pad>"
+ * in the vocab (src/text.rs:70-73). */
+int clipgpu_tokenizer_create(const char* tokenizer_json, int context_length, int64_t pad_id,
+                             clipgpu_tokenizer** out);
+void clipgpu_tokenizer_destroy(clipgpu_tokenizer* t);
+/* texts: n NUL-terminated UTF-8 strings.  lowercase != 0 applies str::to_lowercase first
+ * (tokenizer_needs_lowercase, src/text.rs:115-117).  ids, mask: [n][context_length]. */
+int clipgpu_tokenize(clipgpu_tokenizer* t, const char* const* texts, int64_t n, int lowercase, int64_t* ids,
+                     int64_t* mask);
+/* Token id of a vocab string, or -1. */
+int64_t clipgpu_tokenizer_token_id(const clipgpu_tokenizer* t, const char* token);
+int64_t clipgpu_tokenizer_vocab_size(const clipgpu_tokenizer* t);
+
+/* ---- live kernel timing -------------------------------------------------------------------
+ * Records HIP events around every launch whose category bit is set in `mask` (on the launch
+ * stream), for the device-resident entry points.  Categories: 0 patch_embed, 1 stem_ln, 2 qkv,
+ * 3 attention, 4 out_proj, 5 layernorm, 6 c_fc, 7 c_proj, 8 head.  enable() resets totals;
+ * read() waits for the recorded events and returns the summed ms and launch count. */
+int clipgpu_profile_enable(clipgpu_engine* e, unsigned mask);
+int clipgpu_profile_read(clipgpu_engine* e, int category, double* total_ms, int64_t* launches);
+const char* clipgpu_profile_category_name(int category);
+
+/* ---- test hooks --------------------------------------------------------------------------
+ * The seeded weight generator shared with the oracle (bit-exact). */
+int clipgpu_synth_tensor(uint64_t seed, const char* name, double std, double offset, float* out, int64_t n);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CLIPGPU_H */

@@ -1,0 +1,41 @@
+/*
+ * clipgpu kernel-level test hooks (not part of the drop-in surface).
+ *
+ * Each hook uploads host f32 buffers, runs ONE gfx950 kernel of the hot path on
+ * device 0, and copies the result back, so tests/ can check every kernel in
+ * isolation against a numpy fp32/fp64 reference of the same op.  All return 0 on
+ * success (message via clipgpu_last_error()).  dtype: CLIPGPU_DTYPE_BF16 / _F16.
+ */
+#ifndef CLIPGPU_TESTING_H
+#define CLIPGPU_TESTING_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* out[M][N] = act(A[M][K] . W[N][K]^T + bias[N]) (act: 0 none, 1 quick_gelu, 2 gelu, 3 gelu_tanh).
+ * mode 0: 16-bit output (returned as f32); mode 1: residual (out = resid + ...); mode 2: f32 output.
+ * bias and resid may be NULL. */
+int clipgpu_test_gemm(int dtype, int mode, int act, int64_t M, int64_t N, int64_t K, const float* A,
+                      const float* W, const float* bias, const float* resid, float* out);
+
+/* qkv: [B*N][3*D] f32 (rounded to 16-bit on upload); out: [B*N][D]. */
+int clipgpu_test_attention(int dtype, int64_t B, int64_t N, int64_t H, int causal, const float* qkv, float* out);
+
+/* out[r] = LN(x[r]) (16-bit output returned as f32). */
+int clipgpu_test_layernorm(int dtype, int64_t rows, int64_t D, float eps, const float* x, const float* w,
+                           const float* b, float* out);
+
+/* Patch-embedding GEMM from normalised f32 NCHW pixels (mode 0) or u8 NHWC (mode 1):
+ * x_out[B*(G*G+1)][D]: rows of patch tokens = conv + pos (CLS rows untouched = 0). */
+int clipgpu_test_patch_embed(int dtype, int mode, int64_t B, int64_t S, int64_t P, int64_t D, const void* pixels,
+                             const float mean[3], const float std[3], const float* conv_w, const float* pos,
+                             float* x_out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CLIPGPU_TESTING_H */

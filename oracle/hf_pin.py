@@ -1,0 +1,101 @@
+"""Independent implementation used to pin ``clip_ref`` — TEST INFRASTRUCTURE.
+
+Loads the oracle's seeded open_clip-named weights into HF ``transformers``
+``CLIPVisionModelWithProjection`` / ``CLIPTextModelWithProjection`` (same
+architecture as open_clip's OpenAI-style ViT / text transformer), so the two
+implementations can be compared on identical parameters.  Imported only by
+``tests/`` and ``tests/golden/make_golden.py``.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def _split_block(P, src, dst, D, sd):
+    w = P[src + "attn.in_proj_weight"]
+    b = P[src + "attn.in_proj_bias"]
+    for j, nm in enumerate(("q_proj", "k_proj", "v_proj")):
+        sd[dst + f"self_attn.{nm}.weight"] = w[j * D:(j + 1) * D]
+        sd[dst + f"self_attn.{nm}.bias"] = b[j * D:(j + 1) * D]
+    sd[dst + "self_attn.out_proj.weight"] = P[src + "attn.out_proj.weight"]
+    sd[dst + "self_attn.out_proj.bias"] = P[src + "attn.out_proj.bias"]
+    sd[dst + "layer_norm1.weight"] = P[src + "ln_1.weight"]
+    sd[dst + "layer_norm1.bias"] = P[src + "ln_1.bias"]
+    sd[dst + "layer_norm2.weight"] = P[src + "ln_2.weight"]
+    sd[dst + "layer_norm2.bias"] = P[src + "ln_2.bias"]
+    sd[dst + "mlp.fc1.weight"] = P[src + "mlp.c_fc.weight"]
+    sd[dst + "mlp.fc1.bias"] = P[src + "mlp.c_fc.bias"]
+    sd[dst + "mlp.fc2.weight"] = P[src + "mlp.c_proj.weight"]
+    sd[dst + "mlp.fc2.bias"] = P[src + "mlp.c_proj.bias"]
+
+
+def hf_vision(P, v, dtype="float64"):
+    import torch
+    from transformers import CLIPVisionConfig, CLIPVisionModelWithProjection
+    cfg = CLIPVisionConfig(hidden_size=v.width, intermediate_size=v.mlp_width,
+                           num_hidden_layers=v.layers, num_attention_heads=v.heads,
+                           image_size=v.image_size, patch_size=v.patch_size,
+                           projection_dim=v.embed_dim, hidden_act=v.act,
+                           layer_norm_eps=v.ln_eps, attn_implementation="eager")
+    m = CLIPVisionModelWithProjection(cfg).eval()
+    sd = {
+        "vision_model.embeddings.patch_embedding.weight": P["visual.conv1.weight"],
+        "vision_model.embeddings.class_embedding": P["visual.class_embedding"],
+        "vision_model.embeddings.position_embedding.weight": P["visual.positional_embedding"],
+        "vision_model.pre_layrnorm.weight": P["visual.ln_pre.weight"],
+        "vision_model.pre_layrnorm.bias": P["visual.ln_pre.bias"],
+        "vision_model.post_layernorm.weight": P["visual.ln_post.weight"],
+        "vision_model.post_layernorm.bias": P["visual.ln_post.bias"],
+        "visual_projection.weight": P["visual.proj"].T,
+    }
+    for i in range(v.layers):
+        _split_block(P, f"visual.transformer.resblocks.{i}.",
+                     f"vision_model.encoder.layers.{i}.", v.width, sd)
+    sd = {k: torch.from_numpy(np.ascontiguousarray(a)) for k, a in sd.items()}
+    missing, unexpected = m.load_state_dict(sd, strict=False)
+    missing = [k for k in missing if not k.endswith("position_ids")]
+    assert not missing and not unexpected, (missing, unexpected)
+    return m.to(getattr(torch, dtype))
+
+
+def hf_text(P, t, dtype="float64"):
+    import torch
+    from transformers import CLIPTextConfig, CLIPTextModelWithProjection
+    cfg = CLIPTextConfig(vocab_size=t.vocab_size, hidden_size=t.width,
+                         intermediate_size=t.mlp_width, num_hidden_layers=t.layers,
+                         num_attention_heads=t.heads, max_position_embeddings=t.context_length,
+                         projection_dim=t.embed_dim, hidden_act=t.act, layer_norm_eps=t.ln_eps,
+                         eos_token_id=2,  # legacy switch: pool at argmax(input_ids)
+                         attn_implementation="eager")
+    m = CLIPTextModelWithProjection(cfg).eval()
+    sd = {
+        "text_model.embeddings.token_embedding.weight": P["token_embedding.weight"],
+        "text_model.embeddings.position_embedding.weight": P["positional_embedding"],
+        "text_model.final_layer_norm.weight": P["ln_final.weight"],
+        "text_model.final_layer_norm.bias": P["ln_final.bias"],
+        "text_projection.weight": P["text_projection"].T,
+    }
+    for i in range(t.layers):
+        _split_block(P, f"transformer.resblocks.{i}.", f"text_model.encoder.layers.{i}.", t.width, sd)
+    sd = {k: torch.from_numpy(np.ascontiguousarray(a)) for k, a in sd.items()}
+    missing, unexpected = m.load_state_dict(sd, strict=False)
+    missing = [k for k in missing if not k.endswith("position_ids")]
+    assert not missing and not unexpected, (missing, unexpected)
+    return m.to(getattr(torch, dtype))
+
+
+def hf_encode_image(m, pixels):
+    import torch
+    dt = next(m.parameters()).dtype
+    with torch.no_grad():
+        e = m(pixel_values=torch.from_numpy(np.asarray(pixels)).to(dt)).image_embeds
+        e = torch.nn.functional.normalize(e, dim=-1)
+    return e.double().numpy()
+
+
+def hf_encode_text(m, ids):
+    import torch
+    with torch.no_grad():
+        e = m(input_ids=torch.from_numpy(np.asarray(ids, np.int64))).text_embeds
+        e = torch.nn.functional.normalize(e, dim=-1)
+    return e.double().numpy()

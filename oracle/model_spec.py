@@ -1,0 +1,154 @@
+"""Architecture spec derived from a model dir's ``open_clip_config.json``.
+
+TEST INFRASTRUCTURE (see ``oracle/__init__.py``).
+
+The reference parses only ``embed_dim``, ``vision_cfg.{image_size,layers?,width?}``
+and ``text_cfg.{context_length,hf_tokenizer_name?}`` (``src/config.rs:29-47``)
+because everything else is baked into the ONNX graphs.  The graphs themselves are
+open_clip ``VisionTransformer`` / ``TextTransformer`` modules exported by
+``pull_onnx.py:53-68``; their defaults (head_width 64, mlp_ratio 4, LayerNorm eps
+1e-5, CLS-token pooling, argmax/EOT text pooling, QuickGELU iff
+``model_cfg.quick_gelu``) are restated here.  The C++ engine parses the same file
+independently (``csrc/host/config.cpp``).
+"""
+from __future__ import annotations
+
+import json
+import os
+from dataclasses import dataclass, asdict
+
+
+@dataclass(frozen=True)
+class VisionSpec:
+    image_size: int
+    patch_size: int
+    width: int
+    layers: int
+    heads: int
+    mlp_width: int
+    embed_dim: int
+    act: str            # "quick_gelu" | "gelu" | "gelu_tanh"
+    ln_eps: float = 1e-5
+
+    @property
+    def grid(self) -> int:
+        return self.image_size // self.patch_size
+
+    @property
+    def tokens(self) -> int:
+        return self.grid * self.grid + 1  # + CLS
+
+    @property
+    def head_dim(self) -> int:
+        return self.width // self.heads
+
+
+@dataclass(frozen=True)
+class TextSpec:
+    context_length: int
+    vocab_size: int
+    width: int
+    layers: int
+    heads: int
+    mlp_width: int
+    embed_dim: int
+    act: str
+    ln_eps: float = 1e-5
+
+    @property
+    def head_dim(self) -> int:
+        return self.width // self.heads
+
+
+def _act(model_cfg: dict, sub: dict) -> str:
+    if sub.get("act_layer") in ("gelu_tanh", "gelu_pytorch_tanh"):
+        return "gelu_tanh"
+    return "quick_gelu" if model_cfg.get("quick_gelu", False) else "gelu"
+
+
+def vision_spec_from_cfg(model_cfg: dict) -> VisionSpec:
+    v = model_cfg["vision_cfg"]
+    for unsupported in ("timm_model_name", "attentional_pool", "attn_pooler_queries"):
+        if v.get(unsupported):
+            raise ValueError(f"vision_cfg.{unsupported} is not supported by this oracle")
+    width = int(v.get("width", 768))
+    head_width = int(v.get("head_width", 64))
+    return VisionSpec(
+        image_size=int(v["image_size"]),
+        patch_size=int(v.get("patch_size", 16)),
+        width=width,
+        layers=int(v.get("layers", 12)),
+        heads=width // head_width,
+        mlp_width=int(width * float(v.get("mlp_ratio", 4.0))),
+        embed_dim=int(model_cfg["embed_dim"]),
+        act=_act(model_cfg, v),
+    )
+
+
+def text_spec_from_cfg(model_cfg: dict) -> TextSpec:
+    t = model_cfg["text_cfg"]
+    if t.get("hf_model_name"):
+        raise ValueError("text_cfg.hf_model_name (HF text towers) is not supported by this oracle")
+    width = int(t.get("width", 512))
+    return TextSpec(
+        context_length=int(t.get("context_length", 77)),
+        vocab_size=int(t.get("vocab_size", 49408)),
+        width=width,
+        layers=int(t.get("layers", 12)),
+        heads=int(t.get("heads", 8)),
+        mlp_width=int(width * float(t.get("mlp_ratio", 4.0))),
+        embed_dim=int(model_cfg["embed_dim"]),
+        act=_act(model_cfg, t),
+    )
+
+
+def load_model_dir(model_dir: str):
+    with open(os.path.join(model_dir, "open_clip_config.json")) as f:
+        oc = json.load(f)
+    mc = oc["model_cfg"]
+    return vision_spec_from_cfg(mc), text_spec_from_cfg(mc), oc
+
+
+# ---------------------------------------------------------------------------
+# Canonical configs used by tests and bench (open_clip_config.json contents).
+# ---------------------------------------------------------------------------
+
+OPENAI_MEAN = [0.48145466, 0.4578275, 0.40821073]
+OPENAI_STD = [0.26862954, 0.26130258, 0.27577711]
+
+VIT_B_32_CFG = {
+    "model_cfg": {
+        "embed_dim": 512,
+        "quick_gelu": True,
+        "vision_cfg": {"image_size": 224, "layers": 12, "width": 768, "patch_size": 32},
+        "text_cfg": {"context_length": 77, "vocab_size": 49408, "width": 512,
+                     "heads": 8, "layers": 12},
+    },
+    "preprocess_cfg": {"mean": OPENAI_MEAN, "std": OPENAI_STD},
+}
+
+# Small config with the same structure, for fast oracle/GPU parity cases.
+TINY_CFG = {
+    "model_cfg": {
+        "embed_dim": 64,
+        "quick_gelu": True,
+        "vision_cfg": {"image_size": 64, "layers": 2, "width": 128, "patch_size": 16},
+        "text_cfg": {"context_length": 16, "vocab_size": 1000, "width": 128,
+                     "heads": 2, "layers": 2},
+    },
+    "preprocess_cfg": {"mean": OPENAI_MEAN, "std": OPENAI_STD},
+}
+
+# model_config.json as written by pull_onnx.py:128-150 for an OpenAI CLIP.
+OPENAI_MODEL_CONFIG = {
+    "logit_scale": 100.0,
+    "logit_bias": 0.0,
+    "activation_function": "softmax",
+    "tokenizer_needs_lowercase": False,
+    "pad_id": 0,
+    "vocab_size": 49408,
+}
+
+
+def spec_dict(spec) -> dict:
+    return asdict(spec)

@@ -1,0 +1,158 @@
+"""Per-kernel numerics on the GPU vs numpy references of the same op.
+
+Every kernel of the hot path runs in isolation through include/clipgpu_testing.h
+hooks; inputs are pre-rounded to the kernel's 16-bit operand type so that the
+comparison isolates accumulation/epilogue error.  Tolerances are stated per test.
+"""
+import numpy as np
+import pytest
+
+from oracle import clip_ref
+
+pytestmark = pytest.mark.gpu
+
+BF16, F16 = 0, 1
+
+
+def _lib():
+    from open_clip_inference import _lib
+    return _lib
+
+
+def round16(x, dtype):
+    x = np.asarray(x, np.float32)
+    if dtype == F16:
+        return x.astype(np.float16).astype(np.float32)
+    u = x.view(np.uint32).astype(np.uint64)
+    u = ((u + 0x7FFF + ((u >> 16) & 1)) & 0xFFFF0000).astype(np.uint32)
+    return u.view(np.float32)
+
+
+def ref_act(act, x):
+    return {0: lambda v: v, 1: lambda v: clip_ref.act_fn("quick_gelu", v),
+            2: lambda v: clip_ref.act_fn("gelu", v), 3: lambda v: clip_ref.act_fn("gelu_tanh", v)}[act](x)
+
+
+def run_gemm(dtype, mode, act, A, W, bias=None, resid=None):
+    L = _lib()
+    M, K = A.shape
+    N = W.shape[0]
+    out = np.empty((M, N), np.float32)
+    A = np.ascontiguousarray(A, np.float32)
+    W = np.ascontiguousarray(W, np.float32)
+    b = None if bias is None else np.ascontiguousarray(bias, np.float32)
+    r = None if resid is None else np.ascontiguousarray(resid, np.float32)
+    L.check(L.lib().clipgpu_test_gemm(dtype, mode, act, M, N, K, A.ctypes.data, W.ctypes.data,
+                                      None if b is None else b.ctypes.data,
+                                      None if r is None else r.ctypes.data, out.ctypes.data))
+    return out
+
+
+@pytest.mark.parametrize("dtype", [BF16, F16])
+@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (200, 136, 192), (1000, 768, 768), (77, 64, 512),
+                                   (12800, 768, 3072)])
+def test_gemm_f32_out(dtype, M, N, K):
+    rng = np.random.default_rng(M * 7 + N + K)
+    A = round16(rng.standard_normal((M, K)), dtype)
+    W = round16(rng.standard_normal((N, K)) / np.sqrt(K), dtype)
+    bias = rng.standard_normal(N).astype(np.float32)
+    out = run_gemm(dtype, 2, 0, A, W, bias)
+    ref = A.astype(np.float64) @ W.T.astype(np.float64) + bias
+    # f32 accumulation of exact 16-bit products: |err| <~ 1e-6 * sum|a*b|
+    bound = 3e-5 * (np.abs(A) @ np.abs(W).T) + 1e-6
+    assert np.all(np.abs(out - ref) <= bound)
+
+
+@pytest.mark.parametrize("dtype", [BF16, F16])
+@pytest.mark.parametrize("act", [0, 1, 2, 3])
+def test_gemm_store16_act(dtype, act):
+    M, N, K = 300, 384, 256
+    rng = np.random.default_rng(act)
+    A = round16(rng.standard_normal((M, K)), dtype)
+    W = round16(rng.standard_normal((N, K)) / np.sqrt(K), dtype)
+    bias = rng.standard_normal(N).astype(np.float32)
+    out = run_gemm(dtype, 0, act, A, W, bias)
+    ref = ref_act(act, A.astype(np.float64) @ W.T.astype(np.float64) + bias)
+    rel = 2 ** -8 if dtype == BF16 else 2 ** -11  # one 16-bit output rounding (+ slack)
+    assert np.all(np.abs(out - ref) <= 1.01 * rel * np.abs(ref) + 1e-4)
+
+
+@pytest.mark.parametrize("dtype", [BF16])
+def test_gemm_residual(dtype):
+    M, N, K = 513, 256, 128
+    rng = np.random.default_rng(5)
+    A = round16(rng.standard_normal((M, K)), dtype)
+    W = round16(rng.standard_normal((N, K)) / np.sqrt(K), dtype)
+    bias = rng.standard_normal(N).astype(np.float32)
+    resid = rng.standard_normal((M, N)).astype(np.float32)
+    out = run_gemm(dtype, 1, 0, A, W, bias, resid)
+    ref = resid + A.astype(np.float64) @ W.T.astype(np.float64) + bias
+    assert np.abs(out - ref).max() < 1e-4
+
+
+def ref_attention(qkv, B, N, H, causal):
+    D = H * 64
+    x = qkv.reshape(B, N, 3, H, 64).astype(np.float64)
+    q, k, v = x[:, :, 0].transpose(0, 2, 1, 3), x[:, :, 1].transpose(0, 2, 1, 3), x[:, :, 2].transpose(0, 2, 1, 3)
+    s = q @ k.transpose(0, 1, 3, 2) / 8.0
+    if causal:
+        s = np.where(np.triu(np.ones((N, N), bool), 1), -np.inf, s)
+    o = clip_ref.softmax(s) @ v
+    return o.transpose(0, 2, 1, 3).reshape(B * N, D)
+
+
+@pytest.mark.parametrize("dtype", [BF16, F16])
+@pytest.mark.parametrize("B,N,H,causal", [(3, 50, 12, 0), (4, 77, 8, 1), (2, 17, 2, 0), (2, 100, 2, 1),
+                                          (1, 256, 2, 0), (2, 1, 2, 1)])
+def test_attention(dtype, B, N, H, causal):
+    L = _lib()
+    rng = np.random.default_rng(N + H)
+    qkv = round16(rng.standard_normal((B * N, 3 * H * 64)) * 1.5, dtype)
+    out = np.empty((B * N, H * 64), np.float32)
+    L.check(L.lib().clipgpu_test_attention(dtype, B, N, H, causal, qkv.ctypes.data, out.ctypes.data))
+    ref = ref_attention(qkv, B, N, H, causal)
+    # P and O are rounded to 16 bits: |err| <= ~2 ulp16 of max|v|
+    tol = (2 ** -7 if dtype == BF16 else 2 ** -10) * np.abs(qkv).max()
+    assert np.abs(out - ref).max() < tol
+
+
+@pytest.mark.parametrize("dtype", [BF16, F16])
+@pytest.mark.parametrize("D", [128, 512, 768, 1280])
+def test_layernorm(dtype, D):
+    L = _lib()
+    rng = np.random.default_rng(D)
+    rows = 333
+    x = (rng.standard_normal((rows, D)) * 3 + 1).astype(np.float32)
+    w = (1 + 0.1 * rng.standard_normal(D)).astype(np.float32)
+    b = (0.1 * rng.standard_normal(D)).astype(np.float32)
+    out = np.empty((rows, D), np.float32)
+    L.check(L.lib().clipgpu_test_layernorm(dtype, rows, D, 1e-5, x.ctypes.data, w.ctypes.data, b.ctypes.data,
+                                           out.ctypes.data))
+    ref = clip_ref.layer_norm(x.astype(np.float64), w, b, 1e-5)
+    rel = 2 ** -8 if dtype == BF16 else 2 ** -11
+    assert np.all(np.abs(out - ref) <= 1.01 * rel * np.abs(ref) + 1e-5)
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("S,P,D", [(224, 32, 768), (64, 16, 128)])
+def test_patch_embed(mode, S, P, D):
+    L = _lib()
+    from oracle.model_spec import OPENAI_MEAN, OPENAI_STD
+    from tests.helpers import normalized_pixels
+    rng = np.random.default_rng(S + mode)
+    B, G = 3, S // P
+    u8 = rng.integers(0, 256, (B, S, S, 3), dtype=np.uint8)
+    px = normalized_pixels(u8, OPENAI_MEAN, OPENAI_STD)
+    W = round16(rng.standard_normal((D, 3 * P * P)) / np.sqrt(3 * P * P), BF16)
+    pos = rng.standard_normal((G * G + 1, D)).astype(np.float32)
+    out = np.empty((B * (G * G + 1), D), np.float32)
+    src = px if mode == 0 else u8
+    L.check(L.lib().clipgpu_test_patch_embed(BF16, mode, B, S, P, D, src.ctypes.data, L.f3(OPENAI_MEAN),
+                                             L.f3(OPENAI_STD), W.ctypes.data, pos.ctypes.data, out.ctypes.data))
+    pxr = round16(px, BF16).astype(np.float64)
+    patches = pxr.reshape(B, 3, G, P, G, P).transpose(0, 2, 4, 1, 3, 5).reshape(B, G * G, 3 * P * P)
+    ref = patches @ W.T.astype(np.float64) + pos[1:]
+    got = out.reshape(B, G * G + 1, D)
+    assert np.all(got[:, 0] == 0)  # CLS rows untouched
+    bound = 3e-5 * (np.abs(patches) @ np.abs(W).T) + 1e-5
+    assert np.all(np.abs(got[:, 1:] - ref) <= bound)

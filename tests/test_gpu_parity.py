@@ -1,0 +1,152 @@
+"""End-to-end parity of the HIP engine vs the CPU oracle (fp64 restatement of the
+reference's ONNX graphs, pinned against HF transformers — tests/test_oracle_pin.py).
+
+Tolerance (north_star): cosine(GPU, oracle) >= 0.9999 per embedding row, and the
+GPU rows are unit-norm to 1e-5.  Weights are the seeded synthetic set (identical
+bits on both sides, tests/test_cpu_host.py::test_synth_matches_oracle).
+"""
+import numpy as np
+import pytest
+
+from oracle import clip_ref, weights
+from oracle.model_spec import OPENAI_MEAN, OPENAI_STD, TINY_CFG, VIT_B_32_CFG
+from tests.helpers import COS_TOL, make_model_dir, normalized_pixels, specs
+
+pytestmark = pytest.mark.gpu
+
+_CACHE = {}
+
+
+def oracle_vision(cfg, seed, px):
+    v, _ = specs(cfg)
+    key = ("v", id(cfg), seed)
+    if key not in _CACHE:
+        _CACHE[key] = weights.vision_weights(v, seed)
+    return clip_ref.encode_image(_CACHE[key], v, px)
+
+
+def oracle_text(cfg, seed, ids):
+    _, t = specs(cfg)
+    key = ("t", id(cfg), seed)
+    if key not in _CACHE:
+        _CACHE[key] = weights.text_weights(t, seed)
+    return clip_ref.encode_text(_CACHE[key], t, ids)
+
+
+def engine(cfg, tower, seed=1234, dtype="bf16", max_batch=64):
+    from open_clip_inference.engine import Engine
+    return Engine(make_model_dir(cfg, seed), tower, [0], dtype, max_batch)
+
+
+def check_rows(got, ref):
+    cos = clip_ref.cosine_rows(got, ref)
+    assert got.shape == ref.shape
+    assert np.all(np.abs(np.linalg.norm(got, axis=1) - 1) < 1e-5)
+    assert cos.min() >= COS_TOL, cos.min()
+    return cos
+
+
+@pytest.mark.parametrize("cfg,B", [(TINY_CFG, 3), (VIT_B_32_CFG, 4), (VIT_B_32_CFG, 5)])
+@pytest.mark.parametrize("dtype", ["bf16", "f16"])
+def test_vision_parity(cfg, B, dtype):
+    v, _ = specs(cfg)
+    u8 = weights.synth_images_u8(11 + B, B, v.image_size)
+    px = normalized_pixels(u8, OPENAI_MEAN, OPENAI_STD)
+    e = engine(cfg, 0, dtype=dtype)
+    got = e.embed_pixels(px)
+    check_rows(got, oracle_vision(cfg, 1234, px))
+
+
+@pytest.mark.parametrize("cfg,B,random_eot", [(TINY_CFG, 5, True), (VIT_B_32_CFG, 6, False),
+                                              (VIT_B_32_CFG, 7, True)])
+@pytest.mark.parametrize("dtype", ["bf16", "f16"])
+def test_text_parity(cfg, B, random_eot, dtype):
+    _, t = specs(cfg)
+    ids = weights.synth_token_ids(3 + B, B, t.context_length, t.vocab_size, t.vocab_size - 2,
+                                  t.vocab_size - 1, random_eot=random_eot)
+    e = engine(cfg, 1, dtype=dtype)
+    got = e.embed_tokens(ids)
+    check_rows(got, oracle_text(cfg, 1234, ids))
+
+
+def test_vision_u8_path_matches_f32_path():
+    v, _ = specs(VIT_B_32_CFG)
+    u8 = weights.synth_images_u8(21, 3, v.image_size)
+    e = engine(VIT_B_32_CFG, 0)
+    a = e.embed_u8(u8, OPENAI_MEAN, OPENAI_STD)
+    b = e.embed_pixels(normalized_pixels(u8, OPENAI_MEAN, OPENAI_STD))
+    # device-side normalize_pixels is bit-identical to the host one
+    assert np.array_equal(a, b)
+
+
+def test_vision_chunking_and_order():
+    """B > max_batch is processed in chunks; rows stay in input order."""
+    v, _ = specs(TINY_CFG)
+    u8 = weights.synth_images_u8(5, 11, v.image_size)
+    px = normalized_pixels(u8, OPENAI_MEAN, OPENAI_STD)
+    e = engine(TINY_CFG, 0, max_batch=4)
+    got = e.embed_pixels(px)
+    check_rows(got, oracle_vision(TINY_CFG, 1234, px))
+    single = np.concatenate([e.embed_pixels(px[i:i + 1]) for i in range(0, 11, 5)])
+    assert np.allclose(single, got[0:11:5], atol=1e-6)
+
+
+def test_text_pads_after_eot_do_not_matter():
+    """Causal mask + argmax pooling: tokens after EOT cannot change the output (a18)."""
+    _, t = specs(TINY_CFG)
+    ids = weights.synth_token_ids(9, 4, t.context_length, t.vocab_size, t.vocab_size - 2, t.vocab_size - 1,
+                                  random_eot=True)
+    ids2 = ids.copy()
+    for b in range(4):
+        p = int(np.argmax(ids[b]))
+        ids2[b, p + 1:] = (ids2[b, p + 1:] + 17) % (t.vocab_size - 2)
+    e = engine(TINY_CFG, 1)
+    assert np.array_equal(e.embed_tokens(ids), e.embed_tokens(ids2))
+
+
+def test_errors():
+    from open_clip_inference.error import InferenceError, ShapeError
+    e = engine(TINY_CFG, 0)
+    with pytest.raises(InferenceError, match="Empty batch"):
+        e.embed_pixels(np.zeros((0, 3, 64, 64), np.float32))
+    with pytest.raises(ShapeError):
+        e.embed_pixels(np.zeros((1, 3, 32, 32), np.float32))
+    t = engine(TINY_CFG, 1)
+    with pytest.raises(InferenceError, match="out of range"):
+        t.embed_tokens(np.full((1, 16), 5000, np.int64))
+
+
+def test_device_entry_points():
+    import torch  # device buffers only
+    v, t = specs(TINY_CFG)
+    u8 = weights.synth_images_u8(2, 3, v.image_size)
+    px = normalized_pixels(u8, OPENAI_MEAN, OPENAI_STD)
+    e = engine(TINY_CFG, 0)
+    d_in = torch.from_numpy(px).cuda()
+    d_out = torch.empty((3, v.embed_dim), device="cuda")
+    s = torch.cuda.current_stream()
+    e.embed_pixels_device(d_in.data_ptr(), 3, d_out.data_ptr(), s.cuda_stream)
+    torch.cuda.synchronize()
+    assert np.allclose(d_out.cpu().numpy(), e.embed_pixels(px), atol=1e-6)
+    d_u8 = torch.from_numpy(u8).cuda()
+    e.embed_u8_device(d_u8.data_ptr(), 3, OPENAI_MEAN, OPENAI_STD, d_out.data_ptr(), s.cuda_stream)
+    torch.cuda.synchronize()
+    assert np.allclose(d_out.cpu().numpy(), e.embed_pixels(px), atol=1e-6)
+    ids = weights.synth_token_ids(1, 2, t.context_length, t.vocab_size, t.vocab_size - 2, t.vocab_size - 1)
+    te = engine(TINY_CFG, 1)
+    d_ids = torch.from_numpy(ids).cuda()
+    d_o = torch.empty((2, t.embed_dim), device="cuda")
+    te.embed_tokens_device(d_ids.data_ptr(), 2, d_o.data_ptr(), s.cuda_stream)
+    torch.cuda.synchronize()
+    assert np.allclose(d_o.cpu().numpy(), te.embed_tokens(ids), atol=1e-6)
+
+
+def test_native_library_is_loaded():
+    """The HIP library, not a fallback, is what ran (one libamdhip64 in-process)."""
+    import re
+    from open_clip_inference import _lib
+    _lib.lib()
+    maps = open("/proc/self/maps").read()
+    assert "libclipgpu.so" in maps
+    hip = set(re.findall(r"\S*libamdhip64\S*", maps))
+    assert len(hip) == 1, hip
