@@ -32,6 +32,7 @@ sys.path.insert(0, os.path.join(ROOT, "clip-embedder-rs_amd"))
 
 from open_clip_inference import _lib  # noqa: E402
 from open_clip_inference.engine import Engine, profile_enable, profile_read  # noqa: E402
+from open_clip_inference.parallel import all_gather_rows  # noqa: E402
 
 # ViT-B/32 (open_clip timm/vit_base_patch32_clip_224.openai)
 CFG = {
@@ -144,13 +145,12 @@ def main():
     ve = Engine(mdir, _lib.TOWER_VISION, [local], args.dtype, B_VISION)
     px, ids = synth_inputs(rank, dev)
     out = torch.empty((B_VISION, 512), device=dev, dtype=torch.float32)
-    gathered = torch.empty((world * B_VISION, 512), device=dev, dtype=torch.float32)
     stream = torch.cuda.current_stream(dev)
 
     def vision_step():
         ve.embed_pixels_device(px.data_ptr(), B_VISION, out.data_ptr(), stream.cuda_stream)
-        if world > 1:
-            dist.all_gather_into_tensor(gathered, out)
+        if world > 1:  # one RCCL all-gather of the [256, 512] embedding rows, rank order
+            all_gather_rows(out, world * B_VISION)
 
     def timed(step, steps, warmup, prof_engine=None, prof_cat=None):
         for _ in range(warmup):
@@ -192,12 +192,11 @@ def main():
     if not args.no_text:
         te = Engine(mdir, _lib.TOWER_TEXT, [local], args.dtype, B_TEXT)
         tout = torch.empty((B_TEXT, 512), device=dev, dtype=torch.float32)
-        tgathered = torch.empty((world * B_TEXT, 512), device=dev, dtype=torch.float32)
 
         def text_step():
             te.embed_tokens_device(ids.data_ptr(), B_TEXT, tout.data_ptr(), stream.cuda_stream)
             if world > 1:
-                dist.all_gather_into_tensor(tgathered, tout)
+                all_gather_rows(tout, world * B_TEXT)
 
         tsteps = max(3, args.steps // 2)
         tdt, _ = timed(text_step, tsteps, max(1, args.warmup // 2))

@@ -180,6 +180,11 @@ void resize_rgb8(const uint8_t* rgb, int W, int H, int S, const std::string& int
     y0 = ((double)H - chh) / 2.0;
     x1 = x0 + cw;
     y1 = y0 + chh;
+    // f64 round-off can place the box ~1e-14 outside the image (e.g. 517x389 -> 224): clamp.
+    x0 = std::max(0.0, x0);
+    y0 = std::max(0.0, y0);
+    x1 = std::min((double)W, x1);
+    y1 = std::min((double)H, y1);
   }
   if (interp == "bicubic") resize_conv(rgb, W, H, x0, y0, x1, y1, S, bicubic_filter, 2.0, out);
   else if (interp == "bilinear") resize_conv(rgb, W, H, x0, y0, x1, y1, S, bilinear_filter, 1.0, out);

@@ -141,9 +141,11 @@ class Tokenizer:
         n = len(texts)
         enc = [t.encode("utf-8") for t in texts]
         arr = (c_char_p * max(n, 1))(*enc)
+        lens = np.array([len(e) for e in enc] or [0], np.int64)
         ids = np.empty((n, self.context_length), np.int64)
         mask = np.empty((n, self.context_length), np.int64)
-        check(lib().clipgpu_tokenize(self._h, arr, n, 1 if lowercase else 0, ids.ctypes.data, mask.ctypes.data))
+        check(lib().clipgpu_tokenize(self._h, arr, lens.ctypes.data, n, 1 if lowercase else 0, ids.ctypes.data,
+                                     mask.ctypes.data))
         return ids, mask
 
 

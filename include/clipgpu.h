@@ -117,10 +117,11 @@ int clipgpu_preprocess_batch(const uint8_t* const* images, const int* widths, co
 int clipgpu_tokenizer_create(const char* tokenizer_json, int context_length, int64_t pad_id,
                              clipgpu_tokenizer** out);
 void clipgpu_tokenizer_destroy(clipgpu_tokenizer* t);
-/* texts: n NUL-terminated UTF-8 strings.  lowercase != 0 applies str::to_lowercase first
+/* texts: n UTF-8 strings; lengths[i] = byte length of texts[i] (like a Rust &str, may contain NUL),
+ * or lengths == NULL for NUL-terminated strings.  lowercase != 0 applies str::to_lowercase first
  * (tokenizer_needs_lowercase, src/text.rs:115-117).  ids, mask: [n][context_length]. */
-int clipgpu_tokenize(clipgpu_tokenizer* t, const char* const* texts, int64_t n, int lowercase, int64_t* ids,
-                     int64_t* mask);
+int clipgpu_tokenize(clipgpu_tokenizer* t, const char* const* texts, const int64_t* lengths, int64_t n,
+                     int lowercase, int64_t* ids, int64_t* mask);
 /* Token id of a vocab string, or -1. */
 int64_t clipgpu_tokenizer_token_id(const clipgpu_tokenizer* t, const char* token);
 int64_t clipgpu_tokenizer_vocab_size(const clipgpu_tokenizer* t);

@@ -1,0 +1,117 @@
+"""C ABI checks without a GPU: the library loads, exports every function declared in
+include/*.h, the synthetic weight generator is bit-exact with the oracle, and the
+model-dir / argument error paths map onto ClipError variants (src/error.rs:9-41)."""
+import ctypes
+import glob
+import json
+import os
+import re
+
+import numpy as np
+import pytest
+
+from oracle import weights
+from oracle.model_spec import TINY_CFG, VIT_B_32_CFG, text_spec_from_cfg, vision_spec_from_cfg
+from tests.helpers import make_model_dir
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_functions():
+    names = set()
+    for h in glob.glob(os.path.join(ROOT, "include", "*.h")):
+        src = open(h).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        for m in re.finditer(r"\b(clipgpu_[a-z0-9_]+)\s*\(", src):
+            names.add(m.group(1))
+    return names
+
+
+def test_library_exports_every_declared_symbol():
+    from open_clip_inference import _lib
+    L = _lib.lib()
+    names = declared_functions()
+    assert len(names) >= 25
+    missing = [n for n in names if not hasattr(L, n)]
+    assert not missing, missing
+    assert set(_lib.SYMBOLS) == names  # the ctypes binding covers exactly the headers
+    assert L.clipgpu_abi_version() == 1
+
+
+def test_no_oracle_in_product():
+    """The product package never imports the oracle (test infrastructure only)."""
+    pkg = os.path.join(ROOT, "clip-embedder-rs_amd")
+    for f in glob.glob(os.path.join(pkg, "**", "*.*"), recursive=True):
+        if f.endswith((".py", ".cpp", ".hip", ".hpp", ".h")):
+            assert "oracle" not in open(f, errors="ignore").read().replace("oracle/", ""), f
+
+
+@pytest.mark.parametrize("cfg", [TINY_CFG, VIT_B_32_CFG])
+def test_synth_matches_oracle(cfg):
+    from open_clip_inference import _lib
+    L = _lib.lib()
+    v, t = vision_spec_from_cfg(cfg["model_cfg"]), text_spec_from_cfg(cfg["model_cfg"])
+    params = weights.vision_param_list(v) + weights.text_param_list(t)
+    for name, shape, std, off in params[:40] + params[-10:]:
+        ref = weights.synth_tensor(1234, name, shape, std, off).ravel()
+        out = np.empty(ref.size, np.float32)
+        _lib.check(L.clipgpu_synth_tensor(1234, name.encode(), std, off, out.ctypes.data, out.size))
+        assert np.array_equal(ref.view(np.uint32), out.view(np.uint32)), name
+
+
+def test_create_errors_without_gpu(tmp_path):
+    from open_clip_inference.engine import Engine
+    from open_clip_inference.error import ConfigError, MissingModelFile, ModelFolderNotFound
+    with pytest.raises(ModelFolderNotFound):
+        Engine(str(tmp_path / "nope"), 0)
+    with pytest.raises(MissingModelFile, match="open_clip_config.json"):
+        Engine(str(tmp_path), 0)
+    d = make_model_dir(TINY_CFG)
+    os.remove(os.path.join(d, "clipgpu_synthetic.json"))
+    with pytest.raises(MissingModelFile, match="safetensors"):
+        Engine(d, 0)
+    bad = json.loads(json.dumps(TINY_CFG))
+    bad["model_cfg"]["vision_cfg"]["timm_model_name"] = "vit_so400m"
+    with pytest.raises(ConfigError, match="not supported"):
+        Engine(make_model_dir(bad), 0)
+    bad = json.loads(json.dumps(TINY_CFG))
+    del bad["preprocess_cfg"]
+    with pytest.raises(ConfigError, match="preprocess_cfg"):
+        Engine(make_model_dir(bad), 0)
+
+
+def test_verify_model_dir_mirror(tmp_path):
+    from open_clip_inference.error import MissingModelFile, ModelFolderNotFound
+    from open_clip_inference.model_manager import MODEL_FILES, get_default_base_folder, verify_model_dir
+    assert len(MODEL_FILES) == 9
+    assert get_default_base_folder().endswith(os.path.join(".cache", "open_clip_rs"))
+    with pytest.raises(ModelFolderNotFound):
+        verify_model_dir(str(tmp_path / "x"))
+    d = make_model_dir(TINY_CFG)
+    verify_model_dir(d)
+    with pytest.raises(MissingModelFile, match="tokenizer.json"):
+        verify_model_dir(d, need_tokenizer=True)
+
+
+def test_config_mirror_parses():
+    from open_clip_inference.config import ModelConfig, OpenClipConfig
+    d = make_model_dir(VIT_B_32_CFG)
+    oc = OpenClipConfig.from_file(os.path.join(d, "open_clip_config.json"))
+    assert oc.model_cfg.embed_dim == 512 and oc.model_cfg.vision_cfg.image_size == 224
+    assert oc.model_cfg.text_cfg.context_length == 77
+    assert oc.preprocess_cfg.interpolation == "bicubic" and oc.preprocess_cfg.resize_mode == "shortest"
+    mc = ModelConfig.from_file(os.path.join(d, "model_config.json"))
+    assert mc.logit_scale == 100.0 and mc.pad_id == 0 and mc.activation_function == "softmax"
+
+
+def test_safetensors_header_roundtrip(tmp_path):
+    """open_clip_model.safetensors is accepted as the weight source (loader runs before
+    any device call fails): a wrong-shape file is rejected with a Shape error."""
+    from safetensors.numpy import save_file
+    from open_clip_inference.engine import Engine
+    from open_clip_inference.error import ConfigError
+    d = make_model_dir(TINY_CFG)
+    os.remove(os.path.join(d, "clipgpu_synthetic.json"))
+    save_file({"visual.conv1.weight": np.zeros((3, 3), np.float32)}, os.path.join(d, "open_clip_model.safetensors"))
+    with pytest.raises(ConfigError, match="unexpected shape"):
+        Engine(d, 0)

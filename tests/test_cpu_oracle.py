@@ -1,0 +1,64 @@
+"""Pin the oracle (oracle/clip_ref.py, fp64 restatement of the exported graphs) against
+(a) the committed golden embeddings (regression) and (b) HF transformers CLIP towers
+loaded with the same weights — an independent implementation of the same architecture
+(the reference's own ONNX/open_clip path cannot run offline)."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import clip_ref, weights
+from oracle.model_spec import OPENAI_MEAN, OPENAI_STD, TINY_CFG, VIT_B_32_CFG, text_spec_from_cfg, \
+    vision_spec_from_cfg
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden", "embed_golden.npz")
+
+
+def pixels(v, B):
+    u8 = weights.synth_images_u8(100, B, v.image_size)
+    return ((u8.astype(np.float32) / np.float32(255) - np.asarray(OPENAI_MEAN, np.float32))
+            / np.asarray(OPENAI_STD, np.float32)).transpose(0, 3, 1, 2)
+
+
+@pytest.mark.parametrize("name,cfg,B", [("tiny", TINY_CFG, 3), ("b32", VIT_B_32_CFG, 2)])
+def test_oracle_matches_golden_and_hf(name, cfg, B):
+    g = np.load(GOLD)
+    v, t = vision_spec_from_cfg(cfg["model_cfg"]), text_spec_from_cfg(cfg["model_cfg"])
+    ov = clip_ref.encode_image(weights.vision_weights(v, 1234), v, pixels(v, B))
+    assert np.allclose(ov, g[f"{name}_vision_oracle"], atol=1e-12)
+    assert clip_ref.cosine_rows(g[f"{name}_vision_oracle"], g[f"{name}_vision_hf"]).min() > 1 - 1e-9
+    ids = g[f"{name}_text_ids"]
+    ot = clip_ref.encode_text(weights.text_weights(t, 1234), t, ids)
+    assert np.allclose(ot, g[f"{name}_text_oracle"], atol=1e-12)
+    assert clip_ref.cosine_rows(g[f"{name}_text_oracle"], g[f"{name}_text_hf"]).min() > 1 - 1e-9
+
+
+def test_oracle_vs_hf_live_tiny():
+    pytest.importorskip("transformers")
+    from oracle import hf_pin
+    v, t = vision_spec_from_cfg(TINY_CFG["model_cfg"]), text_spec_from_cfg(TINY_CFG["model_cfg"])
+    P = weights.vision_weights(v, 99)
+    px = pixels(v, 2)
+    assert np.abs(clip_ref.encode_image(P, v, px) - hf_pin.hf_encode_image(hf_pin.hf_vision(P, v), px)).max() < 1e-7
+    PT = weights.text_weights(t, 99)
+    ids = weights.synth_token_ids(5, 3, t.context_length, t.vocab_size, t.vocab_size - 2, t.vocab_size - 1,
+                                  random_eot=True)
+    assert np.abs(clip_ref.encode_text(PT, t, ids) - hf_pin.hf_encode_text(hf_pin.hf_text(PT, t), ids)).max() < 1e-7
+
+
+def test_oracle_properties():
+    v, t = vision_spec_from_cfg(TINY_CFG["model_cfg"]), text_spec_from_cfg(TINY_CFG["model_cfg"])
+    P = weights.vision_weights(v, 3)
+    px = pixels(v, 3)
+    e = clip_ref.encode_image(P, v, px)
+    assert np.allclose(np.linalg.norm(e, axis=1), 1)
+    # batch independence: rows do not interact
+    assert np.allclose(clip_ref.encode_image(P, v, px[1:2]), e[1:2], atol=1e-12)
+    # text: tokens after the first EOT do not change the output
+    PT = weights.text_weights(t, 3)
+    ids = weights.synth_token_ids(8, 2, t.context_length, t.vocab_size, t.vocab_size - 2, t.vocab_size - 1,
+                                  random_eot=True)
+    ids2 = ids.copy()
+    p = int(np.argmax(ids2[0]))
+    ids2[0, p + 1:] = 7
+    assert np.allclose(clip_ref.encode_text(PT, t, ids)[0], clip_ref.encode_text(PT, t, ids2)[0], atol=1e-12)

@@ -1,0 +1,133 @@
+"""End-to-end through the drop-in API (open_clip_inference.{VisionEmbedder, TextEmbedder,
+Clip}, mirror of src/vision.rs / src/text.rs / src/clip.rs) on the GPU: host
+preprocessing + tokenizer (C++) + HIP towers, vs the oracle chain
+(preprocess_ref -> clip_ref, tokenizer_ref -> clip_ref) at cosine >= 0.9999."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import clip_ref, facade_ref, preprocess_ref, weights
+from oracle.model_spec import OPENAI_MEAN, OPENAI_MODEL_CONFIG, OPENAI_STD, TINY_CFG, text_spec_from_cfg, \
+    vision_spec_from_cfg
+from oracle.tokenizer_ref import ClipTokenizerRef
+from tests.helpers import COS_TOL, make_model_dir
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+TOKJ = os.path.join(GOLD, "clip_synth_tokenizer.json")
+
+
+def cfg_with_tokenizer(ctx=16):
+    with open(TOKJ, encoding="utf-8") as f:
+        tj = f.read()
+    vocab = len(json.loads(tj)["model"]["vocab"])
+    cfg = json.loads(json.dumps(TINY_CFG))
+    cfg["model_cfg"]["text_cfg"]["vocab_size"] = vocab
+    cfg["model_cfg"]["text_cfg"]["context_length"] = ctx
+    mc = dict(OPENAI_MODEL_CONFIG, vocab_size=vocab)
+    return cfg, tj, mc
+
+
+@pytest.fixture(scope="module")
+def model():
+    cfg, tj, mc = cfg_with_tokenizer()
+    d = make_model_dir(cfg, seed=77, tokenizer_json=tj, model_config=mc)
+    return cfg, d
+
+
+def images():
+    g = np.load(os.path.join(GOLD, "preprocess_golden.npz"))
+    ims = [g["cat_face_crop"], g["cat_face_224"]]
+    ims += [weights.synth_images_u8(h * 1000 + w, 1, max(h, w))[0][:h, :w].copy()
+            for h, w in ((389, 517), (97, 301))]
+    return ims
+
+
+def oracle_images(cfg, ims):
+    v = vision_spec_from_cfg(cfg["model_cfg"])
+    px = np.stack([preprocess_ref.preprocess(im, v.image_size, OPENAI_MEAN, OPENAI_STD) for im in ims])
+    return clip_ref.encode_image(weights.vision_weights(v, 77), v, px)
+
+
+def oracle_texts(cfg, texts):
+    t = text_spec_from_cfg(cfg["model_cfg"])
+    tok = ClipTokenizerRef(TOKJ, t.context_length, 0)
+    ids = np.array([tok.encode(x)[0] for x in texts], np.int64)
+    return clip_ref.encode_text(weights.text_weights(t, 77), t, ids)
+
+
+TEXTS = ["A photo of a cat", "A photo of a dog", "A photo of a beignet", "Café naïve résumé", "",
+         " ".join(["word"] * 40)]
+
+
+def test_vision_embedder_end_to_end(model):
+    from open_clip_inference import VisionEmbedder
+    cfg, d = model
+    ve = VisionEmbedder.from_local_dir(d).build()
+    ims = images()
+    got = ve.embed_images(ims)
+    assert clip_ref.cosine_rows(got, oracle_images(cfg, ims)).min() >= COS_TOL
+    one = ve.embed_image(ims[0])
+    assert one.shape == (64,) and np.allclose(one, got[0], atol=1e-6)
+    pre = ve.preprocess(ims[2])
+    assert pre.shape == (1, 3, 64, 64)
+
+
+def test_text_embedder_end_to_end(model):
+    from open_clip_inference import TextEmbedder
+    cfg, d = model
+    te = TextEmbedder.from_local_dir(d).build()
+    got = te.embed_texts(TEXTS)
+    assert clip_ref.cosine_rows(got, oracle_texts(cfg, TEXTS)).min() >= COS_TOL
+    ids, mask = te.tokenize(TEXTS)
+    assert ids.shape == (len(TEXTS), 16) and mask.dtype == np.int64
+    assert np.allclose(te.embed_text(TEXTS[1]), got[1], atol=1e-6)
+
+
+def test_clip_facade_and_integration_shape(model):
+    """tests/integration_test.rs:9-36 structure (classify cat_face against three labels); with
+    synthetic weights the semantic assertion (p > 0.99) is replaced by agreement with the
+    oracle facade on oracle embeddings."""
+    from open_clip_inference import Clip
+    cfg, d = model
+    clip = Clip.from_local_dir(d).build()
+    cat = images()[0]
+    labels = TEXTS[:3]
+    res = clip.classify(cat, labels)
+    assert sorted(l for l, _ in res) == sorted(labels)
+    assert abs(sum(p for _, p in res) - 1) < 1e-5
+    assert all(res[i][1] >= res[i + 1][1] for i in range(len(res) - 1))
+    ref = facade_ref.classify(oracle_images(cfg, [cat])[0], oracle_texts(cfg, labels), labels, 100.0, 0.0)
+    # logit_scale 100 amplifies the <= 1e-4 cosine gap of each embedding: compare at 0.05
+    assert np.allclose(sorted(p for _, p in res), sorted(p for _, p in ref), atol=0.05)
+    ranks = clip.rank_images(images(), labels[0])
+    assert sorted(i for i, _ in ranks) == [0, 1, 2, 3]
+    assert isinstance(clip.compare(cat, labels[0]), float)
+    assert clip.get_model_config().logit_scale == 100.0
+
+
+def test_duplicate_and_multi_replica_handle(model):
+    """duplicate() gives an independent handle; a handle with devices [0, 0] exercises the
+    multi-device row-sharding path (two replicas, two host workers) on one GPU."""
+    from open_clip_inference import VisionEmbedder
+    cfg, d = model
+    ve = VisionEmbedder.from_local_dir(d).build()
+    ims = images()
+    a = ve.embed_images(ims)
+    b = ve.duplicate().embed_images(ims)
+    assert np.array_equal(a, b)
+    multi = VisionEmbedder.from_local_dir(d).with_devices([0, 0]).with_max_batch(1).build()
+    assert np.array_equal(multi.embed_images(ims), a)
+
+
+def test_empty_batch_errors(model):
+    from open_clip_inference import TextEmbedder, VisionEmbedder
+    from open_clip_inference.error import InferenceError
+    cfg, d = model
+    with pytest.raises(InferenceError, match="Empty batch"):
+        VisionEmbedder.from_local_dir(d).build().embed_images([])
+    with pytest.raises(InferenceError, match="Empty batch"):
+        TextEmbedder.from_local_dir(d).build().embed_texts([])
