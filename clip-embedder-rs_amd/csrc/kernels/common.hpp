@@ -69,8 +69,8 @@ enum Act { ACT_NONE = 0, ACT_QUICK_GELU = 1, ACT_GELU = 2, ACT_GELU_TANH = 3 };
 
 template <int ACT>
 __device__ __forceinline__ float apply_act(float x) {
-  if constexpr (ACT == ACT_QUICK_GELU) {
-    return x / (1.0f + __expf(-1.702f * x));
+  if constexpr (ACT == ACT_QUICK_GELU) {  // v_exp + v_rcp (1 ulp) instead of an IEEE divide
+    return x * __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * x));
   } else if constexpr (ACT == ACT_GELU) {
     return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
   } else if constexpr (ACT == ACT_GELU_TANH) {

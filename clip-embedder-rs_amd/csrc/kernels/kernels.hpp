@@ -33,7 +33,17 @@ struct GemmParams {
   const void* img; int S, P, G;
   float mean[3], stdv[3];
   const float* pos;          // EPI_PATCH positional embedding [G^2+1][N]
+  int tile;                  // GemmTile (0 = pick by shape)
 };
+
+// Tile configurations of the MFMA GEMM.
+enum GemmTile {
+  TILE_AUTO = 0,
+  TILE_128x128 = 1,  // 4 waves, 64 KiB LDS, 2 blocks / CU (small M)
+  TILE_256x128 = 2,  // 8 waves, 96 KiB LDS
+  TILE_256x256 = 3,  // 8 waves, 128 KiB LDS
+};
+int pick_gemm_tile(int M, int N, int K);
 
 // act: Act enum from common.hpp (only used with EPI_STORE16)
 hipError_t launch_gemm(DType dt, int asrc, int epi, int act, const GemmParams& p, hipStream_t s);

@@ -2,6 +2,7 @@
 // device 0 over host f32 buffers so tests/ can check it against numpy.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <vector>
 
 #include "../../include/clipgpu.h"
@@ -33,6 +34,12 @@ struct DevBuf {
 DType dt_of(int dtype) {
   if (dtype != CLIPGPU_DTYPE_BF16 && dtype != CLIPGPU_DTYPE_F16) throw ClipErr(CLIPGPU_ERR_INVALID, "bad dtype");
   return dtype == CLIPGPU_DTYPE_BF16 ? DT_BF16 : DT_F16;
+}
+
+// CLIPGPU_TEST_TILE=1|2|3 forces a GEMM tile in clipgpu_test_gemm (tile-config coverage).
+int tile_override() {
+  const char* e = getenv("CLIPGPU_TEST_TILE");
+  return e ? atoi(e) : 0;
 }
 
 void up(void* d, const void* h, size_t n) { TCHECK(hipMemcpy(d, h, n, hipMemcpyHostToDevice)); }
@@ -75,6 +82,7 @@ int clipgpu_test_gemm(int dtype, int mode, int act, int64_t M, int64_t N, int64_
     up16(dt, dW.p, W, N * K);
     if (bias) up(dB.p, bias, N * 4);
     GemmParams g{};
+    g.tile = tile_override();
     g.A = dA.p; g.lda = K; g.W = dW.p; g.ldw = K; g.bias = bias ? dB.as<float>() : nullptr;
     g.out = dO.p; g.ldo = N; g.M = (int)M; g.N = (int)N; g.K = (int)K;
     int epi = EPI_STORE16;
@@ -131,6 +139,7 @@ int clipgpu_test_patch_embed(int dtype, int mode, int64_t B, int64_t S, int64_t 
     GemmParams g{};
     g.W = dw.p; g.ldw = K; g.out = dx.p; g.ldo = D; g.M = (int)(B * G * G); g.N = (int)D; g.K = (int)K;
     g.img = dpix.p; g.S = (int)S; g.P = (int)P; g.G = (int)G; g.pos = dpos.as<float>();
+    g.tile = tile_override();
     for (int c = 0; c < 3; ++c) {
       g.mean[c] = mean ? mean[c] : 0.f;
       g.stdv[c] = stdv ? stdv[c] : 1.f;
@@ -138,6 +147,49 @@ int clipgpu_test_patch_embed(int dtype, int mode, int64_t B, int64_t S, int64_t 
     TCHECK(launch_gemm(dt, mode == 0 ? A_IMG_F32 : A_IMG_U8, EPI_PATCH, 0, g, nullptr));
     TCHECK(hipDeviceSynchronize());
     down(x_out, dx.p, B * tokens * D * 4);
+  });
+}
+
+namespace {
+__global__ void fill_random(float* out, long n, uint32_t seed) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    uint32_t z = (uint32_t)i * 2654435761u ^ seed;
+    z ^= z >> 15; z *= 2246822519u; z ^= z >> 13; z *= 3266489917u; z ^= z >> 16;
+    out[i] = ((float)(z >> 8) * (1.0f / 16777216.0f)) * 2.0f - 1.0f;
+  }
+}
+}  // namespace
+
+int clipgpu_test_gemm_bench(int dtype, int epi, int act, int64_t M, int64_t N, int64_t K, int tile, int iters,
+                            double* us_per_launch) {
+  return guarded([&]() {
+    const DType dt = dt_of(dtype);
+    if (M <= 0 || N <= 0 || K <= 0 || K % 64 || iters <= 0 || !us_per_launch)
+      throw ClipErr(CLIPGPU_ERR_INVALID, "bad GEMM bench arguments");
+    DevBuf fA(M * K * 4), fW(N * K * 4), dA(M * K * 2), dW(N * K * 2), dB(N * 4), dO(M * N * 4);
+    hipLaunchKernelGGL(fill_random, dim3(2048), dim3(256), 0, nullptr, fA.as<float>(), (long)(M * K), 1u);
+    hipLaunchKernelGGL(fill_random, dim3(2048), dim3(256), 0, nullptr, fW.as<float>(), (long)(N * K), 2u);
+    hipLaunchKernelGGL(fill_random, dim3(64), dim3(256), 0, nullptr, dB.as<float>(), (long)N, 3u);
+    TCHECK(launch_cast_f32(dt, fA.as<float>(), dA.p, (long)(M * K), nullptr));
+    TCHECK(launch_cast_f32(dt, fW.as<float>(), dW.p, (long)(N * K), nullptr));
+    TCHECK(hipDeviceSynchronize());
+    GemmParams g{};
+    g.A = dA.p; g.lda = K; g.W = dW.p; g.ldw = K; g.bias = dB.as<float>();
+    g.out = dO.p; g.ldo = N; g.M = (int)M; g.N = (int)N; g.K = (int)K; g.tile = tile;
+    const int e = epi == 1 ? EPI_RESID : (epi == 2 ? EPI_STORE32 : EPI_STORE16);
+    for (int i = 0; i < 3; ++i) TCHECK(launch_gemm(dt, A_ROWS, e, epi == 0 ? act : 0, g, nullptr));
+    hipEvent_t a, b;
+    TCHECK(hipEventCreate(&a));
+    TCHECK(hipEventCreate(&b));
+    TCHECK(hipEventRecord(a, nullptr));
+    for (int i = 0; i < iters; ++i) TCHECK(launch_gemm(dt, A_ROWS, e, epi == 0 ? act : 0, g, nullptr));
+    TCHECK(hipEventRecord(b, nullptr));
+    TCHECK(hipEventSynchronize(b));
+    float ms = 0.f;
+    TCHECK(hipEventElapsedTime(&ms, a, b));
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    *us_per_launch = (double)ms * 1000.0 / iters;
   });
 }
 

@@ -34,6 +34,12 @@ int clipgpu_test_patch_embed(int dtype, int mode, int64_t B, int64_t S, int64_t 
                              const float mean[3], const float std[3], const float* conv_w, const float* pos,
                              float* x_out);
 
+/* Device-resident GEMM timing (random operands): `iters` back-to-back launches of the same
+ * GEMM as the engine issues it (epi: 0 store16 (+act), 1 residual f32, 2 store32), tile:
+ * 0 auto, 1 128x128, 2 256x128, 3 256x256.  Returns the mean µs per launch (HIP events). */
+int clipgpu_test_gemm_bench(int dtype, int epi, int act, int64_t M, int64_t N, int64_t K, int tile, int iters,
+                            double* us_per_launch);
+
 #ifdef __cplusplus
 }
 #endif

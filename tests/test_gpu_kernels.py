@@ -48,10 +48,17 @@ def run_gemm(dtype, mode, act, A, W, bias=None, resid=None):
     return out
 
 
+@pytest.fixture(params=[1, 2, 3], ids=["t128x128", "t256x128", "t256x256"])
+def tile(request, monkeypatch):
+    """Every GEMM tile configuration (GemmTile) through the same numerics checks."""
+    monkeypatch.setenv("CLIPGPU_TEST_TILE", str(request.param))
+    return request.param
+
+
 @pytest.mark.parametrize("dtype", [BF16, F16])
 @pytest.mark.parametrize("M,N,K", [(128, 128, 64), (200, 136, 192), (1000, 768, 768), (77, 64, 512),
-                                   (12800, 768, 3072)])
-def test_gemm_f32_out(dtype, M, N, K):
+                                   (12800, 768, 3072), (2600, 3072, 768)])
+def test_gemm_f32_out(dtype, M, N, K, tile):
     rng = np.random.default_rng(M * 7 + N + K)
     A = round16(rng.standard_normal((M, K)), dtype)
     W = round16(rng.standard_normal((N, K)) / np.sqrt(K), dtype)
@@ -65,7 +72,7 @@ def test_gemm_f32_out(dtype, M, N, K):
 
 @pytest.mark.parametrize("dtype", [BF16, F16])
 @pytest.mark.parametrize("act", [0, 1, 2, 3])
-def test_gemm_store16_act(dtype, act):
+def test_gemm_store16_act(dtype, act, tile):
     M, N, K = 300, 384, 256
     rng = np.random.default_rng(act)
     A = round16(rng.standard_normal((M, K)), dtype)
@@ -78,7 +85,7 @@ def test_gemm_store16_act(dtype, act):
 
 
 @pytest.mark.parametrize("dtype", [BF16])
-def test_gemm_residual(dtype):
+def test_gemm_residual(dtype, tile):
     M, N, K = 513, 256, 128
     rng = np.random.default_rng(5)
     A = round16(rng.standard_normal((M, K)), dtype)
@@ -135,7 +142,7 @@ def test_layernorm(dtype, D):
 
 @pytest.mark.parametrize("mode", [0, 1])
 @pytest.mark.parametrize("S,P,D", [(224, 32, 768), (64, 16, 128)])
-def test_patch_embed(mode, S, P, D):
+def test_patch_embed(mode, S, P, D, tile):
     L = _lib()
     from oracle.model_spec import OPENAI_MEAN, OPENAI_STD
     from tests.helpers import normalized_pixels

@@ -21,6 +21,8 @@ for s in $STEPS; do
     tests)
       run pytest_gpu 900 python -m pytest tests -m gpu -q -rf -p no:cacheprovider
       rc=$?; [ $rc -le 1 ] || exit $rc ;;
+    sweep)
+      run gemm_sweep 600 python tools/gemm_sweep.py || exit $? ;;
     smoke)
       run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
     bench)
