@@ -25,6 +25,8 @@
 // operands are swapped so each lane owns 4 consecutive output columns (8 / 16 B
 // epilogue stores).  M and N tails: clamped source rows + masked stores; K must
 // be a multiple of 64.
+#include <utility>
+
 #include "common.hpp"
 #include "kernels.hpp"
 
@@ -41,6 +43,41 @@ __device__ __forceinline__ int tile_off(int r, int c) { return r * 128 + ((c ^ (
 
 template <typename T>
 __device__ __forceinline__ T to16(float v) { return (T)v; }
+
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+
+template <int N, typename F, int... I>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl<N>(f, std::make_integer_sequence<int, N>{});
+}
+
+template <int OFF, typename V>
+__device__ __forceinline__ void ds_read_b128(V& r, uint32_t addr) {
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF));
+}
+
+// s_waitcnt lgkmcnt(0) that names every fragment register as read-write, so no
+// consumer of them can be scheduled above it (cdna_hip_programming.md §5.7 form ii).
+template <typename V, int MI, int NI>
+__device__ __forceinline__ void lgkm_wait_all(V (&a)[MI], V (&b)[NI]) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < MI; ++i) asm volatile("" : "+v"(a[i]));
+#pragma unroll
+  for (int i = 0; i < NI; ++i) asm volatile("" : "+v"(b[i]));
+}
+
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+
 
 // Tile order shared by all blocks: tiles are grouped 8 row panels at a time
 // (walk M first inside a group) so that concurrently running tiles share A and W
@@ -64,7 +101,9 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
   constexpr int TM = BM / WGM, TN = BN / WGN, MI = TM / 16, NI = TN / 16;
   constexpr int A_CHUNKS = BM * 8 / NT;  // register-staged image A: 16-byte chunks per thread
   static_assert(A_INSTR >= 1 && B_INSTR >= 1 && MI >= 1 && NI >= 1, "bad tile");
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  constexpr int BIAS_BYTES = ASRC == A_ROWS ? 2 * 1024 : 0;  // 2 x 256 f32 (tile-parity double buffer)
+  static_assert(BN <= 256, "bias slice is one 1 KiB DMA");
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + BIAS_BYTES];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -101,27 +140,30 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
   // ---- per-tile staging sources ----------------------------------------------
   // glds: wave w, instruction i writes rows (w*INSTR + i)*8 .. +7 (1 KiB); lane
   // l lands at row +(l>>3), slot (l&7), which holds global chunk slot ^ f(row).
-  // 32-bit per-lane element offsets from the kernel-argument base pointers
-  // (host checks that every operand fits in 2^31 elements).
-  int woff[B_INSTR];
-  int aoff[A_INSTR];
+  // Per-lane 32-bit BYTE offsets from the (wave-uniform) kernel-argument base
+  // pointers: the DMA then uses the SGPR-base + VGPR-offset form with these
+  // persistent registers as the offset -- no per-issue address temporaries, whose
+  // reuse by the asm ds_read destinations made hipcc drain vmcnt(0) (host
+  // checks that every operand fits in 2^31 bytes).
+  uint32_t woff[B_INSTR];
+  uint32_t aoff[A_INSTR];
   long img_base[A_CHUNKS];
   int img_row[A_CHUNKS];
-  const T* const Wb = (const T*)p.W;
-  const T* const Ab = (const T*)p.A;
+  const char* const Wb = (const char*)p.W;
+  const char* const Ab = (const char*)p.A;
   auto set_tile = [&](int m0, int n0) {
 #pragma unroll
     for (int i = 0; i < B_INSTR; ++i) {
       const int r = (wave * B_INSTR + i) * 8 + (lane >> 3);
       const int c = (lane & 7) ^ ((r >> 1) & 7);
-      woff[i] = min(n0 + r, p.N - 1) * (int)p.ldw + c * 8;
+      woff[i] = (uint32_t)(min(n0 + r, p.N - 1) * (int)p.ldw + c * 8) * 2u;
     }
     if constexpr (ASRC == A_ROWS) {
 #pragma unroll
       for (int i = 0; i < A_INSTR; ++i) {
         const int r = (wave * A_INSTR + i) * 8 + (lane >> 3);
         const int c = (lane & 7) ^ ((r >> 1) & 7);
-        aoff[i] = min(m0 + r, p.M - 1) * (int)p.lda + c * 8;
+        aoff[i] = (uint32_t)(min(m0 + r, p.M - 1) * (int)p.lda + c * 8) * 2u;
       }
     } else {
       const int G2 = p.G * p.G;
@@ -142,12 +184,14 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
   };
 
   auto stage_w = [&](int kt, char* sB) {
+    const char* const base = Wb + (size_t)kt * (BK * 2);
 #pragma unroll
-    for (int i = 0; i < B_INSTR; ++i) glds16(Wb + (woff[i] + kt * BK), sB + (wave * B_INSTR + i) * 1024);
+    for (int i = 0; i < B_INSTR; ++i) glds16(base + woff[i], sB + (wave * B_INSTR + i) * 1024);
   };
   auto stage_a_rows = [&](int kt, char* sA) {
+    const char* const base = Ab + (size_t)kt * (BK * 2);
 #pragma unroll
-    for (int i = 0; i < A_INSTR; ++i) glds16(Ab + (aoff[i] + kt * BK), sA + (wave * A_INSTR + i) * 1024);
+    for (int i = 0; i < A_INSTR; ++i) glds16(base + aoff[i], sA + (wave * A_INSTR + i) * 1024);
   };
 
   // Image-sourced A: 8 consecutive k (same channel and image row; P % 8 == 0).
@@ -195,6 +239,17 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
     if constexpr (ASRC == A_ROWS) stage_a_rows(kt, sA);
     else load_a_img(kt);
   };
+  // A_ROWS: the tile's bias slice bias[n0 .. n0+255] goes to LDS by one 1 KiB DMA
+  // (wave 0, with the tile's first K-step), so the epilogue needs no global load
+  // (which, issued after the next tile's DMA, would wait for it: vmcnt is in order).
+  auto stage_bias = [&](int n0, int par) {
+    if constexpr (ASRC == A_ROWS) {
+      if (p.bias != nullptr && wave == 0) {
+        const int n = min(n0 + lane * 4, ((p.N - 1) / 4) * 4);  // clamped in-bounds 16 B (N % 4 == 0 checked)
+        glds16(p.bias + n, smem + 2 * STAGE + par * 1024);
+      }
+    }
+  };
 
   // ---- fragment addressing -------------------------------------------------
   const int wm = (wave / WGN) * TM, wn = (wave % WGN) * TN;
@@ -211,30 +266,86 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
   // C[m = wm + mi*16 + fr][n = wn + ni*16 + fq*4 + j], i.e. each lane owns 4
   // consecutive output columns of one row -> 8 / 16-byte epilogue stores.
   f32x4 acc[NI][MI];
-  auto compute = [&](const char* sA, const char* sB) {
+  const uint32_t lds0 = lds_addr(smem);
+  auto mfma_block = [&](auto zero, const V8(&a)[MI], const V8(&b)[NI]) {
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      V8 a[MI], b[NI];
+    for (int ni = 0; ni < NI; ++ni)
 #pragma unroll
-      for (int ni = 0; ni < NI; ++ni) b[ni] = *(const V8*)(sB + offB[kk] + ni * 2048);
+      for (int mi = 0; mi < MI; ++mi)
+        acc[ni][mi] = mfma_16x16x32(b[ni], a[mi], decltype(zero)::value ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[ni][mi]);
+  };
+  // zero: the first K-step of a tile starts the MFMA chain from C = 0 (no
+  // accumulator re-zeroing between tiles).
+  auto compute = [&](auto zero, const char* sA, const char* sB) {
+    if constexpr (ASRC == A_ROWS) {
+      // Fragment reads in inline asm (invisible to hipcc's waitcnt pass, which
+      // would otherwise drain vmcnt(0) -- including the previous tile's epilogue
+      // stores -- in front of them); the kk = 1 reads fly under the kk = 0 MFMAs.
+      const uint32_t aB = lds0 + (uint32_t)(sA - smem), bB = lds0 + (uint32_t)(sB - smem);
+      V8 a0[MI], b0[NI], a1[MI], b1[NI];
+      static_for<NI>([&](auto ni) { ds_read_b128<(int)ni * 2048>(b0[ni], bB + offB[0]); });
+      static_for<MI>([&](auto mi) { ds_read_b128<(int)mi * 2048>(a0[mi], aB + offA[0]); });
+      lgkm_wait_all(a0, b0);
+      // kk = 0 MFMAs row block by row block; a1[mi] is read into the registers
+      // a0[mi] just released, b1 after the last kk = 0 MFMA (48 fragment VGPRs, not 96).
+      static_for<MI>([&](auto mi) {
 #pragma unroll
-      for (int mi = 0; mi < MI; ++mi) a[mi] = *(const V8*)(sA + offA[kk] + mi * 2048);
+        for (int ni = 0; ni < NI; ++ni)
+          acc[ni][mi] = mfma_16x16x32(b0[ni], a0[mi], decltype(zero)::value ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[ni][mi]);
+        __builtin_amdgcn_sched_barrier(0);
+        ds_read_b128<(int)mi * 2048>(a1[mi], aB + offA[1]);
+      });
+      static_for<NI>([&](auto ni) { ds_read_b128<(int)ni * 2048>(b1[ni], bB + offB[1]); });
+      lgkm_wait_all(a1, b1);
+      mfma_block(std::false_type{}, a1, b1);
+    } else {
 #pragma unroll
-      for (int ni = 0; ni < NI; ++ni)
+      for (int kk = 0; kk < 2; ++kk) {
+        V8 a[MI], b[NI];
 #pragma unroll
-        for (int mi = 0; mi < MI; ++mi) acc[ni][mi] = mfma_16x16x32(b[ni], a[mi], acc[ni][mi]);
+        for (int ni = 0; ni < NI; ++ni) b[ni] = *(const V8*)(sB + offB[kk] + ni * 2048);
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi) a[mi] = *(const V8*)(sA + offA[kk] + mi * 2048);
+        if (kk == 0) mfma_block(zero, a, b);
+        else mfma_block(std::false_type{}, a, b);
+      }
     }
   };
 
-  auto epilogue = [&](int m0, int n0) {
+  auto epilogue = [&](int m0, int n0, int bpar) {
     const int G2 = p.G * p.G;
+    // EPI_RESID: the residual rows of column block ni+1 are loaded before block ni
+    // is stored, so no load waits behind this epilogue's own stores.
+    float4 xr[2][MI];
+    auto load_x = [&](int ni, float4 (&dst)[MI]) {
+      const int n = n0 + wn + ni * 16 + fq * 4;
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi) {
+        const int m = m0 + wm + mi * 16 + fr;
+        if (m < p.M && n + 4 <= p.N) dst[mi] = *(const float4*)((const float*)p.out + (long)m * p.ldo + n);
+      }
+    };
+    if constexpr (EPI == EPI_RESID) load_x(0, xr[0]);
 #pragma unroll
     for (int ni = 0; ni < NI; ++ni) {
+      if constexpr (EPI == EPI_RESID) {
+        if (ni + 1 < NI) load_x(ni + 1, xr[(ni + 1) & 1]);
+      }
       const int n = n0 + wn + ni * 16 + fq * 4;
       const bool nfull = n + 4 <= p.N;
-      float bv[4];
+      float bv[4] = {0.f, 0.f, 0.f, 0.f};
+      if (p.bias != nullptr) {
+        if constexpr (ASRC == A_ROWS) {
+          f32x4 b4;
+          ds_read_b128<0>(b4, lds0 + 2 * STAGE + bpar * 1024 + (wn + ni * 16 + fq * 4) * 4);
+          asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(b4)::"memory");
 #pragma unroll
-      for (int j = 0; j < 4; ++j) bv[j] = (p.bias != nullptr && n + j < p.N) ? p.bias[n + j] : 0.f;
+          for (int j = 0; j < 4; ++j) bv[j] = b4[j];
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) bv[j] = n + j < p.N ? p.bias[n + j] : 0.f;
+        }
+      }
 #pragma unroll
       for (int mi = 0; mi < MI; ++mi) {
         const int m = m0 + wm + mi * 16 + fr;
@@ -266,7 +377,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
           if (nfull) {
             float4 w = make_float4(v[0], v[1], v[2], v[3]);
             if constexpr (EPI == EPI_RESID) {
-              const float4 x = *(const float4*)o;
+              const float4 x = xr[ni & 1][mi];
               w.x += x.x; w.y += x.y; w.z += x.z; w.w += x.w;
             } else if constexpr (EPI == EPI_PATCH) {
               const float4 x = *(const float4*)ps;
@@ -293,25 +404,36 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
   tile_coords(t_first, nTm, nTn, BM, BN, m0, n0);
   set_tile(m0, n0);
   stage(0, sA0, sB0);
+  stage_bias(n0, 0);
   if constexpr (ASRC != A_ROWS) store_a_img(sA0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  int parity = 0;  // buffer holding K-step 0 of the current tile
+  // Step barrier: A_ROWS waits only for its own glds (counted) and uses a raw
+  // s_barrier (a __syncthreads() fence would also drain the epilogue stores);
+  // the register-staged image path needs the fence for its ds_writes.
+  auto step_sync = [&]() {
+    if constexpr (ASRC == A_ROWS) {
+      vm_wait<0>();  // only this K-step's glds are outstanding here
+      __builtin_amdgcn_s_barrier();
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  };
+
+  int parity = 0;    // buffer holding K-step 0 of the current tile
+  int bias_par = 0;  // LDS bias buffer of the current tile
   for (int t = t_first; t < t_end; t += t_stride) {
-#pragma unroll
-    for (int ni = 0; ni < NI; ++ni)
-#pragma unroll
-      for (int mi = 0; mi < MI; ++mi) acc[ni][mi] = f32x4{0.f, 0.f, 0.f, 0.f};
     for (int kt = 0; kt + 1 < nk; ++kt) {
       const bool cur1 = (kt & 1) ^ parity;
       char* const sAn = cur1 ? sA0 : sA1;
       char* const sBn = cur1 ? sB0 : sB1;
       stage(kt + 1, sAn, sBn);
-      compute(cur1 ? sA1 : sA0, cur1 ? sB1 : sB0);
+      if (kt == 0) compute(std::true_type{}, cur1 ? sA1 : sA0, cur1 ? sB1 : sB0);
+      else compute(std::false_type{}, cur1 ? sA1 : sA0, cur1 ? sB1 : sB0);
       if constexpr (ASRC != A_ROWS) store_a_img(sAn);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
+      step_sync();
     }
     // last K-step: prefetch the next tile's first K-step under it and the epilogue
     const bool cur1 = ((nk - 1) & 1) ^ parity;
@@ -322,15 +444,27 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
       tile_coords(tn, nTm, nTn, BM, BN, nm0, nn0);
       set_tile(nm0, nn0);
       stage(0, cur1 ? sA0 : sA1, cur1 ? sB0 : sB1);
+      stage_bias(nn0, bias_par ^ 1);
     }
-    compute(cur1 ? sA1 : sA0, cur1 ? sB1 : sB0);
+    if (nk == 1) compute(std::true_type{}, cur1 ? sA1 : sA0, cur1 ? sB1 : sB0);
+    else compute(std::false_type{}, cur1 ? sA1 : sA0, cur1 ? sB1 : sB0);
     if constexpr (ASRC != A_ROWS) {
       if (has_next) store_a_img(cur1 ? sA0 : sA1);
     }
-    epilogue(m0, n0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    epilogue(m0, n0, bias_par);
+    if constexpr (ASRC == A_ROWS) {
+      // Retire the next tile's stage-0 glds but not this tile's output stores
+      // (issued after them; in-order vmcnt): a full tile issues exactly MI*NI
+      // epilogue stores per lane, a partial one may issue fewer -> wait for all.
+      if (m0 + BM <= p.M && n0 + BN <= p.N) vm_wait<MI * NI>();
+      else vm_wait<0>();
+      __builtin_amdgcn_s_barrier();
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
     parity ^= (nk & 1);
+    bias_par ^= 1;
     m0 = nm0;
     n0 = nn0;
   }
@@ -348,6 +482,228 @@ int device_cus() {
   return cus;
 }
 
+// ---------------------------------------------------------------------------
+// Ring-pipelined variant for the 256-row tiles (A from rows).  NS = 4 LDS
+// stages of BK = 32 (64-byte rows); the loads of K-step g+3 are issued right
+// after the barrier of step g, so three steps of global_load_lds stay in flight
+// across barriers, retired by a counted s_waitcnt vmcnt(N) (never 0 in steady
+// state; cdna_hip_programming.md §5 "Pipelining across barriers") and a raw
+// s_barrier (a __syncthreads() would drain vmcnt).  The load cursor runs ahead
+// across tile boundaries of the persistent schedule, so the next tile's first
+// K-steps land under the current tile's last steps and epilogue.
+// ---------------------------------------------------------------------------
+
+// Byte offset of 16-byte chunk c (0..3) of row r in a [rows][32] 16-bit tile.
+// XOR with g[(r>>2)&3], g = {0,2,3,1}: conflict-free 16x16x32 fragment reads
+// (each ds_read_b128 lane group hits 16 distinct 16-byte slots).
+__device__ __forceinline__ int ring_swz(int r) { return (0xB4 >> (((r >> 2) & 3) * 2)) & 3; }
+
+template <typename T, int MI, int NI, int EPI, int ACT>
+__device__ __forceinline__ void epilogue_store(const GemmParams& p, f32x4 (&acc)[NI][MI], int m0, int n0, int wm,
+                                               int wn, int fr, int fq) {
+  typedef typename Vec4<T>::type V4;
+#pragma unroll
+  for (int ni = 0; ni < NI; ++ni) {
+    const int n = n0 + wn + ni * 16 + fq * 4;
+    const bool nfull = n + 4 <= p.N;
+    float bv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bv[j] = (p.bias != nullptr && n + j < p.N) ? p.bias[n + j] : 0.f;
+#pragma unroll
+    for (int mi = 0; mi < MI; ++mi) {
+      const int m = m0 + wm + mi * 16 + fr;
+      if (m >= p.M) continue;
+      float v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = acc[ni][mi][j] + bv[j];
+      if constexpr (EPI == EPI_STORE16) {
+        T* o = (T*)p.out + (long)m * p.ldo + n;
+        if (nfull) {
+          V4 w;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) w[j] = to16<T>(apply_act<ACT>(v[j]));
+          *(V4*)o = w;
+        } else {
+          for (int j = 0; j < 4; ++j)
+            if (n + j < p.N) o[j] = to16<T>(apply_act<ACT>(v[j]));
+        }
+      } else {
+        float* o = (float*)p.out + (long)m * p.ldo + n;
+        if (nfull) {
+          float4 w = make_float4(v[0], v[1], v[2], v[3]);
+          if constexpr (EPI == EPI_RESID) {
+            const float4 x = *(const float4*)o;
+            w.x += x.x; w.y += x.y; w.z += x.z; w.w += x.w;
+          }
+          *(float4*)o = w;
+        } else {
+          for (int j = 0; j < 4; ++j) {
+            if (n + j >= p.N) continue;
+            float r = v[j];
+            if constexpr (EPI == EPI_RESID) r += o[j];
+            o[j] = r;
+          }
+        }
+      }
+    }
+  }
+}
+
+template <typename T, int BM, int BN, int EPI, int ACT>
+__global__ __launch_bounds__(512, 2) void gemm_ring_kernel(GemmParams p) {
+  typedef typename Vec8<T>::type V8;
+  constexpr int WGM = 2, WGN = 4, NW = 8;
+  constexpr int BKS = 32, NS = 4;
+  constexpr int A_BYTES = BM * BKS * 2, B_BYTES = BN * BKS * 2, STAGE = A_BYTES + B_BYTES;
+  constexpr int A_INSTR = BM / 16 / NW, B_INSTR = BN / 16 / NW;  // 1 KiB = 16 rows of 64 B
+  constexpr int LPS = A_INSTR + B_INSTR;                          // vm ops per stage per wave
+  constexpr int TM = BM / WGM, TN = BN / WGN, MI = TM / 16, NI = TN / 16;
+  constexpr int EPI_OPS = MI * NI;  // >= vm ops of a full tile's epilogue (one 8/16-B store per (mi, ni))
+  static_assert(A_INSTR >= 1 && B_INSTR >= 1, "bad ring tile");
+  static_assert(2 * LPS + EPI_OPS <= 63, "vmcnt field");
+  // Fragment reads are inline-asm ds_read_b128: hipcc cannot tell that the DMA
+  // into stage (k+3)%4 does not alias the reads of stage k and would otherwise
+  // drain vmcnt(0) in front of every compiler-visible ds_read (measured in the
+  // .s), which collapses the ring.  Our counted waits + barrier order them.
+  __shared__ __attribute__((aligned(16))) char smem[NS * STAGE];
+  char* const st0 = smem;
+  char* const st1 = smem + STAGE;
+  char* const st2 = smem + 2 * STAGE;
+  char* const st3 = smem + 3 * STAGE;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nTn = (p.N + BN - 1) / BN;
+  const int nTm = (p.M + BM - 1) / BM;
+  const int ntiles = nTn * nTm;
+  const int nks = p.K / BKS;  // multiple of NS (host checks K % 128 == 0)
+
+  const int nb = gridDim.x;
+  int t_first, t_stride, t_end;
+  if (nb % 8 == 0 && nb < ntiles) {
+    const int x = blockIdx.x & 7, nbx = nb >> 3;
+    const int q = ntiles >> 3, r = ntiles & 7;
+    const int start = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
+    t_first = start + (blockIdx.x >> 3);
+    t_stride = nbx;
+    t_end = start + q + (x < r ? 1 : 0);
+  } else {
+    t_first = xcd_remap(blockIdx.x, nb);
+    t_stride = ntiles;
+    t_end = t_first + 1;
+  }
+  if (t_first >= t_end) return;
+  const int my_tiles = (t_end - t_first + t_stride - 1) / t_stride;
+  const int G = my_tiles * nks;  // K-steps this block computes
+
+  // ---- load cursor (runs 3 K-steps ahead of the compute cursor) ----------------
+  const T* const Wb = (const T*)p.W;
+  const T* const Ab = (const T*)p.A;
+  int woff[B_INSTR], aoff[A_INSTR];
+  auto set_tile = [&](int m0, int n0) {
+#pragma unroll
+    for (int i = 0; i < B_INSTR; ++i) {
+      const int r = (wave * B_INSTR + i) * 16 + (lane >> 2);
+      woff[i] = min(n0 + r, p.N - 1) * (int)p.ldw + (((lane & 3) ^ ring_swz(r)) << 3);
+    }
+#pragma unroll
+    for (int i = 0; i < A_INSTR; ++i) {
+      const int r = (wave * A_INSTR + i) * 16 + (lane >> 2);
+      aoff[i] = min(m0 + r, p.M - 1) * (int)p.lda + (((lane & 3) ^ ring_swz(r)) << 3);
+    }
+  };
+  int lt = t_first, ls = 0, lg = 0;
+  {
+    int m0, n0;
+    tile_coords(lt, nTm, nTn, BM, BN, m0, n0);
+    set_tile(m0, n0);
+  }
+  // stage K-step lg (if any) into ring stage `st` (== lg % NS by construction)
+  auto issue_next = [&](char* st) {
+    if (lg >= G) return;
+#pragma unroll
+    for (int i = 0; i < A_INSTR; ++i) glds16(Ab + (aoff[i] + ls * BKS), st + (wave * A_INSTR + i) * 1024);
+#pragma unroll
+    for (int i = 0; i < B_INSTR; ++i)
+      glds16(Wb + (woff[i] + ls * BKS), st + A_BYTES + (wave * B_INSTR + i) * 1024);
+    ++lg;
+    if (++ls == nks) {
+      ls = 0;
+      lt += t_stride;
+      if (lt < t_end) {
+        int m0, n0;
+        tile_coords(lt, nTm, nTn, BM, BN, m0, n0);
+        set_tile(m0, n0);
+      }
+    }
+  };
+
+  // ---- fragments ------------------------------------------------------------------
+  const int wm = (wave / WGN) * TM, wn = (wave % WGN) * TN;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int sw = (fq ^ ring_swz(fr)) << 4;
+  const int offA = (wm + fr) * 64 + sw;
+  const int offB = A_BYTES + (wn + fr) * 64 + sw;
+
+  f32x4 acc[NI][MI];
+  const uint32_t lds0 = lds_addr(smem);
+  auto compute = [&](const char* st) {
+    const uint32_t a_base = lds0 + (uint32_t)(st - smem) + offA;
+    const uint32_t b_base = lds0 + (uint32_t)(st - smem) + offB;
+    V8 a[MI], b[NI];
+    static_for<NI>([&](auto ni) { ds_read_b128<(int)ni * 1024>(b[ni], b_base); });
+    static_for<MI>([&](auto mi) { ds_read_b128<(int)mi * 1024>(a[mi], a_base); });
+    lgkm_wait_all(a, b);
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi) acc[ni][mi] = mfma_16x16x32(b[ni], a[mi], acc[ni][mi]);
+  };
+
+  issue_next(st0);
+  issue_next(st1);
+  issue_next(st2);
+
+  int g = 0;
+  bool prev_full = false;
+  for (int t = t_first; t < t_end; t += t_stride) {
+    int m0, n0;
+    tile_coords(t, nTm, nTn, BM, BN, m0, n0);
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi) acc[ni][mi] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // Step g: retire its loads (younger vm ops = steps g+1, g+2 if issued and, at a
+    // tile's first step, the previous tile's epilogue stores), barrier, issue step
+    // g+3 into the stage every wave finished reading at step g-1, compute.
+    auto step = [&](const char* cur, char* refill, bool first) {
+      const int ahead = (g + 2 < G) ? 2 : (g + 1 < G ? 1 : 0);
+      if (first && prev_full) {
+        if (ahead == 2) vm_wait<2 * LPS + EPI_OPS>();
+        else if (ahead == 1) vm_wait<LPS + EPI_OPS>();
+        else vm_wait<EPI_OPS>();
+      } else {
+        if (ahead == 2) vm_wait<2 * LPS>();
+        else if (ahead == 1) vm_wait<LPS>();
+        else vm_wait<0>();
+      }
+      __builtin_amdgcn_s_barrier();
+      issue_next(refill);
+      compute(cur);
+      ++g;
+    };
+    for (int s = 0; s < nks; s += NS) {
+      step(st0, st3, s == 0);
+      step(st1, st0, false);
+      step(st2, st1, false);
+      step(st3, st2, false);
+    }
+    epilogue_store<T, MI, NI, EPI, ACT>(p, acc, m0, n0, wm, wn, fr, fq);
+    prev_full = (m0 + BM <= p.M) && (n0 + BN <= p.N);
+  }
+}
+
 template <typename T, int BM, int BN, int WGM, int WGN, int ASRC, int EPI, int ACT>
 hipError_t launch_cfg(const GemmParams& p, hipStream_t s) {
   const int nTn = (p.N + BN - 1) / BN, nTm = (p.M + BM - 1) / BM;
@@ -360,6 +716,16 @@ hipError_t launch_cfg(const GemmParams& p, hipStream_t s) {
   return hipGetLastError();
 }
 
+template <typename T, int BM, int BN, int EPI, int ACT>
+hipError_t launch_ring(const GemmParams& p, hipStream_t s) {
+  const int nTn = (p.N + BN - 1) / BN, nTm = (p.M + BM - 1) / BM;
+  const int ntiles = nTn * nTm;
+  const int resident = device_cus();
+  const int grid = ntiles <= resident ? ntiles : resident;
+  hipLaunchKernelGGL((gemm_ring_kernel<T, BM, BN, EPI, ACT>), dim3(grid), dim3(512), 0, s, p);
+  return hipGetLastError();
+}
+
 template <typename T, int ASRC, int EPI, int ACT>
 hipError_t launch_tile(const GemmParams& p, hipStream_t s) {
   if constexpr (ASRC != A_ROWS) {
@@ -369,6 +735,8 @@ hipError_t launch_tile(const GemmParams& p, hipStream_t s) {
     switch (tile) {
       case TILE_256x256: return launch_cfg<T, 256, 256, 2, 4, ASRC, EPI, ACT>(p, s);
       case TILE_256x128: return launch_cfg<T, 256, 128, 2, 4, ASRC, EPI, ACT>(p, s);
+      case TILE_RING_256x256: return launch_ring<T, 256, 256, EPI, ACT>(p, s);
+      case TILE_RING_256x128: return launch_ring<T, 256, 128, EPI, ACT>(p, s);
       default: return launch_cfg<T, 128, 128, 2, 2, ASRC, EPI, ACT>(p, s);
     }
   }
@@ -418,8 +786,11 @@ int pick_gemm_tile(int M, int N, int K) {
 
 hipError_t launch_gemm(DType dt, int asrc, int epi, int act, const GemmParams& p, hipStream_t s) {
   if (p.K % BK != 0 || p.M <= 0 || p.N <= 0) return hipErrorInvalidValue;
+  if (p.bias != nullptr && p.N % 4 != 0) return hipErrorInvalidValue;  // 16-byte bias DMA
   // 32-bit staging offsets
-  if ((long)p.M * p.lda >= (1L << 31) || (long)p.N * p.ldw >= (1L << 31)) return hipErrorInvalidValue;
+  if ((long)p.M * p.lda * 2 >= (1L << 31) || (long)p.N * p.ldw * 2 >= (1L << 31)) return hipErrorInvalidValue;
+  if ((p.tile == TILE_RING_256x256 || p.tile == TILE_RING_256x128) && asrc == A_ROWS && p.K % 128 != 0)
+    return hipErrorInvalidValue;  // (image-sourced A always runs the 128x128 register-staged tile)
   if (asrc != A_ROWS && (p.P % 8 != 0)) return hipErrorInvalidValue;
   return dt == DT_BF16 ? launch_typed<__bf16>(asrc, epi, act, p, s)
                        : launch_typed<_Float16>(asrc, epi, act, p, s);

@@ -42,6 +42,8 @@ enum GemmTile {
   TILE_128x128 = 1,  // 4 waves, 64 KiB LDS, 2 blocks / CU (small M)
   TILE_256x128 = 2,  // 8 waves, 96 KiB LDS
   TILE_256x256 = 3,  // 8 waves, 128 KiB LDS
+  TILE_RING_256x256 = 4,  // 8 waves, 4-stage BK=32 ring, counted vmcnt, 128 KiB LDS
+  TILE_RING_256x128 = 5,  // 8 waves, 4-stage BK=32 ring, 96 KiB LDS
 };
 int pick_gemm_tile(int M, int N, int K);
 

@@ -48,7 +48,7 @@ def run_gemm(dtype, mode, act, A, W, bias=None, resid=None):
     return out
 
 
-@pytest.fixture(params=[1, 2, 3], ids=["t128x128", "t256x128", "t256x256"])
+@pytest.fixture(params=[1, 2, 3, 4, 5], ids=["t128x128", "t256x128", "t256x256", "ring256x256", "ring256x128"])
 def tile(request, monkeypatch):
     """Every GEMM tile configuration (GemmTile) through the same numerics checks."""
     monkeypatch.setenv("CLIPGPU_TEST_TILE", str(request.param))
@@ -57,8 +57,10 @@ def tile(request, monkeypatch):
 
 @pytest.mark.parametrize("dtype", [BF16, F16])
 @pytest.mark.parametrize("M,N,K", [(128, 128, 64), (200, 136, 192), (1000, 768, 768), (77, 64, 512),
-                                   (12800, 768, 3072), (2600, 3072, 768)])
+                                   (12800, 768, 3072), (2600, 3072, 768), (3000, 520, 384)])
 def test_gemm_f32_out(dtype, M, N, K, tile):
+    if tile >= 4 and K % 128:
+        pytest.skip("ring tiles need K % 128 == 0")
     rng = np.random.default_rng(M * 7 + N + K)
     A = round16(rng.standard_normal((M, K)), dtype)
     W = round16(rng.standard_normal((N, K)) / np.sqrt(K), dtype)
@@ -73,7 +75,7 @@ def test_gemm_f32_out(dtype, M, N, K, tile):
 @pytest.mark.parametrize("dtype", [BF16, F16])
 @pytest.mark.parametrize("act", [0, 1, 2, 3])
 def test_gemm_store16_act(dtype, act, tile):
-    M, N, K = 300, 384, 256
+    M, N, K = 600, 384, 256
     rng = np.random.default_rng(act)
     A = round16(rng.standard_normal((M, K)), dtype)
     W = round16(rng.standard_normal((N, K)) / np.sqrt(K), dtype)
@@ -86,7 +88,7 @@ def test_gemm_store16_act(dtype, act, tile):
 
 @pytest.mark.parametrize("dtype", [BF16])
 def test_gemm_residual(dtype, tile):
-    M, N, K = 513, 256, 128
+    M, N, K = 1513, 640, 256
     rng = np.random.default_rng(5)
     A = round16(rng.standard_normal((M, K)), dtype)
     W = round16(rng.standard_normal((N, K)) / np.sqrt(K), dtype)

@@ -20,11 +20,11 @@ SHAPES = [  # name, M, N, K, epi, act
 L = _lib.lib()
 rows = []
 for name, M, N, K, epi, act in SHAPES:
-    for tile in (1, 2, 3):
+    for tile in (1, 2, 3, 4, 5):
         us = ctypes.c_double()
         _lib.check(L.clipgpu_test_gemm_bench(0, epi, act, M, N, K, tile, 20, ctypes.byref(us)))
         tf = 2.0 * M * N * K / (us.value * 1e-6) / 1e12
-        rows.append({"gemm": name, "M": M, "N": N, "K": K, "tile": ["", "128x128", "256x128", "256x256"][tile],
+        rows.append({"gemm": name, "M": M, "N": N, "K": K, "tile": ["", "128x128", "256x128", "256x256", "ring256", "ring128"][tile],
                      "us": round(us.value, 2), "tflops": round(tf, 1)})
         print(f"{name:12s} {M:6d}x{N:5d}x{K:5d} tile {rows[-1]['tile']:8s} {us.value:9.2f} us {tf:7.1f} TF/s",
               flush=True)
