@@ -11,6 +11,8 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <memory>
@@ -22,6 +24,7 @@
 #include <vector>
 
 #include "../../include/clipgpu.h"
+#include "../../include/clipgpu_testing.h"
 #include "host/api_util.hpp"
 #include "host/json.hpp"
 #include "host/model.hpp"
@@ -67,6 +70,11 @@ struct Replica {
   void* in = nullptr;     // device input staging (pixels f32 / u8 / ids)
   void* pin_in = nullptr; // pinned host staging
   float* pin_out = nullptr;
+  // Concurrent sub-batches ("lanes"): each lane runs the whole forward on a
+  // contiguous slice of the batch on its own stream, so one lane's GEMM tail
+  // rounds and memory-bound kernels overlap the other lane's GEMMs.
+  hipStream_t lane[4] = {nullptr, nullptr, nullptr, nullptr};
+  hipEvent_t fork = nullptr, join[4] = {nullptr, nullptr, nullptr, nullptr};
 };
 
 }  // namespace clipgpu
@@ -98,6 +106,11 @@ struct Profiler {
 
 struct clipgpu_engine {
   clipgpu::Profiler prof;
+  // GEMM tile per trunk call site (clipgpu::GemmSite), autotuned at creation for
+  // max_batch rows; batches under half of that use the shape heuristic.
+  int tile[4] = {0, 0, 0, 0};
+  int tuned_rows = 0;
+  int lanes = 1;  // concurrent sub-batches per device (CLIPGPU_LANES, default 2)
   clipgpu::TowerSpec spec;
   clipgpu::PreprocessCfg pre;
   clipgpu::DType dt = clipgpu::DT_BF16;
@@ -249,6 +262,11 @@ void alloc_workspace(clipgpu_engine& e, Replica& r) {
   r.emb = (float*)a.take(sizes[4]);
   r.out = (float*)a.take(sizes[5]);
   r.in = a.take(sizes[6]);
+  for (int i = 0; i < e.lanes; ++i) {
+    HIP_CHECK(hipStreamCreateWithFlags(&r.lane[i], hipStreamNonBlocking));
+    HIP_CHECK(hipEventCreateWithFlags(&r.join[i], hipEventDisableTiming));
+  }
+  HIP_CHECK(hipEventCreateWithFlags(&r.fork, hipEventDisableTiming));
   HIP_CHECK(hipHostMalloc(&r.pin_in, B * e.in_bytes_per_row, hipHostMallocDefault));
   HIP_CHECK(hipHostMalloc((void**)&r.pin_out, B * E * 4, hipHostMallocDefault));
 }
@@ -281,6 +299,8 @@ struct ProfScope {
   }
 };
 
+enum GemmSite { GS_QKV = 0, GS_OUT, GS_FC, GS_PROJ, GS_N };
+
 GemmParams rows_gemm(const void* A, long lda, const void* W, const float* bias, void* out, long ldo, int M, int N,
                      int K) {
   GemmParams g{};
@@ -297,30 +317,98 @@ GemmParams rows_gemm(const void* A, long lda, const void* W, const float* bias, 
   return g;
 }
 
+int site_epi(int site) { return (site == GS_OUT || site == GS_PROJ) ? EPI_RESID : EPI_STORE16; }
+
+GemmParams site_gemm(const clipgpu_engine& e, const Replica& r, const LayerW& L, int site, int rows) {
+  const int D = e.spec.width, MLP = e.spec.mlp_width;
+  switch (site) {
+    case GS_QKV: return rows_gemm(r.h, D, L.wqkv, L.bqkv, r.big, 3 * D, rows, 3 * D, D);
+    case GS_OUT: return rows_gemm(r.h, D, L.wo, L.bo, r.x, D, rows, D, D);
+    case GS_FC: return rows_gemm(r.h, D, L.w1, L.b1, r.big, MLP, rows, MLP, D);
+    default: return rows_gemm(r.big, MLP, L.w2, L.b2, r.x, D, rows, D, MLP);
+  }
+}
+
 // The transformer trunk shared by both towers: L x [LN1 -> QKV -> MHA -> out+res ->
 // LN2 -> fc1+act -> fc2+res], with h already holding ln_1(x) of layer 0.
 void trunk(const clipgpu_engine& e, const Replica& r, int B, int causal, hipStream_t st) {
   const TowerSpec& s = e.spec;
-  const int T = s.tokens(), rows = B * T, D = s.width, MLP = s.mlp_width;
+  const int T = s.tokens(), rows = B * T, D = s.width;
+  const bool tuned = 2 * rows > e.tuned_rows;
   for (int l = 0; l < s.layers; ++l) {
     const LayerW& L = r.w.layers[l];
-    { ProfScope ps(e, PC_QKV, st);
-    check(launch_gemm(e.dt, A_ROWS, EPI_STORE16, ACT_NONE, rows_gemm(r.h, D, L.wqkv, L.bqkv, r.big, 3 * D, rows, 3 * D, D), st), "qkv gemm"); }
+    auto gemm = [&](int site, int cat, const char* what) {
+      ProfScope ps(e, cat, st);
+      GemmParams g = site_gemm(e, r, L, site, rows);
+      g.tile = tuned ? e.tile[site] : TILE_AUTO;
+      check(launch_gemm(e.dt, A_ROWS, site_epi(site), site == GS_FC ? s.act : ACT_NONE, g, st), what);
+    };
+    gemm(GS_QKV, PC_QKV, "qkv gemm");
     { ProfScope ps(e, PC_ATTN, st);
       check(launch_attention(e.dt, r.big, r.h, B, T, s.heads, D, causal, st), "attention"); }
-    { ProfScope ps(e, PC_OUT_PROJ, st);
-      check(launch_gemm(e.dt, A_ROWS, EPI_RESID, ACT_NONE, rows_gemm(r.h, D, L.wo, L.bo, r.x, D, rows, D, D), st), "out_proj gemm"); }
+    gemm(GS_OUT, PC_OUT_PROJ, "out_proj gemm");
     { ProfScope ps(e, PC_LN, st);
       check(launch_ln_rows(e.dt, r.x, L.ln2_w, L.ln2_b, s.ln_eps, r.h, rows, D, st), "ln_2"); }
-    { ProfScope ps(e, PC_C_FC, st);
-      check(launch_gemm(e.dt, A_ROWS, EPI_STORE16, s.act, rows_gemm(r.h, D, L.w1, L.b1, r.big, MLP, rows, MLP, D), st), "c_fc gemm"); }
-    { ProfScope ps(e, PC_C_PROJ, st);
-      check(launch_gemm(e.dt, A_ROWS, EPI_RESID, ACT_NONE, rows_gemm(r.big, MLP, L.w2, L.b2, r.x, D, rows, D, MLP), st), "c_proj gemm"); }
+    gemm(GS_FC, PC_C_FC, "c_fc gemm");
+    gemm(GS_PROJ, PC_C_PROJ, "c_proj gemm");
     if (l + 1 < s.layers) {
       ProfScope ps(e, PC_LN, st);
       check(launch_ln_rows(e.dt, r.x, r.w.layers[l + 1].ln1_w, r.w.layers[l + 1].ln1_b, s.ln_eps, r.h, rows, D, st), "ln_1");
     }
   }
+}
+
+// Times each candidate tile on every trunk GEMM site at max_batch rows (workspace
+// contents are scratch at this point) and keeps the fastest.  Tile choice changes
+// speed only: every tile computes the same sums in the same K order.
+void autotune_tiles(clipgpu_engine& e, Replica& r) {
+  // tuned for the rows one lane runs at max_batch
+  const int rows = (e.max_batch + e.lanes - 1) / e.lanes * e.spec.tokens();
+  e.tuned_rows = rows;
+  const char* env = getenv("CLIPGPU_GEMM_AUTOTUNE");
+  if (env && env[0] == '0') {
+    for (int& t : e.tile) t = TILE_AUTO;
+    return;
+  }
+  if (const char* fixed = getenv("CLIPGPU_GEMM_TILES")) {  // "q,o,f,p": pin every site (tests)
+    int v[4];
+    if (sscanf(fixed, "%d,%d,%d,%d", &v[0], &v[1], &v[2], &v[3]) != 4)
+      throw ClipErr(CLIPGPU_ERR_INVALID, "CLIPGPU_GEMM_TILES must be 'q,o,f,p'");
+    for (int i = 0; i < 4; ++i) {
+      if (v[i] < TILE_AUTO || v[i] > TILE_256x256) throw ClipErr(CLIPGPU_ERR_INVALID, "bad CLIPGPU_GEMM_TILES entry");
+      e.tile[i] = v[i];
+    }
+    return;
+  }
+  const int cands[] = {TILE_128x128, TILE_256x128, TILE_256x256};
+  hipEvent_t a, b;
+  HIP_CHECK(hipEventCreate(&a));
+  HIP_CHECK(hipEventCreate(&b));
+  const LayerW& L = r.w.layers[0];
+  for (int site = 0; site < GS_N; ++site) {
+    float best = 1e30f;
+    int best_tile = TILE_AUTO;
+    for (int t : cands) {
+      GemmParams g = site_gemm(e, r, L, site, rows);
+      g.tile = t;
+      const int act = site == GS_FC ? e.spec.act : ACT_NONE;
+      check(launch_gemm(e.dt, A_ROWS, site_epi(site), act, g, r.stream), "autotune gemm");
+      HIP_CHECK(hipEventRecord(a, r.stream));
+      const int iters = 4;
+      for (int i = 0; i < iters; ++i) check(launch_gemm(e.dt, A_ROWS, site_epi(site), act, g, r.stream), "autotune gemm");
+      HIP_CHECK(hipEventRecord(b, r.stream));
+      HIP_CHECK(hipEventSynchronize(b));
+      float ms = 0.f;
+      HIP_CHECK(hipEventElapsedTime(&ms, a, b));
+      if (ms < best) {
+        best = ms;
+        best_tile = t;
+      }
+    }
+    e.tile[site] = best_tile;
+  }
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
 }
 
 void head(const clipgpu_engine& e, const Replica& r, int B, const int64_t* ids, float* d_out, hipStream_t st) {
@@ -380,6 +468,74 @@ void text_forward(const clipgpu_engine& e, const Replica& r, const int64_t* d_id
   head(e, r, B, d_ids, d_out, st);
 }
 
+// The replica's workspace seen from batch row b0: every activation buffer is
+// batch-major, so a sub-batch is a pointer offset.
+Replica lane_view(const clipgpu_engine& e, const Replica& r, int b0) {
+  const TowerSpec& s = e.spec;
+  const size_t rows = (size_t)b0 * s.tokens(), D = s.width;
+  const size_t wide = std::max((size_t)3 * D, (size_t)s.mlp_width);
+  Replica v = r;
+  v.x = r.x + rows * D;
+  v.h = (char*)r.h + rows * D * 2;
+  v.big = (char*)r.big + rows * wide * 2;
+  v.pooled = (char*)r.pooled + (size_t)b0 * D * 2;
+  v.emb = r.emb + (size_t)b0 * s.embed_dim;
+  return v;
+}
+
+// Batch split for `lanes` concurrent sub-batches: lane i gets rows [b0, b1).
+inline void lane_range(int B, int lanes, int i, int& b0, int& b1) {
+  b0 = (int)((long)B * i / lanes);
+  b1 = (int)((long)B * (i + 1) / lanes);
+}
+
+inline int lanes_for(const clipgpu_engine& e, int B) {
+  return B < 8 * e.lanes ? 1 : e.lanes;  // small batches gain nothing from lanes
+}
+
+// Runs fwd(view, b0, n, stream) on each lane, forked from and joined back to `st`.
+// While profiling, the same per-lane launches run one after another on `st`, so
+// each kernel's HIP-event time is its own (same shapes as the concurrent run).
+template <typename F>
+void run_lanes(const clipgpu_engine& e, const Replica& r, int B, hipStream_t st, F fwd) {
+  const int L = lanes_for(e, B);
+  if (L == 1 || e.prof.mask) {
+    for (int i = 0; i < L; ++i) {
+      int b0, b1;
+      lane_range(B, L, i, b0, b1);
+      fwd(lane_view(e, r, b0), b0, b1 - b0, st);
+    }
+    return;
+  }
+  HIP_CHECK(hipEventRecord(r.fork, st));
+  for (int i = 0; i < L; ++i) {
+    int b0, b1;
+    lane_range(B, L, i, b0, b1);
+    HIP_CHECK(hipStreamWaitEvent(r.lane[i], r.fork, 0));
+    fwd(lane_view(e, r, b0), b0, b1 - b0, r.lane[i]);
+    HIP_CHECK(hipEventRecord(r.join[i], r.lane[i]));
+  }
+  for (int i = 0; i < L; ++i) HIP_CHECK(hipStreamWaitEvent(st, r.join[i], 0));
+}
+
+void vision_forward_lanes(const clipgpu_engine& e, const Replica& r, const void* pixels, int asrc, const float* mean,
+                          const float* stdv, int B, float* d_out, hipStream_t st) {
+  const size_t S = e.spec.image_size;
+  const size_t row_bytes = 3 * S * S * (asrc == A_IMG_F32 ? 4 : 1);
+  const int E = e.spec.embed_dim;
+  run_lanes(e, r, B, st, [&](const Replica& v, int b0, int n, hipStream_t ls) {
+    vision_forward(e, v, (const char*)pixels + b0 * row_bytes, asrc, mean, stdv, n, d_out + (size_t)b0 * E, ls);
+  });
+}
+
+void text_forward_lanes(const clipgpu_engine& e, const Replica& r, const int64_t* d_ids, int B, float* d_out,
+                        hipStream_t st) {
+  const int E = e.spec.embed_dim, T = e.spec.context_length;
+  run_lanes(e, r, B, st, [&](const Replica& v, int b0, int n, hipStream_t ls) {
+    text_forward(e, v, d_ids + (size_t)b0 * T, n, d_out + (size_t)b0 * E, ls);
+  });
+}
+
 enum InKind { IN_F32 = 0, IN_U8 = 1, IN_IDS = 2 };
 
 // Host-buffer forward over a row range of one replica, chunked by max_batch.
@@ -392,9 +548,9 @@ void run_host_shard(clipgpu_engine& e, Replica& r, InKind kind, const void* in, 
     std::memcpy(r.pin_in, (const char*)in + c0 * in_row_bytes, (size_t)n * in_row_bytes);
     HIP_CHECK(hipMemcpyAsync(r.in, r.pin_in, (size_t)n * in_row_bytes, hipMemcpyHostToDevice, r.stream));
     if (kind == IN_IDS)
-      text_forward(e, r, (const int64_t*)r.in, n, r.out, r.stream);
+      text_forward_lanes(e, r, (const int64_t*)r.in, n, r.out, r.stream);
     else
-      vision_forward(e, r, r.in, kind == IN_F32 ? A_IMG_F32 : A_IMG_U8, mean, stdv, n, r.out, r.stream);
+      vision_forward_lanes(e, r, r.in, kind == IN_F32 ? A_IMG_F32 : A_IMG_U8, mean, stdv, n, r.out, r.stream);
     HIP_CHECK(hipMemcpyAsync(r.pin_out, r.out, (size_t)n * E * 4, hipMemcpyDeviceToHost, r.stream));
     HIP_CHECK(hipStreamSynchronize(r.stream));
     std::memcpy(out + c0 * E, r.pin_out, (size_t)n * E * 4);
@@ -440,6 +596,11 @@ void destroy_replica(Replica& r) {
   if (r.pin_in) (void)hipHostFree(r.pin_in);
   if (r.pin_out) (void)hipHostFree(r.pin_out);
   if (r.stream) (void)hipStreamDestroy(r.stream);
+  for (int i = 0; i < 4; ++i) {
+    if (r.lane[i]) (void)hipStreamDestroy(r.lane[i]);
+    if (r.join[i]) (void)hipEventDestroy(r.join[i]);
+  }
+  if (r.fork) (void)hipEventDestroy(r.fork);
   r = Replica();
 }
 
@@ -479,6 +640,8 @@ int clipgpu_create(const char* model_dir, int tower, const int* device_ids, int 
     e->pre = oc.pre;
     e->dt = dtype == CLIPGPU_DTYPE_BF16 ? DT_BF16 : DT_F16;
     e->max_batch = max_batch;
+    if (const char* ln = getenv("CLIPGPU_LANES")) e->lanes = std::max(1, std::min(4, atoi(ln)));
+    else e->lanes = 2;
     const TowerSpec& s = e->spec;
     if (s.width % 64 || s.width / s.heads != 64)
       throw ClipErr(CLIPGPU_ERR_CONFIG, "Configuration error: head_dim must be 64 and width a multiple of 64");
@@ -527,6 +690,7 @@ int clipgpu_create(const char* model_dir, int tower, const int* device_ids, int 
       HIP_CHECK(hipStreamCreateWithFlags(&r.stream, hipStreamNonBlocking));
       upload_weights(*e, r, m);
       alloc_workspace(*e, r);
+      if (i == 0) autotune_tiles(*e, r);  // one tuning, shared by identical devices
     }
     *out = e.release();
   });
@@ -601,7 +765,8 @@ int clipgpu_embed_pixels_device(clipgpu_engine* e, const float* d_nchw, int64_t 
     if (B > e->max_batch) throw ClipErr(CLIPGPU_ERR_INVALID, "B exceeds max_batch");
     Replica& r = e->reps[0];
     HIP_CHECK(hipSetDevice(r.device));
-    vision_forward(*e, r, d_nchw, A_IMG_F32, nullptr, nullptr, (int)B, d_out, stream ? (hipStream_t)stream : r.stream);
+    vision_forward_lanes(*e, r, d_nchw, A_IMG_F32, nullptr, nullptr, (int)B, d_out,
+                         stream ? (hipStream_t)stream : r.stream);
   });
 }
 
@@ -614,7 +779,7 @@ int clipgpu_embed_u8_device(clipgpu_engine* e, const uint8_t* d_nhwc, int64_t B,
     if (!mean || !stdv) throw ClipErr(CLIPGPU_ERR_INVALID, "NULL mean/std");
     Replica& r = e->reps[0];
     HIP_CHECK(hipSetDevice(r.device));
-    vision_forward(*e, r, d_nhwc, A_IMG_U8, mean, stdv, (int)B, d_out, stream ? (hipStream_t)stream : r.stream);
+    vision_forward_lanes(*e, r, d_nhwc, A_IMG_U8, mean, stdv, (int)B, d_out, stream ? (hipStream_t)stream : r.stream);
   });
 }
 
@@ -625,7 +790,14 @@ int clipgpu_embed_tokens_device(clipgpu_engine* e, const int64_t* d_ids, int64_t
     if (B > e->max_batch) throw ClipErr(CLIPGPU_ERR_INVALID, "B exceeds max_batch");
     Replica& r = e->reps[0];
     HIP_CHECK(hipSetDevice(r.device));
-    text_forward(*e, r, d_ids, (int)B, d_out, stream ? (hipStream_t)stream : r.stream);
+    text_forward_lanes(*e, r, d_ids, (int)B, d_out, stream ? (hipStream_t)stream : r.stream);
+  });
+}
+
+int clipgpu_test_engine_tiles(const clipgpu_engine* e, int tiles[4]) {
+  return guarded([&]() {
+    if (!e || !tiles) throw ClipErr(CLIPGPU_ERR_INVALID, "NULL argument");
+    for (int i = 0; i < 4; ++i) tiles[i] = e->tile[i];
   });
 }
 

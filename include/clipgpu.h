@@ -130,7 +130,9 @@ int64_t clipgpu_tokenizer_vocab_size(const clipgpu_tokenizer* t);
  * Records HIP events around every launch whose category bit is set in `mask` (on the launch
  * stream), for the device-resident entry points.  Categories: 0 patch_embed, 1 stem_ln, 2 qkv,
  * 3 attention, 4 out_proj, 5 layernorm, 6 c_fc, 7 c_proj, 8 head.  enable() resets totals;
- * read() waits for the recorded events and returns the summed ms and launch count. */
+ * read() waits for the recorded events and returns the summed ms and launch count.  While a
+ * mask is set, a batch's concurrent sub-batch lanes run one after another on the launch
+ * stream (same launches, no overlap), so each event pair times one kernel alone. */
 int clipgpu_profile_enable(clipgpu_engine* e, unsigned mask);
 int clipgpu_profile_read(clipgpu_engine* e, int category, double* total_ms, int64_t* launches);
 const char* clipgpu_profile_category_name(int category);

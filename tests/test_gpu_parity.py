@@ -5,6 +5,8 @@ Tolerance (north_star): cosine(GPU, oracle) >= 0.9999 per embedding row, and the
 GPU rows are unit-norm to 1e-5.  Weights are the seeded synthetic set (identical
 bits on both sides, tests/test_cpu_host.py::test_synth_matches_oracle).
 """
+from ctypes import c_int
+
 import numpy as np
 import pytest
 
@@ -150,3 +152,54 @@ def test_native_library_is_loaded():
     assert "libclipgpu.so" in maps
     hip = set(re.findall(r"\S*libamdhip64\S*", maps))
     assert len(hip) == 1, hip
+
+
+@pytest.mark.parametrize("tower", [0, 1])
+def test_gemm_tile_choice_is_bit_exact(tower, monkeypatch):
+    """Every GEMM tile computes the same K-ordered sums: the creation-time autotune
+    changes speed, never the embeddings."""
+    from open_clip_inference import _lib
+    v, t = specs(VIT_B_32_CFG)
+    if tower == 0:
+        data = normalized_pixels(weights.synth_images_u8(31, 48, v.image_size), OPENAI_MEAN, OPENAI_STD)
+    else:
+        data = weights.synth_token_ids(31, 48, t.context_length, t.vocab_size, t.vocab_size - 2,
+                                       t.vocab_size - 1, random_eot=True)
+    outs = []
+    for tiles in ["1,1,1,1", "2,2,2,2", "3,3,3,3", None]:
+        if tiles:
+            monkeypatch.setenv("CLIPGPU_GEMM_TILES", tiles)
+        else:
+            monkeypatch.delenv("CLIPGPU_GEMM_TILES", raising=False)
+        e = engine(VIT_B_32_CFG, tower, max_batch=48)
+        got = (c_int * 4)()
+        _lib.check(_lib.lib().clipgpu_test_engine_tiles(e._h, got))
+        if tiles:
+            assert list(got) == [int(x) for x in tiles.split(",")]
+        else:
+            assert all(x in (1, 2, 3) for x in got)
+        outs.append(e.embed_pixels(data) if tower == 0 else e.embed_tokens(data))
+    for o in outs[1:]:
+        assert np.array_equal(o, outs[0])
+
+
+@pytest.mark.parametrize("tower", [0, 1])
+def test_concurrent_lanes_are_bit_exact(tower, monkeypatch):
+    """Splitting a batch over concurrent lanes (sub-batches on their own streams)
+    is invisible in the output: rows never interact outside attention."""
+    v, t = specs(VIT_B_32_CFG)
+    if tower == 0:
+        data = normalized_pixels(weights.synth_images_u8(41, 37, v.image_size), OPENAI_MEAN, OPENAI_STD)
+    else:
+        data = weights.synth_token_ids(41, 37, t.context_length, t.vocab_size, t.vocab_size - 2,
+                                       t.vocab_size - 1, random_eot=True)
+    monkeypatch.setenv("CLIPGPU_GEMM_TILES", "1,1,1,1")
+    outs = []
+    for lanes in ["1", "2", "3", "4"]:
+        monkeypatch.setenv("CLIPGPU_LANES", lanes)
+        e = engine(VIT_B_32_CFG, tower, max_batch=37)
+        outs.append(e.embed_pixels(data) if tower == 0 else e.embed_tokens(data))
+    for o in outs[1:]:
+        assert np.array_equal(o, outs[0])
+    ref = oracle_vision(VIT_B_32_CFG, 1234, data[:4]) if tower == 0 else oracle_text(VIT_B_32_CFG, 1234, data[:4])
+    check_rows(outs[-1][:4], ref)

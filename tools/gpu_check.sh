@@ -31,6 +31,16 @@ for s in $STEPS; do
       run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
           python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline || exit $?
       find gpurun_out/prof -name "*kernel_stats.csv" | head -3 ;;
+    pmc)  # HBM bytes of the roofline kernel: FETCH_SIZE and WRITE_SIZE in separate passes,
+          # GEMM tiles pinned to the ones the un-profiled bench autotuned (profiling skews tuning)
+      export CLIPGPU_GEMM_TILES=$(python3 -c "import json;print([json.loads(l) for l in open('gpurun_out/bench.log') if l.startswith('{')][-1]['gemm_tiles_env'])") || exit 1
+      for C in FETCH_SIZE WRITE_SIZE; do
+        run pmc_$C 600 rocprofv3 --pmc $C --output-format csv -d gpurun_out/pmc_bench/$C -o run -- \
+            python3 bench.py --steps 3 --warmup 1 --no-text --no-cpu-baseline || exit $?
+      done
+      python3 tools/pmc_traffic.py gpurun_out/pmc_bench/FETCH_SIZE gpurun_out/pmc_bench/WRITE_SIZE \
+          gpurun_out/pmc_c_fc.json || exit $?
+      unset CLIPGPU_GEMM_TILES ;;
   esac
 done
 echo "=== done"
