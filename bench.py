@@ -180,7 +180,7 @@ def main():
 
     tiles = (ctypes.c_int * 4)()
     _lib.check(_lib.lib().clipgpu_test_engine_tiles(ve._h, tiles))
-    tile_names = {0: "heuristic", 1: "128x128", 2: "256x128", 3: "256x256"}
+    tile_names = {0: "heuristic", 1: "128x128", 2: "256x128", 3: "256x256", 4: "128x128pipe"}
     gemm_tiles = dict(zip(["qkv", "out_proj", "c_fc", "c_proj"], [tile_names[t] for t in tiles]))
 
     dt, _ = timed(vision_step, args.steps, args.warmup)
@@ -240,7 +240,7 @@ def main():
                                    "synthetic 224x224 per GPU, device-resident input",
                        "global_batch": world * B_VISION, "seq_len": 50,
                        "parallelism": f"dp{world}, {os.environ.get('CLIPGPU_LANES', '2')} concurrent sub-batch lanes/GPU" + (" + RCCL all-gather of [B,512] embeddings" if world > 1 else "")},
-            "roofline": {"bound": "mfma", "kernel": f"gemm_bt_kernel c_fc ({int(fc_rows_per_launch)}x3072x768, +QuickGELU)",
+            "roofline": {"bound": "mfma", "kernel": f"c_fc GEMM ({int(fc_rows_per_launch)}x3072x768, +QuickGELU, tile {gemm_tiles['c_fc']})",
                          "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": load_traffic(),
                          "launches_timed": fc_n, "avg_launch_us": round(fc_avg_s * 1e6, 2)},

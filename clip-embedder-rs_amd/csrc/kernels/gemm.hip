@@ -32,6 +32,27 @@
 
 namespace clipgpu {
 
+// Diagnostic build only (make stamps -> lib/libclipgpu_stamps.so): s_memtime
+// stamps of wave 0 of each block at fixed points of the tile loop
+// (tools/gemm_stamps.py).  The product build compiles them out.
+#ifdef CLIPGPU_GEMM_STAMPS
+constexpr int kStampBlocks = 2048, kStampSlots = 64;
+__device__ unsigned long long g_gemm_stamps[kStampBlocks * kStampSlots];
+#define GEMM_STAMP(slot)                                                                        \
+  do {                                                                                          \
+    if (threadIdx.x == 0 && blockIdx.x < kStampBlocks && (slot) < kStampSlots)                   \
+      g_gemm_stamps[blockIdx.x * kStampSlots + (slot)] = __builtin_amdgcn_s_memtime();        \
+  } while (0)
+#define GEMM_STAMP_REAL(slot)                                                                   \
+  do {                                                                                          \
+    if (threadIdx.x == 0 && blockIdx.x < kStampBlocks)                                          \
+      g_gemm_stamps[blockIdx.x * kStampSlots + (slot)] = __builtin_amdgcn_s_memrealtime();    \
+  } while (0)
+#else
+#define GEMM_STAMP(slot) do {} while (0)
+#define GEMM_STAMP_REAL(slot) do {} while (0)
+#endif
+
 namespace {
 
 constexpr int BK = 64;
@@ -353,6 +374,15 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
         float v[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[j] = acc[ni][mi][j] + bv[j];
+#ifdef CLIPGPU_GEMM_STAMPS
+        if (p.diag & 1) {  // timing experiment: same arithmetic, no store
+          float s = 0.f;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) s += EPI == EPI_STORE16 ? (float)to16<T>(apply_act<ACT>(v[j])) : v[j];
+          if (s == 12345.678f) ((float*)p.out)[0] = s;
+          continue;
+        }
+#endif
         if constexpr (EPI == EPI_STORE16) {
           T* o = (T*)p.out + (long)m * p.ldo + n;
           if (nfull) {
@@ -401,6 +431,8 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
   // ---- persistent tile loop: 2-stage K pipeline, next tile's first K-step
   //      prefetched under the current tile's last K-step and epilogue ----------
   int m0, n0;
+  GEMM_STAMP_REAL(62);
+  GEMM_STAMP(0);
   tile_coords(t_first, nTm, nTn, BM, BN, m0, n0);
   set_tile(m0, n0);
   stage(0, sA0, sB0);
@@ -424,7 +456,10 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
 
   int parity = 0;    // buffer holding K-step 0 of the current tile
   int bias_par = 0;  // LDS bias buffer of the current tile
-  for (int t = t_first; t < t_end; t += t_stride) {
+  GEMM_STAMP(1);
+  int ti = 0;  // (stamps) tile index of this block
+  for (int t = t_first; t < t_end; t += t_stride, ++ti) {
+    GEMM_STAMP(2 + ti * 4);
     for (int kt = 0; kt + 1 < nk; ++kt) {
       const bool cur1 = (kt & 1) ^ parity;
       char* const sAn = cur1 ? sA0 : sA1;
@@ -434,7 +469,9 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
       else compute(std::false_type{}, cur1 ? sA1 : sA0, cur1 ? sB1 : sB0);
       if constexpr (ASRC != A_ROWS) store_a_img(sAn);
       step_sync();
+      if (ti == 0) GEMM_STAMP(34 + kt);
     }
+    GEMM_STAMP(3 + ti * 4);
     // last K-step: prefetch the next tile's first K-step under it and the epilogue
     const bool cur1 = ((nk - 1) & 1) ^ parity;
     const int tn = t + t_stride;
@@ -451,6 +488,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
     if constexpr (ASRC != A_ROWS) {
       if (has_next) store_a_img(cur1 ? sA0 : sA1);
     }
+    GEMM_STAMP(4 + ti * 4);
     epilogue(m0, n0, bias_par);
     if constexpr (ASRC == A_ROWS) {
       // Retire the next tile's stage-0 glds but not this tile's output stores
@@ -463,113 +501,56 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
     }
+    GEMM_STAMP(5 + ti * 4);
     parity ^= (nk & 1);
     bias_par ^= 1;
     m0 = nm0;
     n0 = nn0;
   }
-}
-
-int device_cus() {
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    hipDeviceProp_t prop;
-    if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
-      cus = prop.multiProcessorCount;
-    if (cus <= 0) cus = 256;
-  }
-  return cus;
+  GEMM_STAMP_REAL(63);
 }
 
 // ---------------------------------------------------------------------------
-// Ring-pipelined variant for the 256-row tiles (A from rows).  NS = 4 LDS
-// stages of BK = 32 (64-byte rows); the loads of K-step g+3 are issued right
-// after the barrier of step g, so three steps of global_load_lds stay in flight
-// across barriers, retired by a counted s_waitcnt vmcnt(N) (never 0 in steady
-// state; cdna_hip_programming.md §5 "Pipelining across barriers") and a raw
-// s_barrier (a __syncthreads() would drain vmcnt).  The load cursor runs ahead
-// across tile boundaries of the persistent schedule, so the next tile's first
-// K-steps land under the current tile's last steps and epilogue.
+// Software-pipelined GEMM for row-major A (the trunk GEMMs; K >= 128).
+//
+// Each 64-deep K-step g is two MFMA phases (kk0 = k 0..31, kk1 = k 32..63) with
+// ONE barrier between them:
+//   kk0(g): MFMAs on fragments (a0,b0) of g; ds_read the kk1 fragments of g.
+//   wait lgkm; wait the LDS-DMA of step g+1 (vmcnt); s_barrier.
+//   kk1(g): MFMAs on (a1,b1); ds_read the kk0 fragments of g+1 (other buffer,
+//           landed: every wave passed its vmcnt before the barrier) and issue
+//           the LDS-DMA pieces of step g+2 into g's buffer (free: every wave
+//           holds g's fragments in registers before the barrier).
+// No fragment-read latency is exposed after a barrier and each DMA has a whole
+// K-step to land.  With >= 32 MFMAs per phase the DMA pieces are spread between
+// MFMA groups; the 128x128 tile (16 per phase, two blocks per CU) issues them
+// up front so the other block's MFMAs cover the issue cost.  The DMA cursor
+// runs on across the tiles of the persistent schedule.
+//
+// Output layout: the W (MFMA "A") fragment of column block ni, row i reads W
+// row  wn + (i>>2)*4*NI + ni*4 + (i&3)  so lane (fr, fq) owns the 4*NI
+// CONSECUTIVE output columns wn + fq*4*NI .. +4*NI-1 of row fr: 16-byte
+// epilogue stores (half the store instructions of the 8-byte form; the
+// epilogue tail is store-issue-bound).  The W LDS image is XOR-swizzled by
+// sw(r) = (r & 2) | (bit (2 + log2 NI) of r) << 2, conflict-free for these
+// reads and independent of ni, so every fragment offset is an immediate.
+//
+// Configs: 128x128 (4 waves, 64x64 each, 2 blocks/CU), 256x128 (8 waves,
+// 128x32), 256x256 (8 waves, 128x64).  (A 4-wave 256x256 with 128x128 per wave
+// needs 256 accumulator AGPRs plus > 256 VGPRs and spills: not built.)
 // ---------------------------------------------------------------------------
-
-// Byte offset of 16-byte chunk c (0..3) of row r in a [rows][32] 16-bit tile.
-// XOR with g[(r>>2)&3], g = {0,2,3,1}: conflict-free 16x16x32 fragment reads
-// (each ds_read_b128 lane group hits 16 distinct 16-byte slots).
-__device__ __forceinline__ int ring_swz(int r) { return (0xB4 >> (((r >> 2) & 3) * 2)) & 3; }
-
-template <typename T, int MI, int NI, int EPI, int ACT>
-__device__ __forceinline__ void epilogue_store(const GemmParams& p, f32x4 (&acc)[NI][MI], int m0, int n0, int wm,
-                                               int wn, int fr, int fq) {
-  typedef typename Vec4<T>::type V4;
-#pragma unroll
-  for (int ni = 0; ni < NI; ++ni) {
-    const int n = n0 + wn + ni * 16 + fq * 4;
-    const bool nfull = n + 4 <= p.N;
-    float bv[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) bv[j] = (p.bias != nullptr && n + j < p.N) ? p.bias[n + j] : 0.f;
-#pragma unroll
-    for (int mi = 0; mi < MI; ++mi) {
-      const int m = m0 + wm + mi * 16 + fr;
-      if (m >= p.M) continue;
-      float v[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) v[j] = acc[ni][mi][j] + bv[j];
-      if constexpr (EPI == EPI_STORE16) {
-        T* o = (T*)p.out + (long)m * p.ldo + n;
-        if (nfull) {
-          V4 w;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) w[j] = to16<T>(apply_act<ACT>(v[j]));
-          *(V4*)o = w;
-        } else {
-          for (int j = 0; j < 4; ++j)
-            if (n + j < p.N) o[j] = to16<T>(apply_act<ACT>(v[j]));
-        }
-      } else {
-        float* o = (float*)p.out + (long)m * p.ldo + n;
-        if (nfull) {
-          float4 w = make_float4(v[0], v[1], v[2], v[3]);
-          if constexpr (EPI == EPI_RESID) {
-            const float4 x = *(const float4*)o;
-            w.x += x.x; w.y += x.y; w.z += x.z; w.w += x.w;
-          }
-          *(float4*)o = w;
-        } else {
-          for (int j = 0; j < 4; ++j) {
-            if (n + j >= p.N) continue;
-            float r = v[j];
-            if constexpr (EPI == EPI_RESID) r += o[j];
-            o[j] = r;
-          }
-        }
-      }
-    }
-  }
-}
-
-template <typename T, int BM, int BN, int EPI, int ACT>
-__global__ __launch_bounds__(512, 2) void gemm_ring_kernel(GemmParams p) {
+template <typename T, int BM, int BN, int WGM, int WGN, int EPI, int ACT>
+__global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_pipe_kernel(GemmParams p) {
   typedef typename Vec8<T>::type V8;
-  constexpr int WGM = 2, WGN = 4, NW = 8;
-  constexpr int BKS = 32, NS = 4;
-  constexpr int A_BYTES = BM * BKS * 2, B_BYTES = BN * BKS * 2, STAGE = A_BYTES + B_BYTES;
-  constexpr int A_INSTR = BM / 16 / NW, B_INSTR = BN / 16 / NW;  // 1 KiB = 16 rows of 64 B
-  constexpr int LPS = A_INSTR + B_INSTR;                          // vm ops per stage per wave
+  constexpr int NW = WGM * WGN;
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
+  constexpr int A_INSTR = BM / 8 / NW, B_INSTR = BN / 8 / NW, NP = A_INSTR + B_INSTR;
   constexpr int TM = BM / WGM, TN = BN / WGN, MI = TM / 16, NI = TN / 16;
-  constexpr int EPI_OPS = MI * NI;  // >= vm ops of a full tile's epilogue (one 8/16-B store per (mi, ni))
-  static_assert(A_INSTR >= 1 && B_INSTR >= 1, "bad ring tile");
-  static_assert(2 * LPS + EPI_OPS <= 63, "vmcnt field");
-  // Fragment reads are inline-asm ds_read_b128: hipcc cannot tell that the DMA
-  // into stage (k+3)%4 does not alias the reads of stage k and would otherwise
-  // drain vmcnt(0) in front of every compiler-visible ds_read (measured in the
-  // .s), which collapses the ring.  Our counted waits + barrier order them.
-  __shared__ __attribute__((aligned(16))) char smem[NS * STAGE];
-  char* const st0 = smem;
-  char* const st1 = smem + STAGE;
-  char* const st2 = smem + 2 * STAGE;
-  char* const st3 = smem + 3 * STAGE;
+  constexpr int LG = NI == 2 ? 1 : NI == 4 ? 2 : 3;
+  constexpr bool SPREAD = MI * NI >= 32;
+  static_assert(A_INSTR >= 1 && B_INSTR >= 1 && MI >= 1 && BN <= 256, "bad tile");
+  static_assert(NI == 2 || NI == 4 || NI == 8, "column permutation needs NI in {2,4,8}");
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + 2048];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -577,7 +558,7 @@ __global__ __launch_bounds__(512, 2) void gemm_ring_kernel(GemmParams p) {
   const int nTn = (p.N + BN - 1) / BN;
   const int nTm = (p.M + BM - 1) / BM;
   const int ntiles = nTn * nTm;
-  const int nks = p.K / BKS;  // multiple of NS (host checks K % 128 == 0)
+  const int nk = p.K / BK;
 
   const int nb = gridDim.x;
   int t_first, t_stride, t_end;
@@ -594,114 +575,279 @@ __global__ __launch_bounds__(512, 2) void gemm_ring_kernel(GemmParams p) {
     t_end = t_first + 1;
   }
   if (t_first >= t_end) return;
-  const int my_tiles = (t_end - t_first + t_stride - 1) / t_stride;
-  const int G = my_tiles * nks;  // K-steps this block computes
+  const int total = ((t_end - t_first + t_stride - 1) / t_stride) * nk;  // this block's K-steps
 
-  // ---- load cursor (runs 3 K-steps ahead of the compute cursor) ----------------
-  const T* const Wb = (const T*)p.W;
-  const T* const Ab = (const T*)p.A;
-  int woff[B_INSTR], aoff[A_INSTR];
+  auto swW = [](int r) { return (r & 2) | (((r >> (2 + LG)) & 1) << 2); };
+
+  // ---- LDS-DMA cursor (global step d_g = tile d_ti, K-step d_kt) -----------
+  uint32_t woff[B_INSTR];
+  uint32_t aoff[A_INSTR];
+  const char* const Wb = (const char*)p.W;
+  const char* const Ab = (const char*)p.A;
   auto set_tile = [&](int m0, int n0) {
 #pragma unroll
     for (int i = 0; i < B_INSTR; ++i) {
-      const int r = (wave * B_INSTR + i) * 16 + (lane >> 2);
-      woff[i] = min(n0 + r, p.N - 1) * (int)p.ldw + (((lane & 3) ^ ring_swz(r)) << 3);
+      const int r = (wave * B_INSTR + i) * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ swW(r);
+      woff[i] = (uint32_t)(min(n0 + r, p.N - 1) * (int)p.ldw + c * 8) * 2u;
     }
 #pragma unroll
     for (int i = 0; i < A_INSTR; ++i) {
-      const int r = (wave * A_INSTR + i) * 16 + (lane >> 2);
-      aoff[i] = min(m0 + r, p.M - 1) * (int)p.lda + (((lane & 3) ^ ring_swz(r)) << 3);
+      const int r = (wave * A_INSTR + i) * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ ((r >> 1) & 7);
+      aoff[i] = (uint32_t)(min(m0 + r, p.M - 1) * (int)p.lda + c * 8) * 2u;
     }
   };
-  int lt = t_first, ls = 0, lg = 0;
+  int d_g = 0, d_kt = 0, d_t = t_first, d_n0 = 0, d_ti = 0;
   {
     int m0, n0;
-    tile_coords(lt, nTm, nTn, BM, BN, m0, n0);
+    tile_coords(d_t, nTm, nTn, BM, BN, m0, n0);
     set_tile(m0, n0);
+    d_n0 = n0;
   }
-  // stage K-step lg (if any) into ring stage `st` (== lg % NS by construction)
-  auto issue_next = [&](char* st) {
-    if (lg >= G) return;
-#pragma unroll
-    for (int i = 0; i < A_INSTR; ++i) glds16(Ab + (aoff[i] + ls * BKS), st + (wave * A_INSTR + i) * 1024);
-#pragma unroll
-    for (int i = 0; i < B_INSTR; ++i)
-      glds16(Wb + (woff[i] + ls * BKS), st + A_BYTES + (wave * B_INSTR + i) * 1024);
-    ++lg;
-    if (++ls == nks) {
-      ls = 0;
-      lt += t_stride;
-      if (lt < t_end) {
+  auto dma_piece = [&](auto jc) {  // W pieces first, then A pieces
+    constexpr int j = decltype(jc)::value;
+    char* const st = smem + (d_g & 1) * STAGE;
+    if constexpr (j < B_INSTR) {
+      glds16(Wb + (size_t)d_kt * (BK * 2) + woff[j], st + A_BYTES + (wave * B_INSTR + j) * 1024);
+    } else {
+      constexpr int i = j - B_INSTR;
+      glds16(Ab + (size_t)d_kt * (BK * 2) + aoff[i], st + (wave * A_INSTR + i) * 1024);
+    }
+  };
+  auto dma_bias = [&]() {  // the tile's bias slice, with its first K-step (tile-parity buffer)
+    if (p.bias != nullptr && wave == 0 && d_kt == 0) {
+      const int n = min(d_n0 + lane * 4, ((p.N - 1) / 4) * 4);
+      glds16(p.bias + n, smem + 2 * STAGE + (d_ti & 1) * 1024);
+    }
+  };
+  auto dma_advance = [&]() {
+    ++d_g;
+    if (++d_kt == nk) {
+      d_kt = 0;
+      d_t += t_stride;
+      ++d_ti;
+      if (d_t < t_end) {
         int m0, n0;
-        tile_coords(lt, nTm, nTn, BM, BN, m0, n0);
+        tile_coords(d_t, nTm, nTn, BM, BN, m0, n0);
         set_tile(m0, n0);
+        d_n0 = n0;
       }
     }
   };
+  auto dma_step = [&]() {
+    if (d_g < total) {
+      static_for<NP>([&](auto j) { dma_piece(j); });
+      dma_bias();
+    }
+    dma_advance();
+  };
 
-  // ---- fragments ------------------------------------------------------------------
+  // ---- fragments -------------------------------------------------------------
   const int wm = (wave / WGN) * TM, wn = (wave % WGN) * TN;
   const int fr = lane & 15, fq = lane >> 4;
-  const int sw = (fq ^ ring_swz(fr)) << 4;
-  const int offA = (wm + fr) * 64 + sw;
-  const int offB = A_BYTES + (wn + fr) * 64 + sw;
-
-  f32x4 acc[NI][MI];
+  const int rowB = wn + (fr >> 2) * (4 * NI) + (fr & 3);  // + 4*ni
+  uint32_t offA[2], offB[2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    offA[kk] = (uint32_t)((wm + fr) * 128 + (((kk * 4 + fq) ^ (fr >> 1)) << 4));
+    offB[kk] = (uint32_t)(A_BYTES + rowB * 128 + (((kk * 4 + fq) ^ swW(rowB)) << 4));
+  }
   const uint32_t lds0 = lds_addr(smem);
-  auto compute = [&](const char* st) {
-    const uint32_t a_base = lds0 + (uint32_t)(st - smem) + offA;
-    const uint32_t b_base = lds0 + (uint32_t)(st - smem) + offB;
-    V8 a[MI], b[NI];
-    static_for<NI>([&](auto ni) { ds_read_b128<(int)ni * 1024>(b[ni], b_base); });
-    static_for<MI>([&](auto mi) { ds_read_b128<(int)mi * 1024>(a[mi], a_base); });
-    lgkm_wait_all(a, b);
+  f32x4 acc[NI][MI];
+  V8 a0[MI], b0[NI], a1[MI], b1[NI];
+
+  auto read_b = [&](V8(&b)[NI], uint32_t base) {
+    static_for<NI>([&](auto ni) { ds_read_b128<(int)ni * 512>(b[ni], base); });
+  };
+  auto read_a = [&](V8(&a)[MI], uint32_t base) {
+    static_for<MI>([&](auto mi) { ds_read_b128<(int)mi * 2048>(a[mi], base); });
+  };
+  auto phase0 = [&](auto zero, uint32_t buf) {
+    read_b(b1, buf + offB[1]);
+    static_for<MI>([&](auto mi) {
 #pragma unroll
-    for (int ni = 0; ni < NI; ++ni)
+      for (int ni = 0; ni < NI; ++ni)
+        acc[ni][mi] = mfma_16x16x32(b0[ni], a0[mi], decltype(zero)::value ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[ni][mi]);
+      __builtin_amdgcn_sched_barrier(0);
+      ds_read_b128<(int)mi * 2048>(a1[mi], buf + offA[1]);
+    });
+    lgkm_wait_all(a1, b1);
+  };
+  auto phase1 = [&](bool next, uint32_t nbuf) {
+    const bool dma = d_g < total;
+    if (next) read_b(b0, nbuf + offB[0]);
+    if (dma) {
+      dma_bias();
+      if constexpr (!SPREAD) static_for<NP>([&](auto j) { dma_piece(j); });
+    }
+    static_for<MI>([&](auto mi) {
 #pragma unroll
-      for (int mi = 0; mi < MI; ++mi) acc[ni][mi] = mfma_16x16x32(b[ni], a[mi], acc[ni][mi]);
+      for (int ni = 0; ni < NI; ++ni) acc[ni][mi] = mfma_16x16x32(b1[ni], a1[mi], acc[ni][mi]);
+      __builtin_amdgcn_sched_barrier(0);
+      if (next) ds_read_b128<(int)mi * 2048>(a0[mi], nbuf + offA[0]);
+      if constexpr (SPREAD) {
+        static_for<NP>([&](auto j) {
+          if constexpr (((int)j * MI) / NP == (int)mi) {
+            if (dma) dma_piece(j);
+          }
+        });
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    dma_advance();
+    if (next) lgkm_wait_all(a0, b0);
   };
 
-  issue_next(st0);
-  issue_next(st1);
-  issue_next(st2);
+  // ---- epilogue: lane owns row wm+mi*16+fr, columns nc .. nc+4*NI-1 ------------
+  auto epilogue = [&](int m0, int n0, int bpar) {
+    const int nc = n0 + wn + fq * (4 * NI);
+    const bool nfull = nc + 4 * NI <= p.N;
+    f32x4 bias[NI];
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni) bias[ni] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (p.bias != nullptr) {
+      const uint32_t ba = lds0 + 2 * STAGE + bpar * 1024 + (wn + fq * (4 * NI)) * 4;
+      static_for<NI>([&](auto ni) { ds_read_b128<(int)ni * 16>(bias[ni], ba); });
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni) asm volatile("" : "+v"(bias[ni]));
+    }
+    float4 xr[2][NI];
+    auto load_x = [&](int mi, float4(&dst)[NI]) {
+      const int m = m0 + wm + mi * 16 + fr;
+      if (m < p.M && nfull) {
+        const float* src = (const float*)p.out + (long)m * p.ldo + nc;
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni) dst[ni] = *(const float4*)(src + ni * 4);
+      }
+    };
+    if constexpr (EPI == EPI_RESID) load_x(0, xr[0]);
+#pragma unroll
+    for (int mi = 0; mi < MI; ++mi) {
+      if constexpr (EPI == EPI_RESID) {
+        if (mi + 1 < MI) load_x(mi + 1, xr[(mi + 1) & 1]);
+      }
+      const int m = m0 + wm + mi * 16 + fr;
+      if (m >= p.M) continue;
+      float v[NI][4];
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[ni][j] = acc[ni][mi][j] + bias[ni][j];
+#ifdef CLIPGPU_GEMM_STAMPS
+      if (p.diag & 1) {
+        float s = 0.f;
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) s += EPI == EPI_STORE16 ? (float)to16<T>(apply_act<ACT>(v[ni][j])) : v[ni][j];
+        if (s == 12345.678f) ((float*)p.out)[0] = s;
+        continue;
+      }
+#endif
+      if constexpr (EPI == EPI_STORE16) {
+        T* o = (T*)p.out + (long)m * p.ldo + nc;
+        if (nfull) {
+#pragma unroll
+          for (int h = 0; h < NI / 2; ++h) {
+            V8 w;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) w[e] = to16<T>(apply_act<ACT>(v[2 * h + e / 4][e % 4]));
+            *(V8*)(o + h * 8) = w;
+          }
+        } else {
+#pragma unroll
+          for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if (nc + ni * 4 + j < p.N) o[ni * 4 + j] = to16<T>(apply_act<ACT>(v[ni][j]));
+        }
+      } else {
+        float* o = (float*)p.out + (long)m * p.ldo + nc;
+        if (nfull) {
+#pragma unroll
+          for (int ni = 0; ni < NI; ++ni) {
+            float4 w = make_float4(v[ni][0], v[ni][1], v[ni][2], v[ni][3]);
+            if constexpr (EPI == EPI_RESID) {
+              const float4 x = xr[mi & 1][ni];
+              w.x += x.x; w.y += x.y; w.z += x.z; w.w += x.w;
+            }
+            *(float4*)(o + ni * 4) = w;
+          }
+        } else {
+#pragma unroll
+          for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              if (nc + ni * 4 + j >= p.N) continue;
+              float r = v[ni][j];
+              if constexpr (EPI == EPI_RESID) r += o[ni * 4 + j];
+              o[ni * 4 + j] = r;
+            }
+        }
+      }
+    }
+  };
+  // vm ops a full tile's epilogue leaves in flight behind the DMA of the step after it
+  constexpr int EPI_VM = EPI == EPI_STORE16 ? MI * NI / 2 : (EPI == EPI_RESID ? 2 * MI * NI : MI * NI);
+
+  // ---- prologue: steps 0 and 1 in flight, step 0 landed, its kk0 fragments read
+  GEMM_STAMP_REAL(62);
+  GEMM_STAMP(0);
+  dma_step();
+  vm_wait<0>();
+  __builtin_amdgcn_s_barrier();
+  dma_step();
+  read_b(b0, lds0 + offB[0]);
+  read_a(a0, lds0 + offA[0]);
+  lgkm_wait_all(a0, b0);
+  GEMM_STAMP(1);
 
   int g = 0;
-  bool prev_full = false;
-  for (int t = t_first; t < t_end; t += t_stride) {
+  bool after_full_epi = false;
+  int ti = 0;
+  for (int t = t_first; t < t_end; t += t_stride, ++ti) {
     int m0, n0;
     tile_coords(t, nTm, nTn, BM, BN, m0, n0);
-#pragma unroll
-    for (int ni = 0; ni < NI; ++ni)
-#pragma unroll
-      for (int mi = 0; mi < MI; ++mi) acc[ni][mi] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // Step g: retire its loads (younger vm ops = steps g+1, g+2 if issued and, at a
-    // tile's first step, the previous tile's epilogue stores), barrier, issue step
-    // g+3 into the stage every wave finished reading at step g-1, compute.
-    auto step = [&](const char* cur, char* refill, bool first) {
-      const int ahead = (g + 2 < G) ? 2 : (g + 1 < G ? 1 : 0);
-      if (first && prev_full) {
-        if (ahead == 2) vm_wait<2 * LPS + EPI_OPS>();
-        else if (ahead == 1) vm_wait<LPS + EPI_OPS>();
-        else vm_wait<EPI_OPS>();
-      } else {
-        if (ahead == 2) vm_wait<2 * LPS>();
-        else if (ahead == 1) vm_wait<LPS>();
-        else vm_wait<0>();
-      }
+    GEMM_STAMP(2 + ti * 4);
+    for (int kt = 0; kt < nk; ++kt, ++g) {
+      if (kt + 1 == nk) GEMM_STAMP(3 + ti * 4);
+      const uint32_t buf = lds0 + (g & 1) * STAGE;
+      if (kt == 0) phase0(std::true_type{}, buf);
+      else phase0(std::false_type{}, buf);
+      if (after_full_epi) vm_wait<(EPI_VM < 63 ? EPI_VM : 63)>();
+      else vm_wait<0>();
+      after_full_epi = false;
       __builtin_amdgcn_s_barrier();
-      issue_next(refill);
-      compute(cur);
-      ++g;
-    };
-    for (int s = 0; s < nks; s += NS) {
-      step(st0, st3, s == 0);
-      step(st1, st0, false);
-      step(st2, st1, false);
-      step(st3, st2, false);
+      phase1(kt + 1 < nk, lds0 + ((g + 1) & 1) * STAGE);
+      if (ti == 0 && kt + 1 < nk) GEMM_STAMP(34 + kt);
     }
-    epilogue_store<T, MI, NI, EPI, ACT>(p, acc, m0, n0, wm, wn, fr, fq);
-    prev_full = (m0 + BM <= p.M) && (n0 + BN <= p.N);
+    GEMM_STAMP(4 + ti * 4);
+    epilogue(m0, n0, ti & 1);
+    after_full_epi = m0 + BM <= p.M && n0 + BN <= p.N;  // partial tiles may issue fewer vm ops
+    if (!after_full_epi) vm_wait<0>();
+    if (t + t_stride < t_end) {  // the next tile's step 0 landed at the last barrier
+      const uint32_t buf = lds0 + (g & 1) * STAGE;
+      read_b(b0, buf + offB[0]);
+      read_a(a0, buf + offA[0]);
+      lgkm_wait_all(a0, b0);
+    }
+    GEMM_STAMP(5 + ti * 4);
   }
+  GEMM_STAMP_REAL(63);
+}
+
+int device_cus() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    hipDeviceProp_t prop;
+    if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
+      cus = prop.multiProcessorCount;
+    if (cus <= 0) cus = 256;
+  }
+  return cus;
 }
 
 template <typename T, int BM, int BN, int WGM, int WGN, int ASRC, int EPI, int ACT>
@@ -716,13 +862,13 @@ hipError_t launch_cfg(const GemmParams& p, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <typename T, int BM, int BN, int EPI, int ACT>
-hipError_t launch_ring(const GemmParams& p, hipStream_t s) {
+template <typename T, int BM, int BN, int WGM, int WGN, int EPI, int ACT>
+hipError_t launch_pipe(const GemmParams& p, hipStream_t s) {
   const int nTn = (p.N + BN - 1) / BN, nTm = (p.M + BM - 1) / BM;
   const int ntiles = nTn * nTm;
-  const int resident = device_cus();
+  const int resident = device_cus() * (BM * BN == 128 * 128 ? 2 : 1);
   const int grid = ntiles <= resident ? ntiles : resident;
-  hipLaunchKernelGGL((gemm_ring_kernel<T, BM, BN, EPI, ACT>), dim3(grid), dim3(512), 0, s, p);
+  hipLaunchKernelGGL((gemm_pipe_kernel<T, BM, BN, WGM, WGN, EPI, ACT>), dim3(grid), dim3(WGM * WGN * 64), 0, s, p);
   return hipGetLastError();
 }
 
@@ -732,13 +878,17 @@ hipError_t launch_tile(const GemmParams& p, hipStream_t s) {
     return launch_cfg<T, 128, 128, 2, 2, ASRC, EPI, ACT>(p, s);  // register-staged A: spill-free tile
   } else {
     const int tile = p.tile == TILE_AUTO ? pick_gemm_tile(p.M, p.N, p.K) : p.tile;
-    switch (tile) {
-      case TILE_256x256: return launch_cfg<T, 256, 256, 2, 4, ASRC, EPI, ACT>(p, s);
-      case TILE_256x128: return launch_cfg<T, 256, 128, 2, 4, ASRC, EPI, ACT>(p, s);
-      case TILE_RING_256x256: return launch_ring<T, 256, 256, EPI, ACT>(p, s);
-      case TILE_RING_256x128: return launch_ring<T, 256, 128, EPI, ACT>(p, s);
-      default: return launch_cfg<T, 128, 128, 2, 2, ASRC, EPI, ACT>(p, s);
+    // software-pipelined kernel: K >= 128, 16-byte-aligned 16-bit output rows (diag bit 1: legacy, stamp builds)
+    const bool pipe = p.K >= 2 * BK && !(p.diag & 2) && (EPI != EPI_STORE16 || p.ldo % 8 == 0);
+    if (pipe) {
+      switch (tile) {
+        case TILE_256x256: return launch_pipe<T, 256, 256, 2, 4, EPI, ACT>(p, s);
+        case TILE_256x128: return launch_pipe<T, 256, 128, 2, 4, EPI, ACT>(p, s);
+        case TILE_128x128_PIPE: return launch_pipe<T, 128, 128, 2, 2, EPI, ACT>(p, s);
+        default: break;
+      }
     }
+    return launch_cfg<T, 128, 128, 2, 2, ASRC, EPI, ACT>(p, s);
   }
 }
 
@@ -789,11 +939,20 @@ hipError_t launch_gemm(DType dt, int asrc, int epi, int act, const GemmParams& p
   if (p.bias != nullptr && p.N % 4 != 0) return hipErrorInvalidValue;  // 16-byte bias DMA
   // 32-bit staging offsets
   if ((long)p.M * p.lda * 2 >= (1L << 31) || (long)p.N * p.ldw * 2 >= (1L << 31)) return hipErrorInvalidValue;
-  if ((p.tile == TILE_RING_256x256 || p.tile == TILE_RING_256x128) && asrc == A_ROWS && p.K % 128 != 0)
-    return hipErrorInvalidValue;  // (image-sourced A always runs the 128x128 register-staged tile)
   if (asrc != A_ROWS && (p.P % 8 != 0)) return hipErrorInvalidValue;
   return dt == DT_BF16 ? launch_typed<__bf16>(asrc, epi, act, p, s)
                        : launch_typed<_Float16>(asrc, epi, act, p, s);
 }
+
+#ifdef CLIPGPU_GEMM_STAMPS
+hipError_t read_gemm_stamps(unsigned long long* host, int nblocks, bool clear) {
+  const size_t n = (size_t)std::min(nblocks, kStampBlocks) * kStampSlots * sizeof(unsigned long long);
+  if (clear) {
+    static unsigned long long zeros[kStampBlocks * kStampSlots];
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_gemm_stamps), zeros, sizeof(zeros));
+  }
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_gemm_stamps), n);
+}
+#endif
 
 }  // namespace clipgpu

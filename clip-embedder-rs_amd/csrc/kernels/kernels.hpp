@@ -34,16 +34,16 @@ struct GemmParams {
   float mean[3], stdv[3];
   const float* pos;          // EPI_PATCH positional embedding [G^2+1][N]
   int tile;                  // GemmTile (0 = pick by shape)
+  int diag;                  // stamp build only: bit 0 = skip epilogue stores (timing experiments)
 };
 
 // Tile configurations of the MFMA GEMM.
 enum GemmTile {
   TILE_AUTO = 0,
-  TILE_128x128 = 1,  // 4 waves, 64 KiB LDS, 2 blocks / CU (small M)
-  TILE_256x128 = 2,  // 8 waves, 96 KiB LDS
-  TILE_256x256 = 3,  // 8 waves, 128 KiB LDS
-  TILE_RING_256x256 = 4,  // 8 waves, 4-stage BK=32 ring, counted vmcnt, 128 KiB LDS
-  TILE_RING_256x128 = 5,  // 8 waves, 4-stage BK=32 ring, 96 KiB LDS
+  TILE_128x128 = 1,       // gemm_bt_kernel: 4 waves, 64 KiB LDS, 2 blocks / CU
+  TILE_256x128 = 2,       // gemm_pipe_kernel: 8 waves, 96 KiB LDS
+  TILE_256x256 = 3,       // gemm_pipe_kernel: 8 waves, 128 KiB LDS
+  TILE_128x128_PIPE = 4,  // gemm_pipe_kernel: 4 waves, 64 KiB LDS, 2 blocks / CU
 };
 int pick_gemm_tile(int M, int N, int K);
 
@@ -80,5 +80,10 @@ hipError_t launch_l2norm(const float* in, float* out, int B, int E, hipStream_t 
 
 // f32 -> T16 conversion (weight upload).
 hipError_t launch_cast_f32(DType dt, const float* in, void* out, long n, hipStream_t s);
+
+#ifdef CLIPGPU_GEMM_STAMPS
+// Diagnostic build: copy (or clear) the per-block s_memtime stamps of the last GEMM launch.
+hipError_t read_gemm_stamps(unsigned long long* host, int nblocks, bool clear);
+#endif
 
 }  // namespace clipgpu

@@ -193,4 +193,31 @@ int clipgpu_test_gemm_bench(int dtype, int epi, int act, int64_t M, int64_t N, i
   });
 }
 
+#ifdef CLIPGPU_GEMM_STAMPS
+// Diagnostic build only (not in the headers): one timed-after-warmup GEMM launch
+// with s_memtime stamps; out receives nblocks x 64 u64 (see gemm.hip slots).
+int clipgpu_diag_gemm_stamps(int dtype, int epi, int act, int64_t M, int64_t N, int64_t K, int tile,
+                             unsigned long long* out, int nblocks, int diag) {
+  return guarded([&]() {
+    const DType dt = dt_of(dtype);
+    DevBuf fA(M * K * 4), fW(N * K * 4), dA(M * K * 2), dW(N * K * 2), dB(N * 4), dO(M * N * 4);
+    hipLaunchKernelGGL(fill_random, dim3(2048), dim3(256), 0, nullptr, fA.as<float>(), (long)(M * K), 1u);
+    hipLaunchKernelGGL(fill_random, dim3(2048), dim3(256), 0, nullptr, fW.as<float>(), (long)(N * K), 2u);
+    hipLaunchKernelGGL(fill_random, dim3(64), dim3(256), 0, nullptr, dB.as<float>(), (long)N, 3u);
+    TCHECK(launch_cast_f32(dt, fA.as<float>(), dA.p, (long)(M * K), nullptr));
+    TCHECK(launch_cast_f32(dt, fW.as<float>(), dW.p, (long)(N * K), nullptr));
+    GemmParams g{};
+    g.A = dA.p; g.lda = K; g.W = dW.p; g.ldw = K; g.bias = dB.as<float>();
+    g.out = dO.p; g.ldo = N; g.M = (int)M; g.N = (int)N; g.K = (int)K; g.tile = tile; g.diag = diag;
+    const int e = epi == 1 ? EPI_RESID : (epi == 2 ? EPI_STORE32 : EPI_STORE16);
+    for (int i = 0; i < 20; ++i) TCHECK(launch_gemm(dt, A_ROWS, e, epi == 0 ? act : 0, g, nullptr));
+    TCHECK(hipDeviceSynchronize());
+    TCHECK(read_gemm_stamps(nullptr, nblocks, true));
+    TCHECK(launch_gemm(dt, A_ROWS, e, epi == 0 ? act : 0, g, nullptr));
+    TCHECK(hipDeviceSynchronize());
+    TCHECK(read_gemm_stamps(out, nblocks, false));
+  });
+}
+#endif
+
 }  // extern "C"

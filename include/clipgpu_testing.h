@@ -36,12 +36,12 @@ int clipgpu_test_patch_embed(int dtype, int mode, int64_t B, int64_t S, int64_t 
 
 /* Device-resident GEMM timing (random operands): `iters` back-to-back launches of the same
  * GEMM as the engine issues it (epi: 0 store16 (+act), 1 residual f32, 2 store32), tile:
- * 0 auto, 1 128x128, 2 256x128, 3 256x256.  Returns the mean µs per launch (HIP events). */
+ * 0 auto, 1 128x128, 2 256x128, 3 256x256, 4 128x128 pipelined.  Returns the mean µs per launch (HIP events). */
 int clipgpu_test_gemm_bench(int dtype, int epi, int act, int64_t M, int64_t N, int64_t K, int tile, int iters,
                             double* us_per_launch);
 
 /* GEMM tile chosen per trunk call site of an engine (0 qkv, 1 out_proj, 2 c_fc, 3 c_proj):
- * 1 128x128, 2 256x128, 3 256x256, 0 shape heuristic.  Before clipgpu_create, set
+ * 1 128x128, 2 256x128, 3 256x256, 4 128x128 pipelined, 0 shape heuristic.  Before clipgpu_create, set
  * CLIPGPU_GEMM_AUTOTUNE=0 to skip the creation-time tuning, or CLIPGPU_GEMM_TILES="q,o,f,p"
  * to pin the four sites. */
 struct clipgpu_engine;
