@@ -657,21 +657,8 @@ int clipgpu_create(const char* model_dir, int tower, const int* device_ids, int 
     }
     // weights
     TensorMap m;
-    const std::string st_path = dir + "/open_clip_model.safetensors";
-    const std::string syn_path = dir + "/clipgpu_synthetic.json";
     try {
-      if (file_exists(st_path)) {
-        m = load_safetensors(st_path, s);
-      } else if (file_exists(syn_path)) {
-        json::ValuePtr j = json::parse_file(syn_path);
-        const json::Value* sd = j->get("seed");
-        if (!sd) throw std::runtime_error("Configuration error: clipgpu_synthetic.json has no seed");
-        m = synth_weights(s, (uint64_t)sd->as_num(0));
-      } else {
-        throw ClipErr(CLIPGPU_ERR_CONFIG, "Missing model file 'open_clip_model.safetensors' in folder '" + dir + "'");
-      }
-    } catch (const ClipErr&) {
-      throw;
+      m = load_tower_weights(dir, s);
     } catch (const std::runtime_error& ex) {
       throw ClipErr(CLIPGPU_ERR_CONFIG, ex.what());
     }
@@ -791,6 +778,25 @@ int clipgpu_embed_tokens_device(clipgpu_engine* e, const int64_t* d_ids, int64_t
     Replica& r = e->reps[0];
     HIP_CHECK(hipSetDevice(r.device));
     text_forward_lanes(*e, r, d_ids, (int)B, d_out, stream ? (hipStream_t)stream : r.stream);
+  });
+}
+
+int clipgpu_test_read_weights(const char* model_dir, int tower, const char* name, float* out, int64_t n) {
+  return guarded([&]() {
+    if (!model_dir || !name || !out) throw ClipErr(CLIPGPU_ERR_INVALID, "NULL argument");
+    if (tower != CLIPGPU_TOWER_VISION && tower != CLIPGPU_TOWER_TEXT) throw ClipErr(CLIPGPU_ERR_INVALID, "bad tower");
+    const std::string dir(model_dir);
+    TensorMap m;
+    try {
+      const OpenClipConfig oc = load_open_clip_config(dir + "/open_clip_config.json");
+      m = load_tower_weights(dir, tower == CLIPGPU_TOWER_VISION ? oc.vision : oc.text);
+    } catch (const std::runtime_error& ex) {
+      throw ClipErr(CLIPGPU_ERR_CONFIG, ex.what());
+    }
+    auto it = m.find(name);
+    if (it == m.end()) throw ClipErr(CLIPGPU_ERR_INVALID, std::string("no parameter ") + name);
+    if (it->second.numel() != n) throw ClipErr(CLIPGPU_ERR_INVALID, "size mismatch for " + std::string(name));
+    std::memcpy(out, it->second.data.data(), (size_t)n * sizeof(float));
   });
 }
 

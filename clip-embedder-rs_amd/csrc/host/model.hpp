@@ -82,4 +82,12 @@ TensorMap synth_weights(const TowerSpec& spec, uint64_t seed);
 // open_clip_model.safetensors (F32 / F16 / BF16) -> f32 host tensors of one tower.
 TensorMap load_safetensors(const std::string& path, const TowerSpec& spec);
 
+// visual.onnx / text.onnx initializers (+ external .onnx.data), the reference's model
+// folder layout (src/model_manager.rs:8-18) -> f32 host tensors of one tower.
+TensorMap load_onnx(const std::string& path, const TowerSpec& spec);
+
+// The weight source of a model folder, in order: open_clip_model.safetensors,
+// visual.onnx / text.onnx, clipgpu_synthetic.json {"seed": N}.  Throws runtime_error.
+TensorMap load_tower_weights(const std::string& dir, const TowerSpec& spec);
+
 }  // namespace clipgpu

@@ -109,7 +109,7 @@ TensorMap synth_weights(const TowerSpec& spec, uint64_t seed) {
   return m;
 }
 
-static float half_to_float(uint16_t h) {
+float half_to_float(uint16_t h) {
   const uint32_t sign = (uint32_t)(h & 0x8000) << 16;
   uint32_t exp = (h >> 10) & 0x1F, man = h & 0x3FF;
   uint32_t bits;
@@ -193,6 +193,26 @@ TensorMap load_safetensors(const std::string& path, const TowerSpec& spec) {
   }
   munmap(map, size);
   return out;
+}
+
+static bool is_file(const std::string& p) {
+  struct stat st;
+  return ::stat(p.c_str(), &st) == 0 && S_ISREG(st.st_mode);
+}
+
+TensorMap load_tower_weights(const std::string& dir, const TowerSpec& spec) {
+  const std::string st_path = dir + "/open_clip_model.safetensors";
+  const std::string onnx_name = spec.tower == TOWER_VISION ? "visual.onnx" : "text.onnx";
+  const std::string syn_path = dir + "/clipgpu_synthetic.json";
+  if (is_file(st_path)) return load_safetensors(st_path, spec);
+  if (is_file(dir + "/" + onnx_name)) return load_onnx(dir + "/" + onnx_name, spec);  // pull_onnx.py export
+  if (is_file(syn_path)) {
+    json::ValuePtr j = json::parse_file(syn_path);
+    const json::Value* sd = j->get("seed");
+    if (!sd) throw std::runtime_error("Configuration error: clipgpu_synthetic.json has no seed");
+    return synth_weights(spec, (uint64_t)sd->as_num(0));
+  }
+  throw std::runtime_error("Missing model file '" + onnx_name + "' in folder '" + dir + "'");
 }
 
 }  // namespace clipgpu

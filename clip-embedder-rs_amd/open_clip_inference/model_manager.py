@@ -2,10 +2,11 @@
 
 The reference requires the nine files of ``MODEL_FILES`` (src/model_manager.rs:8-18)
 because ONNX Runtime executes ``visual.onnx`` / ``text.onnx``.  The clipgpu engine
-reads the same configs and tokenizer, and takes its weights from
-``open_clip_model.safetensors`` (or a seeded ``clipgpu_synthetic.json``); ONNX
-initializer ingestion is the next scope row.  HF download
-(``get_hf_model``) is out of scope: no network.
+reads the same configs and tokenizer and takes its weights from, in order,
+``open_clip_model.safetensors``, the initializers of ``visual.onnx`` / ``text.onnx``
+(+ ``.onnx.data``; csrc/host/onnx.cpp) -- so a folder made by pull_onnx.py works as
+is -- or a seeded ``clipgpu_synthetic.json``.  HF download (``get_hf_model``) is out
+of scope: no network.
 """
 from __future__ import annotations
 
@@ -27,7 +28,7 @@ MODEL_FILES = [
 ]
 
 CONFIG_FILES = ["model_config.json", "open_clip_config.json"]
-WEIGHT_SOURCES = ["open_clip_model.safetensors", "clipgpu_synthetic.json"]
+WEIGHT_SOURCES = ["open_clip_model.safetensors", "visual.onnx", "text.onnx", "clipgpu_synthetic.json"]
 
 
 def get_default_base_folder() -> str:  # src/model_manager.rs:43-49
@@ -46,4 +47,4 @@ def verify_model_dir(model_dir: str, need_tokenizer: bool = False) -> None:  # s
         if not os.path.isfile(os.path.join(model_dir, f)):
             raise MissingModelFile(f"Missing model file '{f}' in folder '{model_dir}'")
     if not any(os.path.isfile(os.path.join(model_dir, w)) for w in WEIGHT_SOURCES):
-        raise MissingModelFile(f"Missing model file '{WEIGHT_SOURCES[0]}' in folder '{model_dir}'")
+        raise MissingModelFile(f"Missing model file 'visual.onnx' in folder '{model_dir}'")

@@ -52,8 +52,11 @@ int clipgpu_abi_version(void);
 /* ---- engine lifecycle ----------------------------------------------------------------
  * Replaces OnnxSession::new (src/onnx.rs:13-30) as called by VisionEmbedder::from_local_dir
  * (src/vision.rs:58-84) / TextEmbedder::from_local_dir (src/text.rs:54-101).
- * model_dir must hold open_clip_config.json and model_config.json plus a weight source:
- * open_clip_model.safetensors, or clipgpu_synthetic.json {"seed": N} (seeded weights).
+ * model_dir must hold open_clip_config.json and model_config.json plus a weight source, in
+ * this order of preference: open_clip_model.safetensors; the reference's own export
+ * visual.onnx / text.onnx (+ .onnx.data external data, pull_onnx.py:170-195; initializers by
+ * open_clip name, with or without the "model." wrapper prefix); or clipgpu_synthetic.json
+ * {"seed": N} (seeded weights).
  * device_ids/n_devices: the GPUs this handle replicates the weights onto (data-parallel
  * batch sharding across them); NULL/0 = device 0.  max_batch: rows per device per launch
  * (larger batches are processed in chunks). */

@@ -40,6 +40,11 @@ int clipgpu_test_patch_embed(int dtype, int mode, int64_t B, int64_t S, int64_t 
 int clipgpu_test_gemm_bench(int dtype, int epi, int act, int64_t M, int64_t N, int64_t K, int tile, int iters,
                             double* us_per_launch);
 
+/* Host only (no GPU): the f32 parameter `name` (open_clip state-dict name) of one tower as
+ * clipgpu_create would load it from model_dir (safetensors / visual|text.onnx / synthetic);
+ * n = element count. */
+int clipgpu_test_read_weights(const char* model_dir, int tower, const char* name, float* out, int64_t n);
+
 /* GEMM tile chosen per trunk call site of an engine (0 qkv, 1 out_proj, 2 c_fc, 3 c_proj):
  * 1 128x128, 2 256x128, 3 256x256, 4 128x128 pipelined, 0 shape heuristic.  Before clipgpu_create, set
  * CLIPGPU_GEMM_AUTOTUNE=0 to skip the creation-time tuning, or CLIPGPU_GEMM_TILES="q,o,f,p"

@@ -68,7 +68,7 @@ def test_create_errors_without_gpu(tmp_path):
         Engine(str(tmp_path), 0)
     d = make_model_dir(TINY_CFG)
     os.remove(os.path.join(d, "clipgpu_synthetic.json"))
-    with pytest.raises(MissingModelFile, match="safetensors"):
+    with pytest.raises(MissingModelFile, match="visual.onnx"):
         Engine(d, 0)
     bad = json.loads(json.dumps(TINY_CFG))
     bad["model_cfg"]["vision_cfg"]["timm_model_name"] = "vit_so400m"

@@ -204,3 +204,33 @@ def test_concurrent_lanes_are_bit_exact(tower, monkeypatch):
         assert np.array_equal(o, outs[0])
     ref = oracle_vision(VIT_B_32_CFG, 1234, data[:4]) if tower == 0 else oracle_text(VIT_B_32_CFG, 1234, data[:4])
     check_rows(outs[-1][:4], ref)
+
+
+@pytest.mark.parametrize("external", [False, True])
+def test_onnx_model_folder_matches_seeded_weights(tmp_path, external):
+    """A model folder in the reference's own format (visual.onnx / text.onnx from a
+    torch.onnx.export with pull_onnx.py's arguments) embeds bit-identically to the same
+    weights given as seeds."""
+    import json
+    from open_clip_inference.engine import Engine
+    from oracle.model_spec import OPENAI_MODEL_CONFIG
+    from tests.onnx_export import export_model_dir
+    d = tmp_path / "onnx"
+    d.mkdir()
+    with open(d / "open_clip_config.json", "w") as f:
+        json.dump(TINY_CFG, f)
+    with open(d / "model_config.json", "w") as f:
+        json.dump(OPENAI_MODEL_CONFIG, f)
+    v, t = specs(TINY_CFG)
+    export_model_dir(str(d), v, t, seed=1234, external=external)
+    px = normalized_pixels(weights.synth_images_u8(8, 5, v.image_size), OPENAI_MEAN, OPENAI_STD)
+    ids = weights.synth_token_ids(8, 5, t.context_length, t.vocab_size, t.vocab_size - 2, t.vocab_size - 1,
+                                  random_eot=True)
+    for tower, data in ((0, px), (1, ids)):
+        a = Engine(str(d), tower, [0], "bf16", 16)
+        b = engine(TINY_CFG, tower, seed=1234, max_batch=16)
+        ea = a.embed_pixels(data) if tower == 0 else a.embed_tokens(data)
+        eb = b.embed_pixels(data) if tower == 0 else b.embed_tokens(data)
+        assert np.array_equal(ea, eb)
+        ref = oracle_vision(TINY_CFG, 1234, data) if tower == 0 else oracle_text(TINY_CFG, 1234, data)
+        check_rows(ea, ref)
