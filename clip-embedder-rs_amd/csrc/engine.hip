@@ -125,6 +125,13 @@ namespace clipgpu {
 namespace {
 
 inline size_t align256(size_t n) { return (n + 255) & ~size_t(255); }
+inline int round64(int n) { return (n + 63) / 64 * 64; }
+// GEMM K / N dims are multiples of 64: the MLP hidden width and the patch-embedding
+// K = 3*P*P are zero-padded (exact: padded c_fc rows / bias are 0 and act(0) = 0 for
+// every supported activation; padded conv columns multiply zero-filled pixels).
+inline int mlp_pad(const TowerSpec& s) { return round64(s.mlp_width); }
+inline int kpatch(const TowerSpec& s) { return 3 * s.patch_size * s.patch_size; }
+inline int kpatch_pad(const TowerSpec& s) { return round64(kpatch(s)); }
 
 bool file_exists(const std::string& p) {
   struct stat st;
@@ -153,6 +160,10 @@ struct Bump {
 size_t weight_bytes(const TowerSpec& s, const TensorMap& m) {
   size_t total = 0;
   for (const ParamDesc& p : tower_params(s)) total += align256((size_t)need(m, p.name).numel() * 4);
+  // zero padding of the MLP hidden width and of the patch K (16-bit matrices + f32 bias)
+  const size_t mpad = (size_t)(mlp_pad(s) - s.mlp_width);
+  total += (size_t)s.layers * (mpad * s.width * 4 + mpad * 4 + 1024);
+  if (s.tower == TOWER_VISION) total += (size_t)(kpatch_pad(s) - kpatch(s)) * s.width * 2 + 256;
   return total + 4096;
 }
 
@@ -176,6 +187,14 @@ void upload_weights(clipgpu_engine& e, Replica& r, const TensorMap& m) {
   for (const ParamDesc& p : tower_params(s)) max16 = std::max(max16, (size_t)need(m, p.name).numel());
   float* staging = nullptr;
   HIP_CHECK(hipMalloc(&staging, max16 * 4));
+  std::vector<float*> extra_staging;
+  auto staging_pad = [&](size_t n) {  // a padded matrix may exceed max16
+    if (n <= max16) return staging;
+    float* p = nullptr;
+    HIP_CHECK(hipMalloc(&p, n * 4));
+    extra_staging.push_back(p);
+    return p;
+  };
   auto f32 = [&](const std::string& k) {
     const HostTensor& t = need(m, k);
     float* p = (float*)a.take(t.data.size() * 4);
@@ -186,6 +205,30 @@ void upload_weights(clipgpu_engine& e, Replica& r, const TensorMap& m) {
     const HostTensor& t = need(m, k);
     void* p = a.take(t.data.size() * 2);
     upload_16(e.dt, t.data.data(), t.data.size(), p, staging, r.stream);
+    return p;
+  };
+  // [R][C] -> zero-padded [Rp][Cp] (16-bit)
+  auto w16_pad = [&](const std::string& k, int64_t Rp, int64_t Cp) {
+    const HostTensor& t = need(m, k);
+    const int64_t R = t.shape[0], C = t.numel() / t.shape[0];
+    if (Rp == R && Cp == C) {
+      void* p = a.take(t.data.size() * 2);
+      upload_16(e.dt, t.data.data(), t.data.size(), p, staging, r.stream);
+      return p;
+    }
+    std::vector<float> pad((size_t)(Rp * Cp), 0.f);
+    for (int64_t i = 0; i < R; ++i)
+      std::memcpy(&pad[(size_t)(i * Cp)], &t.data[(size_t)(i * C)], (size_t)C * 4);
+    void* p = a.take(pad.size() * 2);
+    upload_16(e.dt, pad.data(), pad.size(), p, staging_pad(pad.size()), r.stream);
+    return p;
+  };
+  auto f32_pad = [&](const std::string& k, int64_t n) {
+    const HostTensor& t = need(m, k);
+    std::vector<float> pad((size_t)n, 0.f);
+    std::memcpy(pad.data(), t.data.data(), t.data.size() * 4);
+    float* p = (float*)a.take(pad.size() * 4);
+    HIP_CHECK(hipMemcpy(p, pad.data(), pad.size() * 4, hipMemcpyHostToDevice));
     return p;
   };
   auto w16_transposed = [&](const std::string& k) {  // [D][E] -> [E][D]
@@ -201,7 +244,7 @@ void upload_weights(clipgpu_engine& e, Replica& r, const TensorMap& m) {
   DevWeights& w = r.w;
   std::string pre;
   if (s.tower == TOWER_VISION) {
-    w.conv_w = w16("visual.conv1.weight");
+    w.conv_w = w16_pad("visual.conv1.weight", D, kpatch_pad(s));
     w.cls = f32("visual.class_embedding");
     w.pos = f32("visual.positional_embedding");
     w.lnpre_w = f32("visual.ln_pre.weight");
@@ -223,9 +266,9 @@ void upload_weights(clipgpu_engine& e, Replica& r, const TensorMap& m) {
     L.bo = f32(p + "attn.out_proj.bias");
     L.ln2_w = f32(p + "ln_2.weight");
     L.ln2_b = f32(p + "ln_2.bias");
-    L.w1 = w16(p + "mlp.c_fc.weight");
-    L.b1 = f32(p + "mlp.c_fc.bias");
-    L.w2 = w16(p + "mlp.c_proj.weight");
+    L.w1 = w16_pad(p + "mlp.c_fc.weight", mlp_pad(s), D);
+    L.b1 = f32_pad(p + "mlp.c_fc.bias", mlp_pad(s));
+    L.w2 = w16_pad(p + "mlp.c_proj.weight", D, mlp_pad(s));
     L.b2 = f32(p + "mlp.c_proj.bias");
     w.layers.push_back(L);
   }
@@ -241,12 +284,13 @@ void upload_weights(clipgpu_engine& e, Replica& r, const TensorMap& m) {
   (void)D;
   (void)E;
   HIP_CHECK(hipFree(staging));
+  for (float* p : extra_staging) HIP_CHECK(hipFree(p));
 }
 
 void alloc_workspace(clipgpu_engine& e, Replica& r) {
   const TowerSpec& s = e.spec;
   const size_t B = (size_t)e.max_batch, rows = B * (size_t)s.tokens(), D = s.width;
-  const size_t wide = std::max((size_t)3 * D, (size_t)s.mlp_width);
+  const size_t wide = std::max((size_t)3 * D, (size_t)mlp_pad(s));
   const size_t E = s.embed_dim;
   const size_t sizes[] = {rows * D * 4, rows * D * 2, rows * wide * 2, B * D * 2, B * E * 4, B * E * 4,
                           B * e.in_bytes_per_row};
@@ -320,7 +364,7 @@ GemmParams rows_gemm(const void* A, long lda, const void* W, const float* bias, 
 int site_epi(int site) { return (site == GS_OUT || site == GS_PROJ) ? EPI_RESID : EPI_STORE16; }
 
 GemmParams site_gemm(const clipgpu_engine& e, const Replica& r, const LayerW& L, int site, int rows) {
-  const int D = e.spec.width, MLP = e.spec.mlp_width;
+  const int D = e.spec.width, MLP = mlp_pad(e.spec);
   switch (site) {
     case GS_QKV: return rows_gemm(r.h, D, L.wqkv, L.bqkv, r.big, 3 * D, rows, 3 * D, D);
     case GS_OUT: return rows_gemm(r.h, D, L.wo, L.bo, r.x, D, rows, D, D);
@@ -427,13 +471,14 @@ void vision_forward(const clipgpu_engine& e, const Replica& r, const void* pixel
   const int D = s.width, G = s.grid(), P = s.patch_size;
   GemmParams g{};
   g.W = r.w.conv_w;
-  g.ldw = 3 * P * P;
+  g.ldw = kpatch_pad(s);
   g.bias = nullptr;  // OpenAI-style conv1 has no bias
   g.out = r.x;
   g.ldo = D;
   g.M = B * G * G;
   g.N = D;
-  g.K = 3 * P * P;
+  g.K = kpatch_pad(s);
+  g.Kv = kpatch(s);
   g.img = pixels;
   g.S = s.image_size;
   g.P = P;
@@ -473,7 +518,7 @@ void text_forward(const clipgpu_engine& e, const Replica& r, const int64_t* d_id
 Replica lane_view(const clipgpu_engine& e, const Replica& r, int b0) {
   const TowerSpec& s = e.spec;
   const size_t rows = (size_t)b0 * s.tokens(), D = s.width;
-  const size_t wide = std::max((size_t)3 * D, (size_t)s.mlp_width);
+  const size_t wide = std::max((size_t)3 * D, (size_t)mlp_pad(s));
   Replica v = r;
   v.x = r.x + rows * D;
   v.h = (char*)r.h + rows * D * 2;
@@ -643,14 +688,16 @@ int clipgpu_create(const char* model_dir, int tower, const int* device_ids, int 
     if (const char* ln = getenv("CLIPGPU_LANES")) e->lanes = std::max(1, std::min(4, atoi(ln)));
     else e->lanes = 2;
     const TowerSpec& s = e->spec;
-    if (s.width % 64 || s.width / s.heads != 64)
-      throw ClipErr(CLIPGPU_ERR_CONFIG, "Configuration error: head_dim must be 64 and width a multiple of 64");
-    if (s.mlp_width % 64) throw ClipErr(CLIPGPU_ERR_CONFIG, "Configuration error: mlp width must be a multiple of 64");
+    if (s.heads <= 0 || s.width % s.heads || s.width % 64)
+      throw ClipErr(CLIPGPU_ERR_CONFIG, "Configuration error: width must be a multiple of 64 and of heads");
+    const int hd = s.width / s.heads;
+    if (hd != 64 && hd != 72 && hd != 80)
+      throw ClipErr(CLIPGPU_ERR_CONFIG, "Configuration error: head dim " + std::to_string(hd) + " not supported (64, 72, 80)");
     if (s.width > 1280) throw ClipErr(CLIPGPU_ERR_CONFIG, "Configuration error: width > 1280 not supported yet");
-    if (s.tokens() > 256) throw ClipErr(CLIPGPU_ERR_CONFIG, "Configuration error: > 256 tokens not supported yet");
+    if (s.tokens() > 1024) throw ClipErr(CLIPGPU_ERR_CONFIG, "Configuration error: > 1024 tokens not supported yet");
     if (s.tower == TOWER_VISION) {
-      if (s.patch_size % 8 || (3 * s.patch_size * s.patch_size) % 64 || s.image_size % s.patch_size)
-        throw ClipErr(CLIPGPU_ERR_CONFIG, "Configuration error: unsupported patch geometry");
+      if (s.image_size % s.patch_size)
+        throw ClipErr(CLIPGPU_ERR_CONFIG, "Configuration error: image_size must be a multiple of patch_size");
       e->in_bytes_per_row = (size_t)3 * s.image_size * s.image_size * 4;  // f32 (u8 path uses a quarter)
     } else {
       e->in_bytes_per_row = (size_t)s.context_length * 8;

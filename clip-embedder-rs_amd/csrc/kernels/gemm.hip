@@ -219,27 +219,49 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
   float areg[A_CHUNKS][8];
   auto load_a_img = [&](int kt) {
     const int PP = p.P * p.P;
+    const int Kv = p.Kv > 0 ? p.Kv : p.K;
 #pragma unroll
     for (int i = 0; i < A_CHUNKS; ++i) {
       const int c = (tid + NT * i) & 7;
       const int k = kt * BK + c * 8;
-      const int ch = k / PP, rem = k - ch * PP;
-      const int ky = rem / p.P, kx = rem - ky * p.P;
-      if constexpr (ASRC == A_IMG_F32) {
-        const float* src = (const float*)p.img + img_base[i] + ((long)ch * p.S + ky) * p.S + kx;
-        const float4 v0 = *(const float4*)src;
-        const float4 v1 = *(const float4*)(src + 4);
-        areg[i][0] = v0.x; areg[i][1] = v0.y; areg[i][2] = v0.z; areg[i][3] = v0.w;
-        areg[i][4] = v1.x; areg[i][5] = v1.y; areg[i][6] = v1.z; areg[i][7] = v1.w;
-      } else {
-        const uint8_t* src = (const uint8_t*)p.img + img_base[i] + ((long)ky * p.S + kx) * 3 + ch;
-        const float mu = p.mean[0] * (ch == 0) + p.mean[1] * (ch == 1) + p.mean[2] * (ch == 2);
-        const float sd = p.stdv[0] * (ch == 0) + p.stdv[1] * (ch == 1) + p.stdv[2] * (ch == 2);
+      if (p.P % 8 == 0 && k + 8 <= Kv) {  // 8 consecutive k = 8 pixels of one image row
+        const int ch = k / PP, rem = k - ch * PP;
+        const int ky = rem / p.P, kx = rem - ky * p.P;
+        if constexpr (ASRC == A_IMG_F32) {
+          const float* src = (const float*)p.img + img_base[i] + ((long)ch * p.S + ky) * p.S + kx;
+          const float4 v0 = *(const float4*)src;
+          const float4 v1 = *(const float4*)(src + 4);
+          areg[i][0] = v0.x; areg[i][1] = v0.y; areg[i][2] = v0.z; areg[i][3] = v0.w;
+          areg[i][4] = v1.x; areg[i][5] = v1.y; areg[i][6] = v1.z; areg[i][7] = v1.w;
+        } else {
+          const uint8_t* src = (const uint8_t*)p.img + img_base[i] + ((long)ky * p.S + kx) * 3 + ch;
+          const float mu = p.mean[0] * (ch == 0) + p.mean[1] * (ch == 1) + p.mean[2] * (ch == 2);
+          const float sd = p.stdv[0] * (ch == 0) + p.stdv[1] * (ch == 1) + p.stdv[2] * (ch == 2);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            // src/vision.rs:254-255: (p / 255 - mean[c]) / std[c]
+            const float val = (float)src[e * 3] / 255.0f;
+            areg[i][e] = (val - mu) / sd;
+          }
+        }
+      } else {  // patch rows not a multiple of 8 (P = 14) or the zero-padded K tail
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          // src/vision.rs:254-255: (p / 255 - mean[c]) / std[c]
-          const float val = (float)src[e * 3] / 255.0f;
-          areg[i][e] = (val - mu) / sd;
+          const int kk = k + e;
+          float val = 0.f;
+          if (kk < Kv) {
+            const int ch = kk / PP, rem = kk - ch * PP;
+            const int ky = rem / p.P, kx = rem - ky * p.P;
+            if constexpr (ASRC == A_IMG_F32) {
+              val = ((const float*)p.img)[img_base[i] + ((long)ch * p.S + ky) * p.S + kx];
+            } else {
+              const float mu = p.mean[0] * (ch == 0) + p.mean[1] * (ch == 1) + p.mean[2] * (ch == 2);
+              const float sd = p.stdv[0] * (ch == 0) + p.stdv[1] * (ch == 1) + p.stdv[2] * (ch == 2);
+              const float u = (float)((const uint8_t*)p.img)[img_base[i] + ((long)ky * p.S + kx) * 3 + ch] / 255.0f;
+              val = (u - mu) / sd;
+            }
+          }
+          areg[i][e] = val;
         }
       }
     }
@@ -939,7 +961,7 @@ hipError_t launch_gemm(DType dt, int asrc, int epi, int act, const GemmParams& p
   if (p.bias != nullptr && p.N % 4 != 0) return hipErrorInvalidValue;  // 16-byte bias DMA
   // 32-bit staging offsets
   if ((long)p.M * p.lda * 2 >= (1L << 31) || (long)p.N * p.ldw * 2 >= (1L << 31)) return hipErrorInvalidValue;
-  if (asrc != A_ROWS && (p.P % 8 != 0)) return hipErrorInvalidValue;
+  if (asrc != A_ROWS && (p.Kv > p.K || p.Kv < 0)) return hipErrorInvalidValue;
   return dt == DT_BF16 ? launch_typed<__bf16>(asrc, epi, act, p, s)
                        : launch_typed<_Float16>(asrc, epi, act, p, s);
 }

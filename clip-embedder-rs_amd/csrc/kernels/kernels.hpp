@@ -31,6 +31,7 @@ struct GemmParams {
   int M, N, K;
   // image sources (A_IMG_*)
   const void* img; int S, P, G;
+  int Kv;                    // image sources: valid K = 3*P*P (K is padded to a multiple of 64; k >= Kv reads 0)
   float mean[3], stdv[3];
   const float* pos;          // EPI_PATCH positional embedding [G^2+1][N]
   int tile;                  // GemmTile (0 = pick by shape)

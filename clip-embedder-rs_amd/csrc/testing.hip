@@ -99,10 +99,11 @@ int clipgpu_test_gemm(int dtype, int mode, int act, int64_t M, int64_t N, int64_
   });
 }
 
-int clipgpu_test_attention(int dtype, int64_t B, int64_t N, int64_t H, int causal, const float* qkv, float* out) {
+int clipgpu_test_attention(int dtype, int64_t B, int64_t N, int64_t H, int64_t HD, int causal, const float* qkv,
+                           float* out) {
   return guarded([&]() {
     const DType dt = dt_of(dtype);
-    const int64_t D = H * 64;
+    const int64_t D = H * HD;
     DevBuf dq(B * N * 3 * D * 2), dO(B * N * D * 2);
     up16(dt, dq.p, qkv, B * N * 3 * D);
     TCHECK(launch_attention(dt, dq.p, dO.p, (int)B, (int)N, (int)H, (int)D, causal, nullptr));
@@ -130,14 +131,18 @@ int clipgpu_test_patch_embed(int dtype, int mode, int64_t B, int64_t S, int64_t 
                              float* x_out) {
   return guarded([&]() {
     const DType dt = dt_of(dtype);
-    const int64_t G = S / P, K = 3 * P * P, tokens = G * G + 1;
+    const int64_t G = S / P, K = 3 * P * P, Kp = (K + 63) / 64 * 64, tokens = G * G + 1;
     const size_t pix_bytes = mode == 0 ? (size_t)B * 3 * S * S * 4 : (size_t)B * S * S * 3;
-    DevBuf dpix(pix_bytes), dw(D * K * 2), dpos(tokens * D * 4), dx(B * tokens * D * 4);
+    DevBuf dpix(pix_bytes), dw(D * Kp * 2), dpos(tokens * D * 4), dx(B * tokens * D * 4);
     up(dpix.p, pixels, pix_bytes);
-    up16(dt, dw.p, conv_w, D * K);
+    std::vector<float> wpad((size_t)(D * Kp), 0.f);  // conv weight zero-padded to K % 64 == 0 (as the engine does)
+    for (int64_t r = 0; r < D; ++r)
+      for (int64_t k = 0; k < K; ++k) wpad[(size_t)(r * Kp + k)] = conv_w[r * K + k];
+    up16(dt, dw.p, wpad.data(), D * Kp);
     up(dpos.p, pos, tokens * D * 4);
     GemmParams g{};
-    g.W = dw.p; g.ldw = K; g.out = dx.p; g.ldo = D; g.M = (int)(B * G * G); g.N = (int)D; g.K = (int)K;
+    g.W = dw.p; g.ldw = Kp; g.out = dx.p; g.ldo = D; g.M = (int)(B * G * G); g.N = (int)D; g.K = (int)Kp;
+    g.Kv = (int)K;
     g.img = dpix.p; g.S = (int)S; g.P = (int)P; g.G = (int)G; g.pos = dpos.as<float>();
     g.tile = tile_override();
     for (int c = 0; c < 3; ++c) {

@@ -49,7 +49,7 @@ _PROTOS = [
     ("clipgpu_synth_tensor", c_int, [c_uint64, c_char_p, c_double, c_double, c_void_p, c_int64]),
     # include/clipgpu_testing.h
     ("clipgpu_test_gemm", c_int, [c_int, c_int, c_int, c_int64, c_int64, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
-    ("clipgpu_test_attention", c_int, [c_int, c_int64, c_int64, c_int64, c_int, c_void_p, c_void_p]),
+    ("clipgpu_test_attention", c_int, [c_int, c_int64, c_int64, c_int64, c_int64, c_int, c_void_p, c_void_p]),
     ("clipgpu_test_layernorm", c_int, [c_int, c_int64, c_int64, c_float, c_void_p, c_void_p, c_void_p, c_void_p]),
     ("clipgpu_test_gemm_bench", c_int, [c_int, c_int, c_int, c_int64, c_int64, c_int64, c_int, c_int, POINTER(c_double)]),
     ("clipgpu_test_engine_tiles", c_int, [c_void_p, POINTER(c_int)]),

@@ -21,8 +21,9 @@ extern "C" {
 int clipgpu_test_gemm(int dtype, int mode, int act, int64_t M, int64_t N, int64_t K, const float* A,
                       const float* W, const float* bias, const float* resid, float* out);
 
-/* qkv: [B*N][3*D] f32 (rounded to 16-bit on upload); out: [B*N][D]. */
-int clipgpu_test_attention(int dtype, int64_t B, int64_t N, int64_t H, int causal, const float* qkv, float* out);
+/* qkv: [B*N][3*D] f32 (rounded to 16-bit on upload), D = H * HD (HD in {64, 72, 80}); out: [B*N][D]. */
+int clipgpu_test_attention(int dtype, int64_t B, int64_t N, int64_t H, int64_t HD, int causal, const float* qkv,
+                           float* out);
 
 /* out[r] = LN(x[r]) (16-bit output returned as f32). */
 int clipgpu_test_layernorm(int dtype, int64_t rows, int64_t D, float eps, const float* x, const float* w,

@@ -139,6 +139,36 @@ TINY_CFG = {
     "preprocess_cfg": {"mean": OPENAI_MEAN, "std": OPENAI_STD},
 }
 
+# DFN5B-CLIP-ViT-H-14-378 (BASELINE.json configs[4]; open_clip hf-hub:apple/DFN5B-CLIP-ViT-H-14-378):
+# patch 14 (K = 588), head_width 80, nn.GELU (no quick_gelu), 730 vision tokens.
+VIT_H_14_378_CFG = {
+    "model_cfg": {
+        "embed_dim": 1024,
+        "vision_cfg": {"image_size": 378, "layers": 32, "width": 1280, "head_width": 80, "patch_size": 14},
+        "text_cfg": {"context_length": 77, "vocab_size": 49408, "width": 1024, "heads": 16, "layers": 24},
+    },
+    "preprocess_cfg": {"mean": OPENAI_MEAN, "std": OPENAI_STD},
+}
+
+# ViT-H-structured small configs: patch 14, head dim 80, erf GELU; the long one has
+# 17 x 17 + 1 = 290 tokens (tiled attention, partial tiles).
+TINY_H14_CFG = {
+    "model_cfg": {
+        "embed_dim": 64,
+        "vision_cfg": {"image_size": 70, "layers": 2, "width": 320, "head_width": 80, "patch_size": 14},
+        "text_cfg": {"context_length": 16, "vocab_size": 1000, "width": 128, "heads": 2, "layers": 2},
+    },
+    "preprocess_cfg": {"mean": OPENAI_MEAN, "std": OPENAI_STD},
+}
+LONG_H14_CFG = {
+    "model_cfg": {
+        "embed_dim": 64,
+        "vision_cfg": {"image_size": 238, "layers": 2, "width": 320, "head_width": 80, "patch_size": 14},
+        "text_cfg": {"context_length": 16, "vocab_size": 1000, "width": 128, "heads": 2, "layers": 2},
+    },
+    "preprocess_cfg": {"mean": OPENAI_MEAN, "std": OPENAI_STD},
+}
+
 # model_config.json as written by pull_onnx.py:128-150 for an OpenAI CLIP.
 OPENAI_MODEL_CONFIG = {
     "logit_scale": 100.0,

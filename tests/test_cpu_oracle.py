@@ -33,10 +33,13 @@ def test_oracle_matches_golden_and_hf(name, cfg, B):
     assert clip_ref.cosine_rows(g[f"{name}_text_oracle"], g[f"{name}_text_hf"]).min() > 1 - 1e-9
 
 
-def test_oracle_vs_hf_live_tiny():
+@pytest.mark.parametrize("cfg_name", ["TINY_CFG", "TINY_H14_CFG", "LONG_H14_CFG"])
+def test_oracle_vs_hf_live_tiny(cfg_name):
+    """Also the ViT-H/14 structure (patch 14, head dim 80, erf GELU, 290 tokens)."""
     pytest.importorskip("transformers")
-    from oracle import hf_pin
-    v, t = vision_spec_from_cfg(TINY_CFG["model_cfg"]), text_spec_from_cfg(TINY_CFG["model_cfg"])
+    from oracle import hf_pin, model_spec
+    cfg = getattr(model_spec, cfg_name)
+    v, t = vision_spec_from_cfg(cfg["model_cfg"]), text_spec_from_cfg(cfg["model_cfg"])
     P = weights.vision_weights(v, 99)
     px = pixels(v, 2)
     assert np.abs(clip_ref.encode_image(P, v, px) - hf_pin.hf_encode_image(hf_pin.hf_vision(P, v), px)).max() < 1e-7

@@ -118,11 +118,11 @@ def test_gemm_persistent_multi_tile(mode, tile):
         assert np.abs(out - ref).max() < 1e-4
 
 
-def ref_attention(qkv, B, N, H, causal):
-    D = H * 64
-    x = qkv.reshape(B, N, 3, H, 64).astype(np.float64)
+def ref_attention(qkv, B, N, H, causal, HD=64):
+    D = H * HD
+    x = qkv.reshape(B, N, 3, H, HD).astype(np.float64)
     q, k, v = x[:, :, 0].transpose(0, 2, 1, 3), x[:, :, 1].transpose(0, 2, 1, 3), x[:, :, 2].transpose(0, 2, 1, 3)
-    s = q @ k.transpose(0, 1, 3, 2) / 8.0
+    s = q @ k.transpose(0, 1, 3, 2) / np.sqrt(HD)
     if causal:
         s = np.where(np.triu(np.ones((N, N), bool), 1), -np.inf, s)
     o = clip_ref.softmax(s) @ v
@@ -137,9 +137,27 @@ def test_attention(dtype, B, N, H, causal):
     rng = np.random.default_rng(N + H)
     qkv = round16(rng.standard_normal((B * N, 3 * H * 64)) * 1.5, dtype)
     out = np.empty((B * N, H * 64), np.float32)
-    L.check(L.lib().clipgpu_test_attention(dtype, B, N, H, causal, qkv.ctypes.data, out.ctypes.data))
+    L.check(L.lib().clipgpu_test_attention(dtype, B, N, H, 64, causal, qkv.ctypes.data, out.ctypes.data))
     ref = ref_attention(qkv, B, N, H, causal)
     # P and O are rounded to 16 bits: |err| <= ~2 ulp16 of max|v|
+    tol = (2 ** -7 if dtype == BF16 else 2 ** -10) * np.abs(qkv).max()
+    assert np.abs(out - ref).max() < tol
+
+
+@pytest.mark.parametrize("dtype", [BF16, F16])
+@pytest.mark.parametrize("B,N,H,HD,causal", [(2, 300, 2, 64, 0), (2, 300, 2, 64, 1), (2, 577, 2, 72, 0),
+                                             (2, 730, 2, 80, 0), (3, 130, 3, 80, 1), (2, 64, 1, 72, 0),
+                                             (1, 1025, 1, 64, 1)])
+def test_attention_tiled(dtype, B, N, H, HD, causal):
+    """Tiled online-softmax kernel: long sequences (SigLIP2-384 576 tokens, ViT-H/14-378 730) and
+    head dims 72 / 80 (scale 1/sqrt(HD)), partial last key/query tiles, causal masks."""
+    L = _lib()
+    rng = np.random.default_rng(N * 3 + HD + causal)
+    D = H * HD
+    qkv = round16(rng.standard_normal((B * N, 3 * D)), dtype)
+    out = np.empty((B * N, D), np.float32)
+    L.check(L.lib().clipgpu_test_attention(dtype, B, N, H, HD, causal, qkv.ctypes.data, out.ctypes.data))
+    ref = ref_attention(qkv, B, N, H, causal, HD)
     tol = (2 ** -7 if dtype == BF16 else 2 ** -10) * np.abs(qkv).max()
     assert np.abs(out - ref).max() < tol
 
@@ -162,7 +180,7 @@ def test_layernorm(dtype, D):
 
 
 @pytest.mark.parametrize("mode", [0, 1])
-@pytest.mark.parametrize("S,P,D", [(224, 32, 768), (64, 16, 128)])
+@pytest.mark.parametrize("S,P,D", [(224, 32, 768), (64, 16, 128), (70, 14, 160), (378, 14, 1280)])
 def test_patch_embed(mode, S, P, D, tile):
     L = _lib()
     from oracle.model_spec import OPENAI_MEAN, OPENAI_STD

@@ -11,7 +11,8 @@ import numpy as np
 import pytest
 
 from oracle import clip_ref, weights
-from oracle.model_spec import OPENAI_MEAN, OPENAI_STD, TINY_CFG, VIT_B_32_CFG
+from oracle.model_spec import (LONG_H14_CFG, OPENAI_MEAN, OPENAI_STD, TINY_CFG, TINY_H14_CFG, VIT_B_32_CFG,
+                               VIT_H_14_378_CFG)
 from tests.helpers import COS_TOL, make_model_dir, normalized_pixels, specs
 
 pytestmark = pytest.mark.gpu
@@ -234,3 +235,30 @@ def test_onnx_model_folder_matches_seeded_weights(tmp_path, external):
         assert np.array_equal(ea, eb)
         ref = oracle_vision(TINY_CFG, 1234, data) if tower == 0 else oracle_text(TINY_CFG, 1234, data)
         check_rows(ea, ref)
+
+
+@pytest.mark.parametrize("cfg,B", [(TINY_H14_CFG, 3), (LONG_H14_CFG, 2)])
+@pytest.mark.parametrize("dtype", ["bf16", "f16"])
+def test_vit_h14_structure_parity(cfg, B, dtype):
+    """ViT-H/14 structure (BASELINE configs[4]): patch 14 (K = 588 zero-padded to 640,
+    element-wise patch gather), head dim 80, erf GELU, up to 290 tokens (tiled attention)."""
+    v, t = specs(cfg)
+    u8 = weights.synth_images_u8(41 + B, B, v.image_size)
+    e = engine(cfg, 0, dtype=dtype)
+    got = e.embed_pixels(normalized_pixels(u8, OPENAI_MEAN, OPENAI_STD))
+    check_rows(got, oracle_vision(cfg, 1234, normalized_pixels(u8, OPENAI_MEAN, OPENAI_STD)))
+    assert np.array_equal(got, e.embed_u8(u8, OPENAI_MEAN, OPENAI_STD))
+
+
+def test_vit_h14_378_full_dims():
+    """DFN5B-CLIP-ViT-H-14-378 at full size (32 x 1280, 730 tokens; text 24 x 1024) vs the fp64
+    oracle on seeded weights."""
+    v, t = specs(VIT_H_14_378_CFG)
+    u8 = weights.synth_images_u8(3, 2, v.image_size)
+    px = normalized_pixels(u8, OPENAI_MEAN, OPENAI_STD)
+    e = engine(VIT_H_14_378_CFG, 0, max_batch=2)
+    check_rows(e.embed_pixels(px), oracle_vision(VIT_H_14_378_CFG, 1234, px))
+    ids = weights.synth_token_ids(4, 3, t.context_length, t.vocab_size, t.vocab_size - 2, t.vocab_size - 1,
+                                  random_eot=True)
+    te = engine(VIT_H_14_378_CFG, 1, max_batch=3)
+    check_rows(te.embed_tokens(ids), oracle_text(VIT_H_14_378_CFG, 1234, ids))
