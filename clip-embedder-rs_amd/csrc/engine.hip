@@ -46,8 +46,17 @@ struct LayerW {
   void *wqkv, *wo, *w1, *w2;
 };
 
+// MAP attention-pool head of the SigLIP family (timm AttentionPoolLatent).
+struct MapHeadW {
+  float* q = nullptr;                 // [D] f32: latent . Wq^T + bq (the same for every image)
+  void *wkv = nullptr, *wproj = nullptr, *w1 = nullptr, *w2 = nullptr;  // 16-bit [N][K]
+  float *bkv = nullptr, *bproj = nullptr, *norm_w = nullptr, *norm_b = nullptr, *b1 = nullptr, *b2 = nullptr;
+};
+
 struct DevWeights {
-  void* conv_w = nullptr;  // [D][3*P*P] 16-bit
+  void* conv_w = nullptr;  // [D][Kpad] 16-bit (K = 3*P*P zero-padded to a multiple of 64)
+  float* conv_b = nullptr; // SigLIP patch-embedding bias (nullptr for CLIP)
+  MapHeadW map;
   float *cls = nullptr, *pos = nullptr, *lnpre_w = nullptr, *lnpre_b = nullptr;
   float* tok = nullptr;  // text token table [V][D] f32
   std::vector<LayerW> layers;
@@ -164,6 +173,7 @@ size_t weight_bytes(const TowerSpec& s, const TensorMap& m) {
   const size_t mpad = (size_t)(mlp_pad(s) - s.mlp_width);
   total += (size_t)s.layers * (mpad * s.width * 4 + mpad * 4 + 1024);
   if (s.tower == TOWER_VISION) total += (size_t)(kpatch_pad(s) - kpatch(s)) * s.width * 2 + 256;
+  if (s.family == FAMILY_SIGLIP) total += (mpad * s.width * 4 + mpad * 4) + (size_t)s.width * 4 + 4096;
   return total + 4096;
 }
 
@@ -231,6 +241,11 @@ void upload_weights(clipgpu_engine& e, Replica& r, const TensorMap& m) {
     HIP_CHECK(hipMemcpy(p, pad.data(), pad.size() * 4, hipMemcpyHostToDevice));
     return p;
   };
+  auto a_take_f32 = [&](const std::vector<float>& v) {
+    float* p = (float*)a.take(v.size() * 4);
+    HIP_CHECK(hipMemcpy(p, v.data(), v.size() * 4, hipMemcpyHostToDevice));
+    return p;
+  };
   auto w16_transposed = [&](const std::string& k) {  // [D][E] -> [E][D]
     const HostTensor& t = need(m, k);
     const int64_t R = t.shape[0], C = t.shape[1];
@@ -243,7 +258,27 @@ void upload_weights(clipgpu_engine& e, Replica& r, const TensorMap& m) {
   };
   DevWeights& w = r.w;
   std::string pre;
-  if (s.tower == TOWER_VISION) {
+  const bool siglip = s.tower == TOWER_VISION && s.family == FAMILY_SIGLIP;
+  // parameter names of the two families (open_clip CLIP / timm ViT trunk)
+  const char* n_ln1w = siglip ? "norm1.weight" : "ln_1.weight";
+  const char* n_ln1b = siglip ? "norm1.bias" : "ln_1.bias";
+  const char* n_qkvw = siglip ? "attn.qkv.weight" : "attn.in_proj_weight";
+  const char* n_qkvb = siglip ? "attn.qkv.bias" : "attn.in_proj_bias";
+  const char* n_ow = siglip ? "attn.proj.weight" : "attn.out_proj.weight";
+  const char* n_ob = siglip ? "attn.proj.bias" : "attn.out_proj.bias";
+  const char* n_ln2w = siglip ? "norm2.weight" : "ln_2.weight";
+  const char* n_ln2b = siglip ? "norm2.bias" : "ln_2.bias";
+  const char* n_fc1w = siglip ? "mlp.fc1.weight" : "mlp.c_fc.weight";
+  const char* n_fc1b = siglip ? "mlp.fc1.bias" : "mlp.c_fc.bias";
+  const char* n_fc2w = siglip ? "mlp.fc2.weight" : "mlp.c_proj.weight";
+  const char* n_fc2b = siglip ? "mlp.fc2.bias" : "mlp.c_proj.bias";
+  if (siglip) {
+    const std::string t = "visual.trunk.";
+    w.conv_w = w16_pad(t + "patch_embed.proj.weight", D, kpatch_pad(s));
+    w.conv_b = f32(t + "patch_embed.proj.bias");
+    w.pos = f32(t + "pos_embed");
+    pre = t + "blocks.";
+  } else if (s.tower == TOWER_VISION) {
     w.conv_w = w16_pad("visual.conv1.weight", D, kpatch_pad(s));
     w.cls = f32("visual.class_embedding");
     w.pos = f32("visual.positional_embedding");
@@ -258,21 +293,47 @@ void upload_weights(clipgpu_engine& e, Replica& r, const TensorMap& m) {
   for (int l = 0; l < s.layers; ++l) {
     const std::string p = pre + std::to_string(l) + ".";
     LayerW L;
-    L.ln1_w = f32(p + "ln_1.weight");
-    L.ln1_b = f32(p + "ln_1.bias");
-    L.wqkv = w16(p + "attn.in_proj_weight");
-    L.bqkv = f32(p + "attn.in_proj_bias");
-    L.wo = w16(p + "attn.out_proj.weight");
-    L.bo = f32(p + "attn.out_proj.bias");
-    L.ln2_w = f32(p + "ln_2.weight");
-    L.ln2_b = f32(p + "ln_2.bias");
-    L.w1 = w16_pad(p + "mlp.c_fc.weight", mlp_pad(s), D);
-    L.b1 = f32_pad(p + "mlp.c_fc.bias", mlp_pad(s));
-    L.w2 = w16_pad(p + "mlp.c_proj.weight", D, mlp_pad(s));
-    L.b2 = f32(p + "mlp.c_proj.bias");
+    L.ln1_w = f32(p + n_ln1w);
+    L.ln1_b = f32(p + n_ln1b);
+    L.wqkv = w16(p + n_qkvw);
+    L.bqkv = f32(p + n_qkvb);
+    L.wo = w16(p + n_ow);
+    L.bo = f32(p + n_ob);
+    L.ln2_w = f32(p + n_ln2w);
+    L.ln2_b = f32(p + n_ln2b);
+    L.w1 = w16_pad(p + n_fc1w, mlp_pad(s), D);
+    L.b1 = f32_pad(p + n_fc1b, mlp_pad(s));
+    L.w2 = w16_pad(p + n_fc2w, D, mlp_pad(s));
+    L.b2 = f32(p + n_fc2b);
     w.layers.push_back(L);
   }
-  if (s.tower == TOWER_VISION) {
+  if (siglip) {
+    const std::string t = "visual.trunk.", a = "visual.trunk.attn_pool.";
+    w.lnpost_w = f32(t + "norm.weight");  // final norm, before the attention pool
+    w.lnpost_b = f32(t + "norm.bias");
+    {  // q = latent . Wq^T + bq, shared by every image (f64 accumulation)
+      const HostTensor& lat = need(m, a + "latent");
+      const HostTensor& wq = need(m, a + "q.weight");
+      const HostTensor& bq = need(m, a + "q.bias");
+      std::vector<float> q((size_t)D);
+      for (int j = 0; j < D; ++j) {
+        double acc = bq.data[(size_t)j];
+        for (int i = 0; i < D; ++i) acc += (double)lat.data[(size_t)i] * wq.data[(size_t)j * D + i];
+        q[(size_t)j] = (float)acc;
+      }
+      w.map.q = (float*)a_take_f32(q);
+    }
+    w.map.wkv = w16(a + "kv.weight");
+    w.map.bkv = f32(a + "kv.bias");
+    w.map.wproj = w16(a + "proj.weight");
+    w.map.bproj = f32(a + "proj.bias");
+    w.map.norm_w = f32(a + "norm.weight");
+    w.map.norm_b = f32(a + "norm.bias");
+    w.map.w1 = w16_pad(a + "mlp.fc1.weight", mlp_pad(s), D);
+    w.map.b1 = f32_pad(a + "mlp.fc1.bias", mlp_pad(s));
+    w.map.w2 = w16_pad(a + "mlp.fc2.weight", D, mlp_pad(s));
+    w.map.b2 = f32(a + "mlp.fc2.bias");
+  } else if (s.tower == TOWER_VISION) {
     w.lnpost_w = f32("visual.ln_post.weight");
     w.lnpost_b = f32("visual.ln_post.bias");
     w.proj_t = w16_transposed("visual.proj");
@@ -464,6 +525,29 @@ void head(const clipgpu_engine& e, const Replica& r, int B, const int64_t* ids, 
   check(launch_l2norm(r.emb, d_out, B, E, st), "l2norm");
 }
 
+// SigLIP tail (timm VisionTransformer.norm + AttentionPoolLatent, timm_proj "none"):
+// LN(all tokens) -> [k|v] GEMM -> MAP attention with the precomputed latent query -> proj
+// -> y + MLP(LN(y)) -> L2 normalise.  Scratch: h (tokens, then the pooled LN), big ([k|v],
+// then the MLP hidden), pooled (attention output), x's first B rows (y, f32).
+void head_map(const clipgpu_engine& e, const Replica& r, int B, float* d_out, hipStream_t st) {
+  const TowerSpec& s = e.spec;
+  const int D = s.width, T = s.tokens(), M = mlp_pad(s);
+  const MapHeadW& mw = r.w.map;
+  ProfScope ps(e, PC_HEAD, st);
+  check(launch_ln_rows(e.dt, r.x, r.w.lnpost_w, r.w.lnpost_b, s.ln_eps, r.h, B * T, D, st), "norm");
+  check(launch_gemm(e.dt, A_ROWS, EPI_STORE16, ACT_NONE, rows_gemm(r.h, D, mw.wkv, mw.bkv, r.big, 2 * D, B * T, 2 * D, D),
+                    st), "attn_pool kv gemm");
+  check(launch_map_attention(e.dt, mw.q, r.big, r.pooled, B, T, s.heads, D, st), "attn_pool attention");
+  check(launch_gemm(e.dt, A_ROWS, EPI_STORE32, ACT_NONE, rows_gemm(r.pooled, D, mw.wproj, mw.bproj, r.x, D, B, D, D), st),
+        "attn_pool proj gemm");
+  check(launch_ln_rows(e.dt, r.x, mw.norm_w, mw.norm_b, s.ln_eps, r.h, B, D, st), "attn_pool norm");
+  check(launch_gemm(e.dt, A_ROWS, EPI_STORE16, s.act, rows_gemm(r.h, D, mw.w1, mw.b1, r.big, M, B, M, D), st),
+        "attn_pool fc1 gemm");
+  check(launch_gemm(e.dt, A_ROWS, EPI_RESID, ACT_NONE, rows_gemm(r.big, M, mw.w2, mw.b2, r.x, D, B, D, M), st),
+        "attn_pool fc2 gemm");
+  check(launch_l2norm(r.x, d_out, B, D, st), "l2norm");
+}
+
 // asrc: A_IMG_F32 (pixels = normalised f32 NCHW) or A_IMG_U8 (NHWC u8 + mean/std)
 void vision_forward(const clipgpu_engine& e, const Replica& r, const void* pixels, int asrc, const float* mean,
                     const float* stdv, int B, float* d_out, hipStream_t st) {
@@ -472,7 +556,6 @@ void vision_forward(const clipgpu_engine& e, const Replica& r, const void* pixel
   GemmParams g{};
   g.W = r.w.conv_w;
   g.ldw = kpatch_pad(s);
-  g.bias = nullptr;  // OpenAI-style conv1 has no bias
   g.out = r.x;
   g.ldo = D;
   g.M = B * G * G;
@@ -488,8 +571,18 @@ void vision_forward(const clipgpu_engine& e, const Replica& r, const void* pixel
     g.mean[c] = mean ? mean[c] : 0.f;
     g.stdv[c] = stdv ? stdv[c] : 1.f;
   }
+  g.bias = r.w.conv_b;
+  g.cls = s.cls() ? 1 : 0;
   { ProfScope ps(e, PC_PATCH, st);
     check(launch_gemm(e.dt, asrc, EPI_PATCH, ACT_NONE, g, st), "patch gemm"); }
+  if (s.family == FAMILY_SIGLIP) {  // no class token, no pre-norm: x = patches + bias + pos
+    { ProfScope ps(e, PC_STEM, st);
+      check(launch_ln_rows(e.dt, r.x, r.w.layers[0].ln1_w, r.w.layers[0].ln1_b, s.ln_eps, r.h, B * s.tokens(), D, st),
+            "ln_1"); }
+    trunk(e, r, B, 0, st);
+    head_map(e, r, B, d_out, st);
+    return;
+  }
   {
   ProfScope ps(e, PC_STEM, st);
   check(launch_vision_embed_ln(e.dt, r.x, r.w.cls, r.w.pos, r.w.lnpre_w, r.w.lnpre_b, r.w.layers[0].ln1_w,

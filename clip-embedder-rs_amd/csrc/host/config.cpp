@@ -29,6 +29,38 @@ static int act_from(const json::Value& model_cfg, const json::Value* sub) {
   return (q && q->as_bool(false)) ? 1 : 2;  // ACT_QUICK_GELU : ACT_GELU
 }
 
+static int geti(const json::Value* o, const char* k, int dflt);
+
+// timm SigLIP ViTs as open_clip TimmModel builds them (timm_model_name -> patch, width,
+// depth, heads, mlp hidden): global_pool "map", GELU(tanh), LayerNorm eps 1e-6, no class
+// token, no pre-norm, patch-embedding conv with bias (oracle/model_spec.py TIMM_SIGLIP).
+static void timm_siglip_spec(const std::string& name, const json::Value* v, TowerSpec& vs) {
+  struct Row { const char* prefix; int patch, width, layers, heads, mlp; };
+  static const Row rows[] = {
+      {"vit_base_patch16_siglip_", 16, 768, 12, 12, 3072},     {"vit_large_patch16_siglip_", 16, 1024, 24, 16, 4096},
+      {"vit_so400m_patch14_siglip_", 14, 1152, 27, 16, 4304},  {"vit_so400m_patch16_siglip_", 16, 1152, 27, 16, 4304},
+      {"vit_giantopt_patch16_siglip_", 16, 1536, 40, 16, 6144},
+  };
+  const Row* hit = nullptr;
+  for (const Row& r : rows)
+    if (name.rfind(r.prefix, 0) == 0) hit = &r;
+  if (!hit) throw std::runtime_error("Configuration error: timm model '" + name + "' is not supported");
+  const json::Value* pool = v->get("timm_pool");
+  const json::Value* proj = v->get("timm_proj");
+  if ((pool && !pool->is_null() && pool->as_str("") != "map") ||
+      (proj && !proj->is_null() && proj->as_str("") != "none"))
+    throw std::runtime_error("Configuration error: only timm_pool 'map' with timm_proj 'none' is supported");
+  const json::Value* d = v->get("clipgpu_dims");  // synthetic test configs only: explicit (reduced) dims
+  vs.family = FAMILY_SIGLIP;
+  vs.patch_size = geti(d, "patch_size", hit->patch);
+  vs.width = geti(d, "width", hit->width);
+  vs.layers = geti(d, "layers", hit->layers);
+  vs.heads = geti(d, "heads", hit->heads);
+  vs.mlp_width = geti(d, "mlp_width", hit->mlp);
+  vs.act = 3;  // ACT_GELU_TANH
+  vs.ln_eps = 1e-6f;
+}
+
 static int geti(const json::Value* o, const char* k, int dflt) {
   const json::Value* v = o ? o->get(k) : nullptr;
   return v ? (int)v->as_num(dflt) : dflt;
@@ -48,21 +80,29 @@ OpenClipConfig load_open_clip_config(const std::string& path) {
 
   const json::Value* v = mc->get("vision_cfg");
   if (!v || !v->get("image_size")) throw std::runtime_error("Configuration error: vision_cfg.image_size missing");
-  for (const char* bad : {"timm_model_name", "attentional_pool"}) {
-    const json::Value* x = v->get(bad);
+  {
+    const json::Value* x = v->get("attentional_pool");
     if (x && !x->is_null() && !(x->kind == json::Value::BOOL && !x->b))
-      throw std::runtime_error(std::string("Configuration error: vision_cfg.") + bad + " is not supported yet");
+      throw std::runtime_error("Configuration error: vision_cfg.attentional_pool is not supported yet");
   }
   TowerSpec& vs = c.vision;
   vs.tower = TOWER_VISION;
   vs.image_size = geti(v, "image_size", 224);
-  vs.patch_size = geti(v, "patch_size", 16);
-  vs.width = geti(v, "width", 768);
-  vs.layers = geti(v, "layers", 12);
-  vs.heads = vs.width / geti(v, "head_width", 64);
-  vs.mlp_width = (int)(vs.width * getd(v, "mlp_ratio", 4.0));
-  vs.embed_dim = c.embed_dim;
-  vs.act = act_from(*mc, v);
+  const json::Value* timm = v->get("timm_model_name");
+  if (timm && !timm->is_null()) {
+    timm_siglip_spec(timm->as_str(""), v, vs);
+    if (c.embed_dim != vs.width)
+      throw std::runtime_error("Configuration error: timm_proj 'none' needs embed_dim == width");
+    vs.embed_dim = c.embed_dim;
+  } else {
+    vs.patch_size = geti(v, "patch_size", 16);
+    vs.width = geti(v, "width", 768);
+    vs.layers = geti(v, "layers", 12);
+    vs.heads = vs.width / geti(v, "head_width", 64);
+    vs.mlp_width = (int)(vs.width * getd(v, "mlp_ratio", 4.0));
+    vs.embed_dim = c.embed_dim;
+    vs.act = act_from(*mc, v);
+  }
 
   const json::Value* t = mc->get("text_cfg");
   if (!t || !t->get("context_length"))

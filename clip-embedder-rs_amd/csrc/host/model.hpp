@@ -26,6 +26,7 @@ struct ModelConfig {
 };
 
 enum Tower { TOWER_VISION = 0, TOWER_TEXT = 1 };
+enum Family { FAMILY_CLIP = 0, FAMILY_SIGLIP = 1 };
 
 // Architecture of one tower.  The reference never parses most of these
 // (src/config.rs:36-47) because they are baked into the ONNX graphs; we derive
@@ -37,8 +38,13 @@ struct TowerSpec {
   float ln_eps = 1e-5f;
   // vision
   int image_size = 0, patch_size = 0;
+  // FAMILY_CLIP: open_clip VisionTransformer (CLS token, ln_pre, CLS pooling, proj).
+  // FAMILY_SIGLIP: timm ViT trunk of open_clip TimmModel (no CLS, no pre-norm, patch-conv
+  // bias, final norm, MAP attention-pool head, timm_proj "none"; names visual.trunk.*).
+  int family = 0;
+  bool cls() const { return family == 0; }
   int grid() const { return patch_size ? image_size / patch_size : 0; }
-  int tokens() const { return tower == TOWER_VISION ? grid() * grid() + 1 : context_length; }
+  int tokens() const { return tower == TOWER_VISION ? grid() * grid() + (cls() ? 1 : 0) : context_length; }
   // text
   int context_length = 0, vocab_size = 0;
 };

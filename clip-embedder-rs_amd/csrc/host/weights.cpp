@@ -71,7 +71,54 @@ static void block_params(std::vector<ParamDesc>& out, const std::string& pre, in
   out.push_back({pre + "mlp.c_proj.bias", {D}, LIN_BIAS_STD, 0.0});
 }
 
+static void timm_block_params(std::vector<ParamDesc>& out, const std::string& pre, int64_t D, int64_t M, int64_t L) {
+  const double attn_std = std::pow((double)D, -0.5);
+  const double proj_std = std::pow((double)D, -0.5) * std::pow((double)(2 * L), -0.5);
+  const double fc_std = std::pow((double)(2 * D), -0.5);
+  out.push_back({pre + "norm1.weight", {D}, LN_GAIN_STD, 1.0});
+  out.push_back({pre + "norm1.bias", {D}, LN_BIAS_STD, 0.0});
+  out.push_back({pre + "attn.qkv.weight", {3 * D, D}, attn_std, 0.0});
+  out.push_back({pre + "attn.qkv.bias", {3 * D}, LIN_BIAS_STD, 0.0});
+  out.push_back({pre + "attn.proj.weight", {D, D}, proj_std, 0.0});
+  out.push_back({pre + "attn.proj.bias", {D}, LIN_BIAS_STD, 0.0});
+  out.push_back({pre + "norm2.weight", {D}, LN_GAIN_STD, 1.0});
+  out.push_back({pre + "norm2.bias", {D}, LN_BIAS_STD, 0.0});
+  out.push_back({pre + "mlp.fc1.weight", {M, D}, fc_std, 0.0});
+  out.push_back({pre + "mlp.fc1.bias", {M}, LIN_BIAS_STD, 0.0});
+  out.push_back({pre + "mlp.fc2.weight", {D, M}, proj_std, 0.0});
+  out.push_back({pre + "mlp.fc2.bias", {D}, LIN_BIAS_STD, 0.0});
+}
+
+// open_clip TimmModel over a timm SigLIP ViT (oracle/weights.py siglip_vision_param_list).
+static std::vector<ParamDesc> siglip_vision_params(const TowerSpec& s) {
+  std::vector<ParamDesc> out;
+  const int64_t D = s.width, L = s.layers, M = s.mlp_width, p = s.patch_size, G = s.grid();
+  const double rD = std::pow((double)D, -0.5);
+  const std::string t = "visual.trunk.", a = "visual.trunk.attn_pool.";
+  out.push_back({t + "patch_embed.proj.weight", {D, 3, p, p}, std::pow((double)(3 * p * p), -0.5), 0.0});
+  out.push_back({t + "patch_embed.proj.bias", {D}, LIN_BIAS_STD, 0.0});
+  out.push_back({t + "pos_embed", {1, G * G, D}, rD, 0.0});
+  for (int i = 0; i < L; ++i) timm_block_params(out, t + "blocks." + std::to_string(i) + ".", D, M, L);
+  out.push_back({t + "norm.weight", {D}, LN_GAIN_STD, 1.0});
+  out.push_back({t + "norm.bias", {D}, LN_BIAS_STD, 0.0});
+  out.push_back({a + "latent", {1, 1, D}, rD, 0.0});
+  out.push_back({a + "q.weight", {D, D}, rD, 0.0});
+  out.push_back({a + "q.bias", {D}, LIN_BIAS_STD, 0.0});
+  out.push_back({a + "kv.weight", {2 * D, D}, rD, 0.0});
+  out.push_back({a + "kv.bias", {2 * D}, LIN_BIAS_STD, 0.0});
+  out.push_back({a + "proj.weight", {D, D}, rD, 0.0});
+  out.push_back({a + "proj.bias", {D}, LIN_BIAS_STD, 0.0});
+  out.push_back({a + "norm.weight", {D}, LN_GAIN_STD, 1.0});
+  out.push_back({a + "norm.bias", {D}, LN_BIAS_STD, 0.0});
+  out.push_back({a + "mlp.fc1.weight", {M, D}, std::pow((double)(2 * D), -0.5), 0.0});
+  out.push_back({a + "mlp.fc1.bias", {M}, LIN_BIAS_STD, 0.0});
+  out.push_back({a + "mlp.fc2.weight", {D, M}, rD, 0.0});
+  out.push_back({a + "mlp.fc2.bias", {D}, LIN_BIAS_STD, 0.0});
+  return out;
+}
+
 std::vector<ParamDesc> tower_params(const TowerSpec& s) {
+  if (s.tower == TOWER_VISION && s.family == FAMILY_SIGLIP) return siglip_vision_params(s);
   std::vector<ParamDesc> out;
   const int64_t D = s.width, L = s.layers, M = s.mlp_width, E = s.embed_dim;
   if (s.tower == TOWER_VISION) {

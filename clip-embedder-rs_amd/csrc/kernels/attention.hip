@@ -195,11 +195,12 @@ __global__ __launch_bounds__(256) void flash_attn_kernel(const T* __restrict__ q
   const int fr = lane & 15, fq = lane >> 4;
 
   // zero the padding that tile loads never write: K head-dim pad, V^T pad rows
-  for (int q = tid; q < KT * (HK / 8 - CH); q += 256) {
-    const int r = q / (HK / 8 - CH), c = CH + q % (HK / 8 - CH);
-    *(V8*)(sK + r * KROW + c * 16) = V8{};
+  if constexpr (HK > HD) {
+    constexpr int PADC = HK / 8 - CH;
+    for (int q = tid; q < KT * PADC; q += 256) *(V8*)(sK + (q / PADC) * KROW + (CH + q % PADC) * 16) = V8{};
   }
-  for (int q = tid; q < (HV - HD) * KT; q += 256) *(T*)(sVt + (HD + q / KT) * VROW + (q % KT) * 2) = (T)0.f;
+  if constexpr (HV > HD)
+    for (int q = tid; q < (HV - HD) * KT; q += 256) *(T*)(sVt + (HD + q / KT) * VROW + (q % KT) * 2) = (T)0.f;
 
   // this wave's 16 queries: Q fragments (head dim zero-padded to HK)
   const int q0 = qb * 64 + wave * 16;
@@ -326,7 +327,71 @@ hipError_t launch_flash_hd(const void* qkv, void* out, int B, int N, int H, int 
   return hipErrorInvalidValue;
 }
 
+// MAP attention pool (timm AttentionPoolLatent; oracle/clip_ref.py encode_image_siglip): one
+// learned query per head over the N tokens of one image.  One 256-thread block per (image,
+// head): scores by threads over keys, block softmax, then waves split the keys and lanes
+// the head dims for o = sum_n p_n v_n.  Memory-bound and tiny next to the trunk.
+template <typename T>
+__global__ __launch_bounds__(256) void map_attn_kernel(const float* __restrict__ q, const T* __restrict__ kv,
+                                                       T* __restrict__ out, int N, int H, int D, float scale) {
+  __shared__ float sS[1024];
+  __shared__ float sO[4][128];
+  __shared__ float red[4];
+  const int b = blockIdx.x / H, h = blockIdx.x % H, hd = D / H;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const T* kvb = kv + (long)b * N * 2 * D;
+  const float* qh = q + (long)h * hd;
+  float lmax = -INFINITY;
+  for (int n = tid; n < N; n += 256) {
+    const T* kr = kvb + (long)n * 2 * D + (long)h * hd;
+    float s = 0.f;
+    for (int d = 0; d < hd; ++d) s += qh[d] * (float)kr[d];
+    s *= scale;
+    sS[n] = s;
+    lmax = fmaxf(lmax, s);
+  }
+  lmax = wave_max(lmax);
+  if (lane == 0) red[wave] = lmax;
+  __syncthreads();
+  const float m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  __syncthreads();
+  float lsum = 0.f;
+  for (int n = tid; n < N; n += 256) {
+    const float e = __expf(sS[n] - m);
+    sS[n] = e;
+    lsum += e;
+  }
+  lsum = wave_sum(lsum);
+  if (lane == 0) red[wave] = lsum;
+  __syncthreads();
+  const float inv = 1.0f / (red[0] + red[1] + red[2] + red[3]);
+  float o0 = 0.f, o1 = 0.f;
+  for (int n = wave; n < N; n += 4) {
+    const T* vr = kvb + (long)n * 2 * D + D + (long)h * hd;
+    const float pn = sS[n];
+    if (lane < hd) o0 += pn * (float)vr[lane];
+    if (lane + 64 < hd) o1 += pn * (float)vr[lane + 64];
+  }
+  sO[wave][lane] = o0;
+  sO[wave][lane + 64] = o1;
+  __syncthreads();
+  if (tid < hd) out[(long)b * D + (long)h * hd + tid] = (T)((sO[0][tid] + sO[1][tid] + sO[2][tid] + sO[3][tid]) * inv);
+}
+
 }  // namespace
+
+hipError_t launch_map_attention(DType dt, const float* q, const void* kv, void* out, int B, int N, int H, int D,
+                                hipStream_t s) {
+  if (B <= 0 || N <= 0 || N > 1024 || H <= 0 || D % H || D / H > 128) return hipErrorInvalidValue;
+  const float scale = 1.0f / sqrtf((float)(D / H));
+  if (dt == DT_BF16)
+    hipLaunchKernelGGL(map_attn_kernel<__bf16>, dim3(B * H), dim3(256), 0, s, q, (const __bf16*)kv, (__bf16*)out, N, H,
+                       D, scale);
+  else
+    hipLaunchKernelGGL(map_attn_kernel<_Float16>, dim3(B * H), dim3(256), 0, s, q, (const _Float16*)kv,
+                       (_Float16*)out, N, H, D, scale);
+  return hipGetLastError();
+}
 
 hipError_t launch_attention(DType dt, const void* qkv, void* out, int B, int N, int H, int D, int causal,
                             hipStream_t s) {

@@ -421,8 +421,8 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
           const float* ps = nullptr;
           if constexpr (EPI == EPI_PATCH) {
             const int b = m / G2, pp = m - b * G2;
-            o = (float*)p.out + ((long)b * (G2 + 1) + 1 + pp) * p.ldo + n;
-            ps = p.pos + (long)(1 + pp) * p.N + n;
+            o = (float*)p.out + ((long)b * (G2 + p.cls) + p.cls + pp) * p.ldo + n;
+            ps = p.pos + (long)(p.cls + pp) * p.N + n;
           } else {
             o = (float*)p.out + (long)m * p.ldo + n;
           }

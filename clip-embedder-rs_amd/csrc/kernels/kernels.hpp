@@ -32,6 +32,7 @@ struct GemmParams {
   // image sources (A_IMG_*)
   const void* img; int S, P, G;
   int Kv;                    // image sources: valid K = 3*P*P (K is padded to a multiple of 64; k >= Kv reads 0)
+  int cls;                   // EPI_PATCH: 1 = token 0 of each image is a class token (rows / pos shifted by one)
   float mean[3], stdv[3];
   const float* pos;          // EPI_PATCH positional embedding [G^2+1][N]
   int tile;                  // GemmTile (0 = pick by shape)
@@ -53,6 +54,10 @@ hipError_t launch_gemm(DType dt, int asrc, int epi, int act, const GemmParams& p
 
 // Multi-head self-attention over packed qkv rows [B*N][3*D] -> out [B*N][D];
 // head_dim must be 64; N <= 256.
+// MAP attention pool (timm AttentionPoolLatent, one latent query): q [D] f32 (shared by all
+// images), kv [B*N][2D] 16-bit = [k | v], out [B][D] 16-bit (heads concatenated).
+hipError_t launch_map_attention(DType dt, const float* q, const void* kv, void* out, int B, int N, int H, int D,
+                                hipStream_t s);
 hipError_t launch_attention(DType dt, const void* qkv, void* out, int B, int N, int H, int D,
                             int causal, hipStream_t s);
 

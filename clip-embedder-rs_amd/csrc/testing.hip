@@ -143,6 +143,7 @@ int clipgpu_test_patch_embed(int dtype, int mode, int64_t B, int64_t S, int64_t 
     GemmParams g{};
     g.W = dw.p; g.ldw = Kp; g.out = dx.p; g.ldo = D; g.M = (int)(B * G * G); g.N = (int)D; g.K = (int)Kp;
     g.Kv = (int)K;
+    g.cls = 1;
     g.img = dpix.p; g.S = (int)S; g.P = (int)P; g.G = (int)G; g.pos = dpos.as<float>();
     g.tile = tile_override();
     for (int c = 0; c < 3; ++c) {

@@ -72,9 +72,54 @@ def _cast(P: Dict[str, np.ndarray], dtype):
     return {k: np.asarray(v, dtype=dtype) for k, v in P.items()}
 
 
+def _timm_block(P, pre, x, heads, act, eps):
+    """timm Block (norm1 -> Attention(qkv, proj) -> +, norm2 -> Mlp(fc1, act, fc2) -> +) written as
+    the open_clip block with the fused qkv as in_proj: identical arithmetic."""
+    Q = {pre + "ln_1.weight": P[pre + "norm1.weight"], pre + "ln_1.bias": P[pre + "norm1.bias"],
+         pre + "attn.in_proj_weight": P[pre + "attn.qkv.weight"], pre + "attn.in_proj_bias": P[pre + "attn.qkv.bias"],
+         pre + "attn.out_proj.weight": P[pre + "attn.proj.weight"], pre + "attn.out_proj.bias": P[pre + "attn.proj.bias"],
+         pre + "ln_2.weight": P[pre + "norm2.weight"], pre + "ln_2.bias": P[pre + "norm2.bias"],
+         pre + "mlp.c_fc.weight": P[pre + "mlp.fc1.weight"], pre + "mlp.c_fc.bias": P[pre + "mlp.fc1.bias"],
+         pre + "mlp.c_proj.weight": P[pre + "mlp.fc2.weight"], pre + "mlp.c_proj.bias": P[pre + "mlp.fc2.bias"]}
+    return _resblock(Q, pre, x, heads, act, eps, False)
+
+
+def encode_image_siglip(P: Dict[str, np.ndarray], v: VisionSpec, pixels: np.ndarray,
+                        dtype=np.float64, normalize: bool = True) -> np.ndarray:
+    """open_clip TimmModel over a timm SigLIP ViT (global_pool 'map', timm_proj 'none') + normalize.
+    timm VisionTransformer: patch_embed (conv, bias) -> + pos_embed (no class token, no norm_pre)
+    -> blocks -> norm -> AttentionPoolLatent: q = latent Wq, [k|v] = x Wkv, per-head softmax
+    attention, proj, x + mlp(norm(x)), token 0."""
+    P = _cast(P, dtype)
+    x = np.asarray(pixels, dtype=dtype)
+    B = x.shape[0]
+    p, g, D, H = v.patch_size, v.grid, v.width, v.heads
+    d = D // H
+    t, a = "visual.trunk.", "visual.trunk.attn_pool."
+    patches = x.reshape(B, 3, g, p, g, p).transpose(0, 2, 4, 1, 3, 5).reshape(B, g * g, 3 * p * p)
+    x = patches @ P[t + "patch_embed.proj.weight"].reshape(D, 3 * p * p).T + P[t + "patch_embed.proj.bias"]
+    x = x + P[t + "pos_embed"][0]
+    for i in range(v.layers):
+        x = _timm_block(P, f"{t}blocks.{i}.", x, H, v.act, v.ln_eps)
+    x = layer_norm(x, P[t + "norm.weight"], P[t + "norm.bias"], v.ln_eps)
+    q = (P[a + "latent"].reshape(1, D) @ P[a + "q.weight"].T + P[a + "q.bias"]).reshape(H, d)
+    kv = x @ P[a + "kv.weight"].T + P[a + "kv.bias"]                       # [B, N, 2D]
+    k = kv[..., :D].reshape(B, -1, H, d)
+    vv = kv[..., D:].reshape(B, -1, H, d)
+    s = np.einsum("hd,bnhd->bhn", q, k) / np.sqrt(d)
+    o = np.einsum("bhn,bnhd->bhd", softmax(s), vv).reshape(B, D)
+    y = o @ P[a + "proj.weight"].T + P[a + "proj.bias"]
+    h = act_fn(v.act, layer_norm(y, P[a + "norm.weight"], P[a + "norm.bias"], v.ln_eps) @ P[a + "mlp.fc1.weight"].T
+               + P[a + "mlp.fc1.bias"])
+    y = y + h @ P[a + "mlp.fc2.weight"].T + P[a + "mlp.fc2.bias"]
+    return l2_normalize(y) if normalize else y
+
+
 def encode_image(P: Dict[str, np.ndarray], v: VisionSpec, pixels: np.ndarray,
                  dtype=np.float64, normalize: bool = True) -> np.ndarray:
     """open_clip VisionTransformer.forward + normalize.  pixels: [B,3,S,S] normalised f32."""
+    if v.family == "siglip":
+        return encode_image_siglip(P, v, pixels, dtype, normalize)
     P = _cast(P, dtype)
     x = np.asarray(pixels, dtype=dtype)
     B = x.shape[0]

@@ -99,3 +99,59 @@ def hf_encode_text(m, ids):
         e = m(input_ids=torch.from_numpy(np.asarray(ids, np.int64))).text_embeds
         e = torch.nn.functional.normalize(e, dim=-1)
     return e.double().numpy()
+
+
+def hf_siglip_vision(P, v, dtype="float64"):
+    """HF SiglipVisionModel (vision_use_head: MAP head) with the timm-named seeded weights:
+    qkv splits into q/k/v_proj; the attention-pool latent is the HF probe and [q | kv] its
+    packed nn.MultiheadAttention in_proj."""
+    import torch
+    from transformers import SiglipVisionConfig, SiglipVisionModel
+    cfg = SiglipVisionConfig(hidden_size=v.width, intermediate_size=v.mlp_width, num_hidden_layers=v.layers,
+                             num_attention_heads=v.heads, image_size=v.image_size, patch_size=v.patch_size,
+                             hidden_act="gelu_pytorch_tanh", layer_norm_eps=v.ln_eps, attn_implementation="eager")
+    m = SiglipVisionModel(cfg).eval()
+    t, a, D = "visual.trunk.", "visual.trunk.attn_pool.", v.width
+    sd = {
+        "vision_model.embeddings.patch_embedding.weight": P[t + "patch_embed.proj.weight"],
+        "vision_model.embeddings.patch_embedding.bias": P[t + "patch_embed.proj.bias"],
+        "vision_model.embeddings.position_embedding.weight": P[t + "pos_embed"][0],
+        "vision_model.post_layernorm.weight": P[t + "norm.weight"],
+        "vision_model.post_layernorm.bias": P[t + "norm.bias"],
+        "vision_model.head.probe": P[a + "latent"],
+        "vision_model.head.attention.in_proj_weight": np.concatenate([P[a + "q.weight"], P[a + "kv.weight"]]),
+        "vision_model.head.attention.in_proj_bias": np.concatenate([P[a + "q.bias"], P[a + "kv.bias"]]),
+        "vision_model.head.attention.out_proj.weight": P[a + "proj.weight"],
+        "vision_model.head.attention.out_proj.bias": P[a + "proj.bias"],
+        "vision_model.head.layernorm.weight": P[a + "norm.weight"],
+        "vision_model.head.layernorm.bias": P[a + "norm.bias"],
+        "vision_model.head.mlp.fc1.weight": P[a + "mlp.fc1.weight"],
+        "vision_model.head.mlp.fc1.bias": P[a + "mlp.fc1.bias"],
+        "vision_model.head.mlp.fc2.weight": P[a + "mlp.fc2.weight"],
+        "vision_model.head.mlp.fc2.bias": P[a + "mlp.fc2.bias"],
+    }
+    for i in range(v.layers):
+        src, dst = f"{t}blocks.{i}.", f"vision_model.encoder.layers.{i}."
+        w, b = P[src + "attn.qkv.weight"], P[src + "attn.qkv.bias"]
+        for j, nm in enumerate(("q_proj", "k_proj", "v_proj")):
+            sd[dst + f"self_attn.{nm}.weight"] = w[j * D:(j + 1) * D]
+            sd[dst + f"self_attn.{nm}.bias"] = b[j * D:(j + 1) * D]
+        for hf, tm in (("self_attn.out_proj", "attn.proj"), ("layer_norm1", "norm1"), ("layer_norm2", "norm2"),
+                       ("mlp.fc1", "mlp.fc1"), ("mlp.fc2", "mlp.fc2")):
+            sd[dst + hf + ".weight"] = P[src + tm + ".weight"]
+            sd[dst + hf + ".bias"] = P[src + tm + ".bias"]
+    pre = "" if any(k.startswith("embeddings.") for k in m.state_dict()) else "vision_model."
+    sd = {pre + k[len("vision_model."):]: torch.from_numpy(np.ascontiguousarray(x)) for k, x in sd.items()}
+    missing, unexpected = m.load_state_dict(sd, strict=False)
+    missing = [k for k in missing if not k.endswith("position_ids")]
+    assert not missing and not unexpected, (missing, unexpected)
+    return m.to(getattr(torch, dtype))
+
+
+def hf_siglip_encode_image(m, pixels):
+    import torch
+    dt = next(m.parameters()).dtype
+    with torch.no_grad():
+        e = m(pixel_values=torch.from_numpy(np.asarray(pixels)).to(dt)).pooler_output
+        e = torch.nn.functional.normalize(e, dim=-1)
+    return e.double().numpy()

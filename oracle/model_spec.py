@@ -29,6 +29,10 @@ class VisionSpec:
     embed_dim: int
     act: str            # "quick_gelu" | "gelu" | "gelu_tanh"
     ln_eps: float = 1e-5
+    # "clip": open_clip VisionTransformer (CLS token, ln_pre, CLS pooling, proj);
+    # "siglip": timm ViT trunk of open_clip TimmModel (no CLS, no pre-norm, patch-conv bias,
+    # final norm, MAP attention-pool head, timm_proj "none")
+    family: str = "clip"
 
     @property
     def grid(self) -> int:
@@ -36,7 +40,7 @@ class VisionSpec:
 
     @property
     def tokens(self) -> int:
-        return self.grid * self.grid + 1  # + CLS
+        return self.grid * self.grid + (1 if self.family == "clip" else 0)  # + CLS
 
     @property
     def head_dim(self) -> int:
@@ -66,9 +70,42 @@ def _act(model_cfg: dict, sub: dict) -> str:
     return "quick_gelu" if model_cfg.get("quick_gelu", False) else "gelu"
 
 
+# timm SigLIP ViTs as open_clip TimmModel builds them (timm_model_name -> patch, width, depth,
+# heads, mlp hidden): global_pool "map", GELU(tanh), LayerNorm eps 1e-6, no class token,
+# no pre-norm, patch-embedding conv with bias.
+TIMM_SIGLIP = {}
+for _res in (224, 256, 384, 512):
+    TIMM_SIGLIP[f"vit_base_patch16_siglip_{_res}"] = (16, 768, 12, 12, 3072)
+for _res in (256, 384):
+    TIMM_SIGLIP[f"vit_large_patch16_siglip_{_res}"] = (16, 1024, 24, 16, 4096)
+    TIMM_SIGLIP[f"vit_giantopt_patch16_siglip_{_res}"] = (16, 1536, 40, 16, 6144)
+for _res in (224, 378, 384):
+    TIMM_SIGLIP[f"vit_so400m_patch14_siglip_{_res}"] = (14, 1152, 27, 16, 4304)
+for _res in (256, 384, 512):
+    TIMM_SIGLIP[f"vit_so400m_patch16_siglip_{_res}"] = (16, 1152, 27, 16, 4304)
+
+
+def _siglip_vision_spec(model_cfg: dict, v: dict) -> VisionSpec:
+    name = v["timm_model_name"]
+    if name not in TIMM_SIGLIP:
+        raise ValueError(f"timm model {name} is not supported")
+    if v.get("timm_pool", "map") != "map" or v.get("timm_proj", "none") not in ("none", None):
+        raise ValueError("only timm_pool 'map' with timm_proj 'none' is supported")
+    patch, width, layers, heads, mlp = TIMM_SIGLIP[name]
+    dims = v.get("clipgpu_dims", {})  # synthetic test configs only: explicit (reduced) dims
+    patch, width = int(dims.get("patch_size", patch)), int(dims.get("width", width))
+    layers, heads, mlp = int(dims.get("layers", layers)), int(dims.get("heads", heads)), int(dims.get("mlp_width", mlp))
+    if int(model_cfg["embed_dim"]) != width:
+        raise ValueError("timm_proj 'none' needs embed_dim == width")
+    return VisionSpec(image_size=int(v["image_size"]), patch_size=patch, width=width, layers=layers, heads=heads,
+                      mlp_width=mlp, embed_dim=width, act="gelu_tanh", ln_eps=1e-6, family="siglip")
+
+
 def vision_spec_from_cfg(model_cfg: dict) -> VisionSpec:
     v = model_cfg["vision_cfg"]
-    for unsupported in ("timm_model_name", "attentional_pool", "attn_pooler_queries"):
+    if v.get("timm_model_name"):
+        return _siglip_vision_spec(model_cfg, v)
+    for unsupported in ("attentional_pool", "attn_pooler_queries"):
         if v.get(unsupported):
             raise ValueError(f"vision_cfg.{unsupported} is not supported by this oracle")
     width = int(v.get("width", 768))
@@ -168,6 +205,40 @@ LONG_H14_CFG = {
     },
     "preprocess_cfg": {"mean": OPENAI_MEAN, "std": OPENAI_STD},
 }
+
+# ViT-SO400M-16-SigLIP2-384 (BASELINE.json configs[3]; open_clip hf-hub:timm/ViT-SO400M-16-SigLIP2-384):
+# timm trunk, 576 tokens, head dim 72, MLP 4304 (padded to 4352 on the GPU), MAP pooling.
+SIGLIP_MEAN = [0.5, 0.5, 0.5]
+SIGLIP_STD = [0.5, 0.5, 0.5]
+SO400M_16_SIGLIP2_384_CFG = {
+    "model_cfg": {
+        "embed_dim": 1152,
+        "init_logit_bias": -10,
+        "vision_cfg": {"image_size": 384, "timm_model_name": "vit_so400m_patch16_siglip_384",
+                       "timm_model_pretrained": False, "timm_pool": "map", "timm_proj": "none"},
+        "text_cfg": {"context_length": 64, "vocab_size": 256000, "width": 1152, "heads": 16, "layers": 27,
+                     "mlp_ratio": 3.7362},
+    },
+    "preprocess_cfg": {"mean": SIGLIP_MEAN, "std": SIGLIP_STD, "interpolation": "bicubic", "resize_mode": "squash"},
+}
+
+
+def tiny_siglip_cfg(image_size=64, layers=2, mlp_width=1000):
+    """SigLIP-structured synthetic config: head dim 72 (D = 576, 8 heads), MLP not a multiple of 64."""
+    return {
+        "model_cfg": {
+            "embed_dim": 576,
+            "vision_cfg": {"image_size": image_size, "timm_model_name": "vit_so400m_patch16_siglip_384",
+                           "timm_pool": "map", "timm_proj": "none",
+                           "clipgpu_dims": {"width": 576, "layers": layers, "heads": 8, "mlp_width": mlp_width}},
+            "text_cfg": {"context_length": 16, "vocab_size": 1000, "width": 128, "heads": 2, "layers": 1},
+        },
+        "preprocess_cfg": {"mean": SIGLIP_MEAN, "std": SIGLIP_STD},
+    }
+
+
+TINY_SIGLIP_CFG = tiny_siglip_cfg()
+LONG_SIGLIP_CFG = tiny_siglip_cfg(image_size=384, layers=1)  # 576 tokens
 
 # model_config.json as written by pull_onnx.py:128-150 for an OpenAI CLIP.
 OPENAI_MODEL_CONFIG = {

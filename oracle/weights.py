@@ -98,7 +98,61 @@ def _block_params(prefix: str, D: int, M: int, L: int) -> ParamList:
     ]
 
 
+def _timm_block_params(prefix: str, D: int, M: int, L: int) -> ParamList:
+    attn_std = D ** -0.5
+    proj_std = (D ** -0.5) * ((2 * L) ** -0.5)
+    fc_std = (2 * D) ** -0.5
+    return [
+        (prefix + "norm1.weight", (D,), LN_GAIN_STD, 1.0),
+        (prefix + "norm1.bias", (D,), LN_BIAS_STD, 0.0),
+        (prefix + "attn.qkv.weight", (3 * D, D), attn_std, 0.0),
+        (prefix + "attn.qkv.bias", (3 * D,), LIN_BIAS_STD, 0.0),
+        (prefix + "attn.proj.weight", (D, D), proj_std, 0.0),
+        (prefix + "attn.proj.bias", (D,), LIN_BIAS_STD, 0.0),
+        (prefix + "norm2.weight", (D,), LN_GAIN_STD, 1.0),
+        (prefix + "norm2.bias", (D,), LN_BIAS_STD, 0.0),
+        (prefix + "mlp.fc1.weight", (M, D), fc_std, 0.0),
+        (prefix + "mlp.fc1.bias", (M,), LIN_BIAS_STD, 0.0),
+        (prefix + "mlp.fc2.weight", (D, M), proj_std, 0.0),
+        (prefix + "mlp.fc2.bias", (D,), LIN_BIAS_STD, 0.0),
+    ]
+
+
+def siglip_vision_param_list(v: VisionSpec) -> ParamList:
+    """open_clip TimmModel (visual.trunk = timm VisionTransformer, global_pool 'map')."""
+    D, p, M = v.width, v.patch_size, v.mlp_width
+    t = "visual.trunk."
+    out: ParamList = [
+        (t + "patch_embed.proj.weight", (D, 3, p, p), (3 * p * p) ** -0.5, 0.0),
+        (t + "patch_embed.proj.bias", (D,), LIN_BIAS_STD, 0.0),
+        (t + "pos_embed", (1, v.grid * v.grid, D), D ** -0.5, 0.0),
+    ]
+    for i in range(v.layers):
+        out += _timm_block_params(f"{t}blocks.{i}.", D, M, v.layers)
+    a = t + "attn_pool."
+    out += [
+        (t + "norm.weight", (D,), LN_GAIN_STD, 1.0),
+        (t + "norm.bias", (D,), LN_BIAS_STD, 0.0),
+        (a + "latent", (1, 1, D), D ** -0.5, 0.0),
+        (a + "q.weight", (D, D), D ** -0.5, 0.0),
+        (a + "q.bias", (D,), LIN_BIAS_STD, 0.0),
+        (a + "kv.weight", (2 * D, D), D ** -0.5, 0.0),
+        (a + "kv.bias", (2 * D,), LIN_BIAS_STD, 0.0),
+        (a + "proj.weight", (D, D), D ** -0.5, 0.0),
+        (a + "proj.bias", (D,), LIN_BIAS_STD, 0.0),
+        (a + "norm.weight", (D,), LN_GAIN_STD, 1.0),
+        (a + "norm.bias", (D,), LN_BIAS_STD, 0.0),
+        (a + "mlp.fc1.weight", (M, D), (2 * D) ** -0.5, 0.0),
+        (a + "mlp.fc1.bias", (M,), LIN_BIAS_STD, 0.0),
+        (a + "mlp.fc2.weight", (D, M), D ** -0.5, 0.0),
+        (a + "mlp.fc2.bias", (D,), LIN_BIAS_STD, 0.0),
+    ]
+    return out
+
+
 def vision_param_list(v: VisionSpec) -> ParamList:
+    if v.family == "siglip":
+        return siglip_vision_param_list(v)
     D, p = v.width, v.patch_size
     out: ParamList = [
         ("visual.conv1.weight", (D, 3, p, p), (3 * p * p) ** -0.5, 0.0),

@@ -115,3 +115,20 @@ def test_safetensors_header_roundtrip(tmp_path):
     save_file({"visual.conv1.weight": np.zeros((3, 3), np.float32)}, os.path.join(d, "open_clip_model.safetensors"))
     with pytest.raises(ConfigError, match="unexpected shape"):
         Engine(d, 0)
+
+
+@pytest.mark.parametrize("cfg_name", ["TINY_CFG", "TINY_H14_CFG", "TINY_SIGLIP_CFG"])
+def test_param_inventory_matches_oracle(cfg_name):
+    """csrc/host/weights.cpp tower_params + synth == oracle/weights.py, parameter by parameter
+    (names, shapes, init std/offset): bit-exact through the engine's own weight loader."""
+    from oracle import model_spec
+    from open_clip_inference import _lib
+    cfg = getattr(model_spec, cfg_name)
+    d = make_model_dir(cfg, seed=4321)
+    v, t = vision_spec_from_cfg(cfg["model_cfg"]), text_spec_from_cfg(cfg["model_cfg"])
+    for tower, P in ((0, weights.vision_weights(v, 4321)), (1, weights.text_weights(t, 4321))):
+        for name, ref in P.items():
+            out = np.empty(ref.size, np.float32)
+            _lib.check(_lib.lib().clipgpu_test_read_weights(d.encode(), tower, name.encode(), out.ctypes.data,
+                                                            out.size))
+            assert np.array_equal(out, ref.ravel()), name

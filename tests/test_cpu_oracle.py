@@ -65,3 +65,26 @@ def test_oracle_properties():
     p = int(np.argmax(ids2[0]))
     ids2[0, p + 1:] = 7
     assert np.allclose(clip_ref.encode_text(PT, t, ids)[0], clip_ref.encode_text(PT, t, ids2)[0], atol=1e-12)
+
+
+@pytest.mark.parametrize("cfg_name", ["TINY_SIGLIP_CFG", "LONG_SIGLIP_CFG"])
+def test_siglip_oracle_vs_hf(cfg_name):
+    """SigLIP family (timm trunk + MAP head, BASELINE configs[3] structure) vs HF SiglipVisionModel."""
+    pytest.importorskip("transformers")
+    from oracle import hf_pin, model_spec
+    cfg = getattr(model_spec, cfg_name)
+    v = vision_spec_from_cfg(cfg["model_cfg"])
+    assert v.family == "siglip" and v.head_dim == 72 and v.tokens == v.grid ** 2
+    P = weights.vision_weights(v, 5)
+    px = pixels(v, 2)
+    got = clip_ref.encode_image(P, v, px)
+    ref = hf_pin.hf_siglip_encode_image(hf_pin.hf_siglip_vision(P, v), px)
+    assert np.abs(got - ref).max() < 1e-7
+
+
+def test_so400m_siglip2_spec():
+    from oracle import model_spec
+    v = vision_spec_from_cfg(model_spec.SO400M_16_SIGLIP2_384_CFG["model_cfg"])
+    assert (v.patch_size, v.width, v.layers, v.heads, v.mlp_width, v.tokens, v.head_dim) == \
+        (16, 1152, 27, 16, 4304, 576, 72)
+    assert v.act == "gelu_tanh" and v.ln_eps == 1e-6 and v.embed_dim == 1152

@@ -11,7 +11,8 @@ import numpy as np
 import pytest
 
 from oracle import clip_ref, weights
-from oracle.model_spec import (LONG_H14_CFG, OPENAI_MEAN, OPENAI_STD, TINY_CFG, TINY_H14_CFG, VIT_B_32_CFG,
+from oracle.model_spec import (LONG_H14_CFG, LONG_SIGLIP_CFG, OPENAI_MEAN, OPENAI_STD, SIGLIP_MEAN, SIGLIP_STD,
+                               SO400M_16_SIGLIP2_384_CFG, TINY_CFG, TINY_H14_CFG, TINY_SIGLIP_CFG, VIT_B_32_CFG,
                                VIT_H_14_378_CFG)
 from tests.helpers import COS_TOL, make_model_dir, normalized_pixels, specs
 
@@ -262,3 +263,25 @@ def test_vit_h14_378_full_dims():
                                   random_eot=True)
     te = engine(VIT_H_14_378_CFG, 1, max_batch=3)
     check_rows(te.embed_tokens(ids), oracle_text(VIT_H_14_378_CFG, 1234, ids))
+
+
+@pytest.mark.parametrize("cfg,B", [(TINY_SIGLIP_CFG, 3), (LONG_SIGLIP_CFG, 2)])
+@pytest.mark.parametrize("dtype", ["bf16", "f16"])
+def test_siglip_structure_parity(cfg, B, dtype):
+    """SigLIP family (BASELINE configs[3] structure): timm trunk names, patch-conv bias, no class
+    token, head dim 72, MLP 1000 -> 1024 zero-padded, tanh-GELU, eps 1e-6, MAP head; up to 576 tokens."""
+    v, _ = specs(cfg)
+    u8 = weights.synth_images_u8(51 + B, B, v.image_size)
+    px = normalized_pixels(u8, SIGLIP_MEAN, SIGLIP_STD)
+    e = engine(cfg, 0, dtype=dtype)
+    got = e.embed_pixels(px)
+    check_rows(got, oracle_vision(cfg, 1234, px))
+    assert np.array_equal(got, e.embed_u8(u8, SIGLIP_MEAN, SIGLIP_STD))
+
+
+def test_so400m_siglip2_384_full_dims():
+    """ViT-SO400M-16-SigLIP2-384 vision at full size (27 x 1152, 576 tokens, MLP 4304) vs the oracle."""
+    v, _ = specs(SO400M_16_SIGLIP2_384_CFG)
+    px = normalized_pixels(weights.synth_images_u8(7, 2, v.image_size), SIGLIP_MEAN, SIGLIP_STD)
+    e = engine(SO400M_16_SIGLIP2_384_CFG, 0, max_batch=2)
+    check_rows(e.embed_pixels(px), oracle_vision(SO400M_16_SIGLIP2_384_CFG, 1234, px))
