@@ -22,7 +22,9 @@
 //   4. folded token constants: open_clip's _expand_token(class_embedding).to(dtype)
 //      becomes "onnx::Expand_N" [1,1,D] under the tower's Expand node, and
 //      positional_embedding.to(dtype) becomes "onnx::Add_N" [T,D] under the tower
-//      root's Add node (visual: "/visual/Add", text: "/Add").
+//      root's Add node (visual: "/visual/Add", text: "/Add"); for the timm trunk of
+//      the SigLIP family: "/visual/trunk/Add" (pos_embed) and the attn_pool Expand
+//      (latent).  timm Linear leaves (qkv, proj, fc1, fc2, q, kv) fold like c_fc.
 // The graph is not otherwise interpreted: the engine implements the tower itself.
 #include <fcntl.h>
 #include <sys/mman.h>
@@ -375,16 +377,20 @@ TensorMap load_onnx(const std::string& path, const TowerSpec& spec) {
     // tower root's Expand / Add node
     if ((n.op == "Expand" || n.op == "Add") && !n.inputs.empty()) {
       const std::string mod = module_path(n.name);
-      if (mod == "visual" || mod.empty()) {
-        const std::string pre = mod.empty() ? std::string() : mod + ".";
+      std::string param;
+      if (mod == "visual" || mod.empty())  // open_clip VisionTransformer / text root
+        param = (mod.empty() ? std::string() : mod + ".") + (n.op == "Expand" ? "class_embedding" : "positional_embedding");
+      else if (mod == "visual.trunk" && n.op == "Add")  // timm _pos_embed
+        param = "visual.trunk.pos_embed";
+      else if (mod.size() >= 9 && mod.compare(mod.size() - 9, 9, "attn_pool") == 0 && n.op == "Expand")
+        param = mod + ".latent";  // timm AttentionPoolLatent latent.expand(B, -1, -1)
+      if (!param.empty())
         for (const std::string& in : n.inputs) {
           auto it = by_name.find(in);
           if (it == by_name.end()) continue;
-          folded.emplace(pre + (n.op == "Expand" ? "class_embedding" : "positional_embedding"),
-                         std::make_pair(it->second, false));
+          folded.emplace(param, std::make_pair(it->second, false));
           break;
         }
-      }
       continue;
     }
     if ((n.op != "MatMul" && n.op != "Gemm") || n.inputs.size() < 2) continue;
@@ -395,8 +401,15 @@ TensorMap load_onnx(const std::string& path, const TowerSpec& spec) {
     const size_t dot = mod.find_last_of('.');
     const std::string leaf = dot == std::string::npos ? mod : mod.substr(dot + 1);
     const bool tr = n.op == "MatMul" || n.transB == 0;
-    if (leaf == "attn") folded.emplace(mod + ".in_proj_weight", std::make_pair(it->second, tr));
-    else if (leaf == "c_fc" || leaf == "c_proj" || leaf == "out_proj") folded.emplace(mod + ".weight", std::make_pair(it->second, tr));
+    // open_clip: attn (nn.MultiheadAttention in_proj), c_fc, c_proj, out_proj;
+    // timm: attn.qkv, attn.proj, mlp.fc1, mlp.fc2, attn_pool.q / kv / proj
+    static const char* linear_leaves[] = {"c_fc", "c_proj", "out_proj", "qkv", "proj", "fc1", "fc2", "q", "kv"};
+    if (leaf == "attn") {
+      folded.emplace(mod + ".in_proj_weight", std::make_pair(it->second, tr));
+    } else {
+      for (const char* lf : linear_leaves)
+        if (leaf == lf) folded.emplace(mod + ".weight", std::make_pair(it->second, tr));
+    }
   }
   auto find = [&](const std::string& name, bool& tr) -> const TensorRec* {
     tr = false;

@@ -106,6 +106,141 @@ class ClipModel(nn.Module):
         return nn.functional.normalize(x, dim=-1) if normalize else x
 
 
+# ---- timm SigLIP ViT trunk (open_clip TimmModel, timm_pool "map", timm_proj "none") ------------
+# timm is not installed here: restated with timm's attribute names (VisionTransformer:
+# patch_embed.proj, pos_embed, blocks[i].{norm1, attn.{qkv, proj}, norm2, mlp.{fc1, act, fc2}},
+# norm, attn_pool.{latent, q, kv, proj, norm, mlp.{fc1, fc2}}) and forward order.
+
+class TimmMlp(nn.Module):
+    def __init__(self, d, hidden):
+        super().__init__()
+        self.fc1 = nn.Linear(d, hidden)
+        self.act = nn.GELU(approximate="tanh")
+        self.fc2 = nn.Linear(hidden, d)
+
+    def forward(self, x):
+        return self.fc2(self.act(self.fc1(x)))
+
+
+class TimmAttention(nn.Module):
+    def __init__(self, d, heads):
+        super().__init__()
+        self.heads = heads
+        self.qkv = nn.Linear(d, 3 * d)
+        self.proj = nn.Linear(d, d)
+
+    def forward(self, x):
+        B, N, C = x.shape
+        qkv = self.qkv(x).reshape(B, N, 3, self.heads, C // self.heads).permute(2, 0, 3, 1, 4)
+        q, k, v = qkv.unbind(0)
+        x = nn.functional.scaled_dot_product_attention(q, k, v)
+        return self.proj(x.transpose(1, 2).reshape(B, N, C))
+
+
+class TimmBlock(nn.Module):
+    def __init__(self, d, heads, hidden):
+        super().__init__()
+        self.norm1 = nn.LayerNorm(d, eps=1e-6)
+        self.attn = TimmAttention(d, heads)
+        self.norm2 = nn.LayerNorm(d, eps=1e-6)
+        self.mlp = TimmMlp(d, hidden)
+
+    def forward(self, x):
+        x = x + self.attn(self.norm1(x))
+        return x + self.mlp(self.norm2(x))
+
+
+class PatchEmbed(nn.Module):
+    def __init__(self, p, d):
+        super().__init__()
+        self.proj = nn.Conv2d(3, d, p, p, bias=True)
+
+    def forward(self, x):
+        return self.proj(x).flatten(2).transpose(1, 2)
+
+
+class AttentionPoolLatent(nn.Module):
+    def __init__(self, d, heads, hidden):
+        super().__init__()
+        self.heads = heads
+        self.latent = nn.Parameter(torch.zeros(1, 1, d))
+        self.q = nn.Linear(d, d)
+        self.kv = nn.Linear(d, 2 * d)
+        self.proj = nn.Linear(d, d)
+        self.norm = nn.LayerNorm(d, eps=1e-6)
+        self.mlp = TimmMlp(d, hidden)
+
+    def forward(self, x):
+        B, N, C = x.shape
+        hd = C // self.heads
+        q = self.q(self.latent.expand(B, -1, -1)).reshape(B, 1, self.heads, hd).transpose(1, 2)
+        kv = self.kv(x).reshape(B, N, 2, self.heads, hd).permute(2, 0, 3, 1, 4)
+        k, v = kv.unbind(0)
+        x = nn.functional.scaled_dot_product_attention(q, k, v)
+        x = self.proj(x.transpose(1, 2).reshape(B, 1, C))
+        x = x + self.mlp(self.norm(x))
+        return x[:, 0]
+
+
+class TimmSiglipViT(nn.Module):
+    def __init__(self, v):
+        super().__init__()
+        D = v.width
+        self.patch_embed = PatchEmbed(v.patch_size, D)
+        self.pos_embed = nn.Parameter(torch.zeros(1, v.grid * v.grid, D))
+        self.blocks = nn.ModuleList([TimmBlock(D, v.heads, v.mlp_width) for _ in range(v.layers)])
+        self.norm = nn.LayerNorm(D, eps=1e-6)
+        self.attn_pool = AttentionPoolLatent(D, v.heads, v.mlp_width)
+
+    def forward(self, x):
+        x = self.patch_embed(x)
+        x = x + self.pos_embed
+        for b in self.blocks:
+            x = b(x)
+        return self.attn_pool(self.norm(x))
+
+
+class TimmModel(nn.Module):  # open_clip TimmModel with an empty head (timm_proj "none")
+    def __init__(self, v):
+        super().__init__()
+        self.trunk = TimmSiglipViT(v)
+
+    def forward(self, x):
+        return self.trunk(x)
+
+
+class SiglipVisionOnly(nn.Module):
+    def __init__(self, v):
+        super().__init__()
+        self.visual = TimmModel(v)
+
+    def encode_image(self, x, normalize=False):
+        f = self.visual(x)
+        return nn.functional.normalize(f, dim=-1) if normalize else f
+
+
+def build_siglip_vision(v, seed):
+    from oracle import weights
+    m = SiglipVisionOnly(v).eval()
+    P = weights.vision_weights(v, seed)
+    sd = m.state_dict()
+    assert set(sd) == set(P), set(sd) ^ set(P)
+    m.load_state_dict({k: torch.from_numpy(np.asarray(P[k], np.float32)) for k in sd})
+    return m
+
+
+def export_siglip_visual(d, v, seed, external=False):
+    import warnings
+    m = build_siglip_vision(v, seed)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        _export(VisualWrapper(m), torch.randn(2, 3, v.image_size, v.image_size), os.path.join(d, "visual.onnx"),
+                "pixel_values", "image_embeddings")
+    if external:
+        externalize(os.path.join(d, "visual.onnx"))
+    return m
+
+
 class VisualWrapper(nn.Module):  # pull_onnx.py VisualWrapper
     def __init__(self, model):
         super().__init__()

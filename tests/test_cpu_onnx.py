@@ -91,3 +91,31 @@ def test_onnx_missing_tensor_error(tmp_path):
         _lib.check(_lib.lib().clipgpu_test_read_weights(str(d).encode(), 0,
                                                         b"visual.transformer.resblocks.2.ln_1.weight",
                                                         out.ctypes.data, 4))
+
+
+@pytest.mark.parametrize("external", [False, True])
+def test_onnx_siglip_weights_bit_exact(tmp_path, external):
+    """SigLIP family (timm trunk names): folded qkv/proj/fc1/fc2/q/kv MatMul weights, pos_embed,
+    attn_pool latent, through a real torch.onnx.export of the restated timm module tree."""
+    from oracle.model_spec import TINY_SIGLIP_CFG
+    from tests.onnx_export import build_siglip_vision, export_siglip_visual
+    d = tmp_path / "siglip"
+    d.mkdir()
+    with open(d / "open_clip_config.json", "w") as f:
+        json.dump(TINY_SIGLIP_CFG, f)
+    with open(d / "model_config.json", "w") as f:
+        json.dump(OPENAI_MODEL_CONFIG, f)
+    v, _ = specs(TINY_SIGLIP_CFG)
+    export_siglip_visual(str(d), v, seed=78, external=external)
+    names = initializer_names(os.path.join(d, "visual.onnx"))
+    assert any(n.startswith("onnx::MatMul") for n in names), names
+    for name, ref in weights.vision_weights(v, 78).items():
+        got = _read(str(d), 0, name, ref.shape)
+        assert np.array_equal(got, ref.astype(np.float32)), name
+    # the restated timm module tree also pins the oracle
+    m = build_siglip_vision(v, 78)
+    px = normalized_pixels(weights.synth_images_u8(5, 2, v.image_size), [0.5] * 3, [0.5] * 3)
+    with torch.no_grad():
+        got = m.encode_image(torch.from_numpy(px), normalize=True).double().numpy()
+    ref = clip_ref.encode_image(weights.vision_weights(v, 78), v, px)
+    assert clip_ref.cosine_rows(got, ref).min() > 1 - 1e-6
