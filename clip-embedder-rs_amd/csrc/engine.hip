@@ -84,6 +84,7 @@ struct Replica {
   // rounds and memory-bound kernels overlap the other lane's GEMMs.
   hipStream_t lane[4] = {nullptr, nullptr, nullptr, nullptr};
   hipEvent_t fork = nullptr, join[4] = {nullptr, nullptr, nullptr, nullptr};
+  hipEvent_t done[4] = {nullptr, nullptr, nullptr, nullptr};  // host path: slot's D2H finished
 };
 
 }  // namespace clipgpu
@@ -350,7 +351,9 @@ void upload_weights(clipgpu_engine& e, Replica& r, const TensorMap& m) {
 
 void alloc_workspace(clipgpu_engine& e, Replica& r) {
   const TowerSpec& s = e.spec;
-  const size_t B = (size_t)e.max_batch, rows = B * (size_t)s.tokens(), D = s.width;
+  // lanes x ceil(max_batch / lanes) rows: every host-path slot (run_host_shard) is whole
+  const size_t B = (size_t)((e.max_batch + e.lanes - 1) / e.lanes * e.lanes);
+  const size_t rows = B * (size_t)s.tokens(), D = s.width;
   const size_t wide = std::max((size_t)3 * D, (size_t)mlp_pad(s));
   const size_t E = s.embed_dim;
   const size_t sizes[] = {rows * D * 4, rows * D * 2, rows * wide * 2, B * D * 2, B * E * 4, B * E * 4,
@@ -370,6 +373,7 @@ void alloc_workspace(clipgpu_engine& e, Replica& r) {
   for (int i = 0; i < e.lanes; ++i) {
     HIP_CHECK(hipStreamCreateWithFlags(&r.lane[i], hipStreamNonBlocking));
     HIP_CHECK(hipEventCreateWithFlags(&r.join[i], hipEventDisableTiming));
+    HIP_CHECK(hipEventCreateWithFlags(&r.done[i], hipEventDisableTiming));
   }
   HIP_CHECK(hipEventCreateWithFlags(&r.fork, hipEventDisableTiming));
   HIP_CHECK(hipHostMalloc(&r.pin_in, B * e.in_bytes_per_row, hipHostMallocDefault));
@@ -676,23 +680,65 @@ void text_forward_lanes(const clipgpu_engine& e, const Replica& r, const int64_t
 
 enum InKind { IN_F32 = 0, IN_U8 = 1, IN_IDS = 2 };
 
-// Host-buffer forward over a row range of one replica, chunked by max_batch.
+// Host -> pinned staging copy, split over a few threads when large (one thread moves
+// ~10 GB/s; a 128-image f32 sub-chunk is 77 MB).
+void par_memcpy(void* dst, const void* src, size_t n) {
+  const size_t kMin = 4u << 20;
+  const int nt = (int)std::min<size_t>(8, std::max<size_t>(1, n / kMin));
+  if (nt == 1) {
+    std::memcpy(dst, src, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  const size_t per = (n + nt - 1) / nt;
+  for (int t = 0; t < nt; ++t) {
+    const size_t o = (size_t)t * per;
+    if (o >= n) break;
+    th.emplace_back([=]() { std::memcpy((char*)dst + o, (const char*)src + o, std::min(per, n - o)); });
+  }
+  for (auto& t : th) t.join();
+}
+
+// Host-buffer forward over a row range of one replica.  Pipelined over sub-chunks of one
+// lane each (max_batch / lanes rows): sub-chunk j uses slot j % lanes -- its lane's stream,
+// its rows of the pinned staging / device input / output buffers and its workspace view --
+// so the host copy of sub-chunk j+1 and its H2D overlap the forward of sub-chunk j.  A slot
+// is reused after its previous sub-chunk's D2H event, whose rows are then copied out.
 void run_host_shard(clipgpu_engine& e, Replica& r, InKind kind, const void* in, size_t in_row_bytes, int64_t b0,
                     int64_t b1, const float* mean, const float* stdv, float* out) {
   HIP_CHECK(hipSetDevice(r.device));
-  const int E = e.spec.embed_dim;
-  for (int64_t c0 = b0; c0 < b1; c0 += e.max_batch) {
-    const int n = (int)std::min<int64_t>(e.max_batch, b1 - c0);
-    std::memcpy(r.pin_in, (const char*)in + c0 * in_row_bytes, (size_t)n * in_row_bytes);
-    HIP_CHECK(hipMemcpyAsync(r.in, r.pin_in, (size_t)n * in_row_bytes, hipMemcpyHostToDevice, r.stream));
+  const int E = e.spec.embed_dim, L = e.lanes;
+  const int S = (e.max_batch + L - 1) / L;  // rows per slot
+  struct Pending { int64_t c0 = -1; int n = 0; };
+  Pending pend[4];
+  auto drain = [&](int k) {
+    if (pend[k].c0 < 0) return;
+    HIP_CHECK(hipEventSynchronize(r.done[k]));
+    std::memcpy(out + pend[k].c0 * E, r.pin_out + (size_t)k * S * E, (size_t)pend[k].n * E * 4);
+    pend[k].c0 = -1;
+  };
+  int j = 0;
+  for (int64_t c0 = b0; c0 < b1; c0 += S, ++j) {
+    const int k = j % L;
+    const int n = (int)std::min<int64_t>(S, b1 - c0);
+    drain(k);
+    hipStream_t st = r.lane[k] ? r.lane[k] : r.stream;
+    char* pin = (char*)r.pin_in + (size_t)k * S * in_row_bytes;
+    char* din = (char*)r.in + (size_t)k * S * in_row_bytes;
+    float* dout = r.out + (size_t)k * S * E;
+    par_memcpy(pin, (const char*)in + c0 * in_row_bytes, (size_t)n * in_row_bytes);
+    HIP_CHECK(hipMemcpyAsync(din, pin, (size_t)n * in_row_bytes, hipMemcpyHostToDevice, st));
+    const Replica v = lane_view(e, r, k * S);
     if (kind == IN_IDS)
-      text_forward_lanes(e, r, (const int64_t*)r.in, n, r.out, r.stream);
+      text_forward(e, v, (const int64_t*)din, n, dout, st);
     else
-      vision_forward_lanes(e, r, r.in, kind == IN_F32 ? A_IMG_F32 : A_IMG_U8, mean, stdv, n, r.out, r.stream);
-    HIP_CHECK(hipMemcpyAsync(r.pin_out, r.out, (size_t)n * E * 4, hipMemcpyDeviceToHost, r.stream));
-    HIP_CHECK(hipStreamSynchronize(r.stream));
-    std::memcpy(out + c0 * E, r.pin_out, (size_t)n * E * 4);
+      vision_forward(e, v, din, kind == IN_F32 ? A_IMG_F32 : A_IMG_U8, mean, stdv, n, dout, st);
+    HIP_CHECK(hipMemcpyAsync(r.pin_out + (size_t)k * S * E, dout, (size_t)n * E * 4, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipEventRecord(r.done[k], st));
+    pend[k].c0 = c0;
+    pend[k].n = n;
   }
+  for (int k = 0; k < L; ++k) drain(k);
 }
 
 void run_host(clipgpu_engine& e, InKind kind, const void* in, size_t in_row_bytes, int64_t B, const float* mean,
@@ -737,6 +783,7 @@ void destroy_replica(Replica& r) {
   for (int i = 0; i < 4; ++i) {
     if (r.lane[i]) (void)hipStreamDestroy(r.lane[i]);
     if (r.join[i]) (void)hipEventDestroy(r.join[i]);
+    if (r.done[i]) (void)hipEventDestroy(r.done[i]);
   }
   if (r.fork) (void)hipEventDestroy(r.fork);
   r = Replica();

@@ -1,0 +1,101 @@
+#!/usr/bin/env python3
+"""Throughput of the BASELINE.json large configs and of the host-buffer path (1 GPU).
+
+Not the bench.py contract line: configs[3] / configs[4] are parity-test cases there.  Reported
+here per GPU at the per-GPU share of the BASELINE batch (SO400M-16-SigLIP2-384 vision 1024 / 8 =
+128 images, DFN5B ViT-H/14-378 vision + text 512 / 8 = 64), device-resident inputs, seeded
+weights, plus ViT-B/32 through the HOST entry points (u8 / f32 host buffers, pinned staging,
+H2D + D2H included: the PCIe-inclusive rate SURVEY.md §8d asks to report beside the device one).
+Prints one JSON line per measurement.
+"""
+import json
+import os
+import sys
+import tempfile
+import time
+
+import numpy as np
+import torch  # noqa: F401  (one HIP runtime per process: torch before the native lib)
+
+ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "clip-embedder-rs_amd"))
+
+from open_clip_inference import _lib  # noqa: E402
+from open_clip_inference.engine import Engine  # noqa: E402
+from oracle.model_spec import (OPENAI_MODEL_CONFIG, SO400M_16_SIGLIP2_384_CFG, VIT_B_32_CFG,  # noqa: E402
+                               VIT_H_14_378_CFG)
+
+GFLOP = {"so400m_vision": 518.9, "h14_vision": 1007.0, "h14_text": 47.1, "b32_vision": 8.818}
+
+
+def model_dir(cfg):
+    d = tempfile.mkdtemp(prefix="clipgpu_models_")
+    for name, obj in (("open_clip_config.json", cfg), ("model_config.json", OPENAI_MODEL_CONFIG),
+                      ("clipgpu_synthetic.json", {"seed": 7})):
+        with open(os.path.join(d, name), "w") as f:
+            json.dump(obj, f)
+    return d
+
+
+def timed(fn, steps, warmup):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps
+
+
+def device_leg(name, cfg, tower, B, steps=6, warmup=2):
+    d = model_dir(cfg)
+    e = Engine(d, tower, [0], "bf16", B)
+    s = torch.cuda.current_stream()
+    mc = cfg["model_cfg"]
+    E = mc["embed_dim"]
+    out = torch.empty((B, E), device="cuda")
+    if tower == 0:
+        S = mc["vision_cfg"]["image_size"]
+        x = torch.randn((B, 3, S, S), device="cuda")
+        fn = lambda: e.embed_pixels_device(x.data_ptr(), B, out.data_ptr(), s.cuda_stream)  # noqa: E731
+    else:
+        T, V = mc["text_cfg"]["context_length"], mc["text_cfg"]["vocab_size"]
+        ids = torch.randint(0, V - 2, (B, T), device="cuda", dtype=torch.int64)
+        ids[:, -1] = V - 1
+        fn = lambda: e.embed_tokens_device(ids.data_ptr(), B, out.data_ptr(), s.cuda_stream)  # noqa: E731
+    dt = timed(fn, steps, warmup)
+    rate = B / dt
+    print(json.dumps({"measure": name, "batch_per_gpu": B, "units_per_s": round(rate, 1),
+                      "ms_per_step": round(dt * 1e3, 3), "model_tflops": round(rate * GFLOP[name] / 1e3, 1),
+                      "frac_of_2500": round(rate * GFLOP[name] / 1e3 / 2500, 4), "input": "device-resident"}),
+          flush=True)
+    e.close()
+
+
+def host_leg(B=256, steps=6, warmup=2):
+    d = model_dir(VIT_B_32_CFG)
+    e = Engine(d, 0, [0], "bf16", B)
+    rng = np.random.default_rng(0)
+    u8 = rng.integers(0, 256, (B, 224, 224, 3), dtype=np.uint8)
+    mean, std = VIT_B_32_CFG["preprocess_cfg"]["mean"], VIT_B_32_CFG["preprocess_cfg"]["std"]
+    px = ((u8.astype(np.float32) / 255 - np.asarray(mean, np.float32)) / np.asarray(std, np.float32))
+    px = np.ascontiguousarray(px.transpose(0, 3, 1, 2))
+    for kind, fn in (("host_u8", lambda: e.embed_u8(u8, mean, std)), ("host_f32", lambda: e.embed_pixels(px))):
+        dt = timed(fn, steps, warmup)
+        print(json.dumps({"measure": "b32_vision_" + kind, "batch": B, "units_per_s": round(B / dt, 1),
+                          "ms_per_step": round(dt * 1e3, 3),
+                          "input": "host buffer (pinned staging + H2D/D2H inside the timing)"}), flush=True)
+    e.close()
+
+
+if __name__ == "__main__":
+    which = sys.argv[1:] or ["host", "so400m", "h14"]
+    if "host" in which:
+        host_leg()
+    if "so400m" in which:
+        device_leg("so400m_vision", SO400M_16_SIGLIP2_384_CFG, 0, 128)
+    if "h14" in which:
+        device_leg("h14_vision", VIT_H_14_378_CFG, 0, 64)
+        device_leg("h14_text", VIT_H_14_378_CFG, 1, 64)
