@@ -71,6 +71,7 @@ struct Replica {
   char* work = nullptr;   // activations
   DevWeights w;
   float* x = nullptr;     // [rows][D] f32 residual stream
+  float* slab = nullptr;  // [rows][D] f32 split-K partial of out_proj / c_proj (engine.ksplit == 2)
   void* h = nullptr;      // [rows][D] 16-bit (LN output / attention output)
   void* big = nullptr;    // [rows][max(3D, MLP)] 16-bit (qkv / MLP hidden)
   void* pooled = nullptr; // [B][D] 16-bit
@@ -119,8 +120,15 @@ struct clipgpu_engine {
   // GEMM tile per trunk call site (clipgpu::GemmSite), autotuned at creation for
   // max_batch rows; batches under half of that use the shape heuristic.
   int tile[4] = {0, 0, 0, 0};
+  int tile_patch = 0;  // vision: the patch-embedding GEMM (tuned with the trunk sites)
   int tuned_rows = 0;
   int lanes = 1;  // concurrent sub-batches per device (CLIPGPU_LANES, default 2)
+  // K-slices of the N = width GEMMs (out_proj, c_proj): CLIPGPU_GEMM_SPLIT=1 -> 2, else 1.
+  // Fixed per engine, independent of the batch and lane split, so outputs stay
+  // bit-identical across both; the second slice's partial is added by the next LayerNorm.
+  // Off by default: measured slower at ViT-B/32 lane sizes (profiles/r01_v6_split_sweep.txt:
+  // the extra f32 slab round trip costs more than the better CU fill returns).
+  int ksplit = 1;
   clipgpu::TowerSpec spec;
   clipgpu::PreprocessCfg pre;
   clipgpu::DType dt = clipgpu::DT_BF16;
@@ -142,6 +150,17 @@ inline int round64(int n) { return (n + 63) / 64 * 64; }
 inline int mlp_pad(const TowerSpec& s) { return round64(s.mlp_width); }
 inline int kpatch(const TowerSpec& s) { return 3 * s.patch_size * s.patch_size; }
 inline int kpatch_pad(const TowerSpec& s) { return round64(kpatch(s)); }
+// Elements per token row of the `big` scratch: QKV (3D), the MLP hidden width, and for
+// the vision tower also the staged patch rows (G^2 rows of kpatch_pad per image, which
+// the patch GEMM consumes before layer 0 writes QKV).
+inline size_t big_wide(const TowerSpec& s) {
+  size_t w = std::max((size_t)3 * s.width, (size_t)mlp_pad(s));
+  if (s.tower == TOWER_VISION) {
+    const size_t G = (size_t)s.image_size / s.patch_size, T = (size_t)s.tokens();
+    w = std::max(w, (G * G * (size_t)kpatch_pad(s) + T - 1) / T);
+  }
+  return w;
+}
 
 bool file_exists(const std::string& p) {
   struct stat st;
@@ -354,10 +373,10 @@ void alloc_workspace(clipgpu_engine& e, Replica& r) {
   // lanes x ceil(max_batch / lanes) rows: every host-path slot (run_host_shard) is whole
   const size_t B = (size_t)((e.max_batch + e.lanes - 1) / e.lanes * e.lanes);
   const size_t rows = B * (size_t)s.tokens(), D = s.width;
-  const size_t wide = std::max((size_t)3 * D, (size_t)mlp_pad(s));
+  const size_t wide = big_wide(s);
   const size_t E = s.embed_dim;
   const size_t sizes[] = {rows * D * 4, rows * D * 2, rows * wide * 2, B * D * 2, B * E * 4, B * E * 4,
-                          B * e.in_bytes_per_row};
+                          B * e.in_bytes_per_row, e.ksplit > 1 ? rows * D * 4 : 0};
   size_t total = 0;
   for (size_t z : sizes) total += align256(z);
   HIP_CHECK(hipMalloc(&r.work, total));
@@ -370,6 +389,7 @@ void alloc_workspace(clipgpu_engine& e, Replica& r) {
   r.emb = (float*)a.take(sizes[4]);
   r.out = (float*)a.take(sizes[5]);
   r.in = a.take(sizes[6]);
+  r.slab = e.ksplit > 1 ? (float*)a.take(sizes[7]) : nullptr;
   for (int i = 0; i < e.lanes; ++i) {
     HIP_CHECK(hipStreamCreateWithFlags(&r.lane[i], hipStreamNonBlocking));
     HIP_CHECK(hipEventCreateWithFlags(&r.join[i], hipEventDisableTiming));
@@ -427,15 +447,26 @@ GemmParams rows_gemm(const void* A, long lda, const void* W, const float* bias, 
 }
 
 int site_epi(int site) { return (site == GS_OUT || site == GS_PROJ) ? EPI_RESID : EPI_STORE16; }
+inline bool site_split(const clipgpu_engine& e, int site) {
+  if (e.ksplit < 2 || (site != GS_OUT && site != GS_PROJ)) return false;
+  const int K = site == GS_OUT ? e.spec.width : mlp_pad(e.spec);
+  return K % (64 * e.ksplit) == 0 && K / e.ksplit >= 128;  // >= 2 K-steps per slice
+}
 
 GemmParams site_gemm(const clipgpu_engine& e, const Replica& r, const LayerW& L, int site, int rows) {
   const int D = e.spec.width, MLP = mlp_pad(e.spec);
+  GemmParams g;
   switch (site) {
-    case GS_QKV: return rows_gemm(r.h, D, L.wqkv, L.bqkv, r.big, 3 * D, rows, 3 * D, D);
-    case GS_OUT: return rows_gemm(r.h, D, L.wo, L.bo, r.x, D, rows, D, D);
-    case GS_FC: return rows_gemm(r.h, D, L.w1, L.b1, r.big, MLP, rows, MLP, D);
-    default: return rows_gemm(r.big, MLP, L.w2, L.b2, r.x, D, rows, D, MLP);
+    case GS_QKV: g = rows_gemm(r.h, D, L.wqkv, L.bqkv, r.big, 3 * D, rows, 3 * D, D); break;
+    case GS_OUT: g = rows_gemm(r.h, D, L.wo, L.bo, r.x, D, rows, D, D); break;
+    case GS_FC: g = rows_gemm(r.h, D, L.w1, L.b1, r.big, MLP, rows, MLP, D); break;
+    default: g = rows_gemm(r.big, MLP, L.w2, L.b2, r.x, D, rows, D, MLP); break;
   }
+  if (site_split(e, site)) {
+    g.ksplit = e.ksplit;
+    g.slab = r.slab;
+  }
+  return g;
 }
 
 // The transformer trunk shared by both towers: L x [LN1 -> QKV -> MHA -> out+res ->
@@ -457,12 +488,14 @@ void trunk(const clipgpu_engine& e, const Replica& r, int B, int causal, hipStre
       check(launch_attention(e.dt, r.big, r.h, B, T, s.heads, D, causal, st), "attention"); }
     gemm(GS_OUT, PC_OUT_PROJ, "out_proj gemm");
     { ProfScope ps(e, PC_LN, st);
-      check(launch_ln_rows(e.dt, r.x, L.ln2_w, L.ln2_b, s.ln_eps, r.h, rows, D, st), "ln_2"); }
+      check(launch_ln_rows_add(e.dt, r.x, site_split(e, GS_OUT) ? r.slab : nullptr, L.ln2_w, L.ln2_b, s.ln_eps, r.h,
+                               rows, D, st), "ln_2"); }
     gemm(GS_FC, PC_C_FC, "c_fc gemm");
     gemm(GS_PROJ, PC_C_PROJ, "c_proj gemm");
-    if (l + 1 < s.layers) {
+    if (l + 1 < s.layers) {  // (the last c_proj's slab is added by the head's first LayerNorm)
       ProfScope ps(e, PC_LN, st);
-      check(launch_ln_rows(e.dt, r.x, r.w.layers[l + 1].ln1_w, r.w.layers[l + 1].ln1_b, s.ln_eps, r.h, rows, D, st), "ln_1");
+      check(launch_ln_rows_add(e.dt, r.x, site_split(e, GS_PROJ) ? r.slab : nullptr, r.w.layers[l + 1].ln1_w,
+                               r.w.layers[l + 1].ln1_b, s.ln_eps, r.h, rows, D, st), "ln_1");
     }
   }
 }
@@ -493,18 +526,16 @@ void autotune_tiles(clipgpu_engine& e, Replica& r) {
   hipEvent_t a, b;
   HIP_CHECK(hipEventCreate(&a));
   HIP_CHECK(hipEventCreate(&b));
-  const LayerW& L = r.w.layers[0];
-  for (int site = 0; site < GS_N; ++site) {
+  auto tune = [&](GemmParams g, int epi, int act) {
     float best = 1e30f;
     int best_tile = TILE_AUTO;
     for (int t : cands) {
-      GemmParams g = site_gemm(e, r, L, site, rows);
+      if (g.ksplit > 1 && t == TILE_128x128) continue;  // split-K runs pipelined tiles only
       g.tile = t;
-      const int act = site == GS_FC ? e.spec.act : ACT_NONE;
-      check(launch_gemm(e.dt, A_ROWS, site_epi(site), act, g, r.stream), "autotune gemm");
+      check(launch_gemm(e.dt, A_ROWS, epi, act, g, r.stream), "autotune gemm");
       HIP_CHECK(hipEventRecord(a, r.stream));
       const int iters = 4;
-      for (int i = 0; i < iters; ++i) check(launch_gemm(e.dt, A_ROWS, site_epi(site), act, g, r.stream), "autotune gemm");
+      for (int i = 0; i < iters; ++i) check(launch_gemm(e.dt, A_ROWS, epi, act, g, r.stream), "autotune gemm");
       HIP_CHECK(hipEventRecord(b, r.stream));
       HIP_CHECK(hipEventSynchronize(b));
       float ms = 0.f;
@@ -514,7 +545,19 @@ void autotune_tiles(clipgpu_engine& e, Replica& r) {
         best_tile = t;
       }
     }
-    e.tile[site] = best_tile;
+    return best_tile;
+  };
+  const LayerW& L = r.w.layers[0];
+  for (int site = 0; site < GS_N; ++site)
+    e.tile[site] = tune(site_gemm(e, r, L, site, rows), site_epi(site), site == GS_FC ? e.spec.act : ACT_NONE);
+  if (e.spec.tower == TOWER_VISION) {
+    const TowerSpec& s = e.spec;
+    const int G = s.grid(), Kp = kpatch_pad(s), lane_b = rows / s.tokens();
+    GemmParams g = rows_gemm(r.big, Kp, r.w.conv_w, r.w.conv_b, r.x, s.width, lane_b * G * G, s.width, Kp);
+    g.G = G;
+    g.pos = r.w.pos;
+    g.cls = s.cls() ? 1 : 0;
+    e.tile_patch = tune(g, EPI_PATCH, ACT_NONE);
   }
   (void)hipEventDestroy(a);
   (void)hipEventDestroy(b);
@@ -524,7 +567,8 @@ void head(const clipgpu_engine& e, const Replica& r, int B, const int64_t* ids, 
   const TowerSpec& s = e.spec;
   const int D = s.width, E = s.embed_dim;
   ProfScope ps(e, PC_HEAD, st);
-  check(launch_pool_ln(e.dt, r.x, ids, s.tokens(), r.w.lnpost_w, r.w.lnpost_b, s.ln_eps, r.pooled, B, D, st), "pool+ln");
+  check(launch_pool_ln(e.dt, r.x, site_split(e, GS_PROJ) ? r.slab : nullptr, ids, s.tokens(), r.w.lnpost_w,
+                       r.w.lnpost_b, s.ln_eps, r.pooled, B, D, st), "pool+ln");
   check(launch_gemm(e.dt, A_ROWS, EPI_STORE32, ACT_NONE, rows_gemm(r.pooled, D, r.w.proj_t, nullptr, r.emb, E, B, E, D), st), "proj gemm");
   check(launch_l2norm(r.emb, d_out, B, E, st), "l2norm");
 }
@@ -538,7 +582,8 @@ void head_map(const clipgpu_engine& e, const Replica& r, int B, float* d_out, hi
   const int D = s.width, T = s.tokens(), M = mlp_pad(s);
   const MapHeadW& mw = r.w.map;
   ProfScope ps(e, PC_HEAD, st);
-  check(launch_ln_rows(e.dt, r.x, r.w.lnpost_w, r.w.lnpost_b, s.ln_eps, r.h, B * T, D, st), "norm");
+  check(launch_ln_rows_add(e.dt, r.x, site_split(e, GS_PROJ) ? r.slab : nullptr, r.w.lnpost_w, r.w.lnpost_b,
+                           s.ln_eps, r.h, B * T, D, st), "norm");
   check(launch_gemm(e.dt, A_ROWS, EPI_STORE16, ACT_NONE, rows_gemm(r.h, D, mw.wkv, mw.bkv, r.big, 2 * D, B * T, 2 * D, D),
                     st), "attn_pool kv gemm");
   check(launch_map_attention(e.dt, mw.q, r.big, r.pooled, B, T, s.heads, D, st), "attn_pool attention");
@@ -556,29 +601,17 @@ void head_map(const clipgpu_engine& e, const Replica& r, int B, float* d_out, hi
 void vision_forward(const clipgpu_engine& e, const Replica& r, const void* pixels, int asrc, const float* mean,
                     const float* stdv, int B, float* d_out, hipStream_t st) {
   const TowerSpec& s = e.spec;
-  const int D = s.width, G = s.grid(), P = s.patch_size;
-  GemmParams g{};
-  g.W = r.w.conv_w;
-  g.ldw = kpatch_pad(s);
-  g.out = r.x;
-  g.ldo = D;
-  g.M = B * G * G;
-  g.N = D;
-  g.K = kpatch_pad(s);
-  g.Kv = kpatch(s);
-  g.img = pixels;
-  g.S = s.image_size;
-  g.P = P;
-  g.G = G;
-  g.pos = r.w.pos;
-  for (int c = 0; c < 3; ++c) {
-    g.mean[c] = mean ? mean[c] : 0.f;
-    g.stdv[c] = stdv ? stdv[c] : 1.f;
-  }
-  g.bias = r.w.conv_b;
-  g.cls = s.cls() ? 1 : 0;
+  const int D = s.width, G = s.grid(), P = s.patch_size, Kp = kpatch_pad(s);
   { ProfScope ps(e, PC_PATCH, st);
-    check(launch_gemm(e.dt, asrc, EPI_PATCH, ACT_NONE, g, st), "patch gemm"); }
+    // conv1 = patch rows (16-bit, staged in `big`) x conv_w^T, epilogue + bias + pos -> x
+    check(launch_patch_rows(e.dt, asrc, pixels, mean, stdv, r.big, B, s.image_size, P, kpatch(s), Kp, st),
+          "patch rows");
+    GemmParams g = rows_gemm(r.big, Kp, r.w.conv_w, r.w.conv_b, r.x, D, B * G * G, D, Kp);
+    g.G = G;
+    g.pos = r.w.pos;
+    g.cls = s.cls() ? 1 : 0;
+    g.tile = 2 * B * s.tokens() > e.tuned_rows ? e.tile_patch : TILE_AUTO;
+    check(launch_gemm(e.dt, A_ROWS, EPI_PATCH, ACT_NONE, g, st), "patch gemm"); }
   if (s.family == FAMILY_SIGLIP) {  // no class token, no pre-norm: x = patches + bias + pos
     { ProfScope ps(e, PC_STEM, st);
       check(launch_ln_rows(e.dt, r.x, r.w.layers[0].ln1_w, r.w.layers[0].ln1_b, s.ln_eps, r.h, B * s.tokens(), D, st),
@@ -615,9 +648,10 @@ void text_forward(const clipgpu_engine& e, const Replica& r, const int64_t* d_id
 Replica lane_view(const clipgpu_engine& e, const Replica& r, int b0) {
   const TowerSpec& s = e.spec;
   const size_t rows = (size_t)b0 * s.tokens(), D = s.width;
-  const size_t wide = std::max((size_t)3 * D, (size_t)mlp_pad(s));
+  const size_t wide = big_wide(s);
   Replica v = r;
   v.x = r.x + rows * D;
+  if (r.slab) v.slab = r.slab + rows * D;
   v.h = (char*)r.h + rows * D * 2;
   v.big = (char*)r.big + rows * wide * 2;
   v.pooled = (char*)r.pooled + (size_t)b0 * D * 2;
@@ -828,6 +862,7 @@ int clipgpu_create(const char* model_dir, int tower, const int* device_ids, int 
     if (const char* ln = getenv("CLIPGPU_LANES")) e->lanes = std::max(1, std::min(4, atoi(ln)));
     else e->lanes = 2;
     const TowerSpec& s = e->spec;
+    if (const char* sp = getenv("CLIPGPU_GEMM_SPLIT")) e->ksplit = sp[0] == '1' ? 2 : 1;
     if (s.heads <= 0 || s.width % s.heads || s.width % 64)
       throw ClipErr(CLIPGPU_ERR_CONFIG, "Configuration error: width must be a multiple of 64 and of heads");
     const int hd = s.width / s.heads;

@@ -5,8 +5,10 @@
 // Replaces the MatMul/Gemm/Conv nodes ONNX Runtime executes for the exported
 // graphs (pull_onnx.py:53-68 -> src/vision.rs:108, src/text.rs:158-160):
 // QKV in_proj, out_proj, c_fc (+activation), c_proj (+residual), the conv1
-// patch embedding (im2col-free: A rows are gathered straight from the image)
-// and the final projection.
+// patch embedding and the final projection.
+//
+// The patch-embedding conv runs as a row GEMM over the patch rows staged by
+// launch_patch_rows (patch.hip), with the EPI_PATCH epilogue.
 //
 // One kernel template, three tile shapes (GemmTile):
 //   128x128  4 waves (2x2, 64x64 per wave), 64 KiB LDS, 2 blocks / CU
@@ -17,8 +19,7 @@
 // lane-linear image with the XOR swizzle applied on the SOURCE address and on
 // the ds_read_b128 address (cdna_hip_programming.md §5.4 rule 21),
 // double-buffered: the next K-tile's loads are issued before the current one's
-// MFMAs, one vmcnt(0) + barrier per K-step.  Image-sourced A tiles are
-// register-staged (f32 / u8 -> 16-bit in flight).  Block ids are remapped
+// MFMAs, one vmcnt(0) + barrier per K-step.  Block ids are remapped
 // XCD-aware, then grouped 8 row-panels at a time for L2 reuse.  Persistent:
 // the grid is the resident block count and each block walks its tiles, the
 // next tile's first K-slice staged under the current tile's last K-step.  MFMA
@@ -56,11 +57,6 @@ __device__ unsigned long long g_gemm_stamps[kStampBlocks * kStampSlots];
 namespace {
 
 constexpr int BK = 64;
-
-// Byte offset of 16-byte chunk c (0..7) of row r in a [rows][64] 16-bit tile.
-// Conflict-free for the 16x16x32 fragment reads (16 rows x 4 chunks per
-// ds_read_b128 lane group).
-__device__ __forceinline__ int tile_off(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); }
 
 template <typename T>
 __device__ __forceinline__ T to16(float v) { return (T)v; }
@@ -112,17 +108,16 @@ __device__ __forceinline__ void tile_coords(int t, int nTm, int nTn, int BM, int
   n0 = ((t % per_group) / gsize) * BN;
 }
 
-template <typename T, int BM, int BN, int WGM, int WGN, int ASRC, int EPI, int ACT>
+template <typename T, int BM, int BN, int WGM, int WGN, int EPI, int ACT>
 __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p) {
   typedef typename Vec8<T>::type V8;
   typedef typename Vec4<T>::type V4;
-  constexpr int NW = WGM * WGN, NT = NW * 64;
+  constexpr int NW = WGM * WGN;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
   constexpr int A_INSTR = BM / 8 / NW, B_INSTR = BN / 8 / NW;  // 1 KiB glds per wave-instruction
   constexpr int TM = BM / WGM, TN = BN / WGN, MI = TM / 16, NI = TN / 16;
-  constexpr int A_CHUNKS = BM * 8 / NT;  // register-staged image A: 16-byte chunks per thread
   static_assert(A_INSTR >= 1 && B_INSTR >= 1 && MI >= 1 && NI >= 1, "bad tile");
-  constexpr int BIAS_BYTES = ASRC == A_ROWS ? 2 * 1024 : 0;  // 2 x 256 f32 (tile-parity double buffer)
+  constexpr int BIAS_BYTES = 2 * 1024;  // 2 x 256 f32 (tile-parity double buffer)
   static_assert(BN <= 256, "bias slice is one 1 KiB DMA");
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + BIAS_BYTES];
 
@@ -168,8 +163,6 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
   // checks that every operand fits in 2^31 bytes).
   uint32_t woff[B_INSTR];
   uint32_t aoff[A_INSTR];
-  long img_base[A_CHUNKS];
-  int img_row[A_CHUNKS];
   const char* const Wb = (const char*)p.W;
   const char* const Ab = (const char*)p.A;
   auto set_tile = [&](int m0, int n0) {
@@ -179,28 +172,11 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
       const int c = (lane & 7) ^ ((r >> 1) & 7);
       woff[i] = (uint32_t)(min(n0 + r, p.N - 1) * (int)p.ldw + c * 8) * 2u;
     }
-    if constexpr (ASRC == A_ROWS) {
 #pragma unroll
-      for (int i = 0; i < A_INSTR; ++i) {
-        const int r = (wave * A_INSTR + i) * 8 + (lane >> 3);
-        const int c = (lane & 7) ^ ((r >> 1) & 7);
-        aoff[i] = (uint32_t)(min(m0 + r, p.M - 1) * (int)p.lda + c * 8) * 2u;
-      }
-    } else {
-      const int G2 = p.G * p.G;
-#pragma unroll
-      for (int i = 0; i < A_CHUNKS; ++i) {
-        const int q = tid + NT * i;
-        const int r = q >> 3;
-        img_row[i] = r;
-        const int gm = min(m0 + r, p.M - 1);
-        const int b = gm / G2, pp = gm % G2;
-        const int py = pp / p.G, px = pp % p.G;
-        if constexpr (ASRC == A_IMG_F32)
-          img_base[i] = ((long)b * 3 * p.S + (long)py * p.P) * p.S + (long)px * p.P;
-        else  // NHWC u8
-          img_base[i] = (((long)b * p.S + (long)py * p.P) * p.S + (long)px * p.P) * 3;
-      }
+    for (int i = 0; i < A_INSTR; ++i) {
+      const int r = (wave * A_INSTR + i) * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ ((r >> 1) & 7);
+      aoff[i] = (uint32_t)(min(m0 + r, p.M - 1) * (int)p.lda + c * 8) * 2u;
     }
   };
 
@@ -215,82 +191,18 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
     for (int i = 0; i < A_INSTR; ++i) glds16(base + aoff[i], sA + (wave * A_INSTR + i) * 1024);
   };
 
-  // Image-sourced A: 8 consecutive k (same channel and image row; P % 8 == 0).
-  float areg[A_CHUNKS][8];
-  auto load_a_img = [&](int kt) {
-    const int PP = p.P * p.P;
-    const int Kv = p.Kv > 0 ? p.Kv : p.K;
-#pragma unroll
-    for (int i = 0; i < A_CHUNKS; ++i) {
-      const int c = (tid + NT * i) & 7;
-      const int k = kt * BK + c * 8;
-      if (p.P % 8 == 0 && k + 8 <= Kv) {  // 8 consecutive k = 8 pixels of one image row
-        const int ch = k / PP, rem = k - ch * PP;
-        const int ky = rem / p.P, kx = rem - ky * p.P;
-        if constexpr (ASRC == A_IMG_F32) {
-          const float* src = (const float*)p.img + img_base[i] + ((long)ch * p.S + ky) * p.S + kx;
-          const float4 v0 = *(const float4*)src;
-          const float4 v1 = *(const float4*)(src + 4);
-          areg[i][0] = v0.x; areg[i][1] = v0.y; areg[i][2] = v0.z; areg[i][3] = v0.w;
-          areg[i][4] = v1.x; areg[i][5] = v1.y; areg[i][6] = v1.z; areg[i][7] = v1.w;
-        } else {
-          const uint8_t* src = (const uint8_t*)p.img + img_base[i] + ((long)ky * p.S + kx) * 3 + ch;
-          const float mu = p.mean[0] * (ch == 0) + p.mean[1] * (ch == 1) + p.mean[2] * (ch == 2);
-          const float sd = p.stdv[0] * (ch == 0) + p.stdv[1] * (ch == 1) + p.stdv[2] * (ch == 2);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            // src/vision.rs:254-255: (p / 255 - mean[c]) / std[c]
-            const float val = (float)src[e * 3] / 255.0f;
-            areg[i][e] = (val - mu) / sd;
-          }
-        }
-      } else {  // patch rows not a multiple of 8 (P = 14) or the zero-padded K tail
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const int kk = k + e;
-          float val = 0.f;
-          if (kk < Kv) {
-            const int ch = kk / PP, rem = kk - ch * PP;
-            const int ky = rem / p.P, kx = rem - ky * p.P;
-            if constexpr (ASRC == A_IMG_F32) {
-              val = ((const float*)p.img)[img_base[i] + ((long)ch * p.S + ky) * p.S + kx];
-            } else {
-              const float mu = p.mean[0] * (ch == 0) + p.mean[1] * (ch == 1) + p.mean[2] * (ch == 2);
-              const float sd = p.stdv[0] * (ch == 0) + p.stdv[1] * (ch == 1) + p.stdv[2] * (ch == 2);
-              const float u = (float)((const uint8_t*)p.img)[img_base[i] + ((long)ky * p.S + kx) * 3 + ch] / 255.0f;
-              val = (u - mu) / sd;
-            }
-          }
-          areg[i][e] = val;
-        }
-      }
-    }
-  };
-  auto store_a_img = [&](char* sA) {
-#pragma unroll
-    for (int i = 0; i < A_CHUNKS; ++i) {
-      const int c = (tid + NT * i) & 7;
-      V8 v;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = to16<T>(areg[i][e]);
-      *(V8*)(sA + tile_off(img_row[i], c)) = v;
-    }
-  };
   // Issue the loads of K-step kt of the current tile into buffer (sA, sB).
   auto stage = [&](int kt, char* sA, char* sB) {
     stage_w(kt, sB);
-    if constexpr (ASRC == A_ROWS) stage_a_rows(kt, sA);
-    else load_a_img(kt);
+    stage_a_rows(kt, sA);
   };
-  // A_ROWS: the tile's bias slice bias[n0 .. n0+255] goes to LDS by one 1 KiB DMA
+  // The tile's bias slice bias[n0 .. n0+255] goes to LDS by one 1 KiB DMA
   // (wave 0, with the tile's first K-step), so the epilogue needs no global load
   // (which, issued after the next tile's DMA, would wait for it: vmcnt is in order).
   auto stage_bias = [&](int n0, int par) {
-    if constexpr (ASRC == A_ROWS) {
-      if (p.bias != nullptr && wave == 0) {
-        const int n = min(n0 + lane * 4, ((p.N - 1) / 4) * 4);  // clamped in-bounds 16 B (N % 4 == 0 checked)
-        glds16(p.bias + n, smem + 2 * STAGE + par * 1024);
-      }
+    if (p.bias != nullptr && wave == 0) {
+      const int n = min(n0 + lane * 4, ((p.N - 1) / 4) * 4);  // clamped in-bounds 16 B (N % 4 == 0 checked)
+      glds16(p.bias + n, smem + 2 * STAGE + par * 1024);
     }
   };
 
@@ -320,39 +232,26 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
   // zero: the first K-step of a tile starts the MFMA chain from C = 0 (no
   // accumulator re-zeroing between tiles).
   auto compute = [&](auto zero, const char* sA, const char* sB) {
-    if constexpr (ASRC == A_ROWS) {
-      // Fragment reads in inline asm (invisible to hipcc's waitcnt pass, which
-      // would otherwise drain vmcnt(0) -- including the previous tile's epilogue
-      // stores -- in front of them); the kk = 1 reads fly under the kk = 0 MFMAs.
-      const uint32_t aB = lds0 + (uint32_t)(sA - smem), bB = lds0 + (uint32_t)(sB - smem);
-      V8 a0[MI], b0[NI], a1[MI], b1[NI];
-      static_for<NI>([&](auto ni) { ds_read_b128<(int)ni * 2048>(b0[ni], bB + offB[0]); });
-      static_for<MI>([&](auto mi) { ds_read_b128<(int)mi * 2048>(a0[mi], aB + offA[0]); });
-      lgkm_wait_all(a0, b0);
-      // kk = 0 MFMAs row block by row block; a1[mi] is read into the registers
-      // a0[mi] just released, b1 after the last kk = 0 MFMA (48 fragment VGPRs, not 96).
-      static_for<MI>([&](auto mi) {
+    // Fragment reads in inline asm (invisible to hipcc's waitcnt pass, which
+    // would otherwise drain vmcnt(0) -- including the previous tile's epilogue
+    // stores -- in front of them); the kk = 1 reads fly under the kk = 0 MFMAs.
+    const uint32_t aB = lds0 + (uint32_t)(sA - smem), bB = lds0 + (uint32_t)(sB - smem);
+    V8 a0[MI], b0[NI], a1[MI], b1[NI];
+    static_for<NI>([&](auto ni) { ds_read_b128<(int)ni * 2048>(b0[ni], bB + offB[0]); });
+    static_for<MI>([&](auto mi) { ds_read_b128<(int)mi * 2048>(a0[mi], aB + offA[0]); });
+    lgkm_wait_all(a0, b0);
+    // kk = 0 MFMAs row block by row block; a1[mi] is read into the registers
+    // a0[mi] just released, b1 after the last kk = 0 MFMA (48 fragment VGPRs, not 96).
+    static_for<MI>([&](auto mi) {
 #pragma unroll
-        for (int ni = 0; ni < NI; ++ni)
-          acc[ni][mi] = mfma_16x16x32(b0[ni], a0[mi], decltype(zero)::value ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[ni][mi]);
-        __builtin_amdgcn_sched_barrier(0);
-        ds_read_b128<(int)mi * 2048>(a1[mi], aB + offA[1]);
-      });
-      static_for<NI>([&](auto ni) { ds_read_b128<(int)ni * 2048>(b1[ni], bB + offB[1]); });
-      lgkm_wait_all(a1, b1);
-      mfma_block(std::false_type{}, a1, b1);
-    } else {
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        V8 a[MI], b[NI];
-#pragma unroll
-        for (int ni = 0; ni < NI; ++ni) b[ni] = *(const V8*)(sB + offB[kk] + ni * 2048);
-#pragma unroll
-        for (int mi = 0; mi < MI; ++mi) a[mi] = *(const V8*)(sA + offA[kk] + mi * 2048);
-        if (kk == 0) mfma_block(zero, a, b);
-        else mfma_block(std::false_type{}, a, b);
-      }
-    }
+      for (int ni = 0; ni < NI; ++ni)
+        acc[ni][mi] = mfma_16x16x32(b0[ni], a0[mi], decltype(zero)::value ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[ni][mi]);
+      __builtin_amdgcn_sched_barrier(0);
+      ds_read_b128<(int)mi * 2048>(a1[mi], aB + offA[1]);
+    });
+    static_for<NI>([&](auto ni) { ds_read_b128<(int)ni * 2048>(b1[ni], bB + offB[1]); });
+    lgkm_wait_all(a1, b1);
+    mfma_block(std::false_type{}, a1, b1);
   };
 
   auto epilogue = [&](int m0, int n0, int bpar) {
@@ -378,16 +277,11 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
       const bool nfull = n + 4 <= p.N;
       float bv[4] = {0.f, 0.f, 0.f, 0.f};
       if (p.bias != nullptr) {
-        if constexpr (ASRC == A_ROWS) {
-          f32x4 b4;
-          ds_read_b128<0>(b4, lds0 + 2 * STAGE + bpar * 1024 + (wn + ni * 16 + fq * 4) * 4);
-          asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(b4)::"memory");
+        f32x4 b4;
+        ds_read_b128<0>(b4, lds0 + 2 * STAGE + bpar * 1024 + (wn + ni * 16 + fq * 4) * 4);
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(b4)::"memory");
 #pragma unroll
-          for (int j = 0; j < 4; ++j) bv[j] = b4[j];
-        } else {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) bv[j] = n + j < p.N ? p.bias[n + j] : 0.f;
-        }
+        for (int j = 0; j < 4; ++j) bv[j] = b4[j];
       }
 #pragma unroll
       for (int mi = 0; mi < MI; ++mi) {
@@ -459,21 +353,14 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
   set_tile(m0, n0);
   stage(0, sA0, sB0);
   stage_bias(n0, 0);
-  if constexpr (ASRC != A_ROWS) store_a_img(sA0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  // Step barrier: A_ROWS waits only for its own glds (counted) and uses a raw
-  // s_barrier (a __syncthreads() fence would also drain the epilogue stores);
-  // the register-staged image path needs the fence for its ds_writes.
+  // Step barrier: wait only for this K-step's glds and use a raw s_barrier (a
+  // __syncthreads() fence would also drain the epilogue stores).
   auto step_sync = [&]() {
-    if constexpr (ASRC == A_ROWS) {
-      vm_wait<0>();  // only this K-step's glds are outstanding here
-      __builtin_amdgcn_s_barrier();
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-    }
+    vm_wait<0>();  // only this K-step's glds are outstanding here
+    __builtin_amdgcn_s_barrier();
   };
 
   int parity = 0;    // buffer holding K-step 0 of the current tile
@@ -489,7 +376,6 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
       stage(kt + 1, sAn, sBn);
       if (kt == 0) compute(std::true_type{}, cur1 ? sA1 : sA0, cur1 ? sB1 : sB0);
       else compute(std::false_type{}, cur1 ? sA1 : sA0, cur1 ? sB1 : sB0);
-      if constexpr (ASRC != A_ROWS) store_a_img(sAn);
       step_sync();
       if (ti == 0) GEMM_STAMP(34 + kt);
     }
@@ -507,22 +393,14 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
     }
     if (nk == 1) compute(std::true_type{}, cur1 ? sA1 : sA0, cur1 ? sB1 : sB0);
     else compute(std::false_type{}, cur1 ? sA1 : sA0, cur1 ? sB1 : sB0);
-    if constexpr (ASRC != A_ROWS) {
-      if (has_next) store_a_img(cur1 ? sA0 : sA1);
-    }
     GEMM_STAMP(4 + ti * 4);
     epilogue(m0, n0, bias_par);
-    if constexpr (ASRC == A_ROWS) {
-      // Retire the next tile's stage-0 glds but not this tile's output stores
-      // (issued after them; in-order vmcnt): a full tile issues exactly MI*NI
-      // epilogue stores per lane, a partial one may issue fewer -> wait for all.
-      if (m0 + BM <= p.M && n0 + BN <= p.N) vm_wait<MI * NI>();
-      else vm_wait<0>();
-      __builtin_amdgcn_s_barrier();
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-    }
+    // Retire the next tile's stage-0 glds but not this tile's output stores
+    // (issued after them; in-order vmcnt): a full tile issues exactly MI*NI
+    // epilogue stores per lane, a partial one may issue fewer -> wait for all.
+    if (m0 + BM <= p.M && n0 + BN <= p.N) vm_wait<MI * NI>();
+    else vm_wait<0>();
+    __builtin_amdgcn_s_barrier();
     GEMM_STAMP(5 + ti * 4);
     parity ^= (nk & 1);
     bias_par ^= 1;
@@ -579,8 +457,12 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_pipe_kernel(GemmParams 
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nTn = (p.N + BN - 1) / BN;
   const int nTm = (p.M + BM - 1) / BM;
-  const int ntiles = nTn * nTm;
-  const int nk = p.K / BK;
+  // Work unit u = (tile u / ks, K-slice u % ks): slice 0 runs the epilogue EPI, slices
+  // >= 1 store their f32 partial to p.slab + (slice - 1) * M * ldo (split-K; combined
+  // by the consumer of the output in a fixed order).
+  const int ks = p.ksplit > 1 ? p.ksplit : 1;
+  const int ntiles = nTn * nTm * ks;
+  const int nk = p.K / BK / ks;  // K-steps per unit
 
   const int nb = gridDim.x;
   int t_first, t_stride, t_end;
@@ -598,6 +480,10 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_pipe_kernel(GemmParams 
   }
   if (t_first >= t_end) return;
   const int total = ((t_end - t_first + t_stride - 1) / t_stride) * nk;  // this block's K-steps
+  auto unit_coords = [&](int u, int& m0, int& n0, int& slice) {
+    slice = u % ks;
+    tile_coords(u / ks, nTm, nTn, BM, BN, m0, n0);
+  };
 
   auto swW = [](int r) { return (r & 2) | (((r >> (2 + LG)) & 1) << 2); };
 
@@ -606,25 +492,26 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_pipe_kernel(GemmParams 
   uint32_t aoff[A_INSTR];
   const char* const Wb = (const char*)p.W;
   const char* const Ab = (const char*)p.A;
-  auto set_tile = [&](int m0, int n0) {
+  auto set_tile = [&](int m0, int n0, int slice) {
+    const int k0 = slice * nk * BK;  // first k of the unit's K-slice
 #pragma unroll
     for (int i = 0; i < B_INSTR; ++i) {
       const int r = (wave * B_INSTR + i) * 8 + (lane >> 3);
       const int c = (lane & 7) ^ swW(r);
-      woff[i] = (uint32_t)(min(n0 + r, p.N - 1) * (int)p.ldw + c * 8) * 2u;
+      woff[i] = (uint32_t)(min(n0 + r, p.N - 1) * (int)p.ldw + k0 + c * 8) * 2u;
     }
 #pragma unroll
     for (int i = 0; i < A_INSTR; ++i) {
       const int r = (wave * A_INSTR + i) * 8 + (lane >> 3);
       const int c = (lane & 7) ^ ((r >> 1) & 7);
-      aoff[i] = (uint32_t)(min(m0 + r, p.M - 1) * (int)p.lda + c * 8) * 2u;
+      aoff[i] = (uint32_t)(min(m0 + r, p.M - 1) * (int)p.lda + k0 + c * 8) * 2u;
     }
   };
   int d_g = 0, d_kt = 0, d_t = t_first, d_n0 = 0, d_ti = 0;
   {
-    int m0, n0;
-    tile_coords(d_t, nTm, nTn, BM, BN, m0, n0);
-    set_tile(m0, n0);
+    int m0, n0, sl;
+    unit_coords(d_t, m0, n0, sl);
+    set_tile(m0, n0, sl);
     d_n0 = n0;
   }
   auto dma_piece = [&](auto jc) {  // W pieces first, then A pieces
@@ -650,9 +537,9 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_pipe_kernel(GemmParams 
       d_t += t_stride;
       ++d_ti;
       if (d_t < t_end) {
-        int m0, n0;
-        tile_coords(d_t, nTm, nTn, BM, BN, m0, n0);
-        set_tile(m0, n0);
+        int m0, n0, sl;
+        unit_coords(d_t, m0, n0, sl);
+        set_tile(m0, n0, sl);
         d_n0 = n0;
       }
     }
@@ -722,12 +609,34 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_pipe_kernel(GemmParams 
   };
 
   // ---- epilogue: lane owns row wm+mi*16+fr, columns nc .. nc+4*NI-1 ------------
-  auto epilogue = [&](int m0, int n0, int bpar) {
+  // slice > 0 (split-K partial): plain f32 store of acc to the slab, no bias / residual.
+  auto epilogue = [&](int m0, int n0, int bpar, int slice) {
     const int nc = n0 + wn + fq * (4 * NI);
     const bool nfull = nc + 4 * NI <= p.N;
     f32x4 bias[NI];
 #pragma unroll
     for (int ni = 0; ni < NI; ++ni) bias[ni] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (slice > 0) {
+      float* const slab = p.slab + (long)(slice - 1) * p.M * p.ldo;
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi) {
+        const int m = m0 + wm + mi * 16 + fr;
+        if (m >= p.M) continue;
+        float* o = slab + (long)m * p.ldo + nc;
+        if (nfull) {
+#pragma unroll
+          for (int ni = 0; ni < NI; ++ni)
+            *(float4*)(o + ni * 4) = make_float4(acc[ni][mi][0], acc[ni][mi][1], acc[ni][mi][2], acc[ni][mi][3]);
+        } else {
+#pragma unroll
+          for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if (nc + ni * 4 + j < p.N) o[ni * 4 + j] = acc[ni][mi][j];
+        }
+      }
+      return;
+    }
     if (p.bias != nullptr) {
       const uint32_t ba = lds0 + 2 * STAGE + bpar * 1024 + (wn + fq * (4 * NI)) * 4;
       static_for<NI>([&](auto ni) { ds_read_b128<(int)ni * 16>(bias[ni], ba); });
@@ -735,19 +644,35 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_pipe_kernel(GemmParams 
 #pragma unroll
       for (int ni = 0; ni < NI; ++ni) asm volatile("" : "+v"(bias[ni]));
     }
+    // EPI_RESID adds the residual row x[m]; EPI_PATCH writes patch p of image b to token
+    // row b*(G2+cls) + cls + p and adds pos[cls + p].
+    constexpr bool ADDX = EPI == EPI_RESID || EPI == EPI_PATCH;
+    const int G2 = p.G * p.G;
+    auto out_row = [&](int m) -> long {
+      if constexpr (EPI == EPI_PATCH) {
+        const int b = m / G2;
+        return ((long)b * (G2 + p.cls) + p.cls + (m - b * G2)) * p.ldo;
+      } else {
+        return (long)m * p.ldo;
+      }
+    };
+    auto add_src = [&](int m) -> const float* {
+      if constexpr (EPI == EPI_PATCH) return p.pos + (long)(p.cls + m % G2) * p.N + nc;
+      else return (const float*)p.out + (long)m * p.ldo + nc;
+    };
     float4 xr[2][NI];
     auto load_x = [&](int mi, float4(&dst)[NI]) {
       const int m = m0 + wm + mi * 16 + fr;
       if (m < p.M && nfull) {
-        const float* src = (const float*)p.out + (long)m * p.ldo + nc;
+        const float* src = add_src(m);
 #pragma unroll
         for (int ni = 0; ni < NI; ++ni) dst[ni] = *(const float4*)(src + ni * 4);
       }
     };
-    if constexpr (EPI == EPI_RESID) load_x(0, xr[0]);
+    if constexpr (ADDX) load_x(0, xr[0]);
 #pragma unroll
     for (int mi = 0; mi < MI; ++mi) {
-      if constexpr (EPI == EPI_RESID) {
+      if constexpr (ADDX) {
         if (mi + 1 < MI) load_x(mi + 1, xr[(mi + 1) & 1]);
       }
       const int m = m0 + wm + mi * 16 + fr;
@@ -786,25 +711,26 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_pipe_kernel(GemmParams 
               if (nc + ni * 4 + j < p.N) o[ni * 4 + j] = to16<T>(apply_act<ACT>(v[ni][j]));
         }
       } else {
-        float* o = (float*)p.out + (long)m * p.ldo + nc;
+        float* o = (float*)p.out + out_row(m) + nc;
         if (nfull) {
 #pragma unroll
           for (int ni = 0; ni < NI; ++ni) {
             float4 w = make_float4(v[ni][0], v[ni][1], v[ni][2], v[ni][3]);
-            if constexpr (EPI == EPI_RESID) {
+            if constexpr (ADDX) {
               const float4 x = xr[mi & 1][ni];
               w.x += x.x; w.y += x.y; w.z += x.z; w.w += x.w;
             }
             *(float4*)(o + ni * 4) = w;
           }
         } else {
+          const float* xs = ADDX ? add_src(m) : nullptr;
 #pragma unroll
           for (int ni = 0; ni < NI; ++ni)
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
               if (nc + ni * 4 + j >= p.N) continue;
               float r = v[ni][j];
-              if constexpr (EPI == EPI_RESID) r += o[ni * 4 + j];
+              if constexpr (ADDX) r += xs[ni * 4 + j];
               o[ni * 4 + j] = r;
             }
         }
@@ -812,7 +738,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_pipe_kernel(GemmParams 
     }
   };
   // vm ops a full tile's epilogue leaves in flight behind the DMA of the step after it
-  constexpr int EPI_VM = EPI == EPI_STORE16 ? MI * NI / 2 : (EPI == EPI_RESID ? 2 * MI * NI : MI * NI);
+  constexpr int EPI_VM = EPI == EPI_STORE16 ? MI * NI / 2 : ((EPI == EPI_RESID || EPI == EPI_PATCH) ? 2 * MI * NI : MI * NI);
 
   // ---- prologue: steps 0 and 1 in flight, step 0 landed, its kk0 fragments read
   GEMM_STAMP_REAL(62);
@@ -830,8 +756,8 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_pipe_kernel(GemmParams 
   bool after_full_epi = false;
   int ti = 0;
   for (int t = t_first; t < t_end; t += t_stride, ++ti) {
-    int m0, n0;
-    tile_coords(t, nTm, nTn, BM, BN, m0, n0);
+    int m0, n0, slice;
+    unit_coords(t, m0, n0, slice);
     GEMM_STAMP(2 + ti * 4);
     for (int kt = 0; kt < nk; ++kt, ++g) {
       if (kt + 1 == nk) GEMM_STAMP(3 + ti * 4);
@@ -846,8 +772,9 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_pipe_kernel(GemmParams 
       if (ti == 0 && kt + 1 < nk) GEMM_STAMP(34 + kt);
     }
     GEMM_STAMP(4 + ti * 4);
-    epilogue(m0, n0, ti & 1);
-    after_full_epi = m0 + BM <= p.M && n0 + BN <= p.N;  // partial tiles may issue fewer vm ops
+    epilogue(m0, n0, ti & 1, slice);
+    // partial tiles and slab units issue fewer vm ops than EPI_VM: drain them
+    after_full_epi = slice == 0 && m0 + BM <= p.M && n0 + BN <= p.N;
     if (!after_full_epi) vm_wait<0>();
     if (t + t_stride < t_end) {  // the next tile's step 0 landed at the last barrier
       const uint32_t buf = lds0 + (g & 1) * STAGE;
@@ -872,14 +799,14 @@ int device_cus() {
   return cus;
 }
 
-template <typename T, int BM, int BN, int WGM, int WGN, int ASRC, int EPI, int ACT>
+template <typename T, int BM, int BN, int WGM, int WGN, int EPI, int ACT>
 hipError_t launch_cfg(const GemmParams& p, hipStream_t s) {
   const int nTn = (p.N + BN - 1) / BN, nTm = (p.M + BM - 1) / BM;
   const int ntiles = nTn * nTm;
   // resident blocks: one 8-wave block (96-128 KiB LDS) or two 4-wave blocks (64 KiB) per CU
   const int resident = device_cus() * (WGM * WGN == 4 ? 2 : 1);
   const int grid = ntiles <= resident ? ntiles : resident;
-  hipLaunchKernelGGL((gemm_bt_kernel<T, BM, BN, WGM, WGN, ASRC, EPI, ACT>), dim3(grid), dim3(WGM * WGN * 64), 0, s,
+  hipLaunchKernelGGL((gemm_bt_kernel<T, BM, BN, WGM, WGN, EPI, ACT>), dim3(grid), dim3(WGM * WGN * 64), 0, s,
                      p);
   return hipGetLastError();
 }
@@ -887,52 +814,51 @@ hipError_t launch_cfg(const GemmParams& p, hipStream_t s) {
 template <typename T, int BM, int BN, int WGM, int WGN, int EPI, int ACT>
 hipError_t launch_pipe(const GemmParams& p, hipStream_t s) {
   const int nTn = (p.N + BN - 1) / BN, nTm = (p.M + BM - 1) / BM;
-  const int ntiles = nTn * nTm;
+  const int ntiles = nTn * nTm * (p.ksplit > 1 ? p.ksplit : 1);
   const int resident = device_cus() * (BM * BN == 128 * 128 ? 2 : 1);
   const int grid = ntiles <= resident ? ntiles : resident;
   hipLaunchKernelGGL((gemm_pipe_kernel<T, BM, BN, WGM, WGN, EPI, ACT>), dim3(grid), dim3(WGM * WGN * 64), 0, s, p);
   return hipGetLastError();
 }
 
-template <typename T, int ASRC, int EPI, int ACT>
+template <typename T, int EPI, int ACT>
 hipError_t launch_tile(const GemmParams& p, hipStream_t s) {
-  if constexpr (ASRC != A_ROWS) {
-    return launch_cfg<T, 128, 128, 2, 2, ASRC, EPI, ACT>(p, s);  // register-staged A: spill-free tile
-  } else {
-    const int tile = p.tile == TILE_AUTO ? pick_gemm_tile(p.M, p.N, p.K) : p.tile;
-    // software-pipelined kernel: K >= 128, 16-byte-aligned 16-bit output rows (diag bit 1: legacy, stamp builds)
-    const bool pipe = p.K >= 2 * BK && !(p.diag & 2) && (EPI != EPI_STORE16 || p.ldo % 8 == 0);
-    if (pipe) {
-      switch (tile) {
-        case TILE_256x256: return launch_pipe<T, 256, 256, 2, 4, EPI, ACT>(p, s);
-        case TILE_256x128: return launch_pipe<T, 256, 128, 2, 4, EPI, ACT>(p, s);
-        case TILE_128x128_PIPE: return launch_pipe<T, 128, 128, 2, 2, EPI, ACT>(p, s);
-        default: break;
-      }
+  const int tile = p.tile == TILE_AUTO ? pick_gemm_tile(p.M, p.N, p.K) : p.tile;
+  // software-pipelined kernel: K >= 128, 16-byte-aligned 16-bit output rows (diag bit 1: legacy, stamp builds)
+  const bool pipe = p.K >= 2 * BK && !(p.diag & 2) && (EPI != EPI_STORE16 || p.ldo % 8 == 0);
+  if (p.ksplit > 1) {  // split-K runs on the pipelined kernel only (128x128 -> its pipelined form)
+    if (!pipe) return hipErrorInvalidValue;
+    switch (tile) {
+      case TILE_256x256: return launch_pipe<T, 256, 256, 2, 4, EPI, ACT>(p, s);
+      case TILE_256x128: return launch_pipe<T, 256, 128, 2, 4, EPI, ACT>(p, s);
+      default: return launch_pipe<T, 128, 128, 2, 2, EPI, ACT>(p, s);
     }
-    return launch_cfg<T, 128, 128, 2, 2, ASRC, EPI, ACT>(p, s);
   }
+  if (pipe) {
+    switch (tile) {
+      case TILE_256x256: return launch_pipe<T, 256, 256, 2, 4, EPI, ACT>(p, s);
+      case TILE_256x128: return launch_pipe<T, 256, 128, 2, 4, EPI, ACT>(p, s);
+      case TILE_128x128_PIPE: return launch_pipe<T, 128, 128, 2, 2, EPI, ACT>(p, s);
+      default: break;
+    }
+  }
+  return launch_cfg<T, 128, 128, 2, 2, EPI, ACT>(p, s);
 }
 
 template <typename T>
-hipError_t launch_typed(int asrc, int epi, int act, const GemmParams& p, hipStream_t s) {
-  if (asrc == A_ROWS) {
-    if (epi == EPI_STORE16) {
+hipError_t launch_typed(int epi, int act, const GemmParams& p, hipStream_t s) {
+  switch (epi) {
+    case EPI_STORE16:
       switch (act) {
-        case ACT_NONE: return launch_tile<T, A_ROWS, EPI_STORE16, ACT_NONE>(p, s);
-        case ACT_QUICK_GELU: return launch_tile<T, A_ROWS, EPI_STORE16, ACT_QUICK_GELU>(p, s);
-        case ACT_GELU: return launch_tile<T, A_ROWS, EPI_STORE16, ACT_GELU>(p, s);
-        case ACT_GELU_TANH: return launch_tile<T, A_ROWS, EPI_STORE16, ACT_GELU_TANH>(p, s);
+        case ACT_NONE: return launch_tile<T, EPI_STORE16, ACT_NONE>(p, s);
+        case ACT_QUICK_GELU: return launch_tile<T, EPI_STORE16, ACT_QUICK_GELU>(p, s);
+        case ACT_GELU: return launch_tile<T, EPI_STORE16, ACT_GELU>(p, s);
+        case ACT_GELU_TANH: return launch_tile<T, EPI_STORE16, ACT_GELU_TANH>(p, s);
       }
-    } else if (epi == EPI_RESID) {
-      return launch_tile<T, A_ROWS, EPI_RESID, ACT_NONE>(p, s);
-    } else if (epi == EPI_STORE32) {
-      return launch_tile<T, A_ROWS, EPI_STORE32, ACT_NONE>(p, s);
-    }
-  } else if (asrc == A_IMG_F32 && epi == EPI_PATCH) {
-    return launch_tile<T, A_IMG_F32, EPI_PATCH, ACT_NONE>(p, s);
-  } else if (asrc == A_IMG_U8 && epi == EPI_PATCH) {
-    return launch_tile<T, A_IMG_U8, EPI_PATCH, ACT_NONE>(p, s);
+      break;
+    case EPI_RESID: return launch_tile<T, EPI_RESID, ACT_NONE>(p, s);
+    case EPI_STORE32: return launch_tile<T, EPI_STORE32, ACT_NONE>(p, s);
+    case EPI_PATCH: return launch_tile<T, EPI_PATCH, ACT_NONE>(p, s);  // rows from launch_patch_rows
   }
   return hipErrorInvalidValue;
 }
@@ -961,9 +887,13 @@ hipError_t launch_gemm(DType dt, int asrc, int epi, int act, const GemmParams& p
   if (p.bias != nullptr && p.N % 4 != 0) return hipErrorInvalidValue;  // 16-byte bias DMA
   // 32-bit staging offsets
   if ((long)p.M * p.lda * 2 >= (1L << 31) || (long)p.N * p.ldw * 2 >= (1L << 31)) return hipErrorInvalidValue;
-  if (asrc != A_ROWS && (p.Kv > p.K || p.Kv < 0)) return hipErrorInvalidValue;
-  return dt == DT_BF16 ? launch_typed<__bf16>(asrc, epi, act, p, s)
-                       : launch_typed<_Float16>(asrc, epi, act, p, s);
+  if (asrc != A_ROWS) return hipErrorInvalidValue;  // pixels go through launch_patch_rows first
+  if (p.ksplit > 1) {  // each K-slice >= 2 K-steps (pipelined kernel); f32 epilogues only; a slab
+    if (p.K % (BK * p.ksplit) != 0 || p.K / p.ksplit < 2 * BK || p.slab == nullptr ||
+        (epi != EPI_RESID && epi != EPI_STORE32) || p.ldo % 4 != 0)
+      return hipErrorInvalidValue;
+  }
+  return dt == DT_BF16 ? launch_typed<__bf16>(epi, act, p, s) : launch_typed<_Float16>(epi, act, p, s);
 }
 
 #ifdef CLIPGPU_GEMM_STAMPS

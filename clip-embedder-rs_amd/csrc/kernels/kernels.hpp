@@ -9,18 +9,18 @@ namespace clipgpu {
 
 enum DType { DT_BF16 = 0, DT_F16 = 1 };
 
-// Source of the GEMM A operand.
+// Source of the GEMM A operand (launch_gemm takes A_ROWS only) / of the patch rows.
 enum ASrc {
   A_ROWS = 0,     // T16 [M][lda], staged by global_load_lds
-  A_IMG_F32 = 1,  // im2col-free patch rows from normalised f32 NCHW pixels
-  A_IMG_U8 = 2,   // im2col-free patch rows from u8 NHWC pixels, normalised on load
+  A_IMG_F32 = 1,  // launch_patch_rows: normalised f32 NCHW pixels
+  A_IMG_U8 = 2,   // launch_patch_rows: u8 NHWC pixels, normalised on load
 };
 // GEMM epilogue.
 enum Epi {
   EPI_STORE16 = 0,  // out16[m][n] = act(acc + bias[n])
   EPI_RESID = 1,    // out32[m][n] += acc + bias[n]        (residual stream, in place)
   EPI_STORE32 = 2,  // out32[m][n] = acc + bias[n]
-  EPI_PATCH = 3,    // x[b*(G^2+1) + 1 + p][n] = acc + bias[n] + pos[1 + p][n]
+  EPI_PATCH = 3,    // x[b*(G^2+cls) + cls + p][n] = acc + bias[n] + pos[cls + p][n]
 };
 
 struct GemmParams {
@@ -29,13 +29,13 @@ struct GemmParams {
   const float* bias;         // [N] or nullptr
   void* out; long ldo;
   int M, N, K;
-  // image sources (A_IMG_*)
-  const void* img; int S, P, G;
-  int Kv;                    // image sources: valid K = 3*P*P (K is padded to a multiple of 64; k >= Kv reads 0)
+  int G;                     // EPI_PATCH: patch grid (G^2 patch rows per image)
   int cls;                   // EPI_PATCH: 1 = token 0 of each image is a class token (rows / pos shifted by one)
-  float mean[3], stdv[3];
-  const float* pos;          // EPI_PATCH positional embedding [G^2+1][N]
+  const float* pos;          // EPI_PATCH positional embedding [G^2+cls][N]
   int tile;                  // GemmTile (0 = pick by shape)
+  int ksplit;                // split-K slices (0/1 = none); EPI_RESID / EPI_STORE32 only: slice 0 runs the
+                             // epilogue, slice s >= 1 stores its f32 partial to slab[(s-1)*M*ldo + m*ldo + n]
+  float* slab;
   int diag;                  // stamp build only: bit 0 = skip epilogue stores (timing experiments)
 };
 
@@ -64,6 +64,9 @@ hipError_t launch_attention(DType dt, const void* qkv, void* out, int B, int N, 
 // out16[r] = LN(x[r]) for r < rows.
 hipError_t launch_ln_rows(DType dt, const float* x, const float* w, const float* b, float eps,
                           void* out16, int rows, int D, hipStream_t s);
+// slab != nullptr: x[r] += slab[r] (stored) first -- the split-K combine of the GEMM that wrote x.
+hipError_t launch_ln_rows_add(DType dt, float* x, const float* slab, const float* w, const float* b, float eps,
+                              void* out16, int rows, int D, hipStream_t s);
 
 // Vision stem tail: CLS row = cls + pos[0]; x = ln_pre(x) (in place); h = ln_1(x).
 hipError_t launch_vision_embed_ln(DType dt, float* x, const float* cls, const float* pos,
@@ -77,9 +80,16 @@ hipError_t launch_text_embed_ln(DType dt, const int64_t* ids, const float* tok, 
                                 void* h, int B, int T, int D, int vocab, hipStream_t s);
 
 // Pool one row per sequence (CLS: ids == nullptr; else first argmax of ids) and LN it.
-hipError_t launch_pool_ln(DType dt, const float* x, const int64_t* ids, int tokens,
+// slab (nullable): split-K partial of the last c_proj, added to the pooled row.
+hipError_t launch_pool_ln(DType dt, const float* x, const float* slab, const int64_t* ids, int tokens,
                           const float* w, const float* b, float eps, void* out16, int B, int D,
                           hipStream_t s);
+
+// Patch rows of the patch-embedding conv: out[b*G*G + p][k] (16-bit, row stride Kp) from
+// normalised f32 NCHW (src = A_IMG_F32) or u8 NHWC normalised with mean/std (A_IMG_U8);
+// k = ch*P*P + ky*P + kx, zero for Kv <= k < Kp.  G = S / P.
+hipError_t launch_patch_rows(DType dt, int src, const void* img, const float* mean, const float* stdv, void* out,
+                             int B, int S, int P, int Kv, int Kp, hipStream_t s);
 
 // out[r] = in[r] / max(||in[r]||_2, 1e-12)
 hipError_t launch_l2norm(const float* in, float* out, int B, int E, hipStream_t s);

@@ -86,13 +86,29 @@ __device__ __forceinline__ void store_row32(float* dst, const RowRegs& r, int D4
   }
 }
 
+__device__ __forceinline__ void add_row(RowRegs& r, const RowRegs& a) {
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    r.v[i].x += a.v[i].x; r.v[i].y += a.v[i].y; r.v[i].z += a.v[i].z; r.v[i].w += a.v[i].w;
+  }
+}
+
+// slab != nullptr: first combine the split-K partial of the GEMM that wrote x
+// (x += slab, stored back), then LN -- the launch-boundary split-K reduce.
 template <typename T>
-__global__ __launch_bounds__(256) void ln_rows_kernel(const float* __restrict__ x, const float* w, const float* b,
-                                                      float eps, T* __restrict__ out, int rows, int D) {
+__global__ __launch_bounds__(256) void ln_rows_kernel(float* __restrict__ x, const float* __restrict__ slab,
+                                                      const float* w, const float* b, float eps,
+                                                      T* __restrict__ out, int rows, int D) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= rows) return;
   RowRegs r, o;
   load_row(x + (long)row * D, D >> 2, lane, r);
+  if (slab != nullptr) {
+    RowRegs a;
+    load_row(slab + (long)row * D, D >> 2, lane, a);
+    add_row(r, a);
+    store_row32(x + (long)row * D, r, D >> 2, lane);
+  }
   layer_norm_regs(r, o, w, b, eps, D, lane);
   store_row16(out + (long)row * D, o, D >> 2, lane);
 }
@@ -149,9 +165,9 @@ __global__ __launch_bounds__(256) void text_embed_ln_kernel(const int64_t* __res
 }
 
 template <typename T>
-__global__ __launch_bounds__(256) void pool_ln_kernel(const float* __restrict__ x, const int64_t* __restrict__ ids,
-                                                      int tokens, const float* w, const float* b, float eps,
-                                                      T* __restrict__ out, int B, int D) {
+__global__ __launch_bounds__(256) void pool_ln_kernel(const float* __restrict__ x, const float* __restrict__ slab,
+                                                      const int64_t* __restrict__ ids, int tokens, const float* w,
+                                                      const float* b, float eps, T* __restrict__ out, int B, int D) {
   const int bi = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (bi >= B) return;
   int src = 0;
@@ -172,6 +188,11 @@ __global__ __launch_bounds__(256) void pool_ln_kernel(const float* __restrict__ 
   }
   RowRegs r, y;
   load_row(x + ((long)bi * tokens + src) * D, D >> 2, lane, r);
+  if (slab != nullptr) {  // split-K partial of the last c_proj (x itself is not updated)
+    RowRegs a;
+    load_row(slab + ((long)bi * tokens + src) * D, D >> 2, lane, a);
+    add_row(r, a);
+  }
   layer_norm_regs(r, y, w, b, eps, D, lane);
   store_row16(out + (long)bi * D, y, D >> 2, lane);
 }
@@ -205,11 +226,18 @@ inline dim3 rows_grid(int rows) { return dim3((rows + 3) / 4); }
 
 hipError_t launch_ln_rows(DType dt, const float* x, const float* w, const float* b, float eps, void* out16,
                           int rows, int D, hipStream_t s) {
+  return launch_ln_rows_add(dt, const_cast<float*>(x), nullptr, w, b, eps, out16, rows, D, s);
+}
+
+hipError_t launch_ln_rows_add(DType dt, float* x, const float* slab, const float* w, const float* b, float eps,
+                              void* out16, int rows, int D, hipStream_t s) {
   if (D % 4 || D > 256 * MAXV) return hipErrorInvalidValue;
   if (dt == DT_BF16)
-    hipLaunchKernelGGL(ln_rows_kernel<__bf16>, rows_grid(rows), dim3(256), 0, s, x, w, b, eps, (__bf16*)out16, rows, D);
+    hipLaunchKernelGGL(ln_rows_kernel<__bf16>, rows_grid(rows), dim3(256), 0, s, x, slab, w, b, eps, (__bf16*)out16,
+                       rows, D);
   else
-    hipLaunchKernelGGL(ln_rows_kernel<_Float16>, rows_grid(rows), dim3(256), 0, s, x, w, b, eps, (_Float16*)out16, rows, D);
+    hipLaunchKernelGGL(ln_rows_kernel<_Float16>, rows_grid(rows), dim3(256), 0, s, x, slab, w, b, eps,
+                       (_Float16*)out16, rows, D);
   return hipGetLastError();
 }
 
@@ -241,14 +269,14 @@ hipError_t launch_text_embed_ln(DType dt, const int64_t* ids, const float* tok, 
   return hipGetLastError();
 }
 
-hipError_t launch_pool_ln(DType dt, const float* x, const int64_t* ids, int tokens, const float* w,
-                          const float* b, float eps, void* out16, int B, int D, hipStream_t s) {
+hipError_t launch_pool_ln(DType dt, const float* x, const float* slab, const int64_t* ids, int tokens,
+                          const float* w, const float* b, float eps, void* out16, int B, int D, hipStream_t s) {
   if (D % 4 || D > 256 * MAXV) return hipErrorInvalidValue;
   if (dt == DT_BF16)
-    hipLaunchKernelGGL(pool_ln_kernel<__bf16>, rows_grid(B), dim3(256), 0, s, x, ids, tokens, w, b, eps,
+    hipLaunchKernelGGL(pool_ln_kernel<__bf16>, rows_grid(B), dim3(256), 0, s, x, slab, ids, tokens, w, b, eps,
                        (__bf16*)out16, B, D);
   else
-    hipLaunchKernelGGL(pool_ln_kernel<_Float16>, rows_grid(B), dim3(256), 0, s, x, ids, tokens, w, b, eps,
+    hipLaunchKernelGGL(pool_ln_kernel<_Float16>, rows_grid(B), dim3(256), 0, s, x, slab, ids, tokens, w, b, eps,
                        (_Float16*)out16, B, D);
   return hipGetLastError();
 }

@@ -41,6 +41,11 @@ int tile_override() {
   const char* e = getenv("CLIPGPU_TEST_TILE");
   return e ? atoi(e) : 0;
 }
+// K-slices for the f32-epilogue GEMM hooks (CLIPGPU_TEST_KSPLIT, default 1).
+int ksplit_override() {
+  const char* e = getenv("CLIPGPU_TEST_KSPLIT");
+  return e ? atoi(e) : 1;
+}
 
 void up(void* d, const void* h, size_t n) { TCHECK(hipMemcpy(d, h, n, hipMemcpyHostToDevice)); }
 void down(void* h, const void* d, size_t n) { TCHECK(hipMemcpy(h, d, n, hipMemcpyDeviceToHost)); }
@@ -92,10 +97,22 @@ int clipgpu_test_gemm(int dtype, int mode, int act, int64_t M, int64_t N, int64_
     } else if (mode == 2) {
       epi = EPI_STORE32;
     }
+    const int ks = mode == 0 ? 1 : ksplit_override();
+    DevBuf dS(ks > 1 ? (size_t)(ks - 1) * M * N * 4 : 4);
+    if (ks > 1) {
+      g.ksplit = ks;
+      g.slab = dS.as<float>();
+    }
     TCHECK(launch_gemm(dt, A_ROWS, epi, mode == 0 ? act : 0, g, nullptr));
     TCHECK(hipDeviceSynchronize());
     if (mode == 0) down16(dt, out, dO.p, M * N);
     else down(out, dO.p, M * N * 4);
+    if (ks > 1) {  // the consumer's combine, in slice order (launch_ln_rows_add's x += slab)
+      std::vector<float> part((size_t)(ks - 1) * M * N);
+      down(part.data(), dS.p, part.size() * 4);
+      for (int sl = 0; sl < ks - 1; ++sl)
+        for (size_t i = 0; i < (size_t)(M * N); ++i) out[i] += part[(size_t)sl * M * N + i];
+    }
   });
 }
 
@@ -140,19 +157,34 @@ int clipgpu_test_patch_embed(int dtype, int mode, int64_t B, int64_t S, int64_t 
       for (int64_t k = 0; k < K; ++k) wpad[(size_t)(r * Kp + k)] = conv_w[r * K + k];
     up16(dt, dw.p, wpad.data(), D * Kp);
     up(dpos.p, pos, tokens * D * 4);
+    // the engine's stem: patch rows (16-bit) -> row GEMM with the patch epilogue
+    DevBuf drows(B * G * G * Kp * 2);
+    TCHECK(launch_patch_rows(dt, mode == 0 ? A_IMG_F32 : A_IMG_U8, dpix.p, mean, stdv, drows.p, (int)B, (int)S,
+                             (int)P, (int)K, (int)Kp, nullptr));
     GemmParams g{};
+    g.A = drows.p; g.lda = Kp;
     g.W = dw.p; g.ldw = Kp; g.out = dx.p; g.ldo = D; g.M = (int)(B * G * G); g.N = (int)D; g.K = (int)Kp;
-    g.Kv = (int)K;
     g.cls = 1;
-    g.img = dpix.p; g.S = (int)S; g.P = (int)P; g.G = (int)G; g.pos = dpos.as<float>();
+    g.G = (int)G; g.pos = dpos.as<float>();
     g.tile = tile_override();
-    for (int c = 0; c < 3; ++c) {
-      g.mean[c] = mean ? mean[c] : 0.f;
-      g.stdv[c] = stdv ? stdv[c] : 1.f;
-    }
-    TCHECK(launch_gemm(dt, mode == 0 ? A_IMG_F32 : A_IMG_U8, EPI_PATCH, 0, g, nullptr));
+    TCHECK(launch_gemm(dt, A_ROWS, EPI_PATCH, 0, g, nullptr));
     TCHECK(hipDeviceSynchronize());
     down(x_out, dx.p, B * tokens * D * 4);
+  });
+}
+
+int clipgpu_test_patch_rows(int dtype, int mode, int64_t B, int64_t S, int64_t P, const void* pixels,
+                            const float mean[3], const float stdv[3], float* rows_out) {
+  return guarded([&]() {
+    const DType dt = dt_of(dtype);
+    const int64_t G = S / P, K = 3 * P * P, Kp = (K + 63) / 64 * 64;
+    const size_t pix_bytes = mode == 0 ? (size_t)B * 3 * S * S * 4 : (size_t)B * S * S * 3;
+    DevBuf dpix(pix_bytes), drows(B * G * G * Kp * 2);
+    up(dpix.p, pixels, pix_bytes);
+    TCHECK(launch_patch_rows(dt, mode == 0 ? A_IMG_F32 : A_IMG_U8, dpix.p, mean, stdv, drows.p, (int)B, (int)S,
+                             (int)P, (int)K, (int)Kp, nullptr));
+    TCHECK(hipDeviceSynchronize());
+    down16(dt, rows_out, drows.p, B * G * G * Kp);
   });
 }
 
@@ -183,6 +215,12 @@ int clipgpu_test_gemm_bench(int dtype, int epi, int act, int64_t M, int64_t N, i
     g.A = dA.p; g.lda = K; g.W = dW.p; g.ldw = K; g.bias = dB.as<float>();
     g.out = dO.p; g.ldo = N; g.M = (int)M; g.N = (int)N; g.K = (int)K; g.tile = tile;
     const int e = epi == 1 ? EPI_RESID : (epi == 2 ? EPI_STORE32 : EPI_STORE16);
+    const int ks = e == EPI_STORE16 ? 1 : ksplit_override();
+    DevBuf dS(ks > 1 ? (size_t)(ks - 1) * M * N * 4 : 4);
+    if (ks > 1) {
+      g.ksplit = ks;
+      g.slab = dS.as<float>();
+    }
     for (int i = 0; i < 3; ++i) TCHECK(launch_gemm(dt, A_ROWS, e, epi == 0 ? act : 0, g, nullptr));
     hipEvent_t a, b;
     TCHECK(hipEventCreate(&a));

@@ -55,6 +55,7 @@ _PROTOS = [
     ("clipgpu_test_engine_tiles", c_int, [c_void_p, POINTER(c_int)]),
     ("clipgpu_test_read_weights", c_int, [c_char_p, c_int, c_char_p, c_void_p, c_int64]),
     ("clipgpu_test_patch_embed", c_int, [c_int, c_int, c_int64, c_int64, c_int64, c_int64, c_void_p, POINTER(c_float), POINTER(c_float), c_void_p, c_void_p, c_void_p]),
+    ("clipgpu_test_patch_rows", c_int, [c_int, c_int, c_int64, c_int64, c_int64, c_void_p, POINTER(c_float), POINTER(c_float), c_void_p]),
 ]
 
 SYMBOLS = [p[0] for p in _PROTOS]

@@ -29,11 +29,16 @@ int clipgpu_test_attention(int dtype, int64_t B, int64_t N, int64_t H, int64_t H
 int clipgpu_test_layernorm(int dtype, int64_t rows, int64_t D, float eps, const float* x, const float* w,
                            const float* b, float* out);
 
-/* Patch-embedding GEMM from normalised f32 NCHW pixels (mode 0) or u8 NHWC (mode 1):
+/* Patch-embedding stem from normalised f32 NCHW pixels (mode 0) or u8 NHWC (mode 1), as the
+ * engine runs it (patch rows, then the row GEMM with the patch epilogue):
  * x_out[B*(G*G+1)][D]: rows of patch tokens = conv + pos (CLS rows untouched = 0). */
 int clipgpu_test_patch_embed(int dtype, int mode, int64_t B, int64_t S, int64_t P, int64_t D, const void* pixels,
                              const float mean[3], const float std[3], const float* conv_w, const float* pos,
                              float* x_out);
+
+/* The staged 16-bit patch rows alone: rows_out[B*G*G][Kp] (as f32), Kp = 3*P*P rounded up to 64. */
+int clipgpu_test_patch_rows(int dtype, int mode, int64_t B, int64_t S, int64_t P, const void* pixels,
+                            const float mean[3], const float std[3], float* rows_out);
 
 /* Device-resident GEMM timing (random operands): `iters` back-to-back launches of the same
  * GEMM as the engine issues it (epi: 0 store16 (+act), 1 residual f32, 2 store32), tile:

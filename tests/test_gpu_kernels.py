@@ -97,6 +97,28 @@ def test_gemm_residual(dtype, tile):
     assert np.abs(out - ref).max() < 1e-4
 
 
+@pytest.mark.parametrize("ks", [2, 3])
+@pytest.mark.parametrize("mode,M,N,K", [(1, 6400, 768, 3072), (1, 1513, 640, 256), (2, 3000, 520, 384),
+                                        (1, 8300, 2056, 768)])
+def test_gemm_split_k(ks, mode, M, N, K, tile, monkeypatch):
+    """Split-K (the engine's out_proj / c_proj when max_batch leaves the chip under-filled):
+    slice 0 runs the epilogue, slices >= 1 store f32 partials that the consumer adds in
+    slice order; persistent multi-unit walks, M / N tails."""
+    if K % (64 * ks) or K // ks < 128:
+        pytest.skip("slice shorter than 2 K-steps")
+    monkeypatch.setenv("CLIPGPU_TEST_KSPLIT", str(ks))
+    dtype = BF16
+    rng = np.random.default_rng(M + N + K + ks)
+    A = round16(rng.standard_normal((M, K)), dtype)
+    W = round16(rng.standard_normal((N, K)) / np.sqrt(K), dtype)
+    bias = rng.standard_normal(N).astype(np.float32)
+    resid = rng.standard_normal((M, N)).astype(np.float32) if mode == 1 else None
+    out = run_gemm(dtype, mode, 0, A, W, bias, resid)
+    ref = A.astype(np.float64) @ W.T.astype(np.float64) + bias + (0 if resid is None else resid)
+    bound = 3e-5 * (np.abs(A) @ np.abs(W).T) + 1e-5
+    assert np.all(np.abs(out - ref) <= bound)
+
+
 @pytest.mark.parametrize("mode", [0, 1])
 def test_gemm_persistent_multi_tile(mode, tile):
     """ntiles > grid for every tile config (each block walks >= 2 tiles, the pipelined
@@ -177,6 +199,28 @@ def test_layernorm(dtype, D):
     ref = clip_ref.layer_norm(x.astype(np.float64), w, b, 1e-5)
     rel = 2 ** -8 if dtype == BF16 else 2 ** -11
     assert np.all(np.abs(out - ref) <= 1.01 * rel * np.abs(ref) + 1e-5)
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("S,P", [(224, 32), (64, 16), (70, 14), (384, 16)])
+def test_patch_rows_bit_exact(mode, S, P):
+    """Staged patch rows == bf16(normalised pixels) in conv1's (ch, ky, kx) order, zero K padding;
+    the u8 source normalises exactly as normalize_pixels (src/vision.rs:235-259)."""
+    L = _lib()
+    from oracle.model_spec import OPENAI_MEAN, OPENAI_STD
+    from tests.helpers import normalized_pixels
+    rng = np.random.default_rng(7 * S + mode)
+    B, G, K = 2, S // P, 3 * P * P
+    Kp = (K + 63) // 64 * 64
+    u8 = rng.integers(0, 256, (B, S, S, 3), dtype=np.uint8)
+    px = normalized_pixels(u8, OPENAI_MEAN, OPENAI_STD)
+    src = px if mode == 0 else u8
+    out = np.empty((B * G * G, Kp), np.float32)
+    L.check(L.lib().clipgpu_test_patch_rows(BF16, mode, B, S, P, src.ctypes.data, L.f3(OPENAI_MEAN),
+                                            L.f3(OPENAI_STD), out.ctypes.data))
+    ref = round16(px, BF16).reshape(B, 3, G, P, G, P).transpose(0, 2, 4, 1, 3, 5).reshape(B * G * G, K)
+    assert np.array_equal(out[:, :K], ref)
+    assert np.all(out[:, K:] == 0)
 
 
 @pytest.mark.parametrize("mode", [0, 1])

@@ -187,6 +187,28 @@ def test_gemm_tile_choice_is_bit_exact(tower, monkeypatch):
 
 
 @pytest.mark.parametrize("tower", [0, 1])
+def test_split_k_on_and_off_match_oracle(tower, monkeypatch):
+    """out_proj / c_proj with and without the K split (combined by the next LayerNorm /
+    the pooling LN) both meet the north-star tolerance; the split is fixed per engine, so
+    batch sizes inside one engine stay bit-identical."""
+    v, t = specs(VIT_B_32_CFG)
+    if tower == 0:
+        data = normalized_pixels(weights.synth_images_u8(43, 9, v.image_size), OPENAI_MEAN, OPENAI_STD)
+        ref = oracle_vision(VIT_B_32_CFG, 1234, data)
+    else:
+        data = weights.synth_token_ids(43, 9, t.context_length, t.vocab_size, t.vocab_size - 2,
+                                       t.vocab_size - 1, random_eot=True)
+        ref = oracle_text(VIT_B_32_CFG, 1234, data)
+    for split in ["0", "1"]:
+        monkeypatch.setenv("CLIPGPU_GEMM_SPLIT", split)
+        e = engine(VIT_B_32_CFG, tower, max_batch=9)
+        full = e.embed_pixels(data) if tower == 0 else e.embed_tokens(data)
+        check_rows(full, ref)
+        one = e.embed_pixels(data[3:4]) if tower == 0 else e.embed_tokens(data[3:4])
+        assert np.array_equal(one[0], full[3])
+
+
+@pytest.mark.parametrize("tower", [0, 1])
 def test_concurrent_lanes_are_bit_exact(tower, monkeypatch):
     """Splitting a batch over concurrent lanes (sub-batches on their own streams)
     is invisible in the output: rows never interact outside attention."""
