@@ -28,6 +28,7 @@
 #include "host/api_util.hpp"
 #include "host/json.hpp"
 #include "host/model.hpp"
+#include "host/resize_plan.hpp"
 #include "kernels/common.hpp"
 #include "kernels/kernels.hpp"
 
@@ -86,6 +87,17 @@ struct Replica {
   hipStream_t lane[4] = {nullptr, nullptr, nullptr, nullptr};
   hipEvent_t fork = nullptr, join[4] = {nullptr, nullptr, nullptr, nullptr};
   hipEvent_t done[4] = {nullptr, nullptr, nullptr, nullptr};  // host path: slot's D2H finished
+  // Decoded-image path (clipgpu_embed_images_rgb8): per slot, pinned staging and a device
+  // arena of [descriptors | ints | raw RGB8 images], and the resize intermediate.  Grown
+  // on demand (images have any size); reused across calls.
+  struct ImageSlot {
+    char* pin = nullptr;
+    size_t pin_cap = 0;
+    char* dev = nullptr;
+    size_t dev_cap = 0;
+    uint8_t* tmp = nullptr;
+    size_t tmp_cap = 0;
+  } islot[4];
 };
 
 }  // namespace clipgpu
@@ -806,6 +818,174 @@ void run_host(clipgpu_engine& e, InKind kind, const void* in, size_t in_row_byte
     if (codes[g]) throw ClipErr(codes[g], "device " + std::to_string(e.reps[g].device) + ": " + errs[g]);
 }
 
+// ---- decoded RGB8 images -> embeddings, crop/resize on the GPU -------------------------
+// Host: per image a ResizePlan (the same fixed-point tables as the host resize); device:
+// launch_resize into the slot's u8 NHWC input rows, then the u8 vision forward (normalise
+// + patch rows + trunk).  Chunks of <= one lane's rows (and <= kChunkRawBytes of source
+// pixels) pipelined over the lane slots as run_host_shard does.
+constexpr size_t kChunkRawBytes = 256u << 20;
+
+struct ResizeBatch {
+  std::vector<ResizeImage> d;
+  std::vector<int> ints;
+  std::vector<size_t> raw_off;  // per image, in the raw region
+  size_t raw_bytes = 0, tmp_bytes = 0;
+  int max_th = 0;
+};
+
+inline size_t align16(size_t n) { return (n + 15) & ~size_t(15); }
+
+ResizeBatch plan_resize_batch(int S, const std::string& interp, const std::string& mode, const int* W, const int* H,
+                              int64_t i0, int n) {
+  ResizeBatch b;
+  b.d.resize(n);
+  b.raw_off.resize(n);
+  for (int i = 0; i < n; ++i) {
+    const ResizePlan p = make_resize_plan(W[i0 + i], H[i0 + i], S, interp, mode);
+    ResizeImage& d = b.d[i];
+    d.W = p.W;
+    d.th = p.need_h ? p.th : 0;
+    d.yfirst = p.yfirst;
+    d.need_h = p.need_h;
+    d.need_v = p.need_v;
+    d.h_ksize = p.h.ksize;
+    d.v_ksize = p.v.ksize;
+    auto put = [&](const std::vector<int>& v) {
+      const long off = (long)b.ints.size();
+      b.ints.insert(b.ints.end(), v.begin(), v.end());
+      return off;
+    };
+    d.h_bounds = put(p.h.bounds);
+    d.h_coef = put(std::vector<int>(p.h.k.begin(), p.h.k.end()));
+    d.v_bounds = put(p.v.bounds);
+    d.v_coef = put(std::vector<int>(p.v.k.begin(), p.v.k.end()));
+    b.raw_off[i] = b.raw_bytes;
+    d.src = (long)b.raw_bytes;  // relative to the raw region
+    b.raw_bytes = align16(b.raw_bytes + (size_t)p.W * p.H * 3);
+    d.tmp = (long)b.tmp_bytes;
+    if (p.need_h) b.tmp_bytes = align16(b.tmp_bytes + (size_t)p.th * S * 3);
+    b.max_th = std::max(b.max_th, d.th);
+  }
+  return b;
+}
+
+void grow_pinned(char*& p, size_t& cap, size_t need) {
+  if (need <= cap) return;
+  if (p) HIP_CHECK(hipHostFree(p));
+  p = nullptr;
+  cap = 0;
+  HIP_CHECK(hipHostMalloc((void**)&p, need, hipHostMallocDefault));
+  cap = need;
+}
+template <typename P>
+void grow_device(P*& p, size_t& cap, size_t need) {
+  if (need <= cap) return;
+  if (p) HIP_CHECK(hipFree(p));
+  p = nullptr;
+  cap = 0;
+  HIP_CHECK(hipMalloc((void**)&p, need));
+  cap = need;
+}
+
+void run_images_shard(clipgpu_engine& e, Replica& r, const uint8_t* const* images, const int* W, const int* H,
+                      int64_t b0, int64_t b1, float* out) {
+  HIP_CHECK(hipSetDevice(r.device));
+  const int E = e.spec.embed_dim, L = e.lanes, S = e.spec.image_size;
+  const int rows = (e.max_batch + L - 1) / L;  // rows per slot
+  struct Pending { int64_t c0 = -1; int n = 0; };
+  Pending pend[4];
+  auto drain = [&](int k) {
+    if (pend[k].c0 < 0) return;
+    HIP_CHECK(hipEventSynchronize(r.done[k]));
+    std::memcpy(out + pend[k].c0 * E, r.pin_out + (size_t)k * rows * E, (size_t)pend[k].n * E * 4);
+    pend[k].c0 = -1;
+  };
+  int j = 0;
+  for (int64_t c0 = b0; c0 < b1; ++j) {
+    // chunk: up to `rows` images and kChunkRawBytes of source pixels (at least one image)
+    int n = 0;
+    size_t raw = 0;
+    while (c0 + n < b1 && n < rows) {
+      const size_t sz = (size_t)W[c0 + n] * H[c0 + n] * 3;
+      if (n > 0 && raw + sz > kChunkRawBytes) break;
+      raw += sz;
+      ++n;
+    }
+    const int k = j % L;
+    drain(k);
+    hipStream_t st = r.lane[k] ? r.lane[k] : r.stream;
+    const ResizeBatch b = plan_resize_batch(S, e.pre.interpolation, e.pre.resize_mode, W, H, c0, n);
+    const size_t desc_bytes = align16(b.d.size() * sizeof(ResizeImage));
+    const size_t ints_bytes = align16(b.ints.size() * sizeof(int));
+    const size_t total = desc_bytes + ints_bytes + b.raw_bytes;
+    Replica::ImageSlot& sl = r.islot[k];
+    grow_pinned(sl.pin, sl.pin_cap, total);
+    grow_device(sl.dev, sl.dev_cap, total);
+    grow_device(sl.tmp, sl.tmp_cap, std::max<size_t>(b.tmp_bytes, 16));
+    std::memcpy(sl.pin, b.d.data(), b.d.size() * sizeof(ResizeImage));
+    std::memcpy(sl.pin + desc_bytes, b.ints.data(), b.ints.size() * sizeof(int));
+    {  // pack the source images into pinned staging: images split over up to 8 copy threads
+      char* const raw_pin = sl.pin + desc_bytes + ints_bytes;
+      auto copy_range = [&](int i0, int i1) {
+        for (int i = i0; i < i1; ++i)
+          std::memcpy(raw_pin + b.raw_off[i], images[c0 + i], (size_t)W[c0 + i] * H[c0 + i] * 3);
+      };
+      const int nt = (int)std::min<size_t>({8, (size_t)n, std::max<size_t>(1, b.raw_bytes / (4u << 20))});
+      if (nt <= 1) {
+        if (n == 1) par_memcpy(raw_pin, images[c0], (size_t)W[c0] * H[c0] * 3);
+        else copy_range(0, n);
+      } else {
+        std::vector<std::thread> th;
+        for (int t = 0; t < nt; ++t) th.emplace_back(copy_range, n * t / nt, n * (t + 1) / nt);
+        for (auto& t : th) t.join();
+      }
+    }
+    HIP_CHECK(hipMemcpyAsync(sl.dev, sl.pin, total, hipMemcpyHostToDevice, st));
+    uint8_t* din = (uint8_t*)r.in + (size_t)k * rows * e.in_bytes_per_row;  // u8 [n][S][S][3]
+    check(launch_resize((const uint8_t*)sl.dev + desc_bytes + ints_bytes, sl.tmp, (const int*)(sl.dev + desc_bytes),
+                        (const ResizeImage*)sl.dev, n, b.max_th, S, din, st), "resize");
+    float* dout = r.out + (size_t)k * rows * E;
+    vision_forward(e, lane_view(e, r, k * rows), din, A_IMG_U8, e.pre.mean, e.pre.stdv, n, dout, st);
+    HIP_CHECK(hipMemcpyAsync(r.pin_out + (size_t)k * rows * E, dout, (size_t)n * E * 4, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipEventRecord(r.done[k], st));
+    pend[k].c0 = c0;
+    pend[k].n = n;
+    c0 += n;
+  }
+  for (int k = 0; k < L; ++k) drain(k);
+}
+
+// Contiguous row blocks over the replicas (rank order == input order), one host thread each.
+template <typename F>
+void run_sharded(clipgpu_engine& e, int64_t B, F shard) {
+  const int G = (int)e.reps.size();
+  if (G == 1) {
+    shard(e.reps[0], (int64_t)0, B);
+    return;
+  }
+  std::vector<std::thread> th;
+  std::vector<std::string> errs(G);
+  std::vector<int> codes(G, 0);
+  for (int g = 0; g < G; ++g) {
+    const int64_t b0 = B * g / G, b1 = B * (g + 1) / G;
+    if (b0 == b1) continue;
+    th.emplace_back([&, g, b0, b1]() {
+      try {
+        shard(e.reps[g], b0, b1);
+      } catch (const ClipErr& ex) {
+        codes[g] = ex.code;
+        errs[g] = ex.what();
+      } catch (const std::exception& ex) {
+        codes[g] = CLIPGPU_ERR_DEVICE;
+        errs[g] = ex.what();
+      }
+    });
+  }
+  for (auto& t : th) t.join();
+  for (int g = 0; g < G; ++g)
+    if (codes[g]) throw ClipErr(codes[g], "device " + std::to_string(e.reps[g].device) + ": " + errs[g]);
+}
+
 void destroy_replica(Replica& r) {
   (void)hipSetDevice(r.device);
   if (r.stream) (void)hipStreamSynchronize(r.stream);
@@ -820,6 +1000,11 @@ void destroy_replica(Replica& r) {
     if (r.done[i]) (void)hipEventDestroy(r.done[i]);
   }
   if (r.fork) (void)hipEventDestroy(r.fork);
+  for (auto& sl : r.islot) {
+    if (sl.pin) (void)hipHostFree(sl.pin);
+    if (sl.dev) (void)hipFree(sl.dev);
+    if (sl.tmp) (void)hipFree(sl.tmp);
+  }
   r = Replica();
 }
 
@@ -992,6 +1177,23 @@ int clipgpu_embed_u8_device(clipgpu_engine* e, const uint8_t* d_nhwc, int64_t B,
   });
 }
 
+int clipgpu_embed_images_rgb8(clipgpu_engine* e, const uint8_t* const* images, const int* widths,
+                              const int* heights, int64_t n, float* out) {
+  return guarded([&]() {
+    need_tower(e, TOWER_VISION);
+    if (n <= 0) throw ClipErr(CLIPGPU_ERR_INVALID, "Empty batch");  // src/vision.rs:121-123
+    if (!images || !widths || !heights || !out) throw ClipErr(CLIPGPU_ERR_INVALID, "NULL buffer");
+    for (int64_t i = 0; i < n; ++i) {
+      if (!images[i]) throw ClipErr(CLIPGPU_ERR_INVALID, "NULL image");
+      if (widths[i] <= 0 || heights[i] <= 0) throw ClipErr(CLIPGPU_ERR_INVALID, "Resize error: empty image");
+    }
+    std::lock_guard<std::mutex> lk(e->mu);
+    run_sharded(*e, n, [&](Replica& r, int64_t b0, int64_t b1) {
+      run_images_shard(*e, r, images, widths, heights, b0, b1, out);
+    });
+  });
+}
+
 int clipgpu_embed_tokens_device(clipgpu_engine* e, const int64_t* d_ids, int64_t B, float* d_out, void* stream) {
   return guarded([&]() {
     need_tower(e, TOWER_TEXT);
@@ -1000,6 +1202,38 @@ int clipgpu_embed_tokens_device(clipgpu_engine* e, const int64_t* d_ids, int64_t
     Replica& r = e->reps[0];
     HIP_CHECK(hipSetDevice(r.device));
     text_forward_lanes(*e, r, d_ids, (int)B, d_out, stream ? (hipStream_t)stream : r.stream);
+  });
+}
+
+int clipgpu_test_resize_rgb8_gpu(const uint8_t* const* images, const int* widths, const int* heights, int64_t n,
+                                 int size, const char* interpolation, const char* resize_mode, uint8_t* out) {
+  return guarded([&]() {
+    if (n <= 0 || n > 65535 || size <= 0) throw ClipErr(CLIPGPU_ERR_INVALID, "bad resize batch");
+    const ResizeBatch b = plan_resize_batch(size, interpolation ? interpolation : "bicubic",
+                                            resize_mode ? resize_mode : "shortest", widths, heights, 0, (int)n);
+    const size_t desc_bytes = align16(b.d.size() * sizeof(ResizeImage));
+    const size_t ints_bytes = align16(b.ints.size() * sizeof(int));
+    std::vector<char> host(desc_bytes + ints_bytes + b.raw_bytes);
+    std::memcpy(host.data(), b.d.data(), b.d.size() * sizeof(ResizeImage));
+    std::memcpy(host.data() + desc_bytes, b.ints.data(), b.ints.size() * sizeof(int));
+    for (int64_t i = 0; i < n; ++i)
+      std::memcpy(host.data() + desc_bytes + ints_bytes + b.raw_off[i], images[i], (size_t)widths[i] * heights[i] * 3);
+    char* dev = nullptr;
+    uint8_t *tmp = nullptr, *dout = nullptr;
+    const size_t out_bytes = (size_t)n * size * size * 3;
+    HIP_CHECK(hipMalloc((void**)&dev, host.size()));
+    HIP_CHECK(hipMalloc((void**)&tmp, std::max<size_t>(b.tmp_bytes, 16)));
+    HIP_CHECK(hipMalloc((void**)&dout, out_bytes));
+    HIP_CHECK(hipMemcpy(dev, host.data(), host.size(), hipMemcpyHostToDevice));
+    const hipError_t err = launch_resize((const uint8_t*)dev + desc_bytes + ints_bytes, tmp,
+                                         (const int*)(dev + desc_bytes), (const ResizeImage*)dev, (int)n, b.max_th,
+                                         size, dout, nullptr);
+    const hipError_t err2 = hipMemcpy(out, dout, out_bytes, hipMemcpyDeviceToHost);
+    (void)hipFree(dev);
+    (void)hipFree(tmp);
+    (void)hipFree(dout);
+    check(err, "resize");
+    check(err2, "resize copy-out");
   });
 }
 

@@ -27,12 +27,13 @@
 
 #include "../../../include/clipgpu.h"
 #include "api_util.hpp"
+#include "resize_plan.hpp"
 
 namespace clipgpu {
 
 namespace {
 
-constexpr int PRECISION_BITS = 32 - 8 - 2;
+constexpr int PRECISION_BITS = kResizePrecisionBits;
 
 double bicubic_filter(double x) {  // Keys cubic, a = -0.5 (CatmullRom)
   const double a = -0.5;
@@ -47,14 +48,8 @@ double bilinear_filter(double x) {
   return 0.0;
 }
 
-struct Coeffs {
-  int ksize = 0;
-  std::vector<int> bounds;  // [out][2] = xmin, count
-  std::vector<int32_t> k;   // [out][ksize] fixed point
-};
-
-Coeffs precompute(int in_size, double in0, double in1, int out_size, double (*filter)(double), double support0) {
-  Coeffs c;
+AxisPlan precompute(int in_size, double in0, double in1, int out_size, double (*filter)(double), double support0) {
+  AxisPlan c;
   const double scale = (in1 - in0) / out_size;
   const double filterscale = scale < 1.0 ? 1.0 : scale;
   const double support = support0 * filterscale;
@@ -86,91 +81,31 @@ Coeffs precompute(int in_size, double in0, double in1, int out_size, double (*fi
   return c;
 }
 
+// Nearest: output i reads input index floor(in0 + (i + 0.5) * scale), clamped.
+AxisPlan nearest_axis(int in_size, double in0, double in1, int out_size) {
+  AxisPlan c;
+  c.ksize = 1;
+  c.bounds.resize((size_t)out_size * 2);
+  c.k.assign((size_t)out_size, 1 << PRECISION_BITS);
+  const double sc = (in1 - in0) / out_size;
+  for (int i = 0; i < out_size; ++i) {
+    int x = (int)(in0 + (i + 0.5) * sc);
+    x = std::min(std::max(x, 0), in_size - 1);
+    c.bounds[(size_t)i * 2] = x;
+    c.bounds[(size_t)i * 2 + 1] = 1;
+  }
+  return c;
+}
+
 inline uint8_t clip8(int64_t in) {
   if (in >= ((int64_t)1 << PRECISION_BITS << 8)) return 255;
   if (in <= 0) return 0;
   return (uint8_t)(in >> PRECISION_BITS);
 }
 
-// Separable convolution resize of an RGB8 image restricted to box.
-void resize_conv(const uint8_t* src, int W, int H, double x0, double y0, double x1, double y1, int S,
-                 double (*filter)(double), double support, uint8_t* dst) {
-  const Coeffs ch = precompute(W, x0, x1, S, filter, support);
-  Coeffs cv = precompute(H, y0, y1, S, filter, support);
-  const bool need_h = S != W || x0 != 0.0 || x1 != (double)S;
-  const bool need_v = S != H || y0 != 0.0 || y1 != (double)S;
-  const int yfirst = cv.bounds[0];
-  const int ylast = cv.bounds[(size_t)(S - 1) * 2] + cv.bounds[(size_t)(S - 1) * 2 + 1];
-  std::vector<uint8_t> tmp;
-  const uint8_t* vin = src;
-  int vin_w = W;
-  if (need_h) {
-    for (int i = 0; i < S; ++i) cv.bounds[(size_t)i * 2] -= yfirst;
-    const int th = ylast - yfirst;
-    tmp.resize((size_t)S * th * 3);
-    for (int yy = 0; yy < th; ++yy) {
-      const uint8_t* row = src + (size_t)(yy + yfirst) * W * 3;
-      for (int xx = 0; xx < S; ++xx) {
-        const int xmin = ch.bounds[(size_t)xx * 2], cnt = ch.bounds[(size_t)xx * 2 + 1];
-        const int32_t* k = &ch.k[(size_t)xx * ch.ksize];
-        int64_t s0 = 1 << (PRECISION_BITS - 1), s1 = s0, s2 = s0;
-        for (int x = 0; x < cnt; ++x) {
-          const uint8_t* p = row + (size_t)(x + xmin) * 3;
-          s0 += (int64_t)p[0] * k[x];
-          s1 += (int64_t)p[1] * k[x];
-          s2 += (int64_t)p[2] * k[x];
-        }
-        uint8_t* o = &tmp[((size_t)yy * S + xx) * 3];
-        o[0] = clip8(s0);
-        o[1] = clip8(s1);
-        o[2] = clip8(s2);
-      }
-    }
-    vin = tmp.data();
-    vin_w = S;
-  } else if (yfirst != 0) {
-    // no horizontal pass: vertical bounds refer to source rows directly
-  }
-  if (need_v) {
-    for (int yy = 0; yy < S; ++yy) {
-      const int ymin = cv.bounds[(size_t)yy * 2], cnt = cv.bounds[(size_t)yy * 2 + 1];
-      const int32_t* k = &cv.k[(size_t)yy * cv.ksize];
-      for (int xx = 0; xx < S; ++xx) {
-        int64_t s0 = 1 << (PRECISION_BITS - 1), s1 = s0, s2 = s0;
-        for (int y = 0; y < cnt; ++y) {
-          const uint8_t* p = vin + ((size_t)(y + ymin) * vin_w + xx) * 3;
-          s0 += (int64_t)p[0] * k[y];
-          s1 += (int64_t)p[1] * k[y];
-          s2 += (int64_t)p[2] * k[y];
-        }
-        uint8_t* o = dst + ((size_t)yy * S + xx) * 3;
-        o[0] = clip8(s0);
-        o[1] = clip8(s1);
-        o[2] = clip8(s2);
-      }
-    }
-  } else {
-    for (int yy = 0; yy < S; ++yy) std::memcpy(dst + (size_t)yy * S * 3, vin + (size_t)yy * vin_w * 3, (size_t)S * 3);
-  }
-}
+}  // namespace
 
-void resize_nearest(const uint8_t* src, int W, int H, double x0, double y0, double x1, double y1, int S,
-                    uint8_t* dst) {
-  const double sx = (x1 - x0) / S, sy = (y1 - y0) / S;
-  for (int yy = 0; yy < S; ++yy) {
-    int y = (int)(y0 + (yy + 0.5) * sy);
-    y = std::min(std::max(y, 0), H - 1);
-    for (int xx = 0; xx < S; ++xx) {
-      int x = (int)(x0 + (xx + 0.5) * sx);
-      x = std::min(std::max(x, 0), W - 1);
-      std::memcpy(dst + ((size_t)yy * S + xx) * 3, src + ((size_t)y * W + x) * 3, 3);
-    }
-  }
-}
-
-void resize_rgb8(const uint8_t* rgb, int W, int H, int S, const std::string& interp, const std::string& mode,
-                 uint8_t* out) {
-  if (!rgb || !out) throw ClipErr(CLIPGPU_ERR_INVALID, "NULL buffer");
+ResizePlan make_resize_plan(int W, int H, int S, const std::string& interp, const std::string& mode) {
   if (W <= 0 || H <= 0 || S <= 0) throw ClipErr(CLIPGPU_ERR_INVALID, "Resize error: empty image");
   double x0 = 0, y0 = 0, x1 = W, y1 = H;
   if (mode != "squash") {  // src/vision.rs:184-192
@@ -186,9 +121,91 @@ void resize_rgb8(const uint8_t* rgb, int W, int H, int S, const std::string& int
     x1 = std::min((double)W, x1);
     y1 = std::min((double)H, y1);
   }
-  if (interp == "bicubic") resize_conv(rgb, W, H, x0, y0, x1, y1, S, bicubic_filter, 2.0, out);
-  else if (interp == "bilinear") resize_conv(rgb, W, H, x0, y0, x1, y1, S, bilinear_filter, 1.0, out);
-  else resize_nearest(rgb, W, H, x0, y0, x1, y1, S, out);
+  ResizePlan p;
+  p.W = W;
+  p.H = H;
+  p.S = S;
+  if (interp == "bicubic" || interp == "bilinear") {
+    double (*f)(double) = interp == "bicubic" ? bicubic_filter : bilinear_filter;
+    const double support = interp == "bicubic" ? 2.0 : 1.0;
+    p.h = precompute(W, x0, x1, S, f, support);
+    p.v = precompute(H, y0, y1, S, f, support);
+    p.need_h = S != W || x0 != 0.0 || x1 != (double)S;
+    p.need_v = S != H || y0 != 0.0 || y1 != (double)S;
+  } else {  // "nearest" and anything else (src/vision.rs:176-180)
+    p.h = nearest_axis(W, x0, x1, S);
+    p.v = nearest_axis(H, y0, y1, S);
+    p.need_h = p.need_v = true;
+  }
+  p.yfirst = 0;
+  p.th = H;
+  if (p.need_h) {  // the horizontal pass only produces the rows the vertical pass reads
+    p.yfirst = p.v.bounds[0];
+    int ylast = 0;
+    for (int i = 0; i < S; ++i) ylast = std::max(ylast, p.v.bounds[(size_t)i * 2] + p.v.bounds[(size_t)i * 2 + 1]);
+    p.th = ylast - p.yfirst;
+    for (int i = 0; i < S; ++i) p.v.bounds[(size_t)i * 2] -= p.yfirst;
+  }
+  return p;
+}
+
+void apply_resize_plan(const ResizePlan& p, const uint8_t* src, uint8_t* dst) {
+  const int S = p.S, W = p.W;
+  std::vector<uint8_t> tmp;
+  const uint8_t* vin = src;
+  int vin_w = W;
+  if (p.need_h) {
+    tmp.resize((size_t)S * p.th * 3);
+    for (int yy = 0; yy < p.th; ++yy) {
+      const uint8_t* row = src + (size_t)(yy + p.yfirst) * W * 3;
+      for (int xx = 0; xx < S; ++xx) {
+        const int xmin = p.h.bounds[(size_t)xx * 2], cnt = p.h.bounds[(size_t)xx * 2 + 1];
+        const int32_t* k = &p.h.k[(size_t)xx * p.h.ksize];
+        int64_t s0 = 1 << (PRECISION_BITS - 1), s1 = s0, s2 = s0;
+        for (int x = 0; x < cnt; ++x) {
+          const uint8_t* q = row + (size_t)(x + xmin) * 3;
+          s0 += (int64_t)q[0] * k[x];
+          s1 += (int64_t)q[1] * k[x];
+          s2 += (int64_t)q[2] * k[x];
+        }
+        uint8_t* o = &tmp[((size_t)yy * S + xx) * 3];
+        o[0] = clip8(s0);
+        o[1] = clip8(s1);
+        o[2] = clip8(s2);
+      }
+    }
+    vin = tmp.data();
+    vin_w = S;
+  }
+  if (p.need_v) {
+    for (int yy = 0; yy < S; ++yy) {
+      const int ymin = p.v.bounds[(size_t)yy * 2], cnt = p.v.bounds[(size_t)yy * 2 + 1];
+      const int32_t* k = &p.v.k[(size_t)yy * p.v.ksize];
+      for (int xx = 0; xx < S; ++xx) {
+        int64_t s0 = 1 << (PRECISION_BITS - 1), s1 = s0, s2 = s0;
+        for (int y = 0; y < cnt; ++y) {
+          const uint8_t* q = vin + ((size_t)(y + ymin) * vin_w + xx) * 3;
+          s0 += (int64_t)q[0] * k[y];
+          s1 += (int64_t)q[1] * k[y];
+          s2 += (int64_t)q[2] * k[y];
+        }
+        uint8_t* o = dst + ((size_t)yy * S + xx) * 3;
+        o[0] = clip8(s0);
+        o[1] = clip8(s1);
+        o[2] = clip8(s2);
+      }
+    }
+  } else {
+    for (int yy = 0; yy < S; ++yy) std::memcpy(dst + (size_t)yy * S * 3, vin + (size_t)yy * vin_w * 3, (size_t)S * 3);
+  }
+}
+
+namespace {
+
+void resize_rgb8(const uint8_t* rgb, int W, int H, int S, const std::string& interp, const std::string& mode,
+                 uint8_t* out) {
+  if (!rgb || !out) throw ClipErr(CLIPGPU_ERR_INVALID, "NULL buffer");
+  apply_resize_plan(make_resize_plan(W, H, S, interp, mode), rgb, out);
 }
 
 void normalize_pixels(const uint8_t* px, int S, const float* mean, const float* stdv, float* out) {

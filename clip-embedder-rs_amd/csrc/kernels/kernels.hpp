@@ -91,6 +91,18 @@ hipError_t launch_pool_ln(DType dt, const float* x, const float* slab, const int
 hipError_t launch_patch_rows(DType dt, int src, const void* img, const float* mean, const float* stdv, void* out,
                              int B, int S, int P, int Kv, int Kp, hipStream_t s);
 
+// GPU crop + resize (kernels/resize.hip) of n RGB8 images to u8 NHWC out[n][S][S][3], from
+// the host's ResizePlan tables: per image a descriptor (offsets into the raw / tmp byte
+// arenas and into the int32 arena holding bounds + fixed-point coefficients).
+struct ResizeImage {
+  long src, tmp;            // byte offsets: source [H][W][3] in raw, pass-1 output [th][S][3] in tmp
+  long h_bounds, h_coef;    // int offsets in ints: [S][2] (first, count), [S][h_ksize]
+  long v_bounds, v_coef;    // [S][2] (relative to the pass input rows), [S][v_ksize]
+  int W, th, yfirst, h_ksize, v_ksize, need_h, need_v, pad;
+};
+hipError_t launch_resize(const uint8_t* raw, uint8_t* tmp, const int* ints, const ResizeImage* d_imgs, int n,
+                         int max_th, int S, uint8_t* out, hipStream_t s);
+
 // out[r] = in[r] / max(||in[r]||_2, 1e-12)
 hipError_t launch_l2norm(const float* in, float* out, int B, int E, hipStream_t s);
 

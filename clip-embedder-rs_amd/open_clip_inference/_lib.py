@@ -35,6 +35,7 @@ _PROTOS = [
     ("clipgpu_embed_pixels_device", c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
     ("clipgpu_embed_u8_device", c_int, [c_void_p, c_void_p, c_int64, POINTER(c_float), POINTER(c_float), c_void_p, c_void_p]),
     ("clipgpu_embed_tokens_device", c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
+    ("clipgpu_embed_images_rgb8", c_int, [c_void_p, POINTER(c_void_p), POINTER(c_int), POINTER(c_int), c_int64, c_void_p]),
     ("clipgpu_preprocess_rgb8", c_int, [c_void_p, c_int, c_int, c_int, c_char_p, c_char_p, POINTER(c_float), POINTER(c_float), c_void_p]),
     ("clipgpu_resize_rgb8", c_int, [c_void_p, c_int, c_int, c_int, c_char_p, c_char_p, c_void_p]),
     ("clipgpu_preprocess_batch", c_int, [POINTER(c_void_p), POINTER(c_int), POINTER(c_int), c_int64, c_int, c_char_p, c_char_p, POINTER(c_float), POINTER(c_float), c_void_p]),
@@ -55,6 +56,7 @@ _PROTOS = [
     ("clipgpu_test_engine_tiles", c_int, [c_void_p, POINTER(c_int)]),
     ("clipgpu_test_read_weights", c_int, [c_char_p, c_int, c_char_p, c_void_p, c_int64]),
     ("clipgpu_test_patch_embed", c_int, [c_int, c_int, c_int64, c_int64, c_int64, c_int64, c_void_p, POINTER(c_float), POINTER(c_float), c_void_p, c_void_p, c_void_p]),
+    ("clipgpu_test_resize_rgb8_gpu", c_int, [POINTER(c_void_p), POINTER(c_int), POINTER(c_int), c_int64, c_int, c_char_p, c_char_p, c_void_p]),
     ("clipgpu_test_patch_rows", c_int, [c_int, c_int, c_int64, c_int64, c_int64, c_void_p, POINTER(c_float), POINTER(c_float), c_void_p]),
 ]
 

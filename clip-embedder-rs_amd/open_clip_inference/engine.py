@@ -69,6 +69,22 @@ class Engine:
                                      out.ctypes.data))
         return out
 
+    def embed_images_rgb8(self, images) -> np.ndarray:
+        """Decoded RGB8 images (HxWx3 uint8, any sizes) -> embeddings, crop/resize/normalise on
+        the GPU with the model folder's preprocess_cfg (clipgpu_embed_images_rgb8)."""
+        arrs = [np.ascontiguousarray(a, dtype=np.uint8) for a in images]
+        n = len(arrs)
+        for a in arrs:
+            if a.ndim != 3 or a.shape[2] != 3:
+                from .error import ShapeError
+                raise ShapeError(f"Shape error: expected [H,W,3] uint8, got {a.shape}")
+        ptrs = (c_void_p * max(n, 1))(*[a.ctypes.data for a in arrs])
+        ws = (c_int * max(n, 1))(*[a.shape[1] for a in arrs])
+        hs = (c_int * max(n, 1))(*[a.shape[0] for a in arrs])
+        out = np.empty((n, self.embed_dim), np.float32)
+        check(lib().clipgpu_embed_images_rgb8(self.handle, ptrs, ws, hs, n, out.ctypes.data))
+        return out
+
     def embed_tokens(self, ids: np.ndarray, mask: Optional[np.ndarray] = None) -> np.ndarray:
         x = np.ascontiguousarray(ids, dtype=np.int64)
         m = None if mask is None else np.ascontiguousarray(mask, dtype=np.int64)
@@ -154,6 +170,19 @@ def resize_rgb8(rgb: np.ndarray, size: int, interpolation: str = "bicubic", resi
     out = np.empty((size, size, 3), np.uint8)
     check(lib().clipgpu_resize_rgb8(x.ctypes.data, x.shape[1], x.shape[0], size, interpolation.encode(),
                                     resize_mode.encode(), out.ctypes.data))
+    return out
+
+
+def resize_rgb8_gpu(images, size: int, interpolation: str = "bicubic", resize_mode: str = "shortest"):
+    """The GPU crop/resize alone (test hook): [n, size, size, 3] uint8."""
+    arrs = [np.ascontiguousarray(a, dtype=np.uint8) for a in images]
+    n = len(arrs)
+    ptrs = (c_void_p * max(n, 1))(*[a.ctypes.data for a in arrs])
+    ws = (c_int * max(n, 1))(*[a.shape[1] for a in arrs])
+    hs = (c_int * max(n, 1))(*[a.shape[0] for a in arrs])
+    out = np.empty((n, size, size, 3), np.uint8)
+    check(lib().clipgpu_test_resize_rgb8_gpu(ptrs, ws, hs, n, size, interpolation.encode(), resize_mode.encode(),
+                                             out.ctypes.data))
     return out
 
 

@@ -99,8 +99,11 @@ class VisionEmbedder:
         return embs.reshape(-1)
 
     def embed_images(self, images) -> np.ndarray:
-        batch = self.preprocess_batch(images)
-        return self.session.embed_pixels(batch)
+        # preprocess_batch + run (src/vision.rs:100-117), with the crop/resize/normalise on the
+        # GPU: bit-identical to self.session.embed_pixels(self.preprocess_batch(images)).
+        if len(images) == 0:
+            raise InferenceError("Empty batch")
+        return self.session.embed_images_rgb8([to_rgb8(im) for im in images])
 
     # -- preprocessing (src/vision.rs:119-140) --
     def preprocess_batch(self, images) -> np.ndarray:

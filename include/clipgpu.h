@@ -96,6 +96,16 @@ int clipgpu_embed_u8_device(clipgpu_engine* e, const uint8_t* d_nhwc, int64_t B,
                             const float std[3], float* d_out, void* stream);
 int clipgpu_embed_tokens_device(clipgpu_engine* e, const int64_t* d_ids, int64_t B, float* d_out, void* stream);
 
+/* Decoded images straight to embeddings, crop/resize on the GPU (a3-a7 on the device).
+ * Replaces preprocess_batch + session.run in VisionEmbedder::embed_images
+ * (src/vision.rs:100-162): images[i] is [heights[i]][widths[i]][3] u8 (DynamicImage::to_rgb8
+ * layout, any size); the model folder's preprocess_cfg (interpolation, resize_mode, mean,
+ * std; src/config.rs:49-64) applies.  The GPU resize uses the host resize's fixed-point
+ * tables, so results are bit-identical to clipgpu_preprocess_batch + clipgpu_embed_pixels.
+ * out: [n,E] f32, L2-normalised. */
+int clipgpu_embed_images_rgb8(clipgpu_engine* e, const uint8_t* const* images, const int* widths, const int* heights,
+                              int64_t n, float* out);
+
 /* ---- host preprocessing (src/vision.rs:119-259) ----------------------------------------
  * rgb: [h][w][3] u8 (DynamicImage::to_rgb8 layout).  Resize with the crop box of
  * resize_with_fast_image_resize (src/vision.rs:164-198): unless resize_mode == "squash",

@@ -36,6 +36,11 @@ int clipgpu_test_patch_embed(int dtype, int mode, int64_t B, int64_t S, int64_t 
                              const float mean[3], const float std[3], const float* conv_w, const float* pos,
                              float* x_out);
 
+/* The GPU crop/resize alone (kernels/resize.hip): out [n][size][size][3] u8, to compare with
+ * clipgpu_resize_rgb8 (host) bit for bit. */
+int clipgpu_test_resize_rgb8_gpu(const uint8_t* const* images, const int* widths, const int* heights, int64_t n,
+                                 int size, const char* interpolation, const char* resize_mode, uint8_t* out);
+
 /* The staged 16-bit patch rows alone: rows_out[B*G*G][Kp] (as f32), Kp = 3*P*P rounded up to 64. */
 int clipgpu_test_patch_rows(int dtype, int mode, int64_t B, int64_t S, int64_t P, const void* pixels,
                             const float mean[3], const float std[3], float* rows_out);

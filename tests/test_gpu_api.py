@@ -131,3 +131,41 @@ def test_empty_batch_errors(model):
         VisionEmbedder.from_local_dir(d).build().embed_images([])
     with pytest.raises(InferenceError, match="Empty batch"):
         TextEmbedder.from_local_dir(d).build().embed_texts([])
+
+
+def resize_cases():
+    rng = np.random.default_rng(5)
+    sizes = [(389, 517), (97, 301), (224, 224), (2000, 1500), (64, 64), (33, 70), (1, 400), (700, 1),
+             (500, 500), (81, 64)]
+    return [rng.integers(0, 256, (h, w, 3), dtype=np.uint8) for h, w in sizes]
+
+
+@pytest.mark.parametrize("interp,mode", [("bicubic", "shortest"), ("bilinear", "shortest"),
+                                         ("nearest", "shortest"), ("bicubic", "squash"), ("bilinear", "squash")])
+@pytest.mark.parametrize("size", [224, 64, 384])
+def test_gpu_resize_bit_exact_vs_host(interp, mode, size):
+    """a5 on the GPU (kernels/resize.hip, clipgpu_embed_images_rgb8's first step) == the host
+    resize (pinned to the oracle / Pillow, test_cpu_preprocess.py) bit for bit: crop box,
+    up- and down-scaling, identity sizes, 1-pixel-wide images."""
+    from open_clip_inference.engine import resize_rgb8, resize_rgb8_gpu
+    ims = resize_cases()
+    got = resize_rgb8_gpu(ims, size, interp, mode)
+    for i, im in enumerate(ims):
+        ref = resize_rgb8(im, size, interp, mode)
+        assert np.array_equal(got[i], ref), (i, im.shape, int(np.abs(got[i].astype(int) - ref).max()))
+
+
+def test_embed_images_rgb8_matches_host_preprocess(model):
+    """Decoded images -> embeddings with the crop/resize/normalise on the GPU: bit-identical to
+    the host preprocess_batch + embed_pixels path, and at the oracle's cosine tolerance; a
+    multi-replica handle shards them in input order."""
+    from open_clip_inference import VisionEmbedder
+    cfg, d = model
+    ve = VisionEmbedder.from_local_dir(d).with_max_batch(4).build()
+    ims = images() + resize_cases()[:6]
+    host = ve.session.embed_pixels(ve.preprocess_batch(ims))
+    gpu = ve.session.embed_images_rgb8(ims)
+    assert np.array_equal(gpu, host)
+    assert clip_ref.cosine_rows(gpu[:4], oracle_images(cfg, ims[:4])).min() >= COS_TOL
+    multi = VisionEmbedder.from_local_dir(d).with_devices([0, 0]).with_max_batch(2).build()
+    assert np.array_equal(multi.session.embed_images_rgb8(ims), gpu)

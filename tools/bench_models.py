@@ -90,10 +90,33 @@ def host_leg(B=256, steps=6, warmup=2):
     e.close()
 
 
+def photos_leg(B=256, H=480, W=640, steps=4, warmup=1):
+    """Decoded 640x480 photos -> embeddings (a3-a7 + forward, BASELINE configs[1] model): the
+    reference's CPU resize path restated (host C++ preprocess_batch thread pool + embed_pixels)
+    against the GPU crop/resize path (clipgpu_embed_images_rgb8); outputs bit-identical."""
+    from open_clip_inference.engine import preprocess_batch_rgb8
+    d = model_dir(VIT_B_32_CFG)
+    e = Engine(d, 0, [0], "bf16", B)
+    rng = np.random.default_rng(1)
+    ims = [rng.integers(0, 256, (H, W, 3), dtype=np.uint8) for _ in range(B)]
+    pc = VIT_B_32_CFG["preprocess_cfg"]
+    legs = (("photos_host_resize", lambda: e.embed_pixels(preprocess_batch_rgb8(ims, 224, "bicubic", "shortest",
+                                                                                 pc["mean"], pc["std"]))),
+            ("photos_gpu_resize", lambda: e.embed_images_rgb8(ims)))
+    for kind, fn in legs:
+        dt = timed(fn, steps, warmup)
+        print(json.dumps({"measure": "b32_vision_" + kind, "batch": B, "image": f"{W}x{H} RGB8 (bicubic, shortest)",
+                          "units_per_s": round(B / dt, 1), "ms_per_step": round(dt * 1e3, 3),
+                          "host_threads": min(16, os.cpu_count() or 1)}), flush=True)
+    e.close()
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["host", "so400m", "h14"]
+    which = sys.argv[1:] or ["host", "photos", "so400m", "h14"]
     if "host" in which:
         host_leg()
+    if "photos" in which:
+        photos_leg()
     if "so400m" in which:
         device_leg("so400m_vision", SO400M_16_SIGLIP2_384_CFG, 0, 128)
     if "h14" in which:
