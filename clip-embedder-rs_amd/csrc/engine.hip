@@ -1194,6 +1194,48 @@ int clipgpu_embed_images_rgb8(clipgpu_engine* e, const uint8_t* const* images, c
   });
 }
 
+static void check_similarity_args(int64_t n_img, int64_t n_txt, int64_t E, int activation, int axis) {
+  if (n_img <= 0 || n_txt <= 0) throw ClipErr(CLIPGPU_ERR_INVALID, "Empty batch");
+  if (E <= 0 || E % 16) throw ClipErr(CLIPGPU_ERR_INVALID, "Shape error: embedding dim must be a multiple of 16");
+  if (n_img > (1L << 22) || n_txt > (1L << 30) || n_img * n_txt > (1L << 40))
+    throw ClipErr(CLIPGPU_ERR_INVALID, "Shape error: similarity matrix too large");
+  if (activation < CLIPGPU_SIM_SOFTMAX || activation > CLIPGPU_SIM_LOGITS || axis < 0 || axis > 1)
+    throw ClipErr(CLIPGPU_ERR_INVALID, "bad activation / axis");
+}
+
+int clipgpu_similarity_device(const float* d_img, int64_t n_img, const float* d_txt, int64_t n_txt, int64_t E,
+                              float logit_scale, float logit_bias, int activation, int axis, float* d_out,
+                              void* stream) {
+  return guarded([&]() {
+    check_similarity_args(n_img, n_txt, E, activation, axis);
+    if (!d_img || !d_txt || !d_out) throw ClipErr(CLIPGPU_ERR_INVALID, "NULL buffer");
+    check(launch_similarity(d_img, (int)n_img, d_txt, (int)n_txt, (int)E, logit_scale, logit_bias, activation, axis,
+                            d_out, (hipStream_t)stream),
+          "similarity");
+  });
+}
+
+int clipgpu_similarity(int device, const float* img, int64_t n_img, const float* txt, int64_t n_txt, int64_t E,
+                       float logit_scale, float logit_bias, int activation, int axis, float* out) {
+  return guarded([&]() {
+    check_similarity_args(n_img, n_txt, E, activation, axis);
+    if (!img || !txt || !out) throw ClipErr(CLIPGPU_ERR_INVALID, "NULL buffer");
+    HIP_CHECK(hipSetDevice(device));
+    const size_t bi = (size_t)n_img * E * 4, bt = (size_t)n_txt * E * 4, bo = (size_t)n_img * n_txt * 4;
+    char* d = nullptr;
+    HIP_CHECK(hipMalloc((void**)&d, align256(bi) + align256(bt) + bo));
+    float *di = (float*)d, *dt = (float*)(d + align256(bi)), *dO = (float*)(d + align256(bi) + align256(bt));
+    hipError_t err = hipMemcpy(di, img, bi, hipMemcpyHostToDevice);
+    if (err == hipSuccess) err = hipMemcpy(dt, txt, bt, hipMemcpyHostToDevice);
+    if (err == hipSuccess)
+      err = launch_similarity(di, (int)n_img, dt, (int)n_txt, (int)E, logit_scale, logit_bias, activation, axis, dO,
+                              nullptr);
+    if (err == hipSuccess) err = hipMemcpy(out, dO, bo, hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    check(err, "similarity");
+  });
+}
+
 int clipgpu_embed_tokens_device(clipgpu_engine* e, const int64_t* d_ids, int64_t B, float* d_out, void* stream) {
   return guarded([&]() {
     need_tower(e, TOWER_TEXT);

@@ -103,6 +103,12 @@ struct ResizeImage {
 hipError_t launch_resize(const uint8_t* raw, uint8_t* tmp, const int* ints, const ResizeImage* d_imgs, int n,
                          int max_th, int S, uint8_t* out, hipStream_t s);
 
+// Clip facade math (kernels/similarity.hip): out[i][j] = act(fmaf(img[i] . txt[j], scale, bias)),
+// act = softmax along axis (1: over labels per image, 0: over images per label), sigmoid, or none.
+enum SimAct { SIM_SOFTMAX = 0, SIM_SIGMOID = 1, SIM_LOGITS = 2 };
+hipError_t launch_similarity(const float* img, int ni, const float* txt, int nt, int E, float scale, float bias,
+                             int activation, int axis, float* out, hipStream_t s);
+
 // out[r] = in[r] / max(||in[r]||_2, 1e-12)
 hipError_t launch_l2norm(const float* in, float* out, int B, int E, hipStream_t s);
 

@@ -44,6 +44,8 @@ _PROTOS = [
     ("clipgpu_tokenize", c_int, [c_void_p, POINTER(c_char_p), c_void_p, c_int64, c_int, c_void_p, c_void_p]),
     ("clipgpu_tokenizer_token_id", c_int64, [c_void_p, c_char_p]),
     ("clipgpu_tokenizer_vocab_size", c_int64, [c_void_p]),
+    ("clipgpu_similarity", c_int, [c_int, c_void_p, c_int64, c_void_p, c_int64, c_int64, c_float, c_float, c_int, c_int, c_void_p]),
+    ("clipgpu_similarity_device", c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int64, c_float, c_float, c_int, c_int, c_void_p, c_void_p]),
     ("clipgpu_profile_enable", c_int, [c_void_p, ctypes.c_uint]),
     ("clipgpu_profile_read", c_int, [c_void_p, c_int, POINTER(c_double), POINTER(c_int64)]),
     ("clipgpu_profile_category_name", c_char_p, [c_int]),

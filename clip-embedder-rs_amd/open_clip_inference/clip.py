@@ -82,6 +82,36 @@ class Clip:
         res.sort(key=lambda x: -x[1])
         return res
 
+    # -- many images x many labels, math on the GPU -------------------
+    def _device_probs(self, img_embs, txt_embs, axis: int) -> np.ndarray:
+        from .engine import similarity
+        scale, bias = self._scale_bias()
+        act = self.text.model_config.activation_function or "softmax"
+        return similarity(img_embs, txt_embs, float(scale), float(bias), "sigmoid" if act == "sigmoid" else "softmax",
+                          axis, self.vision.session.devices[0])
+
+    def classify_many(self, images, labels: Sequence[str]) -> List[List[Tuple[str, float]]]:
+        """classify (src/clip.rs:92-132) for every image of a batch: one image batch, one label
+        batch, the [images x labels] probabilities on the GPU; each list sorted descending."""
+        probs = self._device_probs(self.vision.embed_images(images), self.text.embed_texts(labels), axis=1)
+        out = []
+        for row in probs:
+            res = [(str(l), float(p)) for l, p in zip(labels, row)]
+            res.sort(key=lambda x: -x[1])
+            out.append(res)
+        return out
+
+    def rank_images_many(self, images, texts: Sequence[str]) -> List[List[Tuple[int, float]]]:
+        """rank_images (src/clip.rs:134-170) for every query text: softmax over the images per
+        text on the GPU; one descending (image_index, probability) list per text."""
+        probs = self._device_probs(self.vision.embed_images(images), self.text.embed_texts(texts), axis=0)
+        out = []
+        for col in probs.T:
+            res = [(i, float(p)) for i, p in enumerate(col)]
+            res.sort(key=lambda x: -x[1])
+            out.append(res)
+        return out
+
     @staticmethod
     def softmax(logits) -> np.ndarray:  # src/clip.rs:172-179
         x = np.asarray(logits, np.float32)

@@ -173,6 +173,25 @@ def resize_rgb8(rgb: np.ndarray, size: int, interpolation: str = "bicubic", resi
     return out
 
 
+SIM_ACTIVATIONS = {"softmax": 0, "sigmoid": 1, "logits": 2}
+
+
+def similarity(img_embs: np.ndarray, txt_embs: np.ndarray, logit_scale: float = 1.0, logit_bias: float = 0.0,
+               activation: str = "softmax", axis: int = 1, device: int = 0) -> np.ndarray:
+    """src/clip.rs:79-185 arithmetic for [n_img, E] x [n_txt, E] on the GPU
+    (clipgpu_similarity): [n_img, n_txt] logits / sigmoid / softmax along `axis`."""
+    a = np.ascontiguousarray(img_embs, dtype=np.float32)
+    b = np.ascontiguousarray(txt_embs, dtype=np.float32)
+    if a.ndim != 2 or b.ndim != 2 or a.shape[1] != b.shape[1]:
+        from .error import ShapeError
+        raise ShapeError(f"Shape error: {a.shape} vs {b.shape}")
+    out = np.empty((a.shape[0], b.shape[0]), np.float32)
+    check(lib().clipgpu_similarity(int(device), a.ctypes.data, a.shape[0], b.ctypes.data, b.shape[0], a.shape[1],
+                                   float(logit_scale), float(logit_bias), SIM_ACTIVATIONS[activation], int(axis),
+                                   out.ctypes.data))
+    return out
+
+
 def resize_rgb8_gpu(images, size: int, interpolation: str = "bicubic", resize_mode: str = "shortest"):
     """The GPU crop/resize alone (test hook): [n, size, size, 3] uint8."""
     arrs = [np.ascontiguousarray(a, dtype=np.uint8) for a in images]

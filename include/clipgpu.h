@@ -139,6 +139,23 @@ int clipgpu_tokenize(clipgpu_tokenizer* t, const char* const* texts, const int64
 int64_t clipgpu_tokenizer_token_id(const clipgpu_tokenizer* t, const char* token);
 int64_t clipgpu_tokenizer_vocab_size(const clipgpu_tokenizer* t);
 
+/* ---- Clip facade math for many images x many labels -------------------
+ * The src/clip.rs:79-185 arithmetic on the GPU: logits[i][j] = dot(img[i], txt[j]).mul_add(
+ * logit_scale, logit_bias) (ModelConfig defaults 1.0 / 0.0 are the caller's), then
+ *   activation CLIPGPU_SIM_SOFTMAX: max-subtracted softmax along `axis` -- 1 = over the labels
+ *     of each image (classify, :92-132), 0 = over the images of each label (rank_images,
+ *     :134-170);  CLIPGPU_SIM_SIGMOID: elementwise sigmoid (activation_function "sigmoid");
+ *   CLIPGPU_SIM_LOGITS: the logits themselves (compare, :79-90).
+ * img [n_img][E], txt [n_txt][E] f32 (the embed_* outputs); out [n_img][n_txt] f32; E % 16 == 0.
+ * Host-buffer form on GPU `device`; the _device form takes device pointers and a stream.
+ * (The descending sort of classify / rank_images stays on the host.) */
+enum clipgpu_sim_activation { CLIPGPU_SIM_SOFTMAX = 0, CLIPGPU_SIM_SIGMOID = 1, CLIPGPU_SIM_LOGITS = 2 };
+int clipgpu_similarity(int device, const float* img, int64_t n_img, const float* txt, int64_t n_txt, int64_t E,
+                       float logit_scale, float logit_bias, int activation, int axis, float* out);
+int clipgpu_similarity_device(const float* d_img, int64_t n_img, const float* d_txt, int64_t n_txt, int64_t E,
+                              float logit_scale, float logit_bias, int activation, int axis, float* d_out,
+                              void* stream);
+
 /* ---- live kernel timing -------------------------------------------------------------------
  * Records HIP events around every launch whose category bit is set in `mask` (on the launch
  * stream), for the device-resident entry points.  Categories: 0 patch_embed, 1 stem_ln, 2 qkv,

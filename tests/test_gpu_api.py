@@ -169,3 +169,49 @@ def test_embed_images_rgb8_matches_host_preprocess(model):
     assert clip_ref.cosine_rows(gpu[:4], oracle_images(cfg, ims[:4])).min() >= COS_TOL
     multi = VisionEmbedder.from_local_dir(d).with_devices([0, 0]).with_max_batch(2).build()
     assert np.array_equal(multi.session.embed_images_rgb8(ims), gpu)
+
+
+@pytest.mark.parametrize("ni,nt,E", [(1, 3, 64), (300, 1000, 512), (1000, 1, 768), (65, 129, 1152), (7, 5000, 1024)])
+@pytest.mark.parametrize("act,axis", [("softmax", 1), ("softmax", 0), ("sigmoid", 1), ("logits", 1)])
+def test_similarity_kernel_vs_facade_math(ni, nt, E, act, axis):
+    """The facade arithmetic on the device (kernels/similarity.hip) vs the restated
+    src/clip.rs math in f64 (oracle/facade_ref.py): logits = dot * scale + bias; softmax along
+    either axis / sigmoid.  Exact-f32 MFMA dot products: |err| <= 1e-5 relative."""
+    from open_clip_inference.engine import similarity
+    rng = np.random.default_rng(ni * 7 + nt + E)
+    a = rng.standard_normal((ni, E)).astype(np.float32)
+    a /= np.linalg.norm(a, axis=1, keepdims=True)
+    b = rng.standard_normal((nt, E)).astype(np.float32)
+    b /= np.linalg.norm(b, axis=1, keepdims=True)
+    scale, bias = (100.0, 0.0) if act != "sigmoid" else (10.0, -10.0)
+    got = similarity(a, b, scale, bias, act, axis)
+    logits = a.astype(np.float64) @ b.T.astype(np.float64) * scale + bias
+    if act == "logits":
+        ref = logits
+    elif act == "sigmoid":
+        ref = facade_ref.sigmoid(logits)
+    else:
+        ref = np.apply_along_axis(facade_ref.softmax, axis, logits)
+    tol = 2e-5 * np.abs(ref) + (3e-5 if act == "logits" else 1e-6)
+    assert np.all(np.abs(got - ref) <= tol), float(np.abs(got - ref).max())
+
+
+def test_classify_many_and_rank_images_many(model):
+    """The batched facade (device math) agrees with the per-call facade on the same inputs."""
+    from open_clip_inference import Clip
+    cfg, d = model
+    clip = Clip.from_local_dir(d).build()
+    ims = images()
+    labels = TEXTS[:4]
+    many = clip.classify_many(ims, labels)
+    assert len(many) == len(ims)
+    for im, res in zip(ims, many):
+        one = clip.classify(im, labels)
+        assert [l for l, _ in res] == [l for l, _ in one] or np.allclose([p for _, p in res], [p for _, p in one],
+                                                                         atol=1e-5)
+        assert np.allclose(sorted(p for _, p in res), sorted(p for _, p in one), atol=1e-5)
+    ranks = clip.rank_images_many(ims, labels[:2])
+    for q, res in zip(labels[:2], ranks):
+        one = clip.rank_images(ims, q)
+        assert np.allclose(sorted(p for _, p in res), sorted(p for _, p in one), atol=1e-5)
+        assert sorted(i for i, _ in res) == list(range(len(ims)))

@@ -111,12 +111,35 @@ def photos_leg(B=256, H=480, W=640, steps=4, warmup=1):
     e.close()
 
 
+def similarity_leg(ni=65536, nt=1000, E=512, steps=5, warmup=2):
+    """Facade math on the device: [ni x E] images x [nt x E] labels -> softmax over labels
+    (classify for a whole image set), device-resident embeddings; exact-f32 MFMA."""
+    import ctypes
+    a = torch.nn.functional.normalize(torch.randn(ni, E, device="cuda"), dim=1)
+    b = torch.nn.functional.normalize(torch.randn(nt, E, device="cuda"), dim=1)
+    out = torch.empty(ni, nt, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    L = _lib.lib()
+
+    def run():
+        _lib.check(L.clipgpu_similarity_device(ctypes.c_void_p(a.data_ptr()), ni, ctypes.c_void_p(b.data_ptr()), nt, E,
+                                               100.0, 0.0, 0, 1, ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(s)))
+    dt = timed(run, steps, warmup)
+    ref = torch.softmax(100.0 * a @ b.T, dim=1)
+    err = float((out - ref).abs().max())
+    print(json.dumps({"measure": "similarity_softmax", "n_img": ni, "n_txt": nt, "E": E,
+                      "ms": round(dt * 1e3, 3), "tflops_f32": round(2 * ni * nt * E / dt / 1e12, 1),
+                      "max_abs_err_vs_torch": err}), flush=True)
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["host", "photos", "so400m", "h14"]
+    which = sys.argv[1:] or ["host", "photos", "similarity", "so400m", "h14"]
     if "host" in which:
         host_leg()
     if "photos" in which:
         photos_leg()
+    if "similarity" in which:
+        similarity_leg()
     if "so400m" in which:
         device_leg("so400m_vision", SO400M_16_SIGLIP2_384_CFG, 0, 128)
     if "h14" in which:
