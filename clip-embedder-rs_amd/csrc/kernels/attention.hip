@@ -164,156 +164,226 @@ hipError_t launch_typed(const void* qkv, void* out, int B, int N, int H, int D, 
 // Tiled ("flash") attention for long sequences and head dims 64 / 72 / 80:
 // SigLIP2-384 (576 tokens, d 72), ViT-H/14-378 (730 tokens, d 80).
 //
-// One 256-thread workgroup per (sequence, head, 64-query block); each wave owns
-// 16 queries.  Keys/values stream through LDS in tiles of 64 (K row-major, V
-// transposed; row strides of an odd number of 16-byte slots), S = Q K^T by
-// 16x16x32 MFMA with the head dim zero-padded to HK = 64 / 96, online softmax
-// (running row max m and sum l; O and l rescaled by exp(m_old - m_new)), P to
-// LDS, O += P V with the head dim padded to HV = 64 / 80.  Causal: tiles past
+// One 256-thread workgroup per (sequence, head, 128-query block); each wave owns
+// 32 queries as two 16-query MFMA blocks.  Keys/values stream through LDS in
+// tiles of 64, double-buffered: tile kt+1 is loaded into registers while tile kt
+// is computed and written to the other buffer behind one barrier per tile.
+//
+// Transposed products, so nothing but K and V ever touches LDS:
+//   S^T = K Q^T   (16x16x32 MFMA, A = K rows, B = Q; head dim zero-padded to HK)
+//     -> lane (fr, fq) holds the scores of query fr for keys t*16 + 4fq + j:
+//        the online-softmax row statistics of query fr live in that lane
+//        (max / sum across the 4 lanes of a column: two xor-shuffles);
+//   O^T += V^T P^T (A = V^T by ds_read_b64_tr_b16 from the row-major V tile,
+//        B = P^T straight from the S^T accumulators in a permuted key order
+//        both operands share), so O^T[d][q] also lands in query fr's lane and
+//        the rescale by exp(m_old - m_new) is one scalar per lane.
+// Softmax in base 2 (scale * log2 e folded into the scores).  Causal: tiles past
 // the block's last query are skipped, keys > query masked.
 // ---------------------------------------------------------------------------
+// ds_read_b64_tr_b16 (16-bit lanes; the i16 form, reinterpreted as T)
+template <typename T>
+struct TrRead {
+  typedef T V4 __attribute__((ext_vector_type(4)));
+  typedef short I4 __attribute__((ext_vector_type(4)));
+  static __device__ __forceinline__ V4 read(const char* p) {
+    return __builtin_bit_cast(V4, __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) I4*)p));
+  }
+};
+
 template <typename T, int HD>
-__global__ __launch_bounds__(256) void flash_attn_kernel(const T* __restrict__ qkv, T* __restrict__ out, int N,
-                                                         int H, int D, int causal, float scale) {
+__global__ __launch_bounds__(256, 2) void flash_attn_kernel(const T* __restrict__ qkv, T* __restrict__ out, int N,
+                                                            int H, int D, int causal, float scale_log2) {
   typedef typename Vec8<T>::type V8;
+  typedef typename Vec4<T>::type V4;
+  typedef typename TrRead<T>::V4 TR4;
   constexpr int HK = (HD + 31) / 32 * 32, HV = (HD + 15) / 16 * 16;
-  constexpr int KT = 64;                      // keys per tile
-  constexpr int KROW = HK * 2 + 16;           // bytes: K rows
-  constexpr int VROW = KT * 2 + 16;           // bytes: V^T and P rows
-  constexpr int CH = HD / 8;                  // 16-byte chunks per head row
-  __shared__ __attribute__((aligned(16))) char smem[KT * KROW + HV * VROW + 4 * 16 * VROW];
-  char* const sK = smem;
-  char* const sVt = smem + KT * KROW;
+  constexpr int KT = 64, QW = 32, QB = 4 * QW;  // keys per tile, queries per wave / block
+  constexpr int CH = HD / 8;                    // 16-byte chunks per head row
+  constexpr int KROW = HK * 2 + 16;             // K rows: an odd count of 16-byte slots
+  constexpr int VROW = 160;                     // V rows: 40 banks, so the 8 rows one 32-lane
+                                                // half of a transposed read touches are disjoint
+  static_assert(HV * 2 <= VROW, "V row");
+  constexpr int KBUF = KT * KROW, VBUF = KT * VROW, BUF = KBUF + VBUF;
+  constexpr int PER = (KT * CH + 255) / 256;    // 16-byte chunks of K (and of V) per thread per tile
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int nqb = (N + 63) / 64;
+  const int nqb = (N + QB - 1) / QB;
   const int qb = blockIdx.x % nqb, bh = blockIdx.x / nqb;
   const int b = bh / H, h = bh % H;
   const long ld = 3L * D;
   const T* base = qkv + (long)b * N * ld + (long)h * HD;
-  char* const sP = smem + KT * KROW + HV * VROW + wave * 16 * VROW;
   const int fr = lane & 15, fq = lane >> 4;
 
-  // zero the padding that tile loads never write: K head-dim pad, V^T pad rows
+  // zero the padding that tile stores never write (both buffers): K cols HD..HK, V cols HD..HV
   if constexpr (HK > HD) {
     constexpr int PADC = HK / 8 - CH;
-    for (int q = tid; q < KT * PADC; q += 256) *(V8*)(sK + (q / PADC) * KROW + (CH + q % PADC) * 16) = V8{};
+    for (int q = tid; q < 2 * KT * PADC; q += 256) {
+      const int bf = q / (KT * PADC), r = (q / PADC) % KT, c = CH + q % PADC;
+      *(V8*)(smem + bf * BUF + r * KROW + c * 16) = V8{};
+    }
   }
-  if constexpr (HV > HD)
-    for (int q = tid; q < (HV - HD) * KT; q += 256) *(T*)(sVt + (HD + q / KT) * VROW + (q % KT) * 2) = (T)0.f;
+  if constexpr (HV > HD) {
+    constexpr int PADC = HV / 8 - CH;
+    for (int q = tid; q < 2 * KT * PADC; q += 256) {
+      const int bf = q / (KT * PADC), r = (q / PADC) % KT, c = CH + q % PADC;
+      *(V8*)(smem + bf * BUF + KBUF + r * VROW + c * 16) = V8{};
+    }
+  }
 
-  // this wave's 16 queries: Q fragments (head dim zero-padded to HK)
-  const int q0 = qb * 64 + wave * 16;
-  V8 qa[HK / 32];
-  {
-    const int qr = min(q0 + fr, N - 1);
+  // this wave's 32 queries: Q fragments (B operand: [d][query]), head dim zero-padded to HK
+  const int q0 = qb * QB + wave * QW;
+  V8 qf[2][HK / 32];
+#pragma unroll
+  for (int qi = 0; qi < 2; ++qi) {
+    const int qr = min(q0 + qi * 16 + fr, N - 1);
 #pragma unroll
     for (int kk = 0; kk < HK / 32; ++kk) {
       const int c = kk * 4 + fq;
-      qa[kk] = c < CH ? *(const V8*)(base + (long)qr * ld + c * 8) : V8{};
+      qf[qi][kk] = c < CH ? *(const V8*)(base + (long)qr * ld + c * 8) : V8{};
     }
   }
-  f32x4 o[HV / 16];
+  f32x4 o[2][HV / 16];
 #pragma unroll
-  for (int ni = 0; ni < HV / 16; ++ni) o[ni] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float m[4], l[4];
+  for (int qi = 0; qi < 2; ++qi)
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    m[j] = -INFINITY;
-    l[j] = 0.f;
-  }
+    for (int ni = 0; ni < HV / 16; ++ni) o[qi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
 
-  const int last_key = causal ? min(N, qb * 64 + 64) : N;
-  const int ntiles = (last_key + KT - 1) / KT;
-  for (int kt = 0; kt < ntiles; ++kt) {
-    __syncthreads();  // previous tile fully consumed
-    for (int q = tid; q < KT * CH; q += 256) {
-      const int r = q / CH, c = q % CH, key = kt * KT + r;
-      V8 kv{}, vv{};
-      if (key < N) {
-        kv = *(const V8*)(base + (long)key * ld + D + c * 8);
-        vv = *(const V8*)(base + (long)key * ld + 2 * D + c * 8);
+  V8 kr[PER], vr[PER];
+  auto load_tile = [&](int kt) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int q = tid + 256 * i, r = q / CH, c = q - r * CH, key = kt * KT + r;
+      const bool ok = q < KT * CH && key < N;
+      kr[i] = ok ? *(const V8*)(base + (long)key * ld + D + c * 8) : V8{};
+      vr[i] = ok ? *(const V8*)(base + (long)key * ld + 2 * D + c * 8) : V8{};
+    }
+  };
+  auto store_tile = [&](int bf) {
+    char* const sK = smem + bf * BUF;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int q = tid + 256 * i, r = q / CH, c = q - r * CH;
+      if (q < KT * CH) {
+        *(V8*)(sK + r * KROW + c * 16) = kr[i];
+        *(V8*)(sK + KBUF + r * VROW + c * 16) = vr[i];
       }
-      *(V8*)(sK + r * KROW + c * 16) = kv;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) *(T*)(sVt + (c * 8 + e) * VROW + r * 2) = vv[e];
     }
-    __syncthreads();
+  };
 
-    // S[q][key]: s[t][j] = S[q0 + fq*4 + j][kt*64 + t*16 + fr]
-    f32x4 s[4];
+  const int last_key = causal ? min(N, qb * QB + QB) : N;
+  const int ntiles = (last_key + KT - 1) / KT;
+  load_tile(0);
+  store_tile(0);
+  __syncthreads();
+  for (int kt = 0; kt < ntiles; ++kt) {
+    const char* const sK = smem + (kt & 1) * BUF;
+    const char* const sV = sK + KBUF;
+    if (kt + 1 < ntiles) load_tile(kt + 1);
+
+    // S^T: s[qi][t][j] = S[query q0 + qi*16 + fr][key kt*64 + t*16 + 4fq + j]
+    f32x4 s[2][4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      V8 ka[HK / 32];
 #pragma unroll
-      for (int kk = 0; kk < HK / 32; ++kk) {
-        const V8 kb = *(const V8*)(sK + (t * 16 + fr) * KROW + (kk * 4 + fq) * 16);
-        s[t] = mfma_16x16x32(qa[kk], kb, s[t]);
+      for (int kk = 0; kk < HK / 32; ++kk) ka[kk] = *(const V8*)(sK + (t * 16 + fr) * KROW + (kk * 4 + fq) * 16);
+#pragma unroll
+      for (int qi = 0; qi < 2; ++qi) {
+        s[qi][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < HK / 32; ++kk) s[qi][t] = mfma_16x16x32(ka[kk], qf[qi][kk], s[qi][t]);
       }
     }
+    // online softmax: each lane holds one query (fr) per q-block
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int qrow = q0 + fq * 4 + j;
+    for (int qi = 0; qi < 2; ++qi) {
+      const int qrow = q0 + qi * 16 + fr;
       float mt = -INFINITY;
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const int key = kt * KT + t * 16 + fr;
-        float v = s[t][j] * scale;
-        if (key >= N || (causal && key > qrow)) v = -INFINITY;
-        s[t][j] = v;
-        mt = fmaxf(mt, v);
-      }
-      mt = group16_max(mt);
-      const float mn = fmaxf(m[j], mt);
-      const float corr = __expf(m[j] - mn);  // m[j] = -inf on the first tile: 0
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int key = kt * KT + t * 16 + 4 * fq + j;
+          float v = s[qi][t][j] * scale_log2;
+          if (key >= N || (causal && key > qrow)) v = -INFINITY;
+          s[qi][t][j] = v;
+          mt = fmaxf(mt, v);
+        }
+      mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
+      mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+      const float mn = fmaxf(m[qi], mt);
+      const float corr = exp2f(m[qi] - mn);  // m = -inf on the first tile: 0
       float sum = 0.f;
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const float e = __expf(s[t][j] - mn);
-        s[t][j] = e;
-        sum += e;
-      }
-      l[j] = l[j] * corr + group16_sum(sum);
-      m[j] = mn;
+      for (int t = 0; t < 4; ++t)
 #pragma unroll
-      for (int ni = 0; ni < HV / 16; ++ni) o[ni][j] *= corr;
+        for (int j = 0; j < 4; ++j) {
+          const float e = exp2f(s[qi][t][j] - mn);
+          s[qi][t][j] = e;
+          sum += e;
+        }
+      sum += __shfl_xor(sum, 16, 64);
+      sum += __shfl_xor(sum, 32, 64);
+      l[qi] = l[qi] * corr + sum;
+      m[qi] = mn;
+#pragma unroll
+      for (int ni = 0; ni < HV / 16; ++ni) o[qi][ni] *= corr;
     }
-    // P -> this wave's LDS rows, then O += P V
+    // O^T[d][q] += V^T P^T over 2 k-steps of 32 keys; k order (both operands):
+    // element e of lane quarter fq <-> key 32ks + 16(e >> 2) + 4fq + (e & 3)
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+    for (int ks = 0; ks < 2; ++ks) {
+      V8 pf[2];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) *(T*)(sP + (fq * 4 + j) * VROW + (t * 16 + fr) * 2) = (T)s[t][j];
-    __builtin_amdgcn_wave_barrier();
+      for (int qi = 0; qi < 2; ++qi)
 #pragma unroll
-    for (int ks = 0; ks < KT / 32; ++ks) {
-      const V8 pa = *(const V8*)(sP + fr * VROW + (ks * 32 + fq * 8) * 2);
+        for (int e = 0; e < 8; ++e) pf[qi][e] = (T)s[qi][2 * ks + (e >> 2)][e & 3];
+      const char* const va0 = sV + (32 * ks + 4 * fq + (fr >> 2)) * VROW + 8 * (fr & 3);
 #pragma unroll
       for (int ni = 0; ni < HV / 16; ++ni) {
-        const V8 vb = *(const V8*)(sVt + (ni * 16 + fr) * VROW + (ks * 32 + fq * 8) * 2);
-        o[ni] = mfma_16x16x32(pa, vb, o[ni]);
+        const TR4 lo = TrRead<T>::read(va0 + ni * 32);
+        const TR4 hi = TrRead<T>::read(va0 + 16 * VROW + ni * 32);
+        V8 va;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          va[e] = lo[e];
+          va[e + 4] = hi[e];
+        }
+#pragma unroll
+        for (int qi = 0; qi < 2; ++qi) o[qi][ni] = mfma_16x16x32(va, pf[qi], o[qi][ni]);
       }
     }
-    __builtin_amdgcn_wave_barrier();
+    if (kt + 1 < ntiles) store_tile((kt + 1) & 1);
+    __syncthreads();
   }
+  // O^T[d = ni*16 + 4fq + j][q = fr]: 4 consecutive head dims per lane -> one 8-byte store
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int q = q0 + fq * 4 + j;
+  for (int qi = 0; qi < 2; ++qi) {
+    const int q = q0 + qi * 16 + fr;
     if (q >= N) continue;
-    const float inv = 1.0f / l[j];
+    const float inv = 1.0f / l[qi];
     T* dst = out + ((long)b * N + q) * D + (long)h * HD;
 #pragma unroll
     for (int ni = 0; ni < HV / 16; ++ni) {
-      const int d = ni * 16 + fr;
-      if (d < HD) dst[d] = (T)(o[ni][j] * inv);
+      const int d0 = ni * 16 + 4 * fq;
+      if (d0 < HD) {
+        V4 w;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) w[j] = (T)(o[qi][ni][j] * inv);
+        *(V4*)(dst + d0) = w;
+      }
     }
   }
 }
 
 template <typename T, int HD>
 hipError_t launch_flash(const void* qkv, void* out, int B, int N, int H, int D, int causal, hipStream_t s) {
-  const int nqb = (N + 63) / 64;
+  const int nqb = (N + 127) / 128;
   hipLaunchKernelGGL((flash_attn_kernel<T, HD>), dim3(B * H * nqb), dim3(256), 0, s, (const T*)qkv, (T*)out, N, H, D,
-                     causal, 1.0f / sqrtf((float)HD));
+                     causal, 1.4426950408889634f / sqrtf((float)HD));
   return hipGetLastError();
 }
 
