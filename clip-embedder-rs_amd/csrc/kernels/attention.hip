@@ -7,12 +7,15 @@
 // per (sequence, head), head_dim d = 64.
 //
 // One 256-thread workgroup per (sequence, head).  K (row-major, XOR-swizzled)
-// and V (transposed, padded rows) for the whole sequence sit in LDS; each wave
-// owns 16-query tiles: S = Q K^T via 16x16x32 MFMA with the key on the lane,
-// softmax in registers (row max / sum across the 16 lanes of a row group),
-// unnormalised P -> LDS (16-bit), O = P V via MFMA, 1/rowsum applied in the
-// epilogue.  Padded keys (>= N) and, for text, keys above the diagonal are
-// masked to -inf (open_clip build_causal_mask: triu(-inf, 1)).
+// and V (row-major, 160-byte rows) for the whole sequence sit in LDS; each wave
+// owns 16-query tiles and computes the transposed products of flash_attn_kernel
+// below: S^T = K Q^T (16x16x32 MFMA; lane (fr, fq) holds query fr's scores for
+// keys t*16 + 4fq + j, so the row max / sum are in-lane plus two xor-shuffles),
+// O^T = V^T P^T with V^T read by ds_read_b64_tr_b16 and P^T taken straight from
+// the S^T accumulators (a key order both operands share), 1/rowsum in the
+// epilogue, 8-byte stores of 4 head dims.  Padded keys (>= N) and, for text,
+// keys above the diagonal are masked to -inf (open_clip build_causal_mask:
+// triu(-inf, 1)).
 #include "common.hpp"
 #include "kernels.hpp"
 
@@ -20,53 +23,60 @@ namespace clipgpu {
 
 namespace {
 
+// ds_read_b64_tr_b16 (16-bit lanes; the i16 form, reinterpreted as T): per 16-lane group,
+// lane 4q+p addresses row q, columns 4p..4p+3 of a 4 x 16 block; lane i receives column i.
+template <typename T>
+struct TrRead {
+  typedef T V4 __attribute__((ext_vector_type(4)));
+  typedef short I4 __attribute__((ext_vector_type(4)));
+  static __device__ __forceinline__ V4 read(const char* p) {
+    return __builtin_bit_cast(V4, __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) I4*)p));
+  }
+};
+
 template <typename T, int NKT>
 __global__ __launch_bounds__(256) void attn_kernel(const T* __restrict__ qkv, T* __restrict__ out,
                                                    int N, int H, int D, int causal) {
   typedef typename Vec8<T>::type V8;
+  typedef typename Vec4<T>::type V4;
+  typedef typename TrRead<T>::V4 TR4;
   constexpr int NKP = NKT * 16;          // padded key count (multiple of 32)
-  constexpr int ROW = NKP * 2 + 16;      // byte stride of Vt / P rows (odd # of 16B slots)
+  constexpr int VROW = 160;              // V rows: 40 banks (conflict-free transposed reads)
   constexpr int K_BYTES = NKP * 128;
-  constexpr int VT_BYTES = 64 * ROW;
-  constexpr int P_BYTES = 16 * ROW;
-  __shared__ __attribute__((aligned(16))) char smem[K_BYTES + VT_BYTES + 4 * P_BYTES];
+  __shared__ __attribute__((aligned(16))) char smem[K_BYTES + NKP * VROW];
   char* const sK = smem;
-  char* const sVt = smem + K_BYTES;
+  char* const sV = smem + K_BYTES;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int b = blockIdx.x / H, h = blockIdx.x % H;
   const long ld = 3L * D;
   const T* base = qkv + (long)b * N * ld + h * 64;
 
-  // K rows (swizzled) and V transposed into LDS; zero the padded keys.
+  // K rows (swizzled) and V rows into LDS; zero the padded keys.
   for (int q = tid; q < NKP * 8; q += 256) {
     const int r = q >> 3, c = q & 7;
-    V8 kv, vv;
+    V8 kv{}, vv{};
     if (r < N) {
       kv = *(const V8*)(base + (long)r * ld + D + c * 8);
       vv = *(const V8*)(base + (long)r * ld + 2 * D + c * 8);
-    } else {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) { kv[e] = (T)0.f; vv[e] = (T)0.f; }
     }
     *(V8*)(sK + r * 128 + ((c ^ ((r >> 1) & 7)) << 4)) = kv;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) *(T*)(sVt + (c * 8 + e) * ROW + r * 2) = vv[e];
+    *(V8*)(sV + r * VROW + c * 16) = vv;
   }
   __syncthreads();
 
-  char* const sP = smem + K_BYTES + VT_BYTES + wave * P_BYTES;
   const int fr = lane & 15, fq = lane >> 4;
-  const float scale = 0.125f;  // 1/sqrt(64)
+  const float scale_log2 = 0.125f * 1.4426950408889634f;  // 1/sqrt(64), base-2 softmax
   const int nqt = (N + 15) >> 4;
 
   for (int qt = wave; qt < nqt; qt += 4) {
-    const int qrow_l = min(qt * 16 + fr, N - 1);
-    V8 qa[2];
+    const int q = qt * 16 + fr;
+    const int qrow_l = min(q, N - 1);
+    V8 qf[2];
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) qa[kk] = *(const V8*)(base + (long)qrow_l * ld + kk * 32 + fq * 8);
+    for (int kk = 0; kk < 2; ++kk) qf[kk] = *(const V8*)(base + (long)qrow_l * ld + kk * 32 + fq * 8);
 
-    // S[q][key]: s[t][j] = S[qt*16 + fq*4 + j][t*16 + fr]
+    // S^T: s[t][j] = S[query q][key t*16 + 4fq + j]
     f32x4 s[NKT];
 #pragma unroll
     for (int t = 0; t < NKT; ++t) {
@@ -74,65 +84,69 @@ __global__ __launch_bounds__(256) void attn_kernel(const T* __restrict__ qkv, T*
       const int r = t * 16 + fr;
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
-        const V8 kb = *(const V8*)(sK + r * 128 + (((kk * 4 + fq) ^ (fr >> 1)) << 4));
-        s[t] = mfma_16x16x32(qa[kk], kb, s[t]);
+        const V8 ka = *(const V8*)(sK + r * 128 + (((kk * 4 + fq) ^ (fr >> 1)) << 4));
+        s[t] = mfma_16x16x32(ka, qf[kk], s[t]);
       }
     }
-
-    float inv[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int qrow = qt * 16 + fq * 4 + j;
-      float m = -INFINITY;
-#pragma unroll
-      for (int t = 0; t < NKT; ++t) {
-        const int key = t * 16 + fr;
-        float v = s[t][j] * scale;
-        if (key >= N || (causal && key > qrow)) v = -INFINITY;
-        s[t][j] = v;
-        m = fmaxf(m, v);
-      }
-      m = group16_max(m);
-      float sum = 0.f;
-#pragma unroll
-      for (int t = 0; t < NKT; ++t) {
-        const float e = __expf(s[t][j] - m);
-        s[t][j] = e;
-        sum += e;
-      }
-      sum = group16_sum(sum);
-      inv[j] = 1.0f / sum;
-    }
-
-    // P (unnormalised) -> this wave's LDS rows.
+    float m = -INFINITY;
 #pragma unroll
     for (int t = 0; t < NKT; ++t)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) *(T*)(sP + (fq * 4 + j) * ROW + (t * 16 + fr) * 2) = (T)s[t][j];
-    __builtin_amdgcn_wave_barrier();
+      for (int j = 0; j < 4; ++j) {
+        const int key = t * 16 + 4 * fq + j;
+        float v = s[t][j] * scale_log2;
+        if (key >= N || (causal && key > q)) v = -INFINITY;
+        s[t][j] = v;
+        m = fmaxf(m, v);
+      }
+    m = fmaxf(m, __shfl_xor(m, 16, 64));
+    m = fmaxf(m, __shfl_xor(m, 32, 64));
+    float sum = 0.f;
+#pragma unroll
+    for (int t = 0; t < NKT; ++t)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float e = exp2f(s[t][j] - m);
+        s[t][j] = e;
+        sum += e;
+      }
+    sum += __shfl_xor(sum, 16, 64);
+    sum += __shfl_xor(sum, 32, 64);
 
-    // O = P V: o[ni][j] = O[qt*16 + fq*4 + j][ni*16 + fr]
+    // O^T[d][q] = V^T P^T; k order of step ks: element e of quarter fq <-> key 32ks + 16(e>>2) + 4fq + (e&3)
     f32x4 o[4];
 #pragma unroll
     for (int ni = 0; ni < 4; ++ni) o[ni] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < NKP / 32; ++ks) {
-      const V8 pa = *(const V8*)(sP + fr * ROW + (ks * 32 + fq * 8) * 2);
+      V8 pf;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) pf[e] = (T)s[2 * ks + (e >> 2)][e & 3];
+      const char* const va0 = sV + (32 * ks + 4 * fq + (fr >> 2)) * VROW + 8 * (fr & 3);
 #pragma unroll
       for (int ni = 0; ni < 4; ++ni) {
-        const V8 vb = *(const V8*)(sVt + (ni * 16 + fr) * ROW + (ks * 32 + fq * 8) * 2);
-        o[ni] = mfma_16x16x32(pa, vb, o[ni]);
+        const TR4 lo = TrRead<T>::read(va0 + ni * 32);
+        const TR4 hi = TrRead<T>::read(va0 + 16 * VROW + ni * 32);
+        V8 va;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          va[e] = lo[e];
+          va[e + 4] = hi[e];
+        }
+        o[ni] = mfma_16x16x32(va, pf, o[ni]);
       }
     }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int q = qt * 16 + fq * 4 + j;
-      if (q >= N) continue;
+    if (q < N) {
+      const float inv = 1.0f / sum;
       T* dst = out + ((long)b * N + q) * D + h * 64;
 #pragma unroll
-      for (int ni = 0; ni < 4; ++ni) dst[ni * 16 + fr] = (T)(o[ni][j] * inv[j]);
+      for (int ni = 0; ni < 4; ++ni) {
+        V4 w;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) w[j] = (T)(o[ni][j] * inv);
+        *(V4*)(dst + ni * 16 + 4 * fq) = w;
+      }
     }
-    __builtin_amdgcn_wave_barrier();
   }
 }
 
@@ -181,16 +195,6 @@ hipError_t launch_typed(const void* qkv, void* out, int B, int N, int H, int D, 
 // Softmax in base 2 (scale * log2 e folded into the scores).  Causal: tiles past
 // the block's last query are skipped, keys > query masked.
 // ---------------------------------------------------------------------------
-// ds_read_b64_tr_b16 (16-bit lanes; the i16 form, reinterpreted as T)
-template <typename T>
-struct TrRead {
-  typedef T V4 __attribute__((ext_vector_type(4)));
-  typedef short I4 __attribute__((ext_vector_type(4)));
-  static __device__ __forceinline__ V4 read(const char* p) {
-    return __builtin_bit_cast(V4, __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) I4*)p));
-  }
-};
-
 template <typename T, int HD>
 __global__ __launch_bounds__(256, 2) void flash_attn_kernel(const T* __restrict__ qkv, T* __restrict__ out, int N,
                                                             int H, int D, int causal, float scale_log2) {
