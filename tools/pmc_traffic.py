@@ -8,8 +8,8 @@ counter_collection CSVs of the same `bench.py --no-text` command (separate passe
 two counters cannot share one on gfx950).  Per MI355X_MICROARCH.md §HBM: both counters
 are in KB; FETCH_SIZE reports half the bytes of wide coalesced streaming reads on gfx950,
 so it is doubled; WRITE_SIZE is exact for 16-byte-per-lane stores.
-The kernel is the vision c_fc GEMM: gemm_bt_kernel<T, BM, BN, WGM, WGN, A_ROWS=0,
-EPI_STORE16=0, ACT_QUICK_GELU=1> (the only launch with that instantiation in the vision leg).
+The kernel is the vision c_fc GEMM: gemm_{bt,pipe}_kernel<T, BM, BN, WGM, WGN, EPI_STORE16=0,
+ACT_QUICK_GELU=1> (the only launch with an activation in the vision leg).
 """
 import csv
 import glob
@@ -19,7 +19,7 @@ import re
 import statistics
 import sys
 
-C_FC = re.compile(r"gemm_bt_kernel.*Li0ELi0ELi1EEEv")
+C_FC = re.compile(r"gemm_(bt|pipe)_kernelIDF16bLi\d+ELi\d+ELi\d+ELi\d+ELi0ELi1EEEv")
 
 
 def per_launch_kb(d, counter):
@@ -43,7 +43,7 @@ def main():
     M, N, K = (int(sys.argv[4]) if len(sys.argv) > 4 else 128 * 50), 3072, 768
     compulsory = 2 * (M * K + N * K + M * N) + 4 * N
     res = {
-        "kernel": f"gemm_bt_kernel c_fc ({M}x3072x768, bf16, +QuickGELU)",
+        "kernel": f"c_fc GEMM ({M}x3072x768, bf16, +QuickGELU)",
         "fetch_size_kb_median": f_kb, "write_size_kb_median": w_kb,
         "fetch_dispatches": nf, "write_dispatches": nw,
         "hbm_read_bytes_per_launch": read_b, "hbm_write_bytes_per_launch": write_b,
