@@ -417,26 +417,36 @@ void check(hipError_t err, const char* what) {
     throw ClipErr(CLIPGPU_ERR_DEVICE, std::string("HIP error in ") + what + ": " + hipGetErrorString(err));
 }
 
-// Records [start, stop] events around one launch when its category is enabled.
+// Times the launches of one scope when its category is enabled.  gemm = true (a single
+// launch_gemm inside): the events are handed to the GEMM launcher, which stamps the kernel's
+// own start and end (hipExtLaunchKernelGGL); otherwise [start, stop] are recorded around the
+// scope's launches on the stream (which also counts their dispatch gaps).
 struct ProfScope {
   Profiler* p;
   int cat;
   hipStream_t st;
-  hipEvent_t a = nullptr;
-  ProfScope(const clipgpu_engine& e, int c, hipStream_t s) : p(const_cast<Profiler*>(&e.prof)), cat(c), st(s) {
+  bool gemm;
+  hipEvent_t a = nullptr, b = nullptr;
+  ProfScope(const clipgpu_engine& e, int c, hipStream_t s, bool gemm_scope = false)
+      : p(const_cast<Profiler*>(&e.prof)), cat(c), st(s), gemm(gemm_scope) {
     if (p->mask & (1u << cat)) {
       a = p->get();
-      if (a) (void)hipEventRecord(a, st);
+      b = a ? p->get() : nullptr;
+      if (!b) {
+        a = nullptr;
+      } else if (gemm) {
+        g_gemm_events.start = a;
+        g_gemm_events.stop = b;
+      } else {
+        (void)hipEventRecord(a, st);
+      }
     }
   }
   ~ProfScope() {
-    if (a) {
-      hipEvent_t b = p->get();
-      if (b) {
-        (void)hipEventRecord(b, st);
-        p->pending.push_back({cat, a, b});
-      }
-    }
+    if (!a) return;
+    if (gemm) g_gemm_events = GemmLaunchEvents();  // consumed by the launch (or disarm on error)
+    else (void)hipEventRecord(b, st);
+    p->pending.push_back({cat, a, b});
   }
 };
 
@@ -490,7 +500,7 @@ void trunk(const clipgpu_engine& e, const Replica& r, int B, int causal, hipStre
   for (int l = 0; l < s.layers; ++l) {
     const LayerW& L = r.w.layers[l];
     auto gemm = [&](int site, int cat, const char* what) {
-      ProfScope ps(e, cat, st);
+      ProfScope ps(e, cat, st, /*gemm=*/true);
       GemmParams g = site_gemm(e, r, L, site, rows);
       g.tile = tuned ? e.tile[site] : TILE_AUTO;
       check(launch_gemm(e.dt, A_ROWS, site_epi(site), site == GS_FC ? s.act : ACT_NONE, g, st), what);

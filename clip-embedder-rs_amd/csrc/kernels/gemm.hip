@@ -28,10 +28,25 @@
 // be a multiple of 64.
 #include <utility>
 
+#include <hip/hip_ext.h>
+
 #include "common.hpp"
 #include "kernels.hpp"
 
 namespace clipgpu {
+
+thread_local GemmLaunchEvents g_gemm_events;
+
+// hipLaunchKernelGGL, or the event-stamped ext launch when a profiler armed g_gemm_events.
+template <typename K>
+void gemm_launch(K kernel, int grid, int threads, hipStream_t s, const GemmParams& p) {
+  if (g_gemm_events.start && g_gemm_events.stop) {
+    hipExtLaunchKernelGGL(kernel, dim3(grid), dim3(threads), 0, s, g_gemm_events.start, g_gemm_events.stop, 0, p);
+    g_gemm_events = GemmLaunchEvents();
+  } else {
+    hipLaunchKernelGGL(kernel, dim3(grid), dim3(threads), 0, s, p);
+  }
+}
 
 // Diagnostic build only (make stamps -> lib/libclipgpu_stamps.so): s_memtime
 // stamps of wave 0 of each block at fixed points of the tile loop
@@ -806,8 +821,7 @@ hipError_t launch_cfg(const GemmParams& p, hipStream_t s) {
   // resident blocks: one 8-wave block (96-128 KiB LDS) or two 4-wave blocks (64 KiB) per CU
   const int resident = device_cus() * (WGM * WGN == 4 ? 2 : 1);
   const int grid = ntiles <= resident ? ntiles : resident;
-  hipLaunchKernelGGL((gemm_bt_kernel<T, BM, BN, WGM, WGN, EPI, ACT>), dim3(grid), dim3(WGM * WGN * 64), 0, s,
-                     p);
+  gemm_launch(gemm_bt_kernel<T, BM, BN, WGM, WGN, EPI, ACT>, grid, WGM * WGN * 64, s, p);
   return hipGetLastError();
 }
 
@@ -817,7 +831,7 @@ hipError_t launch_pipe(const GemmParams& p, hipStream_t s) {
   const int ntiles = nTn * nTm * (p.ksplit > 1 ? p.ksplit : 1);
   const int resident = device_cus() * (BM * BN == 128 * 128 ? 2 : 1);
   const int grid = ntiles <= resident ? ntiles : resident;
-  hipLaunchKernelGGL((gemm_pipe_kernel<T, BM, BN, WGM, WGN, EPI, ACT>), dim3(grid), dim3(WGM * WGN * 64), 0, s, p);
+  gemm_launch(gemm_pipe_kernel<T, BM, BN, WGM, WGN, EPI, ACT>, grid, WGM * WGN * 64, s, p);
   return hipGetLastError();
 }
 

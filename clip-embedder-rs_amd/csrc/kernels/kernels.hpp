@@ -52,6 +52,15 @@ int pick_gemm_tile(int M, int N, int K);
 // act: Act enum from common.hpp (only used with EPI_STORE16)
 hipError_t launch_gemm(DType dt, int asrc, int epi, int act, const GemmParams& p, hipStream_t s);
 
+// Kernel-boundary timing of the next GEMM launch on this thread (clipgpu_profile_*): when
+// both events are set, launch_gemm launches through hipExtLaunchKernelGGL with them, so the
+// events stamp the kernel's own start and end (an event pair recorded around a launch also
+// times its dispatch), then clears them.
+struct GemmLaunchEvents {
+  hipEvent_t start = nullptr, stop = nullptr;
+};
+extern thread_local GemmLaunchEvents g_gemm_events;
+
 // Multi-head self-attention over packed qkv rows [B*N][3*D] -> out [B*N][D];
 // head_dim must be 64; N <= 256.
 // MAP attention pool (timm AttentionPoolLatent, one latent query): q [D] f32 (shared by all
