@@ -301,31 +301,38 @@ __global__ __launch_bounds__(256, 2) void flash_attn_kernel(const T* __restrict_
         for (int kk = 0; kk < HK / 32; ++kk) s[qi][t] = mfma_16x16x32(ka[kk], qf[qi][kk], s[qi][t]);
       }
     }
-    // online softmax: each lane holds one query (fr) per q-block
+    // online softmax: each lane holds one query (fr) per q-block.  Max in raw score
+    // units (scale > 0), the scale folded into the exp2 argument (one FMA); masks only on
+    // the tiles that need them (the ragged last tile, causal tiles on the diagonal).
+    const bool mask_tile = kt * KT + KT > N || (causal && kt * KT + KT - 1 > qb * QB);
 #pragma unroll
     for (int qi = 0; qi < 2; ++qi) {
       const int qrow = q0 + qi * 16 + fr;
       float mt = -INFINITY;
+      if (mask_tile) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int key = kt * KT + t * 16 + 4 * fq + j;
+            if (key >= N || (causal && key > qrow)) s[qi][t][j] = -INFINITY;
+          }
+      }
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int key = kt * KT + t * 16 + 4 * fq + j;
-          float v = s[qi][t][j] * scale_log2;
-          if (key >= N || (causal && key > qrow)) v = -INFINITY;
-          s[qi][t][j] = v;
-          mt = fmaxf(mt, v);
-        }
+        for (int j = 0; j < 4; ++j) mt = fmaxf(mt, s[qi][t][j]);
       mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
       mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
       const float mn = fmaxf(m[qi], mt);
-      const float corr = exp2f(m[qi] - mn);  // m = -inf on the first tile: 0
+      const float corr = exp2f((m[qi] - mn) * scale_log2);  // m = -inf on the first tile: 0
+      const float off = -mn * scale_log2;
       float sum = 0.f;
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const float e = exp2f(s[qi][t][j] - mn);
+          const float e = exp2f(fmaf(s[qi][t][j], scale_log2, off));
           s[qi][t][j] = e;
           sum += e;
         }

@@ -67,15 +67,36 @@ __device__ __forceinline__ float group16_max(float v) {
 // tanh-GELU for SigLIP.
 enum Act { ACT_NONE = 0, ACT_QUICK_GELU = 1, ACT_GELU = 2, ACT_GELU_TANH = 3 };
 
+// Epilogue-cost forms (the GEMM epilogue evaluates one per output element; the 16-bit
+// output rounding, 2^-9 relative, dwarfs their error):
+//   QuickGELU  x * sigmoid(1.702 x)                 v_exp + v_rcp
+//   tanh-GELU  0.5 x (1 + tanh(u)) == x * sigmoid(2u), u = sqrt(2/pi) (x + 0.044715 x^3):
+//              the same v_exp + v_rcp (exact identity; tanhf is a long library call)
+//   erf-GELU   0.5 x (1 + erf(x / sqrt 2)), erf by Abramowitz-Stegun 7.1.26 (|err| <= 1.5e-7:
+//              one v_rcp, one v_exp, five FMAs) instead of the library erff
+__device__ __forceinline__ float fast_sigmoid_mul(float x, float z) {  // x * sigmoid(z)
+  return x * __builtin_amdgcn_rcpf(1.0f + __expf(-z));
+}
+__device__ __forceinline__ float fast_erf(float x) {
+  const float ax = fabsf(x);
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, ax, 1.0f));
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  const float y = 1.0f - p * t * __expf(-ax * ax);
+  return copysignf(y, x);
+}
+
 template <int ACT>
 __device__ __forceinline__ float apply_act(float x) {
-  if constexpr (ACT == ACT_QUICK_GELU) {  // v_exp + v_rcp (1 ulp) instead of an IEEE divide
-    return x * __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * x));
+  if constexpr (ACT == ACT_QUICK_GELU) {
+    return fast_sigmoid_mul(x, 1.702f * x);
   } else if constexpr (ACT == ACT_GELU) {
-    return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
+    return 0.5f * x * (1.0f + fast_erf(x * 0.70710678118654752f));
   } else if constexpr (ACT == ACT_GELU_TANH) {
     const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-    return 0.5f * x * (1.0f + tanhf(k0 * (x + k1 * x * x * x)));
+    return fast_sigmoid_mul(x, 2.0f * k0 * fmaf(k1 * x, x * x, x));
   } else {
     return x;
   }
