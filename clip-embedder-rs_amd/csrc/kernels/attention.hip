@@ -16,6 +16,8 @@
 // epilogue, 8-byte stores of 4 head dims.  Padded keys (>= N) and, for text,
 // keys above the diagonal are masked to -inf (open_clip build_causal_mask:
 // triu(-inf, 1)).
+#include <type_traits>
+
 #include "common.hpp"
 #include "kernels.hpp"
 
@@ -302,47 +304,52 @@ __global__ __launch_bounds__(256, 2) void flash_attn_kernel(const T* __restrict_
       }
     }
     // online softmax: each lane holds one query (fr) per q-block.  Max in raw score
-    // units (scale > 0), the scale folded into the exp2 argument (one FMA); masks only on
-    // the tiles that need them (the ragged last tile, causal tiles on the diagonal).
-    const bool mask_tile = kt * KT + KT > N || (causal && kt * KT + KT - 1 > qb * QB);
+    // units (scale > 0), the scale folded into the exp2 argument (one FMA, raw v_exp_f32:
+    // denormal results flush to 0); masks only on the tiles that need them (the ragged
+    // last tile, causal tiles on the diagonal) -- a separate instantiation, so the common
+    // tile carries no mask code.
+    auto softmax = [&](auto masked) {
 #pragma unroll
-    for (int qi = 0; qi < 2; ++qi) {
-      const int qrow = q0 + qi * 16 + fr;
-      float mt = -INFINITY;
-      if (mask_tile) {
+      for (int qi = 0; qi < 2; ++qi) {
+        if constexpr (decltype(masked)::value) {
+          const int qrow = q0 + qi * 16 + fr;
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int key = kt * KT + t * 16 + 4 * fq + j;
+              if (key >= N || (causal && key > qrow)) s[qi][t][j] = -INFINITY;
+            }
+        }
+        float mt = -INFINITY;
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) mt = fmaxf(mt, s[qi][t][j]);
+        mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
+        mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+        const float mn = fmaxf(m[qi], mt);
+        const float corr = __builtin_amdgcn_exp2f((m[qi] - mn) * scale_log2);  // m = -inf first: 0
+        const float off = -mn * scale_log2;
+        float sum = 0.f;
 #pragma unroll
         for (int t = 0; t < 4; ++t)
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            const int key = kt * KT + t * 16 + 4 * fq + j;
-            if (key >= N || (causal && key > qrow)) s[qi][t][j] = -INFINITY;
+            const float e = __builtin_amdgcn_exp2f(fmaf(s[qi][t][j], scale_log2, off));
+            s[qi][t][j] = e;
+            sum += e;
           }
+        sum += __shfl_xor(sum, 16, 64);
+        sum += __shfl_xor(sum, 32, 64);
+        l[qi] = l[qi] * corr + sum;
+        m[qi] = mn;
+#pragma unroll
+        for (int ni = 0; ni < HV / 16; ++ni) o[qi][ni] *= corr;
       }
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) mt = fmaxf(mt, s[qi][t][j]);
-      mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
-      mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
-      const float mn = fmaxf(m[qi], mt);
-      const float corr = exp2f((m[qi] - mn) * scale_log2);  // m = -inf on the first tile: 0
-      const float off = -mn * scale_log2;
-      float sum = 0.f;
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float e = exp2f(fmaf(s[qi][t][j], scale_log2, off));
-          s[qi][t][j] = e;
-          sum += e;
-        }
-      sum += __shfl_xor(sum, 16, 64);
-      sum += __shfl_xor(sum, 32, 64);
-      l[qi] = l[qi] * corr + sum;
-      m[qi] = mn;
-#pragma unroll
-      for (int ni = 0; ni < HV / 16; ++ni) o[qi][ni] *= corr;
-    }
+    };
+    if (kt * KT + KT > N || (causal && kt * KT + KT - 1 > qb * QB)) softmax(std::true_type{});
+    else softmax(std::false_type{});
     // O^T[d][q] += V^T P^T over 2 k-steps of 32 keys; k order (both operands):
     // element e of lane quarter fq <-> key 32ks + 16(e >> 2) + 4fq + (e & 3)
 #pragma unroll
@@ -410,23 +417,31 @@ hipError_t launch_flash_hd(const void* qkv, void* out, int B, int N, int H, int 
 
 // MAP attention pool (timm AttentionPoolLatent; oracle/clip_ref.py encode_image_siglip): one
 // learned query per head over the N tokens of one image.  One 256-thread block per (image,
-// head): scores by threads over keys, block softmax, then waves split the keys and lanes
-// the head dims for o = sum_n p_n v_n.  Memory-bound and tiny next to the trunk.
+// head): scores by threads over keys (16-byte K loads against the f32 query in LDS), block
+// softmax, then o = sum_n p_n v_n with 16 key groups x 16 lanes of 8 head dims (16-byte V
+// loads), the groups summed through LDS.  Memory-bound and tiny next to the trunk.
 template <typename T>
 __global__ __launch_bounds__(256) void map_attn_kernel(const float* __restrict__ q, const T* __restrict__ kv,
                                                        T* __restrict__ out, int N, int H, int D, float scale) {
+  typedef typename Vec8<T>::type V8;
   __shared__ float sS[1024];
-  __shared__ float sO[4][128];
+  __shared__ float sQ[128];
+  __shared__ float sO[16][129];
   __shared__ float red[4];
-  const int b = blockIdx.x / H, h = blockIdx.x % H, hd = D / H;
+  const int b = blockIdx.x / H, h = blockIdx.x % H, hd = D / H, ch = hd / 8;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const T* kvb = kv + (long)b * N * 2 * D;
-  const float* qh = q + (long)h * hd;
+  const T* kvb = kv + (long)b * N * 2 * D + (long)h * hd;
+  if (tid < hd) sQ[tid] = q[(long)h * hd + tid];
+  __syncthreads();
   float lmax = -INFINITY;
   for (int n = tid; n < N; n += 256) {
-    const T* kr = kvb + (long)n * 2 * D + (long)h * hd;
+    const T* kr = kvb + (long)n * 2 * D;
     float s = 0.f;
-    for (int d = 0; d < hd; ++d) s += qh[d] * (float)kr[d];
+    for (int c = 0; c < ch; ++c) {
+      const V8 k8 = *(const V8*)(kr + c * 8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s = fmaf(sQ[c * 8 + e], (float)k8[e], s);
+    }
     s *= scale;
     sS[n] = s;
     lmax = fmaxf(lmax, s);
@@ -446,24 +461,32 @@ __global__ __launch_bounds__(256) void map_attn_kernel(const float* __restrict__
   if (lane == 0) red[wave] = lsum;
   __syncthreads();
   const float inv = 1.0f / (red[0] + red[1] + red[2] + red[3]);
-  float o0 = 0.f, o1 = 0.f;
-  for (int n = wave; n < N; n += 4) {
-    const T* vr = kvb + (long)n * 2 * D + D + (long)h * hd;
-    const float pn = sS[n];
-    if (lane < hd) o0 += pn * (float)vr[lane];
-    if (lane + 64 < hd) o1 += pn * (float)vr[lane + 64];
+  const int g = tid >> 4, c = tid & 15;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c < ch) {
+    for (int n = g; n < N; n += 16) {
+      const V8 v8 = *(const V8*)(kvb + (long)n * 2 * D + D + c * 8);
+      const float pn = sS[n];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] = fmaf(pn, (float)v8[e], acc[e]);
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) sO[g][c * 8 + e] = acc[e];
   }
-  sO[wave][lane] = o0;
-  sO[wave][lane + 64] = o1;
   __syncthreads();
-  if (tid < hd) out[(long)b * D + (long)h * hd + tid] = (T)((sO[0][tid] + sO[1][tid] + sO[2][tid] + sO[3][tid]) * inv);
+  if (tid < hd) {
+    float o = 0.f;
+#pragma unroll
+    for (int gg = 0; gg < 16; ++gg) o += sO[gg][tid];
+    out[(long)b * D + (long)h * hd + tid] = (T)(o * inv);
+  }
 }
 
 }  // namespace
 
 hipError_t launch_map_attention(DType dt, const float* q, const void* kv, void* out, int B, int N, int H, int D,
                                 hipStream_t s) {
-  if (B <= 0 || N <= 0 || N > 1024 || H <= 0 || D % H || D / H > 128) return hipErrorInvalidValue;
+  if (B <= 0 || N <= 0 || N > 1024 || H <= 0 || D % H || D / H > 128 || (D / H) % 8) return hipErrorInvalidValue;
   const float scale = 1.0f / sqrtf((float)(D / H));
   if (dt == DT_BF16)
     hipLaunchKernelGGL(map_attn_kernel<__bf16>, dim3(B * H), dim3(256), 0, s, q, (const __bf16*)kv, (__bf16*)out, N, H,
