@@ -98,6 +98,26 @@ struct Replica {
     uint8_t* tmp = nullptr;
     size_t tmp_cap = 0;
   } islot[4];
+  // Captured forwards (hipGraph), keyed by entry point, buffers and batch; owned here,
+  // shared by the lane views.
+  struct GraphCache* graphs = nullptr;
+  hipEvent_t gin = nullptr, gout = nullptr;  // fork / join around a graph launched for a caller stream
+};
+
+// Replayable forwards: one hipGraphExec per (entry point, input / output buffers, batch,
+// normalisation constants).  A forward is ~90 dependent launches per lane; replaying it
+// as one graph removes the per-launch host cost and most inter-kernel dispatch gaps.
+struct GraphCache {
+  struct Entry {
+    std::vector<uint64_t> key;
+    hipGraphExec_t exec;
+  };
+  std::vector<Entry> entries;
+  static constexpr size_t kMax = 32;
+  void clear() {
+    for (auto& en : entries) (void)hipGraphExecDestroy(en.exec);
+    entries.clear();
+  }
 };
 
 }  // namespace clipgpu
@@ -135,6 +155,7 @@ struct clipgpu_engine {
   int tile_patch = 0;  // vision: the patch-embedding GEMM (tuned with the trunk sites)
   int tuned_rows = 0;
   int lanes = 1;  // concurrent sub-batches per device (CLIPGPU_LANES, default 2)
+  bool graphs = true;  // replay forwards as hipGraphs (CLIPGPU_GRAPHS=0 disables)
   // K-slices of the N = width GEMMs (out_proj, c_proj): CLIPGPU_GEMM_SPLIT=1 -> 2, else 1.
   // Fixed per engine, independent of the batch and lane split, so outputs stay
   // bit-identical across both; the second slice's partial is added by the next LayerNorm.
@@ -408,6 +429,9 @@ void alloc_workspace(clipgpu_engine& e, Replica& r) {
     HIP_CHECK(hipEventCreateWithFlags(&r.done[i], hipEventDisableTiming));
   }
   HIP_CHECK(hipEventCreateWithFlags(&r.fork, hipEventDisableTiming));
+  HIP_CHECK(hipEventCreateWithFlags(&r.gin, hipEventDisableTiming));
+  HIP_CHECK(hipEventCreateWithFlags(&r.gout, hipEventDisableTiming));
+  r.graphs = new GraphCache();
   HIP_CHECK(hipHostMalloc(&r.pin_in, B * e.in_bytes_per_row, hipHostMallocDefault));
   HIP_CHECK(hipHostMalloc((void**)&r.pin_out, B * E * 4, hipHostMallocDefault));
 }
@@ -716,6 +740,61 @@ void run_lanes(const clipgpu_engine& e, const Replica& r, int B, hipStream_t st,
   for (int i = 0; i < L; ++i) HIP_CHECK(hipStreamWaitEvent(st, r.join[i], 0));
 }
 
+// Runs body(stream) as a replayed hipGraph (captured on first use of `key`).  The capture
+// and replay stream is `st` when it is one of the replica's own streams, else the replica's
+// stream, forked from and joined back to `st` by events (a caller's stream may be the
+// legacy null stream, which cannot be captured).  Profiling (per-launch events) and
+// CLIPGPU_GRAPHS=0 run the body directly.
+template <typename F>
+void run_graph(const clipgpu_engine& e, const Replica& r, const std::vector<uint64_t>& key, hipStream_t st, F body) {
+  if (!e.graphs || e.prof.mask || !r.graphs) {
+    body(st);
+    return;
+  }
+  bool own = st == r.stream;
+  for (int i = 0; i < 4; ++i) own = own || (st != nullptr && st == r.lane[i]);
+  hipStream_t gs = own ? st : r.stream;
+  GraphCache& gc = *r.graphs;
+  hipGraphExec_t exec = nullptr;
+  for (auto& en : gc.entries)
+    if (en.key == key) exec = en.exec;
+  if (!own) {
+    HIP_CHECK(hipEventRecord(r.gin, st));
+    HIP_CHECK(hipStreamWaitEvent(gs, r.gin, 0));
+  }
+  if (!exec) {
+    if (gc.entries.size() >= GraphCache::kMax) {
+      HIP_CHECK(hipStreamSynchronize(gs));
+      gc.clear();
+    }
+    hipGraph_t g = nullptr;
+    HIP_CHECK(hipStreamBeginCapture(gs, hipStreamCaptureModeRelaxed));
+    try {
+      body(gs);
+    } catch (...) {
+      (void)hipStreamEndCapture(gs, &g);
+      if (g) (void)hipGraphDestroy(g);
+      throw;
+    }
+    HIP_CHECK(hipStreamEndCapture(gs, &g));
+    const hipError_t ie = hipGraphInstantiate(&exec, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    HIP_CHECK(ie);
+    gc.entries.push_back({key, exec});
+  }
+  HIP_CHECK(hipGraphLaunch(exec, gs));
+  if (!own) {
+    HIP_CHECK(hipEventRecord(r.gout, gs));
+    HIP_CHECK(hipStreamWaitEvent(st, r.gout, 0));
+  }
+}
+
+inline uint64_t fbits(const float* v, int i) {
+  uint32_t u = 0;
+  if (v) std::memcpy(&u, v + i, 4);
+  return u;
+}
+
 void vision_forward_lanes(const clipgpu_engine& e, const Replica& r, const void* pixels, int asrc, const float* mean,
                           const float* stdv, int B, float* d_out, hipStream_t st) {
   const size_t S = e.spec.image_size;
@@ -785,10 +864,15 @@ void run_host_shard(clipgpu_engine& e, Replica& r, InKind kind, const void* in, 
     par_memcpy(pin, (const char*)in + c0 * in_row_bytes, (size_t)n * in_row_bytes);
     HIP_CHECK(hipMemcpyAsync(din, pin, (size_t)n * in_row_bytes, hipMemcpyHostToDevice, st));
     const Replica v = lane_view(e, r, k * S);
-    if (kind == IN_IDS)
-      text_forward(e, v, (const int64_t*)din, n, dout, st);
-    else
-      vision_forward(e, v, din, kind == IN_F32 ? A_IMG_F32 : A_IMG_U8, mean, stdv, n, dout, st);
+    run_graph(e, r,
+              {(uint64_t)(10 + kind), (uint64_t)k, (uint64_t)n, fbits(mean, 0), fbits(mean, 1), fbits(mean, 2),
+               fbits(stdv, 0), fbits(stdv, 1), fbits(stdv, 2)},
+              st, [&](hipStream_t gs) {
+                if (kind == IN_IDS)
+                  text_forward(e, v, (const int64_t*)din, n, dout, gs);
+                else
+                  vision_forward(e, v, din, kind == IN_F32 ? A_IMG_F32 : A_IMG_U8, mean, stdv, n, dout, gs);
+              });
     HIP_CHECK(hipMemcpyAsync(r.pin_out + (size_t)k * S * E, dout, (size_t)n * E * 4, hipMemcpyDeviceToHost, st));
     HIP_CHECK(hipEventRecord(r.done[k], st));
     pend[k].c0 = c0;
@@ -955,7 +1039,9 @@ void run_images_shard(clipgpu_engine& e, Replica& r, const uint8_t* const* image
     check(launch_resize((const uint8_t*)sl.dev + desc_bytes + ints_bytes, sl.tmp, (const int*)(sl.dev + desc_bytes),
                         (const ResizeImage*)sl.dev, n, b.max_th, S, din, st), "resize");
     float* dout = r.out + (size_t)k * rows * E;
-    vision_forward(e, lane_view(e, r, k * rows), din, A_IMG_U8, e.pre.mean, e.pre.stdv, n, dout, st);
+    const Replica v = lane_view(e, r, k * rows);
+    run_graph(e, r, {20, (uint64_t)k, (uint64_t)n}, st,
+              [&](hipStream_t gs) { vision_forward(e, v, din, A_IMG_U8, e.pre.mean, e.pre.stdv, n, dout, gs); });
     HIP_CHECK(hipMemcpyAsync(r.pin_out + (size_t)k * rows * E, dout, (size_t)n * E * 4, hipMemcpyDeviceToHost, st));
     HIP_CHECK(hipEventRecord(r.done[k], st));
     pend[k].c0 = c0;
@@ -1010,6 +1096,12 @@ void destroy_replica(Replica& r) {
     if (r.done[i]) (void)hipEventDestroy(r.done[i]);
   }
   if (r.fork) (void)hipEventDestroy(r.fork);
+  if (r.gin) (void)hipEventDestroy(r.gin);
+  if (r.gout) (void)hipEventDestroy(r.gout);
+  if (r.graphs) {
+    r.graphs->clear();
+    delete r.graphs;
+  }
   for (auto& sl : r.islot) {
     if (sl.pin) (void)hipHostFree(sl.pin);
     if (sl.dev) (void)hipFree(sl.dev);
@@ -1056,6 +1148,7 @@ int clipgpu_create(const char* model_dir, int tower, const int* device_ids, int 
     e->max_batch = max_batch;
     if (const char* ln = getenv("CLIPGPU_LANES")) e->lanes = std::max(1, std::min(4, atoi(ln)));
     else e->lanes = 2;
+    if (const char* gr = getenv("CLIPGPU_GRAPHS")) e->graphs = gr[0] != '0';
     const TowerSpec& s = e->spec;
     if (const char* sp = getenv("CLIPGPU_GEMM_SPLIT")) e->ksplit = sp[0] == '1' ? 2 : 1;
     if (s.heads <= 0 || s.width % s.heads || s.width % 64)
@@ -1169,8 +1262,8 @@ int clipgpu_embed_pixels_device(clipgpu_engine* e, const float* d_nchw, int64_t 
     if (B > e->max_batch) throw ClipErr(CLIPGPU_ERR_INVALID, "B exceeds max_batch");
     Replica& r = e->reps[0];
     HIP_CHECK(hipSetDevice(r.device));
-    vision_forward_lanes(*e, r, d_nchw, A_IMG_F32, nullptr, nullptr, (int)B, d_out,
-                         stream ? (hipStream_t)stream : r.stream);
+    run_graph(*e, r, {1, (uint64_t)d_nchw, (uint64_t)d_out, (uint64_t)B}, stream ? (hipStream_t)stream : r.stream,
+              [&](hipStream_t gs) { vision_forward_lanes(*e, r, d_nchw, A_IMG_F32, nullptr, nullptr, (int)B, d_out, gs); });
   });
 }
 
@@ -1183,7 +1276,11 @@ int clipgpu_embed_u8_device(clipgpu_engine* e, const uint8_t* d_nhwc, int64_t B,
     if (!mean || !stdv) throw ClipErr(CLIPGPU_ERR_INVALID, "NULL mean/std");
     Replica& r = e->reps[0];
     HIP_CHECK(hipSetDevice(r.device));
-    vision_forward_lanes(*e, r, d_nhwc, A_IMG_U8, mean, stdv, (int)B, d_out, stream ? (hipStream_t)stream : r.stream);
+    run_graph(*e, r,
+              {2, (uint64_t)d_nhwc, (uint64_t)d_out, (uint64_t)B, fbits(mean, 0), fbits(mean, 1), fbits(mean, 2),
+               fbits(stdv, 0), fbits(stdv, 1), fbits(stdv, 2)},
+              stream ? (hipStream_t)stream : r.stream,
+              [&](hipStream_t gs) { vision_forward_lanes(*e, r, d_nhwc, A_IMG_U8, mean, stdv, (int)B, d_out, gs); });
   });
 }
 
@@ -1253,7 +1350,8 @@ int clipgpu_embed_tokens_device(clipgpu_engine* e, const int64_t* d_ids, int64_t
     if (B > e->max_batch) throw ClipErr(CLIPGPU_ERR_INVALID, "B exceeds max_batch");
     Replica& r = e->reps[0];
     HIP_CHECK(hipSetDevice(r.device));
-    text_forward_lanes(*e, r, d_ids, (int)B, d_out, stream ? (hipStream_t)stream : r.stream);
+    run_graph(*e, r, {3, (uint64_t)d_ids, (uint64_t)d_out, (uint64_t)B}, stream ? (hipStream_t)stream : r.stream,
+              [&](hipStream_t gs) { text_forward_lanes(*e, r, d_ids, (int)B, d_out, gs); });
   });
 }
 

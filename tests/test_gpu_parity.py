@@ -145,6 +145,55 @@ def test_device_entry_points():
     assert np.allclose(d_o.cpu().numpy(), te.embed_tokens(ids), atol=1e-6)
 
 
+@pytest.mark.parametrize("tower", [0, 1])
+def test_graph_replay_reads_fresh_inputs_and_matches_direct_launches(tower, monkeypatch):
+    """Forwards replayed as hipGraphs (the default) are bit-identical to direct launches
+    (CLIPGPU_GRAPHS=0), and a replay with the same buffers sees new input contents: device
+    entry points (caller stream, fork/join) and host entry points (lane-slot streams)."""
+    import torch
+    v, t = specs(VIT_B_32_CFG)
+    outs = {}
+    for graphs in ["1", "0"]:
+        monkeypatch.setenv("CLIPGPU_GRAPHS", graphs)
+        e = engine(VIT_B_32_CFG, tower, max_batch=20)
+        res = []
+        for seed in (51, 52, 53):
+            if tower == 0:
+                x = normalized_pixels(weights.synth_images_u8(seed, 20, v.image_size), OPENAI_MEAN, OPENAI_STD)
+                host = e.embed_pixels(x)
+            else:
+                x = weights.synth_token_ids(seed, 20, t.context_length, t.vocab_size, t.vocab_size - 2,
+                                            t.vocab_size - 1, random_eot=True)
+                host = e.embed_tokens(x)
+            if seed == 51:
+                d_in = torch.from_numpy(x).cuda()
+                d_out = torch.empty((20, 512), device="cuda")
+            else:
+                d_in.copy_(torch.from_numpy(x))
+            s = torch.cuda.current_stream()
+            if tower == 0:
+                e.embed_pixels_device(d_in.data_ptr(), 20, d_out.data_ptr(), s.cuda_stream)
+            else:
+                e.embed_tokens_device(d_in.data_ptr(), 20, d_out.data_ptr(), s.cuda_stream)
+            torch.cuda.synchronize()
+            dev = d_out.cpu().numpy()
+            assert np.array_equal(dev, host)
+            res.append(host)
+        outs[graphs] = res
+    for a, b in zip(outs["1"], outs["0"]):
+        assert np.array_equal(a, b)
+    assert not np.array_equal(outs["1"][0], outs["1"][1])
+    v0 = outs["1"][2][:3]
+    if tower == 0:
+        ref = oracle_vision(VIT_B_32_CFG, 1234, normalized_pixels(weights.synth_images_u8(53, 20, v.image_size),
+                                                                  OPENAI_MEAN, OPENAI_STD)[:3])
+    else:
+        ref = oracle_text(VIT_B_32_CFG, 1234, weights.synth_token_ids(53, 20, t.context_length, t.vocab_size,
+                                                                      t.vocab_size - 2, t.vocab_size - 1,
+                                                                      random_eot=True)[:3])
+    check_rows(v0, ref)
+
+
 def test_native_library_is_loaded():
     """The HIP library, not a fallback, is what ran (one libamdhip64 in-process)."""
     import re

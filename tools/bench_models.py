@@ -132,14 +132,47 @@ def similarity_leg(ni=65536, nt=1000, E=512, steps=5, warmup=2):
                       "max_abs_err_vs_torch": err}), flush=True)
 
 
+def latency_leg(steps=50, warmup=10):
+    """Single-item latency (the reference's embed_image / embed_text calls, B = 1) through the
+    host entry points: pinned staging + H2D + forward + D2H + synchronise, ViT-B/32."""
+    d = model_dir(VIT_B_32_CFG)
+    mean, std = VIT_B_32_CFG["preprocess_cfg"]["mean"], VIT_B_32_CFG["preprocess_cfg"]["std"]
+    ve = Engine(d, 0, [0], "bf16", 8)
+    te = Engine(d, 1, [0], "bf16", 8)
+    rng = np.random.default_rng(3)
+    u8 = rng.integers(0, 256, (1, 224, 224, 3), dtype=np.uint8)
+    px = np.ascontiguousarray(((u8.astype(np.float32) / 255 - np.asarray(mean, np.float32)) /
+                               np.asarray(std, np.float32)).transpose(0, 3, 1, 2))
+    ids = np.zeros((1, 77), np.int64)
+    ids[0, :5] = [49406, 320, 1125, 539, 49407]
+    photo = [rng.integers(0, 256, (480, 640, 3), dtype=np.uint8)]
+    for name, fn in (("b32_embed_image_f32", lambda: ve.embed_pixels(px)),
+                     ("b32_embed_image_photo_gpu_resize", lambda: ve.embed_images_rgb8(photo)),
+                     ("b32_embed_text", lambda: te.embed_tokens(ids))):
+        for _ in range(warmup):
+            fn()
+        ts = []
+        for _ in range(steps):
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+        ts.sort()
+        print(json.dumps({"measure": "latency_" + name, "batch": 1, "p50_ms": round(ts[len(ts) // 2] * 1e3, 3),
+                          "p90_ms": round(ts[int(len(ts) * 0.9)] * 1e3, 3)}), flush=True)
+    ve.close()
+    te.close()
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["host", "photos", "similarity", "so400m", "h14"]
+    which = sys.argv[1:] or ["host", "photos", "similarity", "latency", "so400m", "h14"]
     if "host" in which:
         host_leg()
     if "photos" in which:
         photos_leg()
     if "similarity" in which:
         similarity_leg()
+    if "latency" in which:
+        latency_leg()
     if "so400m" in which:
         device_leg("so400m_vision", SO400M_16_SIGLIP2_384_CFG, 0, 128)
     if "h14" in which:
