@@ -180,7 +180,8 @@ def main():
 
     tiles = (ctypes.c_int * 4)()
     _lib.check(_lib.lib().clipgpu_test_engine_tiles(ve._h, tiles))
-    tile_names = {0: "heuristic", 1: "128x128", 2: "256x128", 3: "256x256", 4: "128x128pipe"}
+    tile_names = {0: "heuristic", 1: "128x128", 2: "256x128", 3: "256x256", 4: "128x128pipe", 5: "128x64pipe",
+                  6: "64x128pipe"}
     gemm_tiles = dict(zip(["qkv", "out_proj", "c_fc", "c_proj"], [tile_names[t] for t in tiles]))
 
     dt, _ = timed(vision_step, args.steps, args.warmup)

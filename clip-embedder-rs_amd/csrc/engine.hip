@@ -563,12 +563,13 @@ void autotune_tiles(clipgpu_engine& e, Replica& r) {
     if (sscanf(fixed, "%d,%d,%d,%d", &v[0], &v[1], &v[2], &v[3]) != 4)
       throw ClipErr(CLIPGPU_ERR_INVALID, "CLIPGPU_GEMM_TILES must be 'q,o,f,p'");
     for (int i = 0; i < 4; ++i) {
-      if (v[i] < TILE_AUTO || v[i] > TILE_128x128_PIPE) throw ClipErr(CLIPGPU_ERR_INVALID, "bad CLIPGPU_GEMM_TILES entry");
+      if (v[i] < TILE_AUTO || v[i] > TILE_LAST) throw ClipErr(CLIPGPU_ERR_INVALID, "bad CLIPGPU_GEMM_TILES entry");
       e.tile[i] = v[i];
     }
     return;
   }
-  const int cands[] = {TILE_128x128, TILE_128x128_PIPE, TILE_256x128, TILE_256x256};
+  const int cands[] = {TILE_128x128, TILE_128x128_PIPE, TILE_256x128, TILE_256x256, TILE_128x64_PIPE,
+                       TILE_64x128_PIPE};
   hipEvent_t a, b;
   HIP_CHECK(hipEventCreate(&a));
   HIP_CHECK(hipEventCreate(&b));

@@ -26,6 +26,7 @@
 // operands are swapped so each lane owns 4 consecutive output columns (8 / 16 B
 // epilogue stores).  M and N tails: clamped source rows + masked stores; K must
 // be a multiple of 64.
+#include <algorithm>
 #include <utility>
 
 #include <hip/hip_ext.h>
@@ -829,7 +830,10 @@ template <typename T, int BM, int BN, int WGM, int WGN, int EPI, int ACT>
 hipError_t launch_pipe(const GemmParams& p, hipStream_t s) {
   const int nTn = (p.N + BN - 1) / BN, nTm = (p.M + BM - 1) / BM;
   const int ntiles = nTn * nTm * (p.ksplit > 1 ? p.ksplit : 1);
-  const int resident = device_cus() * (BM * BN == 128 * 128 ? 2 : 1);
+  // resident blocks per CU: by LDS (2 stages + 2 KiB bias) and the 8-wave tiles' registers
+  const int lds = 2 * (BM + BN) * BK * 2 + 2048;
+  const int per_cu = WGM * WGN == 8 ? 1 : std::min(3, (160 * 1024) / lds);
+  const int resident = device_cus() * per_cu;
   const int grid = ntiles <= resident ? ntiles : resident;
   gemm_launch(gemm_pipe_kernel<T, BM, BN, WGM, WGN, EPI, ACT>, grid, WGM * WGN * 64, s, p);
   return hipGetLastError();
@@ -845,6 +849,8 @@ hipError_t launch_tile(const GemmParams& p, hipStream_t s) {
     switch (tile) {
       case TILE_256x256: return launch_pipe<T, 256, 256, 2, 4, EPI, ACT>(p, s);
       case TILE_256x128: return launch_pipe<T, 256, 128, 2, 4, EPI, ACT>(p, s);
+      case TILE_128x64_PIPE: return launch_pipe<T, 128, 64, 2, 2, EPI, ACT>(p, s);
+      case TILE_64x128_PIPE: return launch_pipe<T, 64, 128, 2, 2, EPI, ACT>(p, s);
       default: return launch_pipe<T, 128, 128, 2, 2, EPI, ACT>(p, s);
     }
   }
@@ -853,6 +859,8 @@ hipError_t launch_tile(const GemmParams& p, hipStream_t s) {
       case TILE_256x256: return launch_pipe<T, 256, 256, 2, 4, EPI, ACT>(p, s);
       case TILE_256x128: return launch_pipe<T, 256, 128, 2, 4, EPI, ACT>(p, s);
       case TILE_128x128_PIPE: return launch_pipe<T, 128, 128, 2, 2, EPI, ACT>(p, s);
+      case TILE_128x64_PIPE: return launch_pipe<T, 128, 64, 2, 2, EPI, ACT>(p, s);
+      case TILE_64x128_PIPE: return launch_pipe<T, 64, 128, 2, 2, EPI, ACT>(p, s);
       default: break;
     }
   }

@@ -46,6 +46,9 @@ enum GemmTile {
   TILE_256x128 = 2,       // gemm_pipe_kernel: 8 waves, 96 KiB LDS
   TILE_256x256 = 3,       // gemm_pipe_kernel: 8 waves, 128 KiB LDS
   TILE_128x128_PIPE = 4,  // gemm_pipe_kernel: 4 waves, 64 KiB LDS, 2 blocks / CU
+  TILE_128x64_PIPE = 5,   // gemm_pipe_kernel: 4 waves (64x32 each), 48 KiB LDS, 3 blocks / CU
+  TILE_64x128_PIPE = 6,   // gemm_pipe_kernel: 4 waves (32x64 each), 48 KiB LDS, 3 blocks / CU
+  TILE_LAST = TILE_64x128_PIPE,
 };
 int pick_gemm_tile(int M, int N, int K);
 

@@ -48,7 +48,8 @@ def run_gemm(dtype, mode, act, A, W, bias=None, resid=None):
     return out
 
 
-@pytest.fixture(params=[1, 2, 3, 4], ids=["t128x128", "pipe256x128", "pipe256x256", "pipe128x128"])
+@pytest.fixture(params=[1, 2, 3, 4, 5, 6], ids=["t128x128", "pipe256x128", "pipe256x256", "pipe128x128", "pipe128x64",
+                                                "pipe64x128"])
 def tile(request, monkeypatch):
     """Every GEMM tile configuration (GemmTile) through the same numerics checks."""
     monkeypatch.setenv("CLIPGPU_TEST_TILE", str(request.param))

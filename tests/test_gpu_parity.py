@@ -217,7 +217,7 @@ def test_gemm_tile_choice_is_bit_exact(tower, monkeypatch):
         data = weights.synth_token_ids(31, 48, t.context_length, t.vocab_size, t.vocab_size - 2,
                                        t.vocab_size - 1, random_eot=True)
     outs = []
-    pins = ["1,1,1,1", "2,2,2,2", "3,3,3,3", "4,4,4,4", None]
+    pins = ["1,1,1,1", "2,2,2,2", "3,3,3,3", "4,4,4,4", "5,5,5,5", "6,6,6,6", None]
     for tiles in pins:
         if tiles:
             monkeypatch.setenv("CLIPGPU_GEMM_TILES", tiles)
@@ -229,7 +229,7 @@ def test_gemm_tile_choice_is_bit_exact(tower, monkeypatch):
         if tiles:
             assert list(got) == [int(x) for x in tiles.split(",")]
         else:
-            assert all(x in (1, 2, 3, 4) for x in got)
+            assert all(x in (1, 2, 3, 4, 5, 6) for x in got)
         outs.append(e.embed_pixels(data) if tower == 0 else e.embed_tokens(data))
     bad = [(pins[i], float(np.abs(o - outs[0]).max())) for i, o in enumerate(outs) if not np.array_equal(o, outs[0])]
     assert not bad, bad
