@@ -257,37 +257,49 @@ __global__ __launch_bounds__(256, 2) void flash_attn_kernel(const T* __restrict_
     for (int ni = 0; ni < HV / 16; ++ni) o[qi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
   float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
 
-  V8 kr[PER], vr[PER];
-  auto load_tile = [&](int kt) {
+  // Two register sets of K/V chunks: while tile kt is computed from LDS buffer kt & 1,
+  // set (kt + 1) & 1 holds tile kt + 1 (loads issued a tile earlier) and set kt & 1 takes
+  // the loads of tile kt + 2 -- two tiles of latency cover.  The tile loop is unrolled by
+  // two so every register-set index is static.
+  V8 kr[2][PER], vr[2][PER];
+  auto load_tile = [&](int kt, auto setc) {
+    constexpr int S = decltype(setc)::value;
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int q = tid + 256 * i, r = q / CH, c = q - r * CH, key = kt * KT + r;
       const bool ok = q < KT * CH && key < N;
-      kr[i] = ok ? *(const V8*)(base + (long)key * ld + D + c * 8) : V8{};
-      vr[i] = ok ? *(const V8*)(base + (long)key * ld + 2 * D + c * 8) : V8{};
+      kr[S][i] = ok ? *(const V8*)(base + (long)key * ld + D + c * 8) : V8{};
+      vr[S][i] = ok ? *(const V8*)(base + (long)key * ld + 2 * D + c * 8) : V8{};
     }
   };
-  auto store_tile = [&](int bf) {
-    char* const sK = smem + bf * BUF;
+  auto store_tile = [&](auto setc) {  // set S -> LDS buffer S
+    constexpr int S = decltype(setc)::value;
+    char* const sK = smem + S * BUF;
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int q = tid + 256 * i, r = q / CH, c = q - r * CH;
       if (q < KT * CH) {
-        *(V8*)(sK + r * KROW + c * 16) = kr[i];
-        *(V8*)(sK + KBUF + r * VROW + c * 16) = vr[i];
+        *(V8*)(sK + r * KROW + c * 16) = kr[S][i];
+        *(V8*)(sK + KBUF + r * VROW + c * 16) = vr[S][i];
       }
     }
   };
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, 1>;
 
   const int last_key = causal ? min(N, qb * QB + QB) : N;
   const int ntiles = (last_key + KT - 1) / KT;
-  load_tile(0);
-  store_tile(0);
+  load_tile(0, S0{});
+  store_tile(S0{});
+  if (1 < ntiles) load_tile(1, S1{});
   __syncthreads();
-  for (int kt = 0; kt < ntiles; ++kt) {
-    const char* const sK = smem + (kt & 1) * BUF;
+  auto tile_step = [&](int kt, auto par) {
+    constexpr int P = decltype(par)::value;  // == kt & 1
+    using SP = std::integral_constant<int, P>;
+    using SQ = std::integral_constant<int, 1 - P>;
+    const char* const sK = smem + P * BUF;
     const char* const sV = sK + KBUF;
-    if (kt + 1 < ntiles) load_tile(kt + 1);
+    if (kt + 2 < ntiles) load_tile(kt + 2, SP{});
 
     // S^T: s[qi][t][j] = S[query q0 + qi*16 + fr][key kt*64 + t*16 + 4fq + j]
     f32x4 s[2][4];
@@ -374,8 +386,12 @@ __global__ __launch_bounds__(256, 2) void flash_attn_kernel(const T* __restrict_
         for (int qi = 0; qi < 2; ++qi) o[qi][ni] = mfma_16x16x32(va, pf[qi], o[qi][ni]);
       }
     }
-    if (kt + 1 < ntiles) store_tile((kt + 1) & 1);
+    if (kt + 1 < ntiles) store_tile(SQ{});
     __syncthreads();
+  };
+  for (int kt = 0; kt < ntiles; kt += 2) {
+    tile_step(kt, S0{});
+    if (kt + 1 < ntiles) tile_step(kt + 1, S1{});
   }
   // O^T[d = ni*16 + 4fq + j][q = fr]: 4 consecutive head dims per lane -> one 8-byte store
 #pragma unroll
