@@ -814,6 +814,52 @@ void text_forward_lanes(const clipgpu_engine& e, const Replica& r, const int64_t
   });
 }
 
+// Second tuning pass over whole forwards: the per-site autotune times each GEMM alone, but
+// in the forward two lanes' kernels share the chip, so a tile that wins alone can lose there.
+// Coordinate descent: for each trunk site, try every other tile with the rest fixed and keep
+// it if the concurrent-lane forward at max_batch gets >= 1 % faster.  Inputs are the zeroed
+// staging buffer (timing only).  CLIPGPU_TUNE_FORWARD=0 skips it; pinned tiles skip it.
+void tune_forward(clipgpu_engine& e, Replica& r) {
+  const char* env = getenv("CLIPGPU_TUNE_FORWARD");
+  if ((env && env[0] == '0') || getenv("CLIPGPU_GEMM_TILES") || e.max_batch < 64) return;
+  const char* at = getenv("CLIPGPU_GEMM_AUTOTUNE");
+  if (at && at[0] == '0') return;
+  const int B = e.max_batch;
+  hipEvent_t a, b;
+  HIP_CHECK(hipEventCreate(&a));
+  HIP_CHECK(hipEventCreate(&b));
+  auto fwd = [&]() {
+    if (e.spec.tower == TOWER_VISION)
+      vision_forward_lanes(e, r, r.in, A_IMG_F32, nullptr, nullptr, B, r.out, r.stream);
+    else
+      text_forward_lanes(e, r, (const int64_t*)r.in, B, r.out, r.stream);
+  };
+  auto time_fwd = [&]() {
+    fwd();
+    HIP_CHECK(hipEventRecord(a, r.stream));
+    for (int i = 0; i < 3; ++i) fwd();
+    HIP_CHECK(hipEventRecord(b, r.stream));
+    HIP_CHECK(hipEventSynchronize(b));
+    float ms = 0.f;
+    HIP_CHECK(hipEventElapsedTime(&ms, a, b));
+    return ms;
+  };
+  float best = time_fwd();
+  for (int site = 0; site < GS_N; ++site) {
+    const int keep = e.tile[site];
+    for (int t = TILE_128x128; t <= TILE_LAST; ++t) {
+      if (t == keep || (site_split(e, site) && t == TILE_128x128)) continue;
+      const int prev = e.tile[site];
+      e.tile[site] = t;
+      const float ms = time_fwd();
+      if (ms < 0.99f * best) best = ms;
+      else e.tile[site] = prev;
+    }
+  }
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
+}
+
 enum InKind { IN_F32 = 0, IN_U8 = 1, IN_IDS = 2 };
 
 // Host -> pinned staging copy, split over a few threads when large (one thread moves
@@ -1188,7 +1234,10 @@ int clipgpu_create(const char* model_dir, int tower, const int* device_ids, int 
       HIP_CHECK(hipStreamCreateWithFlags(&r.stream, hipStreamNonBlocking));
       upload_weights(*e, r, m);
       alloc_workspace(*e, r);
-      if (i == 0) autotune_tiles(*e, r);  // one tuning, shared by identical devices
+      if (i == 0) {  // one tuning, shared by identical devices
+        autotune_tiles(*e, r);
+        tune_forward(*e, r);
+      }
     }
     *out = e.release();
   });
