@@ -1310,6 +1310,7 @@ int clipgpu_embed_pixels_device(clipgpu_engine* e, const float* d_nchw, int64_t 
     need_tower(e, TOWER_VISION);
     if (B <= 0) throw ClipErr(CLIPGPU_ERR_INVALID, "Empty batch");
     if (B > e->max_batch) throw ClipErr(CLIPGPU_ERR_INVALID, "B exceeds max_batch");
+    std::lock_guard<std::mutex> lk(e->mu);  // one enqueue per handle at a time (graph cache, workspace)
     Replica& r = e->reps[0];
     HIP_CHECK(hipSetDevice(r.device));
     run_graph(*e, r, {1, (uint64_t)d_nchw, (uint64_t)d_out, (uint64_t)B}, stream ? (hipStream_t)stream : r.stream,
@@ -1324,6 +1325,7 @@ int clipgpu_embed_u8_device(clipgpu_engine* e, const uint8_t* d_nhwc, int64_t B,
     if (B <= 0) throw ClipErr(CLIPGPU_ERR_INVALID, "Empty batch");
     if (B > e->max_batch) throw ClipErr(CLIPGPU_ERR_INVALID, "B exceeds max_batch");
     if (!mean || !stdv) throw ClipErr(CLIPGPU_ERR_INVALID, "NULL mean/std");
+    std::lock_guard<std::mutex> lk(e->mu);  // one enqueue per handle at a time (graph cache, workspace)
     Replica& r = e->reps[0];
     HIP_CHECK(hipSetDevice(r.device));
     run_graph(*e, r,
@@ -1398,6 +1400,7 @@ int clipgpu_embed_tokens_device(clipgpu_engine* e, const int64_t* d_ids, int64_t
     need_tower(e, TOWER_TEXT);
     if (B <= 0) throw ClipErr(CLIPGPU_ERR_INVALID, "Empty batch");
     if (B > e->max_batch) throw ClipErr(CLIPGPU_ERR_INVALID, "B exceeds max_batch");
+    std::lock_guard<std::mutex> lk(e->mu);  // one enqueue per handle at a time (graph cache, workspace)
     Replica& r = e->reps[0];
     HIP_CHECK(hipSetDevice(r.device));
     run_graph(*e, r, {3, (uint64_t)d_ids, (uint64_t)d_out, (uint64_t)B}, stream ? (hipStream_t)stream : r.stream,

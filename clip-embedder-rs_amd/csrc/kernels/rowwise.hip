@@ -8,6 +8,8 @@
 //   text stem:   x = token_embedding[ids] + positional_embedding    (a16)
 //   tails:       ln_post(x[:,0]) / ln_final(x[b, argmax(ids[b])])    (a13, a18)
 //   F.normalize: x / max(||x||_2, 1e-12)
+#include <type_traits>
+
 #include "common.hpp"
 #include "kernels.hpp"
 
@@ -17,103 +19,124 @@ namespace {
 
 constexpr int MAXV = 5;  // float4 per lane -> D <= 1280
 
-struct RowRegs {
-  float4 v[MAXV];
+// A row in registers: NV float4 per lane (lane-strided, float4 c = i*64 + lane); only the
+// last of them can fall past D/4.  Kernels are instantiated per NV = ceil(D / 256).
+template <int NV>
+struct Row {
+  float4 v[NV];
 };
 
-__device__ __forceinline__ void load_row(const float* src, int D4, int lane, RowRegs& r) {
-#pragma unroll
-  for (int i = 0; i < MAXV; ++i) {
-    const int c = i * 64 + lane;
-    r.v[i] = c < D4 ? ((const float4*)src)[c] : make_float4(0.f, 0.f, 0.f, 0.f);
-  }
+template <int NV>
+__device__ __forceinline__ bool in_row(int i, int lane, int D4) {
+  return i + 1 < NV || i * 64 + lane < D4;
 }
 
-__device__ __forceinline__ void layer_norm_regs(const RowRegs& in, RowRegs& out, const float* w, const float* b,
+template <int NV>
+__device__ __forceinline__ void load_row(const float* src, int D4, int lane, Row<NV>& r) {
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+    r.v[i] = in_row<NV>(i, lane, D4) ? ((const float4*)src)[i * 64 + lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+// Wave sum: DPP rotations inside each 16-lane row (row_ror 8, 4, 2, 1), then two
+// cross-row xor-shuffles -- 2 LDS-permute round trips instead of 6.
+template <int CTRL>
+__device__ __forceinline__ float dpp_ror(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float wave_sum_fast(float v) {
+  v += dpp_ror<0x128>(v);  // row_ror:8
+  v += dpp_ror<0x124>(v);  // row_ror:4
+  v += dpp_ror<0x122>(v);  // row_ror:2
+  v += dpp_ror<0x121>(v);  // row_ror:1
+  v += __shfl_xor(v, 16, 64);
+  v += __shfl_xor(v, 32, 64);
+  return v;
+}
+
+// torch LayerNorm, two-pass mean / biased variance in f32; g, b preloaded rows.
+template <int NV>
+__device__ __forceinline__ void layer_norm_regs(const Row<NV>& in, Row<NV>& out, const Row<NV>& g, const Row<NV>& b,
                                                 float eps, int D, int lane) {
   const int D4 = D >> 2;
   float s = 0.f;
 #pragma unroll
-  for (int i = 0; i < MAXV; ++i)
-    if (i * 64 + lane < D4) s += in.v[i].x + in.v[i].y + in.v[i].z + in.v[i].w;
-  const float mean = wave_sum(s) / (float)D;
+  for (int i = 0; i < NV; ++i) s += in.v[i].x + in.v[i].y + in.v[i].z + in.v[i].w;  // padding holds 0
+  const float mean = wave_sum_fast(s) / (float)D;
   float q = 0.f;
 #pragma unroll
-  for (int i = 0; i < MAXV; ++i) {
-    const int c = i * 64 + lane;
-    if (c < D4) {
+  for (int i = 0; i < NV; ++i) {
+    if (in_row<NV>(i, lane, D4)) {
       const float a = in.v[i].x - mean, bb = in.v[i].y - mean, cc = in.v[i].z - mean, d = in.v[i].w - mean;
       q += a * a + bb * bb + cc * cc + d * d;
     }
   }
-  const float var = wave_sum(q) / (float)D;
+  const float var = wave_sum_fast(q) / (float)D;
   const float rstd = 1.0f / sqrtf(var + eps);
 #pragma unroll
-  for (int i = 0; i < MAXV; ++i) {
-    const int c = i * 64 + lane;
-    if (c < D4) {
-      const float4 g = ((const float4*)w)[c];
-      const float4 o = ((const float4*)b)[c];
-      out.v[i].x = (in.v[i].x - mean) * rstd * g.x + o.x;
-      out.v[i].y = (in.v[i].y - mean) * rstd * g.y + o.y;
-      out.v[i].z = (in.v[i].z - mean) * rstd * g.z + o.z;
-      out.v[i].w = (in.v[i].w - mean) * rstd * g.w + o.w;
-    } else {
-      out.v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-    }
+  for (int i = 0; i < NV; ++i) {
+    out.v[i].x = (in.v[i].x - mean) * rstd * g.v[i].x + b.v[i].x;
+    out.v[i].y = (in.v[i].y - mean) * rstd * g.v[i].y + b.v[i].y;
+    out.v[i].z = (in.v[i].z - mean) * rstd * g.v[i].z + b.v[i].z;
+    out.v[i].w = (in.v[i].w - mean) * rstd * g.v[i].w + b.v[i].w;
   }
 }
 
-template <typename T>
-__device__ __forceinline__ void store_row16(T* dst, const RowRegs& r, int D4, int lane) {
+template <typename T, int NV>
+__device__ __forceinline__ void store_row16(T* dst, const Row<NV>& r, int D4, int lane) {
   typedef typename Vec4<T>::type V4;
 #pragma unroll
-  for (int i = 0; i < MAXV; ++i) {
-    const int c = i * 64 + lane;
-    if (c < D4) {
+  for (int i = 0; i < NV; ++i) {
+    if (in_row<NV>(i, lane, D4)) {
       V4 o;
       o[0] = (T)r.v[i].x; o[1] = (T)r.v[i].y; o[2] = (T)r.v[i].z; o[3] = (T)r.v[i].w;
-      ((V4*)dst)[c] = o;
+      ((V4*)dst)[i * 64 + lane] = o;
     }
   }
 }
 
-__device__ __forceinline__ void store_row32(float* dst, const RowRegs& r, int D4, int lane) {
+template <int NV>
+__device__ __forceinline__ void store_row32(float* dst, const Row<NV>& r, int D4, int lane) {
 #pragma unroll
-  for (int i = 0; i < MAXV; ++i) {
-    const int c = i * 64 + lane;
-    if (c < D4) ((float4*)dst)[c] = r.v[i];
-  }
+  for (int i = 0; i < NV; ++i)
+    if (in_row<NV>(i, lane, D4)) ((float4*)dst)[i * 64 + lane] = r.v[i];
 }
 
-__device__ __forceinline__ void add_row(RowRegs& r, const RowRegs& a) {
+template <int NV>
+__device__ __forceinline__ void add_row(Row<NV>& r, const Row<NV>& a) {
 #pragma unroll
-  for (int i = 0; i < MAXV; ++i) {
+  for (int i = 0; i < NV; ++i) {
     r.v[i].x += a.v[i].x; r.v[i].y += a.v[i].y; r.v[i].z += a.v[i].z; r.v[i].w += a.v[i].w;
   }
 }
 
+// Every kernel issues all of its row loads (activations and LN parameters) up front, so
+// their latencies overlap instead of following the reductions one round trip at a time.
+
 // slab != nullptr: first combine the split-K partial of the GEMM that wrote x
 // (x += slab, stored back), then LN -- the launch-boundary split-K reduce.
-template <typename T>
+template <typename T, int NV>
 __global__ __launch_bounds__(256) void ln_rows_kernel(float* __restrict__ x, const float* __restrict__ slab,
                                                       const float* w, const float* b, float eps,
                                                       T* __restrict__ out, int rows, int D) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= rows) return;
-  RowRegs r, o;
-  load_row(x + (long)row * D, D >> 2, lane, r);
+  const int D4 = D >> 2;
+  Row<NV> r, o, g, bb;
+  load_row(x + (long)row * D, D4, lane, r);
+  load_row(w, D4, lane, g);
+  load_row(b, D4, lane, bb);
   if (slab != nullptr) {
-    RowRegs a;
-    load_row(slab + (long)row * D, D >> 2, lane, a);
+    Row<NV> a;
+    load_row(slab + (long)row * D, D4, lane, a);
     add_row(r, a);
-    store_row32(x + (long)row * D, r, D >> 2, lane);
+    store_row32(x + (long)row * D, r, D4, lane);
   }
-  layer_norm_regs(r, o, w, b, eps, D, lane);
-  store_row16(out + (long)row * D, o, D >> 2, lane);
+  layer_norm_regs(r, o, g, bb, eps, D, lane);
+  store_row16(out + (long)row * D, o, D4, lane);
 }
 
-template <typename T>
+template <typename T, int NV>
 __global__ __launch_bounds__(256) void vision_embed_ln_kernel(float* __restrict__ x, const float* cls,
                                                               const float* pos, const float* lnpre_w,
                                                               const float* lnpre_b, const float* ln1_w,
@@ -122,26 +145,27 @@ __global__ __launch_bounds__(256) void vision_embed_ln_kernel(float* __restrict_
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= rows) return;
   const int D4 = D >> 2;
-  RowRegs r, y, z;
+  Row<NV> r, y, z, g0, b0, g1, b1;
   if (row % tokens == 0) {  // CLS token: class_embedding + positional_embedding[0]
-    RowRegs c, p;
+    Row<NV> c, p;
     load_row(cls, D4, lane, c);
     load_row(pos, D4, lane, p);
-#pragma unroll
-    for (int i = 0; i < MAXV; ++i) {
-      r.v[i].x = c.v[i].x + p.v[i].x; r.v[i].y = c.v[i].y + p.v[i].y;
-      r.v[i].z = c.v[i].z + p.v[i].z; r.v[i].w = c.v[i].w + p.v[i].w;
-    }
+    r = c;
+    add_row(r, p);
   } else {  // patch rows: conv1 + pos already written by the patch GEMM epilogue
     load_row(x + (long)row * D, D4, lane, r);
   }
-  layer_norm_regs(r, y, lnpre_w, lnpre_b, eps, D, lane);
+  load_row(lnpre_w, D4, lane, g0);
+  load_row(lnpre_b, D4, lane, b0);
+  load_row(ln1_w, D4, lane, g1);
+  load_row(ln1_b, D4, lane, b1);
+  layer_norm_regs(r, y, g0, b0, eps, D, lane);
   store_row32(x + (long)row * D, y, D4, lane);
-  layer_norm_regs(y, z, ln1_w, ln1_b, eps, D, lane);
+  layer_norm_regs(y, z, g1, b1, eps, D, lane);
   store_row16(h + (long)row * D, z, D4, lane);
 }
 
-template <typename T>
+template <typename T, int NV>
 __global__ __launch_bounds__(256) void text_embed_ln_kernel(const int64_t* __restrict__ ids, const float* tok,
                                                             const float* pos, const float* ln1_w,
                                                             const float* ln1_b, float eps, float* __restrict__ x,
@@ -152,24 +176,24 @@ __global__ __launch_bounds__(256) void text_embed_ln_kernel(const int64_t* __res
   const int D4 = D >> 2;
   long id = ids[row];
   id = id < 0 ? 0 : (id >= vocab ? vocab - 1 : id);  // host validates; clamp keeps the gather in bounds
-  RowRegs e, p, y;
+  Row<NV> e, p, y, g, bb;
   load_row(tok + id * D, D4, lane, e);
   load_row(pos + (long)(row % Tctx) * D, D4, lane, p);
-#pragma unroll
-  for (int i = 0; i < MAXV; ++i) {
-    e.v[i].x += p.v[i].x; e.v[i].y += p.v[i].y; e.v[i].z += p.v[i].z; e.v[i].w += p.v[i].w;
-  }
+  load_row(ln1_w, D4, lane, g);
+  load_row(ln1_b, D4, lane, bb);
+  add_row(e, p);
   store_row32(x + (long)row * D, e, D4, lane);
-  layer_norm_regs(e, y, ln1_w, ln1_b, eps, D, lane);
+  layer_norm_regs(e, y, g, bb, eps, D, lane);
   store_row16(h + (long)row * D, y, D4, lane);
 }
 
-template <typename T>
+template <typename T, int NV>
 __global__ __launch_bounds__(256) void pool_ln_kernel(const float* __restrict__ x, const float* __restrict__ slab,
                                                       const int64_t* __restrict__ ids, int tokens, const float* w,
                                                       const float* b, float eps, T* __restrict__ out, int B, int D) {
   const int bi = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (bi >= B) return;
+  const int D4 = D >> 2;
   int src = 0;
   if (ids != nullptr) {  // first index of the maximum id (torch argmax; EOT is the largest id)
     long best = -1;
@@ -186,15 +210,17 @@ __global__ __launch_bounds__(256) void pool_ln_kernel(const float* __restrict__ 
     }
     src = bidx;
   }
-  RowRegs r, y;
-  load_row(x + ((long)bi * tokens + src) * D, D >> 2, lane, r);
+  Row<NV> r, y, g, bb;
+  load_row(x + ((long)bi * tokens + src) * D, D4, lane, r);
+  load_row(w, D4, lane, g);
+  load_row(b, D4, lane, bb);
   if (slab != nullptr) {  // split-K partial of the last c_proj (x itself is not updated)
-    RowRegs a;
-    load_row(slab + ((long)bi * tokens + src) * D, D >> 2, lane, a);
+    Row<NV> a;
+    load_row(slab + ((long)bi * tokens + src) * D, D4, lane, a);
     add_row(r, a);
   }
-  layer_norm_regs(r, y, w, b, eps, D, lane);
-  store_row16(out + (long)bi * D, y, D >> 2, lane);
+  layer_norm_regs(r, y, g, bb, eps, D, lane);
+  store_row16(out + (long)bi * D, y, D4, lane);
 }
 
 __global__ __launch_bounds__(256) void l2norm_kernel(const float* __restrict__ in, float* __restrict__ out, int B,
@@ -218,10 +244,21 @@ inline dim3 rows_grid(int rows) { return dim3((rows + 3) / 4); }
 
 }  // namespace
 
-#define CLIPGPU_DISPATCH(dt, KERNEL, GRID, ...)                                              \
-  do {                                                                                        \
-    if ((dt) == DT_BF16) hipLaunchKernelGGL(KERNEL<__bf16>, GRID, dim3(256), 0, s, __VA_ARGS__); \
-    else hipLaunchKernelGGL(KERNEL<_Float16>, GRID, dim3(256), 0, s, __VA_ARGS__);              \
+// NV = ceil(D / 256) float4 per lane; D % 4 == 0, D <= 1280.
+#define CLIPGPU_ROW_LAUNCH(KERNEL, T, GRID, D, ...)                                                    \
+  do {                                                                                                  \
+    const int nv_ = ((D) / 4 + 63) / 64;                                                                \
+    auto go_ = [&](auto nvc) {                                                                          \
+      constexpr int NVC = decltype(nvc)::value;                                                         \
+      hipLaunchKernelGGL((KERNEL<T, NVC>), GRID, dim3(256), 0, s, __VA_ARGS__);                         \
+    };                                                                                                  \
+    switch (nv_) {                                                                                      \
+      case 1: go_(std::integral_constant<int, 1>{}); break;                                             \
+      case 2: go_(std::integral_constant<int, 2>{}); break;                                             \
+      case 3: go_(std::integral_constant<int, 3>{}); break;                                             \
+      case 4: go_(std::integral_constant<int, 4>{}); break;                                             \
+      default: go_(std::integral_constant<int, 5>{}); break;                                            \
+    }                                                                                                   \
   } while (0)
 
 hipError_t launch_ln_rows(DType dt, const float* x, const float* w, const float* b, float eps, void* out16,
@@ -229,55 +266,56 @@ hipError_t launch_ln_rows(DType dt, const float* x, const float* w, const float*
   return launch_ln_rows_add(dt, const_cast<float*>(x), nullptr, w, b, eps, out16, rows, D, s);
 }
 
+// (16-bit output pointers are passed as void*: the kernel parameter is T*)
 hipError_t launch_ln_rows_add(DType dt, float* x, const float* slab, const float* w, const float* b, float eps,
                               void* out16, int rows, int D, hipStream_t s) {
-  if (D % 4 || D > 256 * MAXV) return hipErrorInvalidValue;
-  if (dt == DT_BF16)
-    hipLaunchKernelGGL(ln_rows_kernel<__bf16>, rows_grid(rows), dim3(256), 0, s, x, slab, w, b, eps, (__bf16*)out16,
-                       rows, D);
-  else
-    hipLaunchKernelGGL(ln_rows_kernel<_Float16>, rows_grid(rows), dim3(256), 0, s, x, slab, w, b, eps,
-                       (_Float16*)out16, rows, D);
+  if (D % 4 || D > 256 * MAXV || D <= 0) return hipErrorInvalidValue;
+  if (dt == DT_BF16) {
+    CLIPGPU_ROW_LAUNCH(ln_rows_kernel, __bf16, rows_grid(rows), D, x, slab, w, b, eps, (__bf16*)out16, rows, D);
+  } else {
+    CLIPGPU_ROW_LAUNCH(ln_rows_kernel, _Float16, rows_grid(rows), D, x, slab, w, b, eps, (_Float16*)out16, rows, D);
+  }
   return hipGetLastError();
 }
 
 hipError_t launch_vision_embed_ln(DType dt, float* x, const float* cls, const float* pos, const float* lnpre_w,
                                   const float* lnpre_b, const float* ln1_w, const float* ln1_b, float eps,
                                   void* h, int B, int tokens, int D, hipStream_t s) {
-  if (D % 4 || D > 256 * MAXV) return hipErrorInvalidValue;
+  if (D % 4 || D > 256 * MAXV || D <= 0) return hipErrorInvalidValue;
   const int rows = B * tokens;
-  if (dt == DT_BF16)
-    hipLaunchKernelGGL(vision_embed_ln_kernel<__bf16>, rows_grid(rows), dim3(256), 0, s, x, cls, pos, lnpre_w,
-                       lnpre_b, ln1_w, ln1_b, eps, (__bf16*)h, rows, tokens, D);
-  else
-    hipLaunchKernelGGL(vision_embed_ln_kernel<_Float16>, rows_grid(rows), dim3(256), 0, s, x, cls, pos, lnpre_w,
-                       lnpre_b, ln1_w, ln1_b, eps, (_Float16*)h, rows, tokens, D);
+  if (dt == DT_BF16) {
+    CLIPGPU_ROW_LAUNCH(vision_embed_ln_kernel, __bf16, rows_grid(rows), D, x, cls, pos, lnpre_w, lnpre_b, ln1_w, ln1_b, eps,
+                       (__bf16*)h, rows, tokens, D);
+  } else {
+    CLIPGPU_ROW_LAUNCH(vision_embed_ln_kernel, _Float16, rows_grid(rows), D, x, cls, pos, lnpre_w, lnpre_b, ln1_w, ln1_b, eps,
+                       (_Float16*)h, rows, tokens, D);
+  }
   return hipGetLastError();
 }
 
 hipError_t launch_text_embed_ln(DType dt, const int64_t* ids, const float* tok, const float* pos,
                                 const float* ln1_w, const float* ln1_b, float eps, float* x, void* h, int B,
                                 int T, int D, int vocab, hipStream_t s) {
-  if (D % 4 || D > 256 * MAXV) return hipErrorInvalidValue;
+  if (D % 4 || D > 256 * MAXV || D <= 0) return hipErrorInvalidValue;
   const int rows = B * T;
-  if (dt == DT_BF16)
-    hipLaunchKernelGGL(text_embed_ln_kernel<__bf16>, rows_grid(rows), dim3(256), 0, s, ids, tok, pos, ln1_w,
-                       ln1_b, eps, x, (__bf16*)h, rows, T, D, vocab);
-  else
-    hipLaunchKernelGGL(text_embed_ln_kernel<_Float16>, rows_grid(rows), dim3(256), 0, s, ids, tok, pos, ln1_w,
-                       ln1_b, eps, x, (_Float16*)h, rows, T, D, vocab);
+  if (dt == DT_BF16) {
+    CLIPGPU_ROW_LAUNCH(text_embed_ln_kernel, __bf16, rows_grid(rows), D, ids, tok, pos, ln1_w, ln1_b, eps, x, (__bf16*)h,
+                       rows, T, D, vocab);
+  } else {
+    CLIPGPU_ROW_LAUNCH(text_embed_ln_kernel, _Float16, rows_grid(rows), D, ids, tok, pos, ln1_w, ln1_b, eps, x, (_Float16*)h,
+                       rows, T, D, vocab);
+  }
   return hipGetLastError();
 }
 
 hipError_t launch_pool_ln(DType dt, const float* x, const float* slab, const int64_t* ids, int tokens,
                           const float* w, const float* b, float eps, void* out16, int B, int D, hipStream_t s) {
-  if (D % 4 || D > 256 * MAXV) return hipErrorInvalidValue;
-  if (dt == DT_BF16)
-    hipLaunchKernelGGL(pool_ln_kernel<__bf16>, rows_grid(B), dim3(256), 0, s, x, slab, ids, tokens, w, b, eps,
-                       (__bf16*)out16, B, D);
-  else
-    hipLaunchKernelGGL(pool_ln_kernel<_Float16>, rows_grid(B), dim3(256), 0, s, x, slab, ids, tokens, w, b, eps,
-                       (_Float16*)out16, B, D);
+  if (D % 4 || D > 256 * MAXV || D <= 0) return hipErrorInvalidValue;
+  if (dt == DT_BF16) {
+    CLIPGPU_ROW_LAUNCH(pool_ln_kernel, __bf16, rows_grid(B), D, x, slab, ids, tokens, w, b, eps, (__bf16*)out16, B, D);
+  } else {
+    CLIPGPU_ROW_LAUNCH(pool_ln_kernel, _Float16, rows_grid(B), D, x, slab, ids, tokens, w, b, eps, (_Float16*)out16, B, D);
+  }
   return hipGetLastError();
 }
 
