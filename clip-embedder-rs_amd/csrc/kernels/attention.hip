@@ -101,8 +101,7 @@ __global__ __launch_bounds__(256) void attn_kernel(const T* __restrict__ qkv, T*
         s[t][j] = v;
         m = fmaxf(m, v);
       }
-    m = fmaxf(m, __shfl_xor(m, 16, 64));
-    m = fmaxf(m, __shfl_xor(m, 32, 64));
+    m = xmax32(xmax16(m));
     float sum = 0.f;
 #pragma unroll
     for (int t = 0; t < NKT; ++t)
@@ -112,8 +111,7 @@ __global__ __launch_bounds__(256) void attn_kernel(const T* __restrict__ qkv, T*
         s[t][j] = e;
         sum += e;
       }
-    sum += __shfl_xor(sum, 16, 64);
-    sum += __shfl_xor(sum, 32, 64);
+    sum = xsum32(xsum16(sum));
 
     // O^T[d][q] = V^T P^T; k order of step ks: element e of quarter fq <-> key 32ks + 16(e>>2) + 4fq + (e&3)
     f32x4 o[4];
@@ -338,8 +336,7 @@ __global__ __launch_bounds__(256, 2) void flash_attn_kernel(const T* __restrict_
         for (int t = 0; t < 4; ++t)
 #pragma unroll
           for (int j = 0; j < 4; ++j) mt = fmaxf(mt, s[qi][t][j]);
-        mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
-        mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+        mt = xmax32(xmax16(mt));
         const float mn = fmaxf(m[qi], mt);
         const float corr = __builtin_amdgcn_exp2f((m[qi] - mn) * scale_log2);  // m = -inf first: 0
         const float off = -mn * scale_log2;
@@ -352,8 +349,7 @@ __global__ __launch_bounds__(256, 2) void flash_attn_kernel(const T* __restrict_
             s[qi][t][j] = e;
             sum += e;
           }
-        sum += __shfl_xor(sum, 16, 64);
-        sum += __shfl_xor(sum, 32, 64);
+        sum = xsum32(xsum16(sum));
         l[qi] = l[qi] * corr + sum;
         m[qi] = mn;
 #pragma unroll

@@ -39,28 +39,66 @@ __device__ __forceinline__ void glds16(const void* gsrc, void* lds_base) {
   __builtin_amdgcn_global_load_lds(gsrc, (lds_void*)lds_base, 16, 0, 0);
 }
 
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+// Cross-lane reductions without the LDS permute unit (each __shfl_xor is a ds_bpermute
+// round trip): inside a 16-lane row by DPP row rotations; between rows by the gfx950
+// permlane swaps.  v_permlane16_swap(x, x) leaves rows {0,0,2,2} in the first result
+// and {1,1,3,3} in the second, so (first op second) is x op x[lane ^ 16] in every lane;
+// v_permlane32_swap likewise for lane ^ 32.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f32(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float row16_sum(float v) {  // sum over the 16 lanes of each row
+  v += dpp_f32<0x128>(v);  // row_ror:8
+  v += dpp_f32<0x124>(v);  // row_ror:4
+  v += dpp_f32<0x122>(v);  // row_ror:2
+  v += dpp_f32<0x121>(v);  // row_ror:1
   return v;
 }
-__device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+__device__ __forceinline__ float row16_max(float v) {
+  v = fmaxf(v, dpp_f32<0x128>(v));
+  v = fmaxf(v, dpp_f32<0x124>(v));
+  v = fmaxf(v, dpp_f32<0x122>(v));
+  v = fmaxf(v, dpp_f32<0x121>(v));
   return v;
 }
+// v_permlane{16,32}_swap as inline asm: the swap writes both of its operands, and with the
+// clang builtin this toolchain folded the second result into the first when the two were
+// combined in one expression (x + x instead of x + x[lane ^ 16]; test_lane_reductions).
+// The leading s_nop covers the VALU-write -> permlane-read hazard the compiler cannot see
+// through the asm.
+__device__ __forceinline__ void swap16(float& a, float& b) {
+  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+}
+__device__ __forceinline__ void swap32(float& a, float& b) {
+  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+}
+__device__ __forceinline__ float xsum16(float v) {  // v + v[lane ^ 16]
+  float a = v, b = v;
+  swap16(a, b);
+  return a + b;
+}
+__device__ __forceinline__ float xsum32(float v) {  // v + v[lane ^ 32]
+  float a = v, b = v;
+  swap32(a, b);
+  return a + b;
+}
+__device__ __forceinline__ float xmax16(float v) {
+  float a = v, b = v;
+  swap16(a, b);
+  return fmaxf(a, b);
+}
+__device__ __forceinline__ float xmax32(float v) {
+  float a = v, b = v;
+  swap32(a, b);
+  return fmaxf(a, b);
+}
+__device__ __forceinline__ float wave_sum(float v) { return xsum32(xsum16(row16_sum(v))); }
+__device__ __forceinline__ float wave_max(float v) { return xmax32(xmax16(row16_max(v))); }
 // Reductions over the 16 lanes that share (lane >> 4): the row groups of a
 // 16x16 MFMA accumulator (col = lane & 15).
-__device__ __forceinline__ float group16_sum(float v) {
-#pragma unroll
-  for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
-__device__ __forceinline__ float group16_max(float v) {
-#pragma unroll
-  for (int o = 8; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
-}
+__device__ __forceinline__ float group16_sum(float v) { return row16_sum(v); }
+__device__ __forceinline__ float group16_max(float v) { return row16_max(v); }
 
 // Activations (epilogue of c_fc).  Reference semantics: open_clip QuickGELU
 // x*sigmoid(1.702x) for OpenAI-style configs, nn.GELU (erf) otherwise,

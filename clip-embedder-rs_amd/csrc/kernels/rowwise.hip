@@ -38,22 +38,6 @@ __device__ __forceinline__ void load_row(const float* src, int D4, int lane, Row
     r.v[i] = in_row<NV>(i, lane, D4) ? ((const float4*)src)[i * 64 + lane] : make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
-// Wave sum: DPP rotations inside each 16-lane row (row_ror 8, 4, 2, 1), then two
-// cross-row xor-shuffles -- 2 LDS-permute round trips instead of 6.
-template <int CTRL>
-__device__ __forceinline__ float dpp_ror(float v) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
-}
-__device__ __forceinline__ float wave_sum_fast(float v) {
-  v += dpp_ror<0x128>(v);  // row_ror:8
-  v += dpp_ror<0x124>(v);  // row_ror:4
-  v += dpp_ror<0x122>(v);  // row_ror:2
-  v += dpp_ror<0x121>(v);  // row_ror:1
-  v += __shfl_xor(v, 16, 64);
-  v += __shfl_xor(v, 32, 64);
-  return v;
-}
-
 // torch LayerNorm, two-pass mean / biased variance in f32; g, b preloaded rows.
 template <int NV>
 __device__ __forceinline__ void layer_norm_regs(const Row<NV>& in, Row<NV>& out, const Row<NV>& g, const Row<NV>& b,
@@ -62,7 +46,7 @@ __device__ __forceinline__ void layer_norm_regs(const Row<NV>& in, Row<NV>& out,
   float s = 0.f;
 #pragma unroll
   for (int i = 0; i < NV; ++i) s += in.v[i].x + in.v[i].y + in.v[i].z + in.v[i].w;  // padding holds 0
-  const float mean = wave_sum_fast(s) / (float)D;
+  const float mean = wave_sum(s) / (float)D;
   float q = 0.f;
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
@@ -71,7 +55,7 @@ __device__ __forceinline__ void layer_norm_regs(const Row<NV>& in, Row<NV>& out,
       q += a * a + bb * bb + cc * cc + d * d;
     }
   }
-  const float var = wave_sum_fast(q) / (float)D;
+  const float var = wave_sum(q) / (float)D;
   const float rstd = 1.0f / sqrtf(var + eps);
 #pragma unroll
   for (int i = 0; i < NV; ++i) {

@@ -198,6 +198,34 @@ __global__ void fill_random(float* out, long n, uint32_t seed) {
 }
 }  // namespace
 
+namespace {
+__global__ void lane_reduce_kernel(const float* in, float* out) {
+  const int l = threadIdx.x;
+  const float v = in[l];
+  out[0 * 64 + l] = wave_sum(v);
+  out[1 * 64 + l] = wave_max(v);
+  out[2 * 64 + l] = xsum16(v);
+  out[3 * 64 + l] = xsum32(v);
+  out[4 * 64 + l] = group16_sum(v);
+  out[5 * 64 + l] = group16_max(v);
+  float a = v, b = v;
+  swap16(a, b);
+  out[6 * 64 + l] = a;
+  out[7 * 64 + l] = b;
+}
+}  // namespace
+
+int clipgpu_test_lane_reduce(const float* in64, float* out512) {
+  return guarded([&]() {
+    DevBuf di(64 * 4), dO(512 * 4);
+    up(di.p, in64, 64 * 4);
+    hipLaunchKernelGGL(lane_reduce_kernel, dim3(1), dim3(64), 0, nullptr, di.as<float>(), dO.as<float>());
+    TCHECK(hipGetLastError());
+    TCHECK(hipDeviceSynchronize());
+    down(out512, dO.p, 512 * 4);
+  });
+}
+
 int clipgpu_test_gemm_bench(int dtype, int epi, int act, int64_t M, int64_t N, int64_t K, int tile, int iters,
                             double* us_per_launch) {
   return guarded([&]() {

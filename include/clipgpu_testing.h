@@ -41,6 +41,11 @@ int clipgpu_test_patch_embed(int dtype, int mode, int64_t B, int64_t S, int64_t 
 int clipgpu_test_resize_rgb8_gpu(const uint8_t* const* images, const int* widths, const int* heights, int64_t n,
                                  int size, const char* interpolation, const char* resize_mode, uint8_t* out);
 
+/* The cross-lane reduction helpers (DPP row rotations + permlane swaps) on one wave: out[k*64 + lane]
+ * for k = 0 wave_sum, 1 wave_max, 2 x + x[lane^16], 3 x + x[lane^32], 4 row-of-16 sum, 5 row-of-16 max,
+ * 6 / 7 the two results of the raw permlane16 swap of (x, x). */
+int clipgpu_test_lane_reduce(const float* in64, float* out512);
+
 /* The staged 16-bit patch rows alone: rows_out[B*G*G][Kp] (as f32), Kp = 3*P*P rounded up to 64. */
 int clipgpu_test_patch_rows(int dtype, int mode, int64_t B, int64_t S, int64_t P, const void* pixels,
                             const float mean[3], const float std[3], float* rows_out);

@@ -247,3 +247,23 @@ def test_patch_embed(mode, S, P, D, tile):
     assert np.all(got[:, 0] == 0)  # CLS rows untouched
     bound = 3e-5 * (np.abs(patches) @ np.abs(W).T) + 1e-5
     assert np.all(np.abs(got[:, 1:] - ref) <= bound)
+
+
+def test_lane_reductions():
+    """DPP row rotations + permlane16/32 swaps (common.hpp) == the reductions they replace."""
+    L = _lib()
+    x = np.random.default_rng(9).standard_normal(64).astype(np.float32)
+    out = np.empty(512, np.float32)
+    L.check(L.lib().clipgpu_test_lane_reduce(x.ctypes.data, out.ctypes.data))
+    o = out.reshape(8, 64)
+    lanes = np.arange(64)
+    assert np.allclose(o[0], x.sum(), rtol=1e-5)
+    assert np.array_equal(o[1], np.full(64, x.max(), np.float32))
+    assert np.allclose(o[2], x + x[lanes ^ 16], rtol=1e-6)
+    assert np.allclose(o[3], x + x[lanes ^ 32], rtol=1e-6)
+    rows = x.reshape(4, 16)
+    assert np.allclose(o[4], np.repeat(rows.sum(1), 16), rtol=1e-5)
+    assert np.array_equal(o[5], np.repeat(rows.max(1), 16))
+    # raw permlane16 swap of (x, x): rows {0,0,2,2} and {1,1,3,3}
+    assert np.array_equal(o[6], np.repeat(rows[[0, 0, 2, 2]], 1, axis=0).ravel())
+    assert np.array_equal(o[7], np.repeat(rows[[1, 1, 3, 3]], 1, axis=0).ravel())
