@@ -42,9 +42,16 @@ namespace clipgpu {
                                             ")");                                                   \
   } while (0)
 
+// MX-fp8 weight matrix (fp8 engines): e4m3 [N][K] + E8M0 scales [N][K/32] (gemm_mx.hip).
+struct MxW {
+  uint8_t* q = nullptr;
+  uint8_t* s = nullptr;
+};
+
 struct LayerW {
   float *ln1_w, *ln1_b, *bqkv, *bo, *ln2_w, *ln2_b, *b1, *b2;
-  void *wqkv, *wo, *w1, *w2;
+  void *wqkv, *wo, *w1, *w2;  // 16-bit (fp8 engines: wo only)
+  MxW mqkv, m1, m2;           // fp8 engines: QKV, c_fc, c_proj
 };
 
 // MAP attention-pool head of the SigLIP family (timm AttentionPoolLatent).
@@ -73,7 +80,9 @@ struct Replica {
   DevWeights w;
   float* x = nullptr;     // [rows][D] f32 residual stream
   float* slab = nullptr;  // [rows][D] f32 split-K partial of out_proj / c_proj (engine.ksplit == 2)
-  void* h = nullptr;      // [rows][D] 16-bit (LN output / attention output)
+  void* h = nullptr;      // [rows][D] 16-bit (LN output / attention output); fp8 engines: LN output as e4m3
+  uint8_t* hs = nullptr;   // fp8 engines: [rows][D/32] scales of the LN output in h
+  uint8_t* bigs = nullptr; // fp8 engines: [rows][MLP/32] scales of the c_fc output (e4m3 in big)
   void* big = nullptr;    // [rows][max(3D, MLP)] 16-bit (qkv / MLP hidden)
   void* pooled = nullptr; // [B][D] 16-bit
   float* emb = nullptr;   // [B][E] f32 (pre-normalisation)
@@ -165,6 +174,10 @@ struct clipgpu_engine {
   clipgpu::TowerSpec spec;
   clipgpu::PreprocessCfg pre;
   clipgpu::DType dt = clipgpu::DT_BF16;
+  // fp8 engine (CLIPGPU_DTYPE_FP8): QKV / c_fc / c_proj run as MX-fp8 GEMMs (e4m3 weights +
+  // activations, E8M0 block scales, v_mfma_scale_f32_32x32x64_f8f6f4); attention, out_proj,
+  // the stems and heads stay bf16.
+  bool mx = false;
   int max_batch = 0;
   size_t in_bytes_per_row = 0;
   std::vector<clipgpu::Replica> reps;
@@ -286,6 +299,26 @@ void upload_weights(clipgpu_engine& e, Replica& r, const TensorMap& m) {
     upload_16(e.dt, pad.data(), pad.size(), p, staging_pad(pad.size()), r.stream);
     return p;
   };
+  // [R][C] f32 -> zero-padded [Rp][Cp] MX-fp8 (quantized on the device)
+  auto wmx_pad = [&](const std::string& k, int64_t Rp, int64_t Cp) {
+    const HostTensor& t = need(m, k);
+    const int64_t R = t.shape[0], C = t.numel() / t.shape[0];
+    std::vector<float> pad;
+    const float* src = t.data.data();
+    if (Rp != R || Cp != C) {
+      pad.assign((size_t)(Rp * Cp), 0.f);
+      for (int64_t i = 0; i < R; ++i) std::memcpy(&pad[(size_t)(i * Cp)], &t.data[(size_t)(i * C)], (size_t)C * 4);
+      src = pad.data();
+    }
+    float* stg = staging_pad((size_t)(Rp * Cp));
+    HIP_CHECK(hipMemcpy(stg, src, (size_t)(Rp * Cp) * 4, hipMemcpyHostToDevice));
+    MxW w;
+    w.q = (uint8_t*)a.take((size_t)(Rp * Cp));
+    w.s = (uint8_t*)a.take((size_t)(Rp * Cp / 32));
+    HIP_CHECK(launch_quant_rows(-1, stg, Cp, w.q, Cp, w.s, Cp / 32, (int)Rp, (int)Cp, r.stream));
+    HIP_CHECK(hipStreamSynchronize(r.stream));
+    return w;
+  };
   auto f32_pad = [&](const std::string& k, int64_t n) {
     const HostTensor& t = need(m, k);
     std::vector<float> pad((size_t)n, 0.f);
@@ -348,15 +381,22 @@ void upload_weights(clipgpu_engine& e, Replica& r, const TensorMap& m) {
     LayerW L;
     L.ln1_w = f32(p + n_ln1w);
     L.ln1_b = f32(p + n_ln1b);
-    L.wqkv = w16(p + n_qkvw);
+    L.wqkv = L.w1 = L.w2 = nullptr;
+    if (e.mx) {
+      L.mqkv = wmx_pad(p + n_qkvw, 3 * D, D);
+      L.m1 = wmx_pad(p + n_fc1w, mlp_pad(s), D);
+      L.m2 = wmx_pad(p + n_fc2w, D, mlp_pad(s));
+    } else {
+      L.wqkv = w16(p + n_qkvw);
+      L.w1 = w16_pad(p + n_fc1w, mlp_pad(s), D);
+      L.w2 = w16_pad(p + n_fc2w, D, mlp_pad(s));
+    }
     L.bqkv = f32(p + n_qkvb);
     L.wo = w16(p + n_ow);
     L.bo = f32(p + n_ob);
     L.ln2_w = f32(p + n_ln2w);
     L.ln2_b = f32(p + n_ln2b);
-    L.w1 = w16_pad(p + n_fc1w, mlp_pad(s), D);
     L.b1 = f32_pad(p + n_fc1b, mlp_pad(s));
-    L.w2 = w16_pad(p + n_fc2w, D, mlp_pad(s));
     L.b2 = f32(p + n_fc2b);
     w.layers.push_back(L);
   }
@@ -408,8 +448,10 @@ void alloc_workspace(clipgpu_engine& e, Replica& r) {
   const size_t rows = B * (size_t)s.tokens(), D = s.width;
   const size_t wide = big_wide(s);
   const size_t E = s.embed_dim;
+  const size_t MLP = (size_t)mlp_pad(s);
   const size_t sizes[] = {rows * D * 4, rows * D * 2, rows * wide * 2, B * D * 2, B * E * 4, B * E * 4,
-                          B * e.in_bytes_per_row, e.ksplit > 1 ? rows * D * 4 : 0};
+                          B * e.in_bytes_per_row, e.ksplit > 1 ? rows * D * 4 : 0,
+                          e.mx ? rows * D / 32 : 0, e.mx ? rows * MLP / 32 : 0};
   size_t total = 0;
   for (size_t z : sizes) total += align256(z);
   HIP_CHECK(hipMalloc(&r.work, total));
@@ -423,6 +465,8 @@ void alloc_workspace(clipgpu_engine& e, Replica& r) {
   r.out = (float*)a.take(sizes[5]);
   r.in = a.take(sizes[6]);
   r.slab = e.ksplit > 1 ? (float*)a.take(sizes[7]) : nullptr;
+  r.hs = e.mx ? (uint8_t*)a.take(sizes[8]) : nullptr;
+  r.bigs = e.mx ? (uint8_t*)a.take(sizes[9]) : nullptr;
   for (int i = 0; i < e.lanes; ++i) {
     HIP_CHECK(hipStreamCreateWithFlags(&r.lane[i], hipStreamNonBlocking));
     HIP_CHECK(hipEventCreateWithFlags(&r.join[i], hipEventDisableTiming));
@@ -515,6 +559,32 @@ GemmParams site_gemm(const clipgpu_engine& e, const Replica& r, const LayerW& L,
   return g;
 }
 
+// fp8 engines: the MX-fp8 GEMM of a trunk site (QKV: LN e4m3 -> 16-bit qkv; c_fc: LN e4m3 ->
+// act -> e4m3 hidden in `big` + scales; c_proj: e4m3 hidden -> residual stream).
+int site_epi_mx(int site) { return site == GS_PROJ ? EPI_RESID : (site == GS_FC ? EPI_STOREQ : EPI_STORE16); }
+
+MxGemmParams site_gemm_mx(const clipgpu_engine& e, const Replica& r, const LayerW& L, int site, int rows) {
+  const int D = e.spec.width, MLP = mlp_pad(e.spec);
+  MxGemmParams g{};
+  g.M = rows;
+  if (site == GS_PROJ) {
+    g.A = (const uint8_t*)r.big; g.lda = MLP; g.As = r.bigs; g.ldas = MLP / 32;
+    g.W = L.m2.q; g.ldw = MLP; g.Ws = L.m2.s; g.ldws = MLP / 32;
+    g.bias = L.b2; g.out = r.x; g.ldo = D; g.N = D; g.K = MLP;
+    return g;
+  }
+  g.A = (const uint8_t*)r.h; g.lda = D; g.As = r.hs; g.ldas = D / 32;
+  g.K = D;
+  if (site == GS_QKV) {
+    g.W = L.mqkv.q; g.ldw = D; g.Ws = L.mqkv.s; g.ldws = D / 32;
+    g.bias = L.bqkv; g.out = r.big; g.ldo = 3 * D; g.N = 3 * D;
+  } else {  // GS_FC
+    g.W = L.m1.q; g.ldw = D; g.Ws = L.m1.s; g.ldws = D / 32;
+    g.bias = L.b1; g.out = r.big; g.ldo = MLP; g.outs = r.bigs; g.ldos = MLP / 32; g.N = MLP;
+  }
+  return g;
+}
+
 // The transformer trunk shared by both towers: L x [LN1 -> QKV -> MHA -> out+res ->
 // LN2 -> fc1+act -> fc2+res], with h already holding ln_1(x) of layer 0.
 void trunk(const clipgpu_engine& e, const Replica& r, int B, int causal, hipStream_t st) {
@@ -525,6 +595,12 @@ void trunk(const clipgpu_engine& e, const Replica& r, int B, int causal, hipStre
     const LayerW& L = r.w.layers[l];
     auto gemm = [&](int site, int cat, const char* what) {
       ProfScope ps(e, cat, st, /*gemm=*/true);
+      if (e.mx && site != GS_OUT) {
+        MxGemmParams g = site_gemm_mx(e, r, L, site, rows);
+        g.tile = tuned ? e.tile[site] : MX_TILE_AUTO;
+        check(launch_gemm_mx(e.dt, site_epi_mx(site), site == GS_FC ? s.act : ACT_NONE, g, st), what);
+        return;
+      }
       GemmParams g = site_gemm(e, r, L, site, rows);
       g.tile = tuned ? e.tile[site] : TILE_AUTO;
       check(launch_gemm(e.dt, A_ROWS, site_epi(site), site == GS_FC ? s.act : ACT_NONE, g, st), what);
@@ -535,13 +611,13 @@ void trunk(const clipgpu_engine& e, const Replica& r, int B, int causal, hipStre
     gemm(GS_OUT, PC_OUT_PROJ, "out_proj gemm");
     { ProfScope ps(e, PC_LN, st);
       check(launch_ln_rows_add(e.dt, r.x, site_split(e, GS_OUT) ? r.slab : nullptr, L.ln2_w, L.ln2_b, s.ln_eps, r.h,
-                               rows, D, st), "ln_2"); }
+                               rows, D, st, r.hs), "ln_2"); }
     gemm(GS_FC, PC_C_FC, "c_fc gemm");
     gemm(GS_PROJ, PC_C_PROJ, "c_proj gemm");
     if (l + 1 < s.layers) {  // (the last c_proj's slab is added by the head's first LayerNorm)
       ProfScope ps(e, PC_LN, st);
       check(launch_ln_rows_add(e.dt, r.x, site_split(e, GS_PROJ) ? r.slab : nullptr, r.w.layers[l + 1].ln1_w,
-                               r.w.layers[l + 1].ln1_b, s.ln_eps, r.h, rows, D, st), "ln_1");
+                               r.w.layers[l + 1].ln1_b, s.ln_eps, r.h, rows, D, st, r.hs), "ln_1");
     }
   }
 }
@@ -565,6 +641,7 @@ void autotune_tiles(clipgpu_engine& e, Replica& r) {
     for (int i = 0; i < 4; ++i) {
       if (v[i] < TILE_AUTO || v[i] > TILE_LAST) throw ClipErr(CLIPGPU_ERR_INVALID, "bad CLIPGPU_GEMM_TILES entry");
       e.tile[i] = v[i];
+      if (e.mx && i != GS_OUT) e.tile[i] = MX_TILE_AUTO;  // the pins name 16-bit tiles
     }
     return;
   }
@@ -595,8 +672,29 @@ void autotune_tiles(clipgpu_engine& e, Replica& r) {
     return best_tile;
   };
   const LayerW& L = r.w.layers[0];
-  for (int site = 0; site < GS_N; ++site)
+  for (int site = 0; site < GS_N; ++site) {
+    if (e.mx && site != GS_OUT) {  // MX sites: the built MX tiles (same timing loop)
+      MxGemmParams g = site_gemm_mx(e, r, L, site, rows);
+      const int epi = site_epi_mx(site), act = site == GS_FC ? e.spec.act : ACT_NONE;
+      float best = 1e30f;
+      for (int t : {MX_TILE_256x128, MX_TILE_128x128}) {
+        g.tile = t;
+        check(launch_gemm_mx(e.dt, epi, act, g, r.stream), "autotune mx gemm");
+        HIP_CHECK(hipEventRecord(a, r.stream));
+        for (int i = 0; i < 4; ++i) check(launch_gemm_mx(e.dt, epi, act, g, r.stream), "autotune mx gemm");
+        HIP_CHECK(hipEventRecord(b, r.stream));
+        HIP_CHECK(hipEventSynchronize(b));
+        float ms = 0.f;
+        HIP_CHECK(hipEventElapsedTime(&ms, a, b));
+        if (ms < best) {
+          best = ms;
+          e.tile[site] = t;
+        }
+      }
+      continue;
+    }
     e.tile[site] = tune(site_gemm(e, r, L, site, rows), site_epi(site), site == GS_FC ? e.spec.act : ACT_NONE);
+  }
   if (e.spec.tower == TOWER_VISION) {
     const TowerSpec& s = e.spec;
     const int G = s.grid(), Kp = kpatch_pad(s), lane_b = rows / s.tokens();
@@ -661,7 +759,8 @@ void vision_forward(const clipgpu_engine& e, const Replica& r, const void* pixel
     check(launch_gemm(e.dt, A_ROWS, EPI_PATCH, ACT_NONE, g, st), "patch gemm"); }
   if (s.family == FAMILY_SIGLIP) {  // no class token, no pre-norm: x = patches + bias + pos
     { ProfScope ps(e, PC_STEM, st);
-      check(launch_ln_rows(e.dt, r.x, r.w.layers[0].ln1_w, r.w.layers[0].ln1_b, s.ln_eps, r.h, B * s.tokens(), D, st),
+      check(launch_ln_rows(e.dt, r.x, r.w.layers[0].ln1_w, r.w.layers[0].ln1_b, s.ln_eps, r.h, B * s.tokens(), D, st,
+                           r.hs),
             "ln_1"); }
     trunk(e, r, B, 0, st);
     head_map(e, r, B, d_out, st);
@@ -670,7 +769,7 @@ void vision_forward(const clipgpu_engine& e, const Replica& r, const void* pixel
   {
   ProfScope ps(e, PC_STEM, st);
   check(launch_vision_embed_ln(e.dt, r.x, r.w.cls, r.w.pos, r.w.lnpre_w, r.w.lnpre_b, r.w.layers[0].ln1_w,
-                               r.w.layers[0].ln1_b, s.ln_eps, r.h, B, s.tokens(), D, st),
+                               r.w.layers[0].ln1_b, s.ln_eps, r.h, B, s.tokens(), D, st, r.hs),
         "embed+ln_pre");
   }
   trunk(e, r, B, 0, st);
@@ -683,7 +782,7 @@ void text_forward(const clipgpu_engine& e, const Replica& r, const int64_t* d_id
   {
   ProfScope ps(e, PC_STEM, st);
   check(launch_text_embed_ln(e.dt, d_ids, r.w.tok, r.w.pos, r.w.layers[0].ln1_w, r.w.layers[0].ln1_b, s.ln_eps,
-                             r.x, r.h, B, s.context_length, s.width, s.vocab_size, st),
+                             r.x, r.h, B, s.context_length, s.width, s.vocab_size, st, r.hs),
         "token embed+ln_1");
   }
   trunk(e, r, B, 1, st);
@@ -701,6 +800,8 @@ Replica lane_view(const clipgpu_engine& e, const Replica& r, int b0) {
   if (r.slab) v.slab = r.slab + rows * D;
   v.h = (char*)r.h + rows * D * 2;
   v.big = (char*)r.big + rows * wide * 2;
+  if (r.hs) v.hs = r.hs + rows * D / 32;
+  if (r.bigs) v.bigs = r.bigs + rows * (size_t)mlp_pad(s) / 32;
   v.pooled = (char*)r.pooled + (size_t)b0 * D * 2;
   v.emb = r.emb + (size_t)b0 * s.embed_dim;
   return v;
@@ -821,7 +922,7 @@ void text_forward_lanes(const clipgpu_engine& e, const Replica& r, const int64_t
 // staging buffer (timing only).  CLIPGPU_TUNE_FORWARD=0 skips it; pinned tiles skip it.
 void tune_forward(clipgpu_engine& e, Replica& r) {
   const char* env = getenv("CLIPGPU_TUNE_FORWARD");
-  if ((env && env[0] == '0') || getenv("CLIPGPU_GEMM_TILES") || e.max_batch < 64) return;
+  if ((env && env[0] == '0') || getenv("CLIPGPU_GEMM_TILES") || e.max_batch < 64 || e.mx) return;
   const char* at = getenv("CLIPGPU_GEMM_AUTOTUNE");
   if (at && at[0] == '0') return;
   const int B = e.max_batch;
@@ -1173,7 +1274,8 @@ int clipgpu_create(const char* model_dir, int tower, const int* device_ids, int 
     *out = nullptr;
     if (!model_dir) throw ClipErr(CLIPGPU_ERR_INVALID, "model_dir is NULL");
     if (tower != CLIPGPU_TOWER_VISION && tower != CLIPGPU_TOWER_TEXT) throw ClipErr(CLIPGPU_ERR_INVALID, "bad tower");
-    if (dtype != CLIPGPU_DTYPE_BF16 && dtype != CLIPGPU_DTYPE_F16) throw ClipErr(CLIPGPU_ERR_INVALID, "bad dtype");
+    if (dtype != CLIPGPU_DTYPE_BF16 && dtype != CLIPGPU_DTYPE_F16 && dtype != CLIPGPU_DTYPE_FP8)
+      throw ClipErr(CLIPGPU_ERR_INVALID, "bad dtype");
     if (max_batch <= 0) throw ClipErr(CLIPGPU_ERR_INVALID, "max_batch must be > 0");
     const std::string dir(model_dir);
     struct stat st;
@@ -1191,7 +1293,8 @@ int clipgpu_create(const char* model_dir, int tower, const int* device_ids, int 
     std::unique_ptr<clipgpu_engine> e(new clipgpu_engine());
     e->spec = tower == CLIPGPU_TOWER_VISION ? oc.vision : oc.text;
     e->pre = oc.pre;
-    e->dt = dtype == CLIPGPU_DTYPE_BF16 ? DT_BF16 : DT_F16;
+    e->dt = dtype == CLIPGPU_DTYPE_F16 ? DT_F16 : DT_BF16;  // fp8 engines keep bf16 outside the MX GEMMs
+    e->mx = dtype == CLIPGPU_DTYPE_FP8;
     e->max_batch = max_batch;
     if (const char* ln = getenv("CLIPGPU_LANES")) e->lanes = std::max(1, std::min(4, atoi(ln)));
     else e->lanes = 2;
@@ -1204,6 +1307,8 @@ int clipgpu_create(const char* model_dir, int tower, const int* device_ids, int 
     if (hd != 64 && hd != 72 && hd != 80)
       throw ClipErr(CLIPGPU_ERR_CONFIG, "Configuration error: head dim " + std::to_string(hd) + " not supported (64, 72, 80)");
     if (s.width > 1280) throw ClipErr(CLIPGPU_ERR_CONFIG, "Configuration error: width > 1280 not supported yet");
+    if (e->mx && (s.width % 128 || mlp_pad(s) % 128))
+      throw ClipErr(CLIPGPU_ERR_CONFIG, "Configuration error: the fp8 path needs width and MLP width % 128 == 0");
     if (s.tokens() > 1024) throw ClipErr(CLIPGPU_ERR_CONFIG, "Configuration error: > 1024 tokens not supported yet");
     if (s.tower == TOWER_VISION) {
       if (s.image_size % s.patch_size)

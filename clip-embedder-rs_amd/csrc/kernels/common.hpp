@@ -12,6 +12,7 @@
 namespace clipgpu {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
@@ -37,6 +38,32 @@ typedef __attribute__((address_space(3))) void lds_void;
 // the wave-uniform `lds_base` + lane*16; the global source is per lane.
 __device__ __forceinline__ void glds16(const void* gsrc, void* lds_base) {
   __builtin_amdgcn_global_load_lds(gsrc, (lds_void*)lds_base, 16, 0, 0);
+}
+// 4-byte form (global_load_lds_dword): lds_base + lane*4.
+__device__ __forceinline__ void glds4(const void* gsrc, void* lds_base) {
+  __builtin_amdgcn_global_load_lds(gsrc, (lds_void*)lds_base, 4, 0, 0);
+}
+
+// ---- MX-fp8 (OCP e4m3fn elements, E8M0 scale per 32 consecutive elements of a row) ----
+// Block exponent: the smallest e with amax <= 448 * 2^e (448 = largest e4m3 value, so no
+// element saturates), from the bits of amax: amax = 1.f * 2^E, 448 = 1.75 * 2^8.  Clamped
+// to the E8M0 range [-127, 127]; the stored scale byte is e + 127.
+__device__ __forceinline__ int mx_exp(float amax) {
+  const uint32_t b = __float_as_uint(amax);
+  const int be = (int)(b >> 23);
+  if (be == 0) return -127;  // zero / denormal block
+  const int e = be - 135 + ((b & 0x7fffffu) > 0x600000u ? 1 : 0);
+  return e < -127 ? -127 : (e > 127 ? 127 : e);
+}
+// 2^-e (exact; 2^-127 is the f32 denormal 0x00400000)
+__device__ __forceinline__ float mx_inv(int e) {
+  return e < 127 ? __uint_as_float((uint32_t)(127 - e) << 23) : __uint_as_float(0x00400000u);
+}
+// four scaled values -> four e4m3 bytes (v_cvt_pk_fp8_f32: round to nearest even)
+__device__ __forceinline__ uint32_t mx_pack4(float a, float b, float c, float d, float inv) {
+  int w = __builtin_amdgcn_cvt_pk_fp8_f32(a * inv, b * inv, 0, false);
+  w = __builtin_amdgcn_cvt_pk_fp8_f32(c * inv, d * inv, w, true);
+  return (uint32_t)w;
 }
 
 // Cross-lane reductions without the LDS permute unit (each __shfl_xor is a ds_bpermute

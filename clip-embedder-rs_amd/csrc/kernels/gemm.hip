@@ -33,21 +33,11 @@
 
 #include "common.hpp"
 #include "kernels.hpp"
+#include "gemm_util.hpp"
 
 namespace clipgpu {
 
 thread_local GemmLaunchEvents g_gemm_events;
-
-// hipLaunchKernelGGL, or the event-stamped ext launch when a profiler armed g_gemm_events.
-template <typename K>
-void gemm_launch(K kernel, int grid, int threads, hipStream_t s, const GemmParams& p) {
-  if (g_gemm_events.start && g_gemm_events.stop) {
-    hipExtLaunchKernelGGL(kernel, dim3(grid), dim3(threads), 0, s, g_gemm_events.start, g_gemm_events.stop, 0, p);
-    g_gemm_events = GemmLaunchEvents();
-  } else {
-    hipLaunchKernelGGL(kernel, dim3(grid), dim3(threads), 0, s, p);
-  }
-}
 
 // Diagnostic build only (make stamps -> lib/libclipgpu_stamps.so): s_memtime
 // stamps of wave 0 of each block at fixed points of the tile loop
@@ -72,57 +62,12 @@ __device__ unsigned long long g_gemm_stamps[kStampBlocks * kStampSlots];
 
 namespace {
 
+using namespace gemm_detail;
+
 constexpr int BK = 64;
 
 template <typename T>
 __device__ __forceinline__ T to16(float v) { return (T)v; }
-
-__device__ __forceinline__ uint32_t lds_addr(const void* p) {
-  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
-}
-
-template <int N, typename F, int... I>
-__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
-  (f(std::integral_constant<int, I>{}), ...);
-}
-template <int N, typename F>
-__device__ __forceinline__ void static_for(F&& f) {
-  static_for_impl<N>(f, std::make_integer_sequence<int, N>{});
-}
-
-template <int OFF, typename V>
-__device__ __forceinline__ void ds_read_b128(V& r, uint32_t addr) {
-  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF));
-}
-
-// s_waitcnt lgkmcnt(0) that names every fragment register as read-write, so no
-// consumer of them can be scheduled above it (cdna_hip_programming.md §5.7 form ii).
-template <typename V, int MI, int NI>
-__device__ __forceinline__ void lgkm_wait_all(V (&a)[MI], V (&b)[NI]) {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-  for (int i = 0; i < MI; ++i) asm volatile("" : "+v"(a[i]));
-#pragma unroll
-  for (int i = 0; i < NI; ++i) asm volatile("" : "+v"(b[i]));
-}
-
-template <int N>
-__device__ __forceinline__ void vm_wait() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
-}
-
-
-// Tile order shared by all blocks: tiles are grouped 8 row panels at a time
-// (walk M first inside a group) so that concurrently running tiles share A and W
-// panels in L2.
-__device__ __forceinline__ void tile_coords(int t, int nTm, int nTn, int BM, int BN, int& m0, int& n0) {
-  constexpr int GROUP = 8;
-  const int per_group = GROUP * nTn;
-  const int first_m = (t / per_group) * GROUP;
-  const int gsize = min(nTm - first_m, GROUP);
-  m0 = (first_m + (t % per_group) % gsize) * BM;
-  n0 = ((t % per_group) / gsize) * BN;
-}
 
 template <typename T, int BM, int BN, int WGM, int WGN, int EPI, int ACT>
 __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p) {
@@ -803,18 +748,6 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_pipe_kernel(GemmParams 
   GEMM_STAMP_REAL(63);
 }
 
-int device_cus() {
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    hipDeviceProp_t prop;
-    if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
-      cus = prop.multiProcessorCount;
-    if (cus <= 0) cus = 256;
-  }
-  return cus;
-}
-
 template <typename T, int BM, int BN, int WGM, int WGN, int EPI, int ACT>
 hipError_t launch_cfg(const GemmParams& p, hipStream_t s) {
   const int nTn = (p.N + BN - 1) / BN, nTm = (p.M + BM - 1) / BM;
@@ -886,6 +819,19 @@ hipError_t launch_typed(int epi, int act, const GemmParams& p, hipStream_t s) {
 }
 
 }  // namespace
+
+int device_cus() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    hipDeviceProp_t prop;
+    if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
+      cus = prop.multiProcessorCount;
+    if (cus <= 0) cus = 256;
+  }
+  return cus;
+}
+
 
 // Tile choice: large-M GEMMs use the 256-row tiles (128 FLOP per staged byte
 // instead of 64); among those, the column tile that wastes the least of the

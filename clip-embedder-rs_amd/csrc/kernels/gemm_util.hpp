@@ -1,0 +1,75 @@
+// Device helpers shared by the MFMA GEMM kernels (gemm.hip, gemm_mx.hip).
+#pragma once
+#include <hip/hip_ext.h>
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <utility>
+
+#include "kernels.hpp"
+
+namespace clipgpu {
+
+// hipLaunchKernelGGL, or the event-stamped ext launch when a profiler armed g_gemm_events.
+template <typename K, typename P>
+inline void gemm_launch(K kernel, int grid, int threads, hipStream_t s, const P& p) {
+  if (g_gemm_events.start && g_gemm_events.stop) {
+    hipExtLaunchKernelGGL(kernel, dim3(grid), dim3(threads), 0, s, g_gemm_events.start, g_gemm_events.stop, 0, p);
+    g_gemm_events = GemmLaunchEvents();
+  } else {
+    hipLaunchKernelGGL(kernel, dim3(grid), dim3(threads), 0, s, p);
+  }
+}
+
+namespace gemm_detail {
+
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+
+template <int N, typename F, int... I>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl<N>(f, std::make_integer_sequence<int, N>{});
+}
+
+template <int OFF, typename V>
+__device__ __forceinline__ void ds_read_b128(V& r, uint32_t addr) {
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF));
+}
+
+// s_waitcnt lgkmcnt(0) that names every fragment register as read-write, so no
+// consumer of them can be scheduled above it (cdna_hip_programming.md §5.7 form ii).
+template <typename V, int MI, int NI>
+__device__ __forceinline__ void lgkm_wait_all(V (&a)[MI], V (&b)[NI]) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < MI; ++i) asm volatile("" : "+v"(a[i]));
+#pragma unroll
+  for (int i = 0; i < NI; ++i) asm volatile("" : "+v"(b[i]));
+}
+
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+
+
+// Tile order shared by all blocks: tiles are grouped 8 row panels at a time
+// (walk M first inside a group) so that concurrently running tiles share A and W
+// panels in L2.
+__device__ __forceinline__ void tile_coords(int t, int nTm, int nTn, int BM, int BN, int& m0, int& n0) {
+  constexpr int GROUP = 8;
+  const int per_group = GROUP * nTn;
+  const int first_m = (t / per_group) * GROUP;
+  const int gsize = min(nTm - first_m, GROUP);
+  m0 = (first_m + (t % per_group) % gsize) * BM;
+  n0 = ((t % per_group) / gsize) * BN;
+}
+
+}  // namespace gemm_detail
+
+}  // namespace clipgpu

@@ -21,6 +21,7 @@ enum Epi {
   EPI_RESID = 1,    // out32[m][n] += acc + bias[n]        (residual stream, in place)
   EPI_STORE32 = 2,  // out32[m][n] = acc + bias[n]
   EPI_PATCH = 3,    // x[b*(G^2+cls) + cls + p][n] = acc + bias[n] + pos[cls + p][n]
+  EPI_STOREQ = 4,   // launch_gemm_mx only: out = MX-fp8 of act(acc + bias[n]) (e4m3 + scales)
 };
 
 struct GemmParams {
@@ -51,6 +52,7 @@ enum GemmTile {
   TILE_LAST = TILE_64x128_PIPE,
 };
 int pick_gemm_tile(int M, int N, int K);
+int device_cus();  // CUs of the current device (cached)
 
 // act: Act enum from common.hpp (only used with EPI_STORE16)
 hipError_t launch_gemm(DType dt, int asrc, int epi, int act, const GemmParams& p, hipStream_t s);
@@ -75,21 +77,23 @@ hipError_t launch_attention(DType dt, const void* qkv, void* out, int B, int N, 
 
 // out16[r] = LN(x[r]) for r < rows.
 hipError_t launch_ln_rows(DType dt, const float* x, const float* w, const float* b, float eps,
-                          void* out16, int rows, int D, hipStream_t s);
+                          void* out16, int rows, int D, hipStream_t s, uint8_t* qs = nullptr);
+// qs != nullptr (these three LN launchers): the output is MX-fp8, out16 = e4m3 bytes [rows][D],
+// qs = scales [rows][D/32] (gemm_mx.hip's A operand); D % 32 == 0.
 // slab != nullptr: x[r] += slab[r] (stored) first -- the split-K combine of the GEMM that wrote x.
 hipError_t launch_ln_rows_add(DType dt, float* x, const float* slab, const float* w, const float* b, float eps,
-                              void* out16, int rows, int D, hipStream_t s);
+                              void* out16, int rows, int D, hipStream_t s, uint8_t* qs = nullptr);
 
 // Vision stem tail: CLS row = cls + pos[0]; x = ln_pre(x) (in place); h = ln_1(x).
 hipError_t launch_vision_embed_ln(DType dt, float* x, const float* cls, const float* pos,
                                   const float* lnpre_w, const float* lnpre_b,
                                   const float* ln1_w, const float* ln1_b, float eps,
-                                  void* h, int B, int tokens, int D, hipStream_t s);
+                                  void* h, int B, int tokens, int D, hipStream_t s, uint8_t* qs = nullptr);
 
 // Text stem: x = tok[ids] + pos; h = ln_1(x).
 hipError_t launch_text_embed_ln(DType dt, const int64_t* ids, const float* tok, const float* pos,
                                 const float* ln1_w, const float* ln1_b, float eps, float* x,
-                                void* h, int B, int T, int D, int vocab, hipStream_t s);
+                                void* h, int B, int T, int D, int vocab, hipStream_t s, uint8_t* qs = nullptr);
 
 // Pool one row per sequence (CLS: ids == nullptr; else first argmax of ids) and LN it.
 // slab (nullable): split-K partial of the last c_proj, added to the pooled row.
@@ -131,5 +135,30 @@ hipError_t launch_cast_f32(DType dt, const float* in, void* out, long n, hipStre
 // Diagnostic build: copy (or clear) the per-block s_memtime stamps of the last GEMM launch.
 hipError_t read_gemm_stamps(unsigned long long* host, int nblocks, bool clear);
 #endif
+
+// ---- MX-fp8 path (gemm_mx.hip) ---------------------------------------------------------
+// An MX-fp8 matrix is OCP e4m3fn bytes [rows][ld] plus E8M0 scale bytes [rows][lds], one per
+// 32 consecutive elements of a row: element = e4m3 * 2^(scale - 127).  K % 128 == 0.
+struct MxGemmParams {
+  const uint8_t* A; long lda; const uint8_t* As; long ldas;  // activations [M][K]
+  const uint8_t* W; long ldw; const uint8_t* Ws; long ldws;  // weights [N][K]
+  const float* bias;                                         // [N] or nullptr
+  void* out; long ldo;     // EPI_STORE16: T16, EPI_RESID / EPI_STORE32: f32, EPI_STOREQ: e4m3 bytes
+  uint8_t* outs; long ldos;  // EPI_STOREQ: the output's scales [M][N/32]
+  int M, N, K;
+  int tile;                // MxTile
+};
+enum MxTile {
+  MX_TILE_AUTO = 0,
+  MX_TILE_256x256 = 1,  // not built: 8 waves x (128x64) spill past 256 registers with the scales
+  MX_TILE_256x128 = 2,  // 8 waves (128x32 each), 101 KiB LDS
+  MX_TILE_128x128 = 3,  // 4 waves (64x64 each), 68 KiB LDS, 2 blocks / CU
+  MX_TILE_LAST = MX_TILE_128x128,
+};
+// epi: EPI_STORE16 (act), EPI_RESID, EPI_STORE32, EPI_STOREQ (act); N % 32 == 0.
+hipError_t launch_gemm_mx(DType dt, int epi, int act, const MxGemmParams& p, hipStream_t s);
+// Rows of f32 (src_dt < 0) or 16-bit (DType) values -> MX-fp8; cols % 32 == 0.
+hipError_t launch_quant_rows(int src_dt, const void* src, long ld, uint8_t* q, long ldq, uint8_t* qs, long ldqs,
+                             int rows, int cols, hipStream_t s);
 
 }  // namespace clipgpu

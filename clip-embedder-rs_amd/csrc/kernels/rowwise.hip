@@ -79,6 +79,34 @@ __device__ __forceinline__ void store_row16(T* dst, const Row<NV>& r, int D4, in
   }
 }
 
+// MX-fp8 row (gemm_mx.hip's A operand): e4m3 bytes + one E8M0 scale per 32 columns.  A
+// 32-column block is 8 consecutive float4 = 8 consecutive lanes of one slot i; D % 32 == 0,
+// so a block is wholly inside or outside the row.
+template <int NV>
+__device__ __forceinline__ void store_row_mx(uint8_t* q, uint8_t* qs, const Row<NV>& r, int D4, int lane) {
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const float4 v = r.v[i];
+    float amax = fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w)));
+    amax = fmaxf(amax, __shfl_xor(amax, 1, 64));
+    amax = fmaxf(amax, __shfl_xor(amax, 2, 64));
+    amax = fmaxf(amax, __shfl_xor(amax, 4, 64));
+    if (in_row<NV>(i, lane, D4)) {
+      const int e = mx_exp(amax);
+      const int c = i * 64 + lane;
+      ((uint32_t*)q)[c] = mx_pack4(v.x, v.y, v.z, v.w, mx_inv(e));
+      if ((lane & 7) == 0) qs[c >> 3] = (uint8_t)(e + 127);
+    }
+  }
+}
+
+// LayerNorm output: 16-bit row, or MX-fp8 (out = e4m3 bytes) when qs != nullptr.
+template <typename T, int NV>
+__device__ __forceinline__ void store_ln_out(T* out, uint8_t* qs, long row, int D, const Row<NV>& r, int lane) {
+  if (qs != nullptr) store_row_mx((uint8_t*)out + row * D, qs + row * (D >> 5), r, D >> 2, lane);
+  else store_row16(out + row * D, r, D >> 2, lane);
+}
+
 template <int NV>
 __device__ __forceinline__ void store_row32(float* dst, const Row<NV>& r, int D4, int lane) {
 #pragma unroll
@@ -102,7 +130,8 @@ __device__ __forceinline__ void add_row(Row<NV>& r, const Row<NV>& a) {
 template <typename T, int NV>
 __global__ __launch_bounds__(256) void ln_rows_kernel(float* __restrict__ x, const float* __restrict__ slab,
                                                       const float* w, const float* b, float eps,
-                                                      T* __restrict__ out, int rows, int D) {
+                                                      T* __restrict__ out, uint8_t* __restrict__ qs, int rows,
+                                                      int D) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= rows) return;
   const int D4 = D >> 2;
@@ -117,7 +146,7 @@ __global__ __launch_bounds__(256) void ln_rows_kernel(float* __restrict__ x, con
     store_row32(x + (long)row * D, r, D4, lane);
   }
   layer_norm_regs(r, o, g, bb, eps, D, lane);
-  store_row16(out + (long)row * D, o, D4, lane);
+  store_ln_out(out, qs, row, D, o, lane);
 }
 
 template <typename T, int NV>
@@ -125,7 +154,7 @@ __global__ __launch_bounds__(256) void vision_embed_ln_kernel(float* __restrict_
                                                               const float* pos, const float* lnpre_w,
                                                               const float* lnpre_b, const float* ln1_w,
                                                               const float* ln1_b, float eps, T* __restrict__ h,
-                                                              int rows, int tokens, int D) {
+                                                              uint8_t* __restrict__ qs, int rows, int tokens, int D) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= rows) return;
   const int D4 = D >> 2;
@@ -146,15 +175,15 @@ __global__ __launch_bounds__(256) void vision_embed_ln_kernel(float* __restrict_
   layer_norm_regs(r, y, g0, b0, eps, D, lane);
   store_row32(x + (long)row * D, y, D4, lane);
   layer_norm_regs(y, z, g1, b1, eps, D, lane);
-  store_row16(h + (long)row * D, z, D4, lane);
+  store_ln_out(h, qs, row, D, z, lane);
 }
 
 template <typename T, int NV>
 __global__ __launch_bounds__(256) void text_embed_ln_kernel(const int64_t* __restrict__ ids, const float* tok,
                                                             const float* pos, const float* ln1_w,
                                                             const float* ln1_b, float eps, float* __restrict__ x,
-                                                            T* __restrict__ h, int rows, int Tctx, int D,
-                                                            int vocab) {
+                                                            T* __restrict__ h, uint8_t* __restrict__ qs, int rows,
+                                                            int Tctx, int D, int vocab) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= rows) return;
   const int D4 = D >> 2;
@@ -168,7 +197,7 @@ __global__ __launch_bounds__(256) void text_embed_ln_kernel(const int64_t* __res
   add_row(e, p);
   store_row32(x + (long)row * D, e, D4, lane);
   layer_norm_regs(e, y, g, bb, eps, D, lane);
-  store_row16(h + (long)row * D, y, D4, lane);
+  store_ln_out(h, qs, row, D, y, lane);
 }
 
 template <typename T, int NV>
@@ -246,48 +275,49 @@ inline dim3 rows_grid(int rows) { return dim3((rows + 3) / 4); }
   } while (0)
 
 hipError_t launch_ln_rows(DType dt, const float* x, const float* w, const float* b, float eps, void* out16,
-                          int rows, int D, hipStream_t s) {
-  return launch_ln_rows_add(dt, const_cast<float*>(x), nullptr, w, b, eps, out16, rows, D, s);
+                          int rows, int D, hipStream_t s, uint8_t* qs) {
+  return launch_ln_rows_add(dt, const_cast<float*>(x), nullptr, w, b, eps, out16, rows, D, s, qs);
 }
 
 // (16-bit output pointers are passed as void*: the kernel parameter is T*)
 hipError_t launch_ln_rows_add(DType dt, float* x, const float* slab, const float* w, const float* b, float eps,
-                              void* out16, int rows, int D, hipStream_t s) {
-  if (D % 4 || D > 256 * MAXV || D <= 0) return hipErrorInvalidValue;
+                              void* out16, int rows, int D, hipStream_t s, uint8_t* qs) {
+  if (D % 4 || D > 256 * MAXV || D <= 0 || (qs != nullptr && D % 32)) return hipErrorInvalidValue;
   if (dt == DT_BF16) {
-    CLIPGPU_ROW_LAUNCH(ln_rows_kernel, __bf16, rows_grid(rows), D, x, slab, w, b, eps, (__bf16*)out16, rows, D);
+    CLIPGPU_ROW_LAUNCH(ln_rows_kernel, __bf16, rows_grid(rows), D, x, slab, w, b, eps, (__bf16*)out16, qs, rows, D);
   } else {
-    CLIPGPU_ROW_LAUNCH(ln_rows_kernel, _Float16, rows_grid(rows), D, x, slab, w, b, eps, (_Float16*)out16, rows, D);
+    CLIPGPU_ROW_LAUNCH(ln_rows_kernel, _Float16, rows_grid(rows), D, x, slab, w, b, eps, (_Float16*)out16, qs, rows,
+                       D);
   }
   return hipGetLastError();
 }
 
 hipError_t launch_vision_embed_ln(DType dt, float* x, const float* cls, const float* pos, const float* lnpre_w,
                                   const float* lnpre_b, const float* ln1_w, const float* ln1_b, float eps,
-                                  void* h, int B, int tokens, int D, hipStream_t s) {
-  if (D % 4 || D > 256 * MAXV || D <= 0) return hipErrorInvalidValue;
+                                  void* h, int B, int tokens, int D, hipStream_t s, uint8_t* qs) {
+  if (D % 4 || D > 256 * MAXV || D <= 0 || (qs != nullptr && D % 32)) return hipErrorInvalidValue;
   const int rows = B * tokens;
   if (dt == DT_BF16) {
     CLIPGPU_ROW_LAUNCH(vision_embed_ln_kernel, __bf16, rows_grid(rows), D, x, cls, pos, lnpre_w, lnpre_b, ln1_w, ln1_b, eps,
-                       (__bf16*)h, rows, tokens, D);
+                       (__bf16*)h, qs, rows, tokens, D);
   } else {
     CLIPGPU_ROW_LAUNCH(vision_embed_ln_kernel, _Float16, rows_grid(rows), D, x, cls, pos, lnpre_w, lnpre_b, ln1_w, ln1_b, eps,
-                       (_Float16*)h, rows, tokens, D);
+                       (_Float16*)h, qs, rows, tokens, D);
   }
   return hipGetLastError();
 }
 
 hipError_t launch_text_embed_ln(DType dt, const int64_t* ids, const float* tok, const float* pos,
                                 const float* ln1_w, const float* ln1_b, float eps, float* x, void* h, int B,
-                                int T, int D, int vocab, hipStream_t s) {
-  if (D % 4 || D > 256 * MAXV || D <= 0) return hipErrorInvalidValue;
+                                int T, int D, int vocab, hipStream_t s, uint8_t* qs) {
+  if (D % 4 || D > 256 * MAXV || D <= 0 || (qs != nullptr && D % 32)) return hipErrorInvalidValue;
   const int rows = B * T;
   if (dt == DT_BF16) {
     CLIPGPU_ROW_LAUNCH(text_embed_ln_kernel, __bf16, rows_grid(rows), D, ids, tok, pos, ln1_w, ln1_b, eps, x, (__bf16*)h,
-                       rows, T, D, vocab);
+                       qs, rows, T, D, vocab);
   } else {
     CLIPGPU_ROW_LAUNCH(text_embed_ln_kernel, _Float16, rows_grid(rows), D, ids, tok, pos, ln1_w, ln1_b, eps, x, (_Float16*)h,
-                       rows, T, D, vocab);
+                       qs, rows, T, D, vocab);
   }
   return hipGetLastError();
 }

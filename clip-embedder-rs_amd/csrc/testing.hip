@@ -265,6 +265,111 @@ int clipgpu_test_gemm_bench(int dtype, int epi, int act, int64_t M, int64_t N, i
   });
 }
 
+int clipgpu_test_quant_rows(int64_t rows, int64_t cols, const float* in, uint8_t* q, uint8_t* qs) {
+  return guarded([&]() {
+    if (rows <= 0 || cols <= 0 || cols % 32) throw ClipErr(CLIPGPU_ERR_INVALID, "bad quant shape (cols % 32 == 0)");
+    DevBuf dx(rows * cols * 4), dq(rows * cols), ds(rows * cols / 32);
+    up(dx.p, in, rows * cols * 4);
+    TCHECK(launch_quant_rows(-1, dx.p, cols, dq.as<uint8_t>(), cols, ds.as<uint8_t>(), cols / 32, (int)rows, (int)cols,
+                             nullptr));
+    TCHECK(hipDeviceSynchronize());
+    down(q, dq.p, rows * cols);
+    down(qs, ds.p, rows * cols / 32);
+  });
+}
+
+int clipgpu_test_layernorm_mx(int64_t rows, int64_t D, float eps, const float* x, const float* w, const float* b,
+                              uint8_t* q, uint8_t* qs) {
+  return guarded([&]() {
+    if (rows <= 0 || D <= 0 || D % 32) throw ClipErr(CLIPGPU_ERR_INVALID, "bad LN shape (D % 32 == 0)");
+    DevBuf dx(rows * D * 4), dw(D * 4), db(D * 4), dq(rows * D), ds(rows * D / 32);
+    up(dx.p, x, rows * D * 4);
+    up(dw.p, w, D * 4);
+    up(db.p, b, D * 4);
+    TCHECK(launch_ln_rows(DT_BF16, dx.as<float>(), dw.as<float>(), db.as<float>(), eps, dq.p, (int)rows, (int)D,
+                          nullptr, ds.as<uint8_t>()));
+    TCHECK(hipDeviceSynchronize());
+    down(q, dq.p, rows * D);
+    down(qs, ds.p, rows * D / 32);
+  });
+}
+
+int clipgpu_test_gemm_mx(int dtype, int mode, int act, int64_t M, int64_t N, int64_t K, const uint8_t* Aq,
+                         const uint8_t* As, const uint8_t* Wq, const uint8_t* Ws, const float* bias, const float* resid,
+                         float* out, uint8_t* outq, uint8_t* outs) {
+  return guarded([&]() {
+    const DType dt = dt_of(dtype);
+    if (M <= 0 || N <= 0 || K <= 0 || K % 128 || N % 32 || mode < 0 || mode > 3)
+      throw ClipErr(CLIPGPU_ERR_INVALID, "bad MX GEMM shape (K % 128 == 0, N % 32 == 0)");
+    DevBuf dA(M * K), dAs(M * K / 32), dW(N * K), dWs(N * K / 32), dB(N * 4), dO(M * N * 4), dOs(M * N / 32);
+    up(dA.p, Aq, M * K);
+    up(dAs.p, As, M * K / 32);
+    up(dW.p, Wq, N * K);
+    up(dWs.p, Ws, N * K / 32);
+    if (bias) up(dB.p, bias, N * 4);
+    MxGemmParams g{};
+    g.A = dA.as<uint8_t>(); g.lda = K; g.As = dAs.as<uint8_t>(); g.ldas = K / 32;
+    g.W = dW.as<uint8_t>(); g.ldw = K; g.Ws = dWs.as<uint8_t>(); g.ldws = K / 32;
+    g.bias = bias ? dB.as<float>() : nullptr;
+    g.out = dO.p; g.M = (int)M; g.N = (int)N; g.K = (int)K; g.tile = tile_override();
+    static const int epis[4] = {EPI_STORE16, EPI_RESID, EPI_STORE32, EPI_STOREQ};
+    const int epi = epis[mode];
+    g.ldo = N;
+    if (epi == EPI_STOREQ) {
+      g.outs = dOs.as<uint8_t>();
+      g.ldos = N / 32;
+    }
+    if (epi == EPI_RESID && resid) up(dO.p, resid, M * N * 4);
+    TCHECK(launch_gemm_mx(dt, epi, (epi == EPI_STORE16 || epi == EPI_STOREQ) ? act : 0, g, nullptr));
+    TCHECK(hipDeviceSynchronize());
+    if (epi == EPI_STORE16) down16(dt, out, dO.p, M * N);
+    else if (epi == EPI_STOREQ) {
+      down(outq, dO.p, M * N);
+      down(outs, dOs.p, M * N / 32);
+    } else down(out, dO.p, M * N * 4);
+  });
+}
+
+int clipgpu_test_gemm_mx_bench(int epi, int act, int64_t M, int64_t N, int64_t K, int tile, int iters,
+                               double* us_per_launch) {
+  return guarded([&]() {
+    if (M <= 0 || N <= 0 || K <= 0 || K % 128 || N % 32 || iters <= 0 || !us_per_launch || epi < 0 || epi > 3)
+      throw ClipErr(CLIPGPU_ERR_INVALID, "bad MX GEMM bench arguments");
+    DevBuf fA(M * K * 4), fW(N * K * 4), dA(M * K), dAs(M * K / 32), dW(N * K), dWs(N * K / 32), dB(N * 4),
+        dO(M * N * 4), dOs(M * N / 32);
+    hipLaunchKernelGGL(fill_random, dim3(2048), dim3(256), 0, nullptr, fA.as<float>(), (long)(M * K), 1u);
+    hipLaunchKernelGGL(fill_random, dim3(2048), dim3(256), 0, nullptr, fW.as<float>(), (long)(N * K), 2u);
+    hipLaunchKernelGGL(fill_random, dim3(64), dim3(256), 0, nullptr, dB.as<float>(), (long)N, 3u);
+    TCHECK(launch_quant_rows(-1, fA.p, K, dA.as<uint8_t>(), K, dAs.as<uint8_t>(), K / 32, (int)M, (int)K, nullptr));
+    TCHECK(launch_quant_rows(-1, fW.p, K, dW.as<uint8_t>(), K, dWs.as<uint8_t>(), K / 32, (int)N, (int)K, nullptr));
+    TCHECK(hipDeviceSynchronize());
+    MxGemmParams g{};
+    g.A = dA.as<uint8_t>(); g.lda = K; g.As = dAs.as<uint8_t>(); g.ldas = K / 32;
+    g.W = dW.as<uint8_t>(); g.ldw = K; g.Ws = dWs.as<uint8_t>(); g.ldws = K / 32;
+    g.bias = dB.as<float>(); g.out = dO.p; g.ldo = N; g.M = (int)M; g.N = (int)N; g.K = (int)K; g.tile = tile;
+    static const int epis[4] = {EPI_STORE16, EPI_RESID, EPI_STORE32, EPI_STOREQ};
+    const int e = epis[epi];
+    if (e == EPI_STOREQ) {
+      g.outs = dOs.as<uint8_t>();
+      g.ldos = N / 32;
+    }
+    const int a = (e == EPI_STORE16 || e == EPI_STOREQ) ? act : 0;
+    for (int i = 0; i < 3; ++i) TCHECK(launch_gemm_mx(DT_BF16, e, a, g, nullptr));
+    hipEvent_t ea, eb;
+    TCHECK(hipEventCreate(&ea));
+    TCHECK(hipEventCreate(&eb));
+    TCHECK(hipEventRecord(ea, nullptr));
+    for (int i = 0; i < iters; ++i) TCHECK(launch_gemm_mx(DT_BF16, e, a, g, nullptr));
+    TCHECK(hipEventRecord(eb, nullptr));
+    TCHECK(hipEventSynchronize(eb));
+    float ms = 0.f;
+    TCHECK(hipEventElapsedTime(&ms, ea, eb));
+    (void)hipEventDestroy(ea);
+    (void)hipEventDestroy(eb);
+    *us_per_launch = (double)ms * 1000.0 / iters;
+  });
+}
+
 #ifdef CLIPGPU_GEMM_STAMPS
 // Diagnostic build only (not in the headers): one timed-after-warmup GEMM launch
 // with s_memtime stamps; out receives nblocks x 64 u64 (see gemm.hip slots).

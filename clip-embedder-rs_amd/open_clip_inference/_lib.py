@@ -19,6 +19,7 @@ TOWER_VISION = 0
 TOWER_TEXT = 1
 DTYPE_BF16 = 0
 DTYPE_F16 = 1
+DTYPE_FP8 = 2  # MX-fp8 trunk GEMMs (BASELINE configs[4] "fp8 MFMA weight path")
 
 # (name, restype, argtypes) — every symbol declared in include/clipgpu.h.
 _PROTOS = [
@@ -61,6 +62,10 @@ _PROTOS = [
     ("clipgpu_test_resize_rgb8_gpu", c_int, [POINTER(c_void_p), POINTER(c_int), POINTER(c_int), c_int64, c_int, c_char_p, c_char_p, c_void_p]),
     ("clipgpu_test_lane_reduce", c_int, [c_void_p, c_void_p]),
     ("clipgpu_test_patch_rows", c_int, [c_int, c_int, c_int64, c_int64, c_int64, c_void_p, POINTER(c_float), POINTER(c_float), c_void_p]),
+    ("clipgpu_test_quant_rows", c_int, [c_int64, c_int64, c_void_p, c_void_p, c_void_p]),
+    ("clipgpu_test_layernorm_mx", c_int, [c_int64, c_int64, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    ("clipgpu_test_gemm_mx", c_int, [c_int, c_int, c_int, c_int64, c_int64, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    ("clipgpu_test_gemm_mx_bench", c_int, [c_int, c_int, c_int64, c_int64, c_int64, c_int, c_int, POINTER(c_double)]),
 ]
 
 SYMBOLS = [p[0] for p in _PROTOS]

@@ -21,7 +21,7 @@ class Engine:
         self.devices = list(devices) if devices else [0]
         self.dtype = dtype
         self.max_batch = int(max_batch)
-        dt = {"bf16": _lib.DTYPE_BF16, "f16": _lib.DTYPE_F16, "fp16": _lib.DTYPE_F16}[dtype]
+        dt = {"bf16": _lib.DTYPE_BF16, "f16": _lib.DTYPE_F16, "fp16": _lib.DTYPE_F16, "fp8": _lib.DTYPE_FP8}[dtype]
         devs = (c_int * len(self.devices))(*self.devices)
         h = c_void_p()
         check(lib().clipgpu_create(model_dir.encode(), tower, devs, len(self.devices), dt, self.max_batch,

@@ -40,7 +40,11 @@ enum clipgpu_status {
 };
 
 enum clipgpu_tower { CLIPGPU_TOWER_VISION = 0, CLIPGPU_TOWER_TEXT = 1 };
-enum clipgpu_dtype { CLIPGPU_DTYPE_BF16 = 0, CLIPGPU_DTYPE_F16 = 1 };
+/* CLIPGPU_DTYPE_FP8: the fp8 weight path of BASELINE configs[4] -- the QKV, c_fc and c_proj
+ * GEMMs run as MX-fp8 (OCP e4m3 weights and activations, E8M0 scale per 32 K-elements,
+ * block-scaled MFMA); attention, out_proj, stems and heads run in bf16.  Needs width and MLP
+ * width % 128 == 0.  Lossy: the embeddings do not meet the bf16 path's cosine bar. */
+enum clipgpu_dtype { CLIPGPU_DTYPE_BF16 = 0, CLIPGPU_DTYPE_F16 = 1, CLIPGPU_DTYPE_FP8 = 2 };
 
 typedef struct clipgpu_engine clipgpu_engine;       /* one tower on one or more GPUs (== one OnnxSession) */
 typedef struct clipgpu_tokenizer clipgpu_tokenizer; /* CLIP BPE tokenizer (== tokenizers::Tokenizer) */

@@ -56,6 +56,27 @@ int clipgpu_test_patch_rows(int dtype, int mode, int64_t B, int64_t S, int64_t P
 int clipgpu_test_gemm_bench(int dtype, int epi, int act, int64_t M, int64_t N, int64_t K, int tile, int iters,
                             double* us_per_launch);
 
+/* MX-fp8 (OCP e4m3fn bytes + one E8M0 scale byte per 32 consecutive elements of a row; element =
+ * e4m3 * 2^(scale - 127)).  Quantizer: in[rows][cols] f32 -> q[rows][cols], qs[rows][cols/32];
+ * cols % 32 == 0. */
+int clipgpu_test_quant_rows(int64_t rows, int64_t cols, const float* in, uint8_t* q, uint8_t* qs);
+
+/* LayerNorm with the MX-fp8 output the fp8 trunk feeds its MX GEMMs (D % 32 == 0). */
+int clipgpu_test_layernorm_mx(int64_t rows, int64_t D, float eps, const float* x, const float* w, const float* b,
+                              uint8_t* q, uint8_t* qs);
+
+/* MX-fp8 GEMM on given MX operands A (Aq [M][K], As [M][K/32]) and W (Wq [N][K], Ws [N][K/32]):
+ * mode 0: act(A.W^T + bias) as 16-bit (returned as f32 in out); 1: out = resid + A.W^T + bias (f32);
+ * 2: f32 A.W^T + bias; 3: MX-fp8 of act(A.W^T + bias) into outq [M][N] / outs [M][N/32].
+ * K % 128 == 0, N % 32 == 0; CLIPGPU_TEST_TILE picks the tile (0 auto, 2 256x128, 3 128x128). */
+int clipgpu_test_gemm_mx(int dtype, int mode, int act, int64_t M, int64_t N, int64_t K, const uint8_t* Aq,
+                         const uint8_t* As, const uint8_t* Wq, const uint8_t* Ws, const float* bias,
+                         const float* resid, float* out, uint8_t* outq, uint8_t* outs);
+
+/* Device-resident MX GEMM timing (random operands quantized on the device), epi as mode above. */
+int clipgpu_test_gemm_mx_bench(int epi, int act, int64_t M, int64_t N, int64_t K, int tile, int iters,
+                               double* us_per_launch);
+
 /* Host only (no GPU): the f32 parameter `name` (open_clip state-dict name) of one tower as
  * clipgpu_create would load it from model_dir (safetensors / visual|text.onnx / synthetic);
  * n = element count. */
