@@ -396,9 +396,12 @@ hipError_t launch_mx_cfg(const MxGemmParams& p, hipStream_t s) {
   return hipGetLastError();
 }
 
+// 128x128 (two 4-wave blocks per CU) measured faster than 256x128 at every trunk shape
+// (profiles/r01_v11_mx_sweep.jsonl: 1.2-1.5 vs 1.0-1.3 PFLOP/s); the engine autotunes per site.
 int pick_mx_tile(int M, int N) {
+  (void)M;
   (void)N;
-  return M < 2048 ? MX_TILE_128x128 : MX_TILE_256x128;
+  return MX_TILE_128x128;
 }
 
 template <typename T, int EPI, int ACT>

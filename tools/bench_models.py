@@ -49,9 +49,9 @@ def timed(fn, steps, warmup):
     return (time.perf_counter() - t0) / steps
 
 
-def device_leg(name, cfg, tower, B, steps=6, warmup=2):
+def device_leg(name, cfg, tower, B, steps=6, warmup=2, dtype="bf16"):
     d = model_dir(cfg)
-    e = Engine(d, tower, [0], "bf16", B)
+    e = Engine(d, tower, [0], dtype, B)
     s = torch.cuda.current_stream()
     mc = cfg["model_cfg"]
     E = mc["embed_dim"]
@@ -67,9 +67,10 @@ def device_leg(name, cfg, tower, B, steps=6, warmup=2):
         fn = lambda: e.embed_tokens_device(ids.data_ptr(), B, out.data_ptr(), s.cuda_stream)  # noqa: E731
     dt = timed(fn, steps, warmup)
     rate = B / dt
-    print(json.dumps({"measure": name, "batch_per_gpu": B, "units_per_s": round(rate, 1),
-                      "ms_per_step": round(dt * 1e3, 3), "model_tflops": round(rate * GFLOP[name] / 1e3, 1),
-                      "frac_of_2500": round(rate * GFLOP[name] / 1e3 / 2500, 4), "input": "device-resident"}),
+    gf = GFLOP[name.replace("_fp8", "")]
+    print(json.dumps({"measure": name, "dtype": dtype, "batch_per_gpu": B, "units_per_s": round(rate, 1),
+                      "ms_per_step": round(dt * 1e3, 3), "model_tflops": round(rate * gf / 1e3, 1),
+                      "frac_of_2500": round(rate * gf / 1e3 / 2500, 4), "input": "device-resident"}),
           flush=True)
     e.close()
 
@@ -178,3 +179,10 @@ if __name__ == "__main__":
     if "h14" in which:
         device_leg("h14_vision", VIT_H_14_378_CFG, 0, 64)
         device_leg("h14_text", VIT_H_14_378_CFG, 1, 64)
+    if "h14fp8" in which:  # configs[4]'s fp8 MFMA weight path (MX-fp8 trunk GEMMs)
+        device_leg("h14_vision_fp8", VIT_H_14_378_CFG, 0, 64, dtype="fp8")
+        device_leg("h14_text_fp8", VIT_H_14_378_CFG, 1, 64, dtype="fp8")
+    if "so400mfp8" in which:
+        device_leg("so400m_vision_fp8", SO400M_16_SIGLIP2_384_CFG, 0, 128, dtype="fp8")
+    if "b32fp8" in which:
+        device_leg("b32_vision_fp8", VIT_B_32_CFG, 0, 256, dtype="fp8")
