@@ -62,16 +62,18 @@ __device__ __forceinline__ f32x16 mfma_mx(const v4i (&w)[2], const v4i (&a)[2], 
 }
 
 template <typename T, int BM, int BN, int WGM, int WGN, int EPI, int ACT>
-__global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_mx_kernel(MxGemmParams p) {
+__global__ __launch_bounds__(WGM* WGN * 64, 2)
+void gemm_mx_kernel(MxGemmParams p) {
   typedef typename Vec8<T>::type V8;
   constexpr int NW = WGM * WGN;
   constexpr int A_BYTES = BM * KB, B_BYTES = BN * KB, S_OFF = A_BYTES + B_BYTES;
   constexpr int STAGE = S_OFF + (BM + BN) * 4;
   constexpr int A_INSTR = BM / 8 / NW, B_INSTR = BN / 8 / NW;
-  constexpr int NSC = (BM + BN) / 64;     // scale pieces (64 rows each): waves 0 .. NSC-1
-  constexpr int NP = A_INSTR + B_INSTR + 1;
+  constexpr int NSC = (BM + BN) / 64;     // scale pieces (64 rows each): piece w + NW*j on wave w
+  constexpr int SPW = (NSC + NW - 1) / NW;
+  constexpr int NP = A_INSTR + B_INSTR + SPW;
   constexpr int TM = BM / WGM, TN = BN / WGN, MI = TM / 32, NI = TN / 32;
-  static_assert(NSC <= NW && A_INSTR >= 1 && B_INSTR >= 1 && MI >= 1 && NI >= 1 && BN <= 256, "bad tile");
+  static_assert(A_INSTR >= 1 && B_INSTR >= 1 && MI >= 1 && NI >= 1 && BN <= 256, "bad tile");
   static_assert(STAGE % 16 == 0, "stage alignment");
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + 2048];
 
@@ -103,10 +105,12 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_mx_kernel(MxGemmParams 
   // ---- LDS-DMA cursor ----------------------------------------------------------
   // 32-bit byte offsets from the kernel-argument bases (the DMA takes SGPR base + VGPR
   // offset; the host checks every operand fits in 2^31 bytes)
-  uint32_t woff[B_INSTR], aoff[A_INSTR], soff = 0;
+  uint32_t woff[B_INSTR], aoff[A_INSTR], soff[SPW];
   const char* const Wb = (const char*)p.W;
   const char* const Ab = (const char*)p.A;
-  const char* const Sb = wave < BM / 64 ? (const char*)p.As : (const char*)p.Ws;  // wave-uniform
+  auto sbase = [&](int j) {  // wave-uniform: piece wave + NW*j stages A scales (< BM/64) or W scales
+    return wave + NW * j < BM / 64 ? (const char*)p.As : (const char*)p.Ws;
+  };
   auto set_tile = [&](int m0, int n0) {
 #pragma unroll
     for (int i = 0; i < B_INSTR; ++i) {
@@ -121,11 +125,16 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_mx_kernel(MxGemmParams 
       const int c = (lane & 7) ^ ((r >> 1) & 7);
       aoff[i] = (uint32_t)min(m0 + r, p.M - 1) * (uint32_t)p.lda + (uint32_t)(c * 16);
     }
-    if (wave < BM / 64) {
-      soff = (uint32_t)min(m0 + wave * 64 + lane, p.M - 1) * (uint32_t)p.ldas;
-    } else if (wave < NSC) {
-      const int r = (wave - BM / 64) * 64 + lane;
-      soff = (uint32_t)min(n0 + (r & ~31) + wperm(r & 31), p.N - 1) * (uint32_t)p.ldws;
+#pragma unroll
+    for (int j = 0; j < SPW; ++j) {
+      const int pc = wave + NW * j;
+      soff[j] = 0;
+      if (pc < BM / 64) {
+        soff[j] = (uint32_t)min(m0 + pc * 64 + lane, p.M - 1) * (uint32_t)p.ldas;
+      } else if (pc < NSC) {
+        const int r = (pc - BM / 64) * 64 + lane;
+        soff[j] = (uint32_t)min(n0 + (r & ~31) + wperm(r & 31), p.N - 1) * (uint32_t)p.ldws;
+      }
     }
   };
   int d_g = 0, d_kt = 0, d_t = t_first, d_n0 = 0, d_ti = 0;
@@ -144,7 +153,8 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_mx_kernel(MxGemmParams 
       constexpr int i = j - B_INSTR;
       glds16(Ab + (size_t)d_kt * KB + aoff[i], st + (wave * A_INSTR + i) * 1024);
     } else {
-      if (wave < NSC) glds4(Sb + (size_t)d_kt * 4 + soff, st + S_OFF + wave * 256);
+      constexpr int jj = j - B_INSTR - A_INSTR;
+      if (wave + NW * jj < NSC) glds4(sbase(jj) + (size_t)d_kt * 4 + soff[jj], st + S_OFF + (wave + NW * jj) * 256);
     }
   };
   auto dma_bias = [&]() {
