@@ -131,7 +131,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-text", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--dtype", default="bf16")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "f16", "fp8"])
+    ap.add_argument("--no-fp8", action="store_true", help="skip the fp8 side measurement")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -182,7 +183,12 @@ def main():
     _lib.check(_lib.lib().clipgpu_test_engine_tiles(ve._h, tiles))
     tile_names = {0: "heuristic", 1: "128x128", 2: "256x128", 3: "256x256", 4: "128x128pipe", 5: "128x64pipe",
                   6: "64x128pipe"}
-    gemm_tiles = dict(zip(["qkv", "out_proj", "c_fc", "c_proj"], [tile_names[t] for t in tiles]))
+    mx_names = {0: "heuristic", 2: "mx256x128", 3: "mx128x128"}  # fp8 engines: QKV / c_fc / c_proj sites
+    fp8 = args.dtype == "fp8"
+    gemm_tiles = {site: (mx_names if fp8 and site != "out_proj" else tile_names)[t]
+                  for site, t in zip(["qkv", "out_proj", "c_fc", "c_proj"], tiles)}
+    # the dominant kernel's peak: the dense bf16 MFMA rate, or the block-scaled MX-fp8 rate (2x)
+    peak = PEAK_BF16_TFLOPS * (2 if fp8 else 1)
 
     dt, _ = timed(vision_step, args.steps, args.warmup)
     images = world * B_VISION * args.steps
@@ -200,6 +206,26 @@ def main():
     fc_avg_s = (fc_ms / 1e3) / max(fc_n, 1)
     achieved = fc_flops / fc_avg_s / 1e12
     whole_tflops = vit_flops(B_VISION) * args.steps / dt / 1e12 / 1.0
+
+    # The fp8 (MX) engine of the same workload beside the bf16 value (BASELINE configs[4]'s
+    # weight path on the bench model): throughput and the cosine of its embeddings to the
+    # bf16 engine's on the same input (the fp8 path is lossy).  Not `value`.
+    fp8_info = None
+    if world == 1 and not fp8 and not args.no_fp8:
+        fe = Engine(mdir, _lib.TOWER_VISION, [local], "fp8", B_VISION)
+        fout = torch.empty_like(out)
+
+        def fp8_step():
+            fe.embed_pixels_device(px.data_ptr(), B_VISION, fout.data_ptr(), stream.cuda_stream)
+        fdt, _ = timed(fp8_step, args.steps, args.warmup)
+        vision_step()
+        torch.cuda.synchronize()
+        cos = torch.nn.functional.cosine_similarity(fout, out, dim=1)
+        fp8_info = {"value": round(B_VISION * args.steps / fdt, 1), "unit": "images/s",
+                    "ms_per_step": round(fdt * 1e3 / args.steps, 3),
+                    "cos_vs_bf16_min": round(float(cos.min()), 6), "cos_vs_bf16_mean": round(float(cos.mean()), 6),
+                    "note": "MX-fp8 QKV/c_fc/c_proj (e4m3 + E8M0 per 32, v_mfma_scale_f32_32x32x64_f8f6f4)"}
+        fe.close()
 
     text = None
     if not args.no_text:
@@ -242,13 +268,14 @@ def main():
                        "global_batch": world * B_VISION, "seq_len": 50,
                        "parallelism": f"dp{world}, {os.environ.get('CLIPGPU_LANES', '2')} concurrent sub-batch lanes/GPU" + (" + RCCL all-gather of [B,512] embeddings" if world > 1 else "")},
             "roofline": {"bound": "mfma", "kernel": f"c_fc GEMM ({int(fc_rows_per_launch)}x3072x768, +QuickGELU, tile {gemm_tiles['c_fc']})",
-                         "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": load_traffic(),
+                         "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
+                         "frac": round(achieved / peak, 4), "traffic": load_traffic() if not fp8 else None,
                          "launches_timed": fc_n, "avg_launch_us": round(fc_avg_s * 1e6, 2)},
             "gemm_tiles": gemm_tiles,
             "gemm_tiles_env": ",".join(str(t) for t in tiles),
             "whole_forward_mfma_tflops_per_gpu": round(whole_tflops, 1),
             "text": text,
+            "fp8": fp8_info,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
