@@ -6,16 +6,18 @@
 // exported by pull_onnx.py:53-68: softmax(Q K^T / sqrt(d) [+ causal mask]) V,
 // per (sequence, head), head_dim d = 64.
 //
-// One 256-thread workgroup per (sequence, head).  K (row-major, XOR-swizzled)
-// and V (row-major, 160-byte rows) for the whole sequence sit in LDS; each wave
-// owns 16-query tiles and computes the transposed products of flash_attn_kernel
+// One workgroup per (sequence, head), one wave per 16-query tile (up to 8; more
+// tiles are walked by 4 waves), so N = 77 runs 5 waves instead of 4 waves with one
+// taking two tiles.  K (row-major, XOR-swizzled) and V (row-major, 160-byte rows) for
+// the whole sequence sit in LDS; each wave computes the transposed products of flash_attn_kernel
 // below: S^T = K Q^T (16x16x32 MFMA; lane (fr, fq) holds query fr's scores for
 // keys t*16 + 4fq + j, so the row max / sum are in-lane plus two xor-shuffles),
 // O^T = V^T P^T with V^T read by ds_read_b64_tr_b16 and P^T taken straight from
 // the S^T accumulators (a key order both operands share), 1/rowsum in the
 // epilogue, 8-byte stores of 4 head dims.  Padded keys (>= N) and, for text,
 // keys above the diagonal are masked to -inf (open_clip build_causal_mask:
-// triu(-inf, 1)).
+// triu(-inf, 1)); causal key tiles wholly above the query tile's diagonal are skipped
+// (their probabilities are exactly 0).
 #include <type_traits>
 
 #include "common.hpp"
@@ -37,7 +39,7 @@ struct TrRead {
 };
 
 template <typename T, int NKT>
-__global__ __launch_bounds__(256) void attn_kernel(const T* __restrict__ qkv, T* __restrict__ out,
+__global__ __launch_bounds__(512) void attn_kernel(const T* __restrict__ qkv, T* __restrict__ out,
                                                    int N, int H, int D, int causal) {
   typedef typename Vec8<T>::type V8;
   typedef typename Vec4<T>::type V4;
@@ -49,13 +51,13 @@ __global__ __launch_bounds__(256) void attn_kernel(const T* __restrict__ qkv, T*
   char* const sK = smem;
   char* const sV = smem + K_BYTES;
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nwaves = blockDim.x >> 6;
   const int b = blockIdx.x / H, h = blockIdx.x % H;
   const long ld = 3L * D;
   const T* base = qkv + (long)b * N * ld + h * 64;
 
   // K rows (swizzled) and V rows into LDS; zero the padded keys.
-  for (int q = tid; q < NKP * 8; q += 256) {
+  for (int q = tid; q < NKP * 8; q += blockDim.x) {
     const int r = q >> 3, c = q & 7;
     V8 kv{}, vv{};
     if (r < N) {
@@ -71,7 +73,9 @@ __global__ __launch_bounds__(256) void attn_kernel(const T* __restrict__ qkv, T*
   const float scale_log2 = 0.125f * 1.4426950408889634f;  // 1/sqrt(64), base-2 softmax
   const int nqt = (N + 15) >> 4;
 
-  for (int qt = wave; qt < nqt; qt += 4) {
+  for (int qt = wave; qt < nqt; qt += nwaves) {
+    // causal: keys past this tile's last query (qt*16 + 15) have probability 0
+    const int kt_end = causal ? qt + 1 : NKT;
     const int q = qt * 16 + fr;
     const int qrow_l = min(q, N - 1);
     V8 qf[2];
@@ -83,6 +87,7 @@ __global__ __launch_bounds__(256) void attn_kernel(const T* __restrict__ qkv, T*
 #pragma unroll
     for (int t = 0; t < NKT; ++t) {
       s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (t >= kt_end) continue;  // (masked to -inf below)
       const int r = t * 16 + fr;
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
@@ -119,6 +124,7 @@ __global__ __launch_bounds__(256) void attn_kernel(const T* __restrict__ qkv, T*
     for (int ni = 0; ni < 4; ++ni) o[ni] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < NKP / 32; ++ks) {
+      if (2 * ks >= kt_end) continue;  // all 32 keys of the step have P = 0
       V8 pf;
 #pragma unroll
       for (int e = 0; e < 8; ++e) pf[e] = (T)s[2 * ks + (e >> 2)][e & 3];
@@ -152,7 +158,9 @@ __global__ __launch_bounds__(256) void attn_kernel(const T* __restrict__ qkv, T*
 
 template <typename T, int NKT>
 hipError_t launch_nkt(const void* qkv, void* out, int B, int N, int H, int D, int causal, hipStream_t s) {
-  hipLaunchKernelGGL((attn_kernel<T, NKT>), dim3(B * H), dim3(256), 0, s, (const T*)qkv, (T*)out, N, H,
+  const int nqt = (N + 15) / 16;
+  const int waves = nqt <= 8 ? nqt : 4;
+  hipLaunchKernelGGL((attn_kernel<T, NKT>), dim3(B * H), dim3(64 * waves), 0, s, (const T*)qkv, (T*)out, N, H,
                      D, causal);
   return hipGetLastError();
 }
