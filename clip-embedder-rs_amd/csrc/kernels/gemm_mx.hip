@@ -267,14 +267,17 @@ void gemm_mx_kernel(MxGemmParams p) {
   };
   auto phase1 = [&](bool next, uint32_t nbuf) {
     const bool dma = d_g < total;
-    if (next) read_b(b0, nbuf, 0);
+    // the next step's kk0 fragments are read unconditionally (on a tile's last step from
+    // the other buffer, unused): a conditional read made the compiler keep a second copy
+    // of the fragment registers across the branch
+    read_b(b0, nbuf, 0);
     if (dma) dma_bias();
     static_for<MI>([&](auto mi) {
 #pragma unroll
       for (int ni = 0; ni < NI; ++ni)
         acc[ni][mi] = mfma_mx<2>(b1[ni], a1[mi], acc[ni][mi], (int)sb[ni], (int)sa[mi]);
       __builtin_amdgcn_sched_barrier(0);
-      if (next) {
+      {
         read_a(a0[mi], nbuf, 0, mi);
         ds_read_b32<(int)mi * 128>(sa[mi], nbuf + offSA);
         if constexpr ((int)mi + 1 == MI) read_sb(nbuf);
@@ -287,7 +290,8 @@ void gemm_mx_kernel(MxGemmParams p) {
       __builtin_amdgcn_sched_barrier(0);
     });
     dma_advance();
-    if (next) wait_frags(a0, b0, true);
+    wait_frags(a0, b0, true);
+    (void)next;
   };
 
   // ---- epilogue: lane owns row wm + mi*32 + r32, columns wn + ni*32 + 16h .. +15 ------
