@@ -546,7 +546,11 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_pipe_kernel(GemmParams 
   };
   auto phase1 = [&](bool next, uint32_t nbuf) {
     const bool dma = d_g < total;
-    if (next) read_b(b0, nbuf + offB[0]);
+    // the next step's kk0 fragments are read unconditionally (on a tile's last step from
+    // the other buffer, unused): a conditional read made the compiler keep a second copy
+    // of the fragment registers across the branch
+    (void)next;
+    read_b(b0, nbuf + offB[0]);
     if (dma) {
       dma_bias();
       if constexpr (!SPREAD) static_for<NP>([&](auto j) { dma_piece(j); });
@@ -555,7 +559,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_pipe_kernel(GemmParams 
 #pragma unroll
       for (int ni = 0; ni < NI; ++ni) acc[ni][mi] = mfma_16x16x32(b1[ni], a1[mi], acc[ni][mi]);
       __builtin_amdgcn_sched_barrier(0);
-      if (next) ds_read_b128<(int)mi * 2048>(a0[mi], nbuf + offA[0]);
+      ds_read_b128<(int)mi * 2048>(a0[mi], nbuf + offA[0]);
       if constexpr (SPREAD) {
         static_for<NP>([&](auto j) {
           if constexpr (((int)j * MI) / NP == (int)mi) {
@@ -566,7 +570,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_pipe_kernel(GemmParams 
       __builtin_amdgcn_sched_barrier(0);
     });
     dma_advance();
-    if (next) lgkm_wait_all(a0, b0);
+    lgkm_wait_all(a0, b0);
   };
 
   // ---- epilogue: lane owns row wm+mi*16+fr, columns nc .. nc+4*NI-1 ------------
