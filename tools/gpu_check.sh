@@ -36,7 +36,7 @@ for s in $STEPS; do
       export CLIPGPU_GEMM_TILES=$(python3 -c "import json;print([json.loads(l) for l in open('gpurun_out/bench.log') if l.startswith('{')][-1]['gemm_tiles_env'])") || exit 1
       for C in FETCH_SIZE WRITE_SIZE; do
         run pmc_$C 600 rocprofv3 --pmc $C --output-format csv -d gpurun_out/pmc_bench/$C -o run -- \
-            python3 bench.py --steps 3 --warmup 1 --no-text --no-cpu-baseline || exit $?
+            python3 bench.py --steps 3 --warmup 1 --no-text --no-cpu-baseline --no-fp8 || exit $?
       done
       python3 tools/pmc_traffic.py gpurun_out/pmc_bench/FETCH_SIZE gpurun_out/pmc_bench/WRITE_SIZE \
           gpurun_out/pmc_c_fc.json || exit $?
