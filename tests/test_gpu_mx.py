@@ -259,3 +259,26 @@ def test_fp8_tiny_and_rejects_unsupported_width():
     cfg["model_cfg"]["vision_cfg"]["width"] = 192  # 3 heads of 64: not a multiple of 128
     with pytest.raises(L.ClipError):
         _engine(cfg, 0, "fp8", 4)
+
+
+def test_fp8_input_paths_agree():
+    """fp8 engines share the bf16 engines' stems: u8 input (normalised while staging the patch
+    rows) gives the f32 path's embeddings bit for bit, and the device-side photo resize path
+    (clipgpu_embed_images_rgb8) equals host preprocess + embed_pixels; a two-replica handle
+    shards in input order."""
+    from oracle import weights
+    from oracle.model_spec import OPENAI_MEAN, OPENAI_STD, VIT_B_32_CFG
+    from tests.helpers import normalized_pixels, specs
+    from open_clip_inference.engine import Engine, preprocess_batch_rgb8
+    from tests.helpers import make_model_dir
+    v, _ = specs(VIT_B_32_CFG)
+    u8 = weights.synth_images_u8(12, 5, v.image_size)
+    e = _engine(VIT_B_32_CFG, 0, "fp8", 8)
+    assert np.array_equal(e.embed_u8(u8, OPENAI_MEAN, OPENAI_STD),
+                          e.embed_pixels(normalized_pixels(u8, OPENAI_MEAN, OPENAI_STD)))
+    rng = np.random.default_rng(3)
+    ims = [rng.integers(0, 256, (h, w, 3), dtype=np.uint8) for h, w in ((480, 640), (300, 200), (224, 224))]
+    host = e.embed_pixels(preprocess_batch_rgb8(ims, 224, "bicubic", "shortest", OPENAI_MEAN, OPENAI_STD))
+    assert np.array_equal(e.embed_images_rgb8(ims), host)
+    multi = Engine(make_model_dir(VIT_B_32_CFG, 1234), 0, [0, 0], "fp8", 2)
+    assert np.array_equal(multi.embed_images_rgb8(ims), host)
