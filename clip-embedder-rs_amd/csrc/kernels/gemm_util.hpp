@@ -8,6 +8,11 @@
 
 #include "kernels.hpp"
 
+// Row panels per tile-order group (tile_coords); a build-time knob for schedule experiments.
+#ifndef CLIPGPU_TILE_GROUP
+#define CLIPGPU_TILE_GROUP 8
+#endif
+
 namespace clipgpu {
 
 // hipLaunchKernelGGL, or the event-stamped ext launch when a profiler armed g_gemm_events.
@@ -62,7 +67,7 @@ __device__ __forceinline__ void vm_wait() {
 // (walk M first inside a group) so that concurrently running tiles share A and W
 // panels in L2.
 __device__ __forceinline__ void tile_coords(int t, int nTm, int nTn, int BM, int BN, int& m0, int& n0) {
-  constexpr int GROUP = 8;
+  constexpr int GROUP = CLIPGPU_TILE_GROUP;
   const int per_group = GROUP * nTn;
   const int first_m = (t / per_group) * GROUP;
   const int gsize = min(nTm - first_m, GROUP);
