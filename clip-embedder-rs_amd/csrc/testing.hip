@@ -265,6 +265,34 @@ int clipgpu_test_gemm_bench(int dtype, int epi, int act, int64_t M, int64_t N, i
   });
 }
 
+int clipgpu_test_attention_bench(int dtype, int64_t B, int64_t N, int64_t H, int64_t HD, int causal, int iters,
+                                 double* us_per_launch) {
+  return guarded([&]() {
+    const DType dt = dt_of(dtype);
+    if (B <= 0 || N <= 0 || H <= 0 || iters <= 0 || !us_per_launch)
+      throw ClipErr(CLIPGPU_ERR_INVALID, "bad attention bench arguments");
+    const int64_t D = H * HD;
+    DevBuf f(B * N * 3 * D * 4), dq(B * N * 3 * D * 2), dO(B * N * D * 2);
+    hipLaunchKernelGGL(fill_random, dim3(2048), dim3(256), 0, nullptr, f.as<float>(), (long)(B * N * 3 * D), 7u);
+    TCHECK(launch_cast_f32(dt, f.as<float>(), dq.p, (long)(B * N * 3 * D), nullptr));
+    for (int i = 0; i < 3; ++i)
+      TCHECK(launch_attention(dt, dq.p, dO.p, (int)B, (int)N, (int)H, (int)D, causal, nullptr));
+    hipEvent_t a, b;
+    TCHECK(hipEventCreate(&a));
+    TCHECK(hipEventCreate(&b));
+    TCHECK(hipEventRecord(a, nullptr));
+    for (int i = 0; i < iters; ++i)
+      TCHECK(launch_attention(dt, dq.p, dO.p, (int)B, (int)N, (int)H, (int)D, causal, nullptr));
+    TCHECK(hipEventRecord(b, nullptr));
+    TCHECK(hipEventSynchronize(b));
+    float ms = 0.f;
+    TCHECK(hipEventElapsedTime(&ms, a, b));
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    *us_per_launch = (double)ms * 1000.0 / iters;
+  });
+}
+
 int clipgpu_test_quant_rows(int64_t rows, int64_t cols, const float* in, uint8_t* q, uint8_t* qs) {
   return guarded([&]() {
     if (rows <= 0 || cols <= 0 || cols % 32) throw ClipErr(CLIPGPU_ERR_INVALID, "bad quant shape (cols % 32 == 0)");

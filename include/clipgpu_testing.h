@@ -56,6 +56,10 @@ int clipgpu_test_patch_rows(int dtype, int mode, int64_t B, int64_t S, int64_t P
 int clipgpu_test_gemm_bench(int dtype, int epi, int act, int64_t M, int64_t N, int64_t K, int tile, int iters,
                             double* us_per_launch);
 
+/* Device-resident attention timing (random 16-bit qkv): mean µs per launch_attention over `iters`. */
+int clipgpu_test_attention_bench(int dtype, int64_t B, int64_t N, int64_t H, int64_t HD, int causal, int iters,
+                                 double* us_per_launch);
+
 /* MX-fp8 (OCP e4m3fn bytes + one E8M0 scale byte per 32 consecutive elements of a row; element =
  * e4m3 * 2^(scale - 127)).  Quantizer: in[rows][cols] f32 -> q[rows][cols], qs[rows][cols/32];
  * cols % 32 == 0. */

@@ -1,0 +1,23 @@
+#!/usr/bin/env python3
+"""Attention kernels alone at the per-lane shapes of the BASELINE configs (GPU box): µs per
+launch and TFLOP/s (4*N^2*hd per (image, head); causal counted dense)."""
+import ctypes
+import json
+import os
+import sys
+
+ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+sys.path.insert(0, os.path.join(ROOT, "clip-embedder-rs_amd"))
+import torch  # noqa: F401,E402
+from open_clip_inference import _lib  # noqa: E402
+
+CASES = [("h14_vision", 32, 730, 16, 80, 0), ("so400m_vision", 64, 576, 16, 72, 0), ("h14_text", 32, 77, 16, 64, 1),
+         ("b32_vision", 128, 50, 12, 64, 0), ("b32_text", 512, 77, 8, 64, 1)]
+
+L = _lib.lib()
+us = ctypes.c_double()
+for name, B, N, H, HD, causal in CASES:
+    _lib.check(L.clipgpu_test_attention_bench(0, B, N, H, HD, causal, 20, ctypes.byref(us)))
+    fl = 4.0 * B * H * N * N * HD
+    print(json.dumps({"case": name, "B": B, "N": N, "H": H, "hd": HD, "us": round(us.value, 1),
+                      "tflops": round(fl / us.value / 1e6, 1)}), flush=True)
