@@ -87,7 +87,9 @@ int clipgpu_test_gemm_mx_bench(int epi, int act, int64_t M, int64_t N, int64_t K
 int clipgpu_test_read_weights(const char* model_dir, int tower, const char* name, float* out, int64_t n);
 
 /* GEMM tile chosen per trunk call site of an engine (0 qkv, 1 out_proj, 2 c_fc, 3 c_proj):
- * 1 128x128, 2 256x128, 3 256x256, 4 128x128 pipelined, 0 shape heuristic.  Before clipgpu_create, set
+ * 1 128x128, 2 256x128, 3 256x256, 4 128x128 pipelined, 5 128x64 pipelined, 6 64x128 pipelined,
+ * 0 shape heuristic; fp8 engines report MxTile ids at the qkv / c_fc / c_proj sites (2 256x128,
+ * 3 128x128).  Before clipgpu_create, set
  * CLIPGPU_GEMM_AUTOTUNE=0 to skip the creation-time tuning, or CLIPGPU_GEMM_TILES="q,o,f,p"
  * to pin the four sites. */
 struct clipgpu_engine;
