@@ -421,7 +421,7 @@ int pick_mx_tile(int M, int N) {
 template <typename T, int EPI, int ACT>
 hipError_t launch_mx_tile(const MxGemmParams& p, hipStream_t s) {
   switch (p.tile == MX_TILE_AUTO ? pick_mx_tile(p.M, p.N) : p.tile) {
-    case MX_TILE_256x128: return launch_mx_cfg<T, 256, 128, 2, 4, EPI, ACT>(p, s);
+    case MX_TILE_256x128: return launch_mx_cfg<T, 256, 128, 4, 2, EPI, ACT>(p, s);
     default: return launch_mx_cfg<T, 128, 128, 2, 2, EPI, ACT>(p, s);
   }
 }

@@ -152,7 +152,7 @@ enum MxTile {
   MX_TILE_AUTO = 0,
   MX_TILE_256x256 = 1,  // not built: 64x128+ per wave spills (> 256 VGPRs at 2 waves / SIMD; the 4-wave
                         // 128x128-per-wave form spills past 512 with the loop-carried fragment copies)
-  MX_TILE_256x128 = 2,  // 8 waves (128x32 each), 101 KiB LDS
+  MX_TILE_256x128 = 2,  // 8 waves (4x2, 64x64 each), 99 KiB LDS, 1 block / CU
   MX_TILE_128x128 = 3,  // 4 waves (64x64 each), 68 KiB LDS, 2 blocks / CU
   MX_TILE_LAST = MX_TILE_128x128,
 };
