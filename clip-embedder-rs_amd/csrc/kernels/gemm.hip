@@ -12,7 +12,7 @@
 //
 // One kernel template, three tile shapes (GemmTile):
 //   128x128  4 waves (2x2, 64x64 per wave), 64 KiB LDS, 2 blocks / CU
-//   256x128  8 waves (2x4, 128x32 per wave), 96 KiB LDS
+//   256x128  8 waves (4x2, 64x64 per wave), 96 KiB LDS
 //   256x256  8 waves (2x4, 128x64 per wave), 128 KiB LDS
 // Each wave issues v_mfma_f32_16x16x32_{bf16,f16} (f32 accumulate).  Operand
 // tiles (BK = 64) are staged global->LDS by global_load_lds_dwordx4 into a
@@ -397,7 +397,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
 // reads and independent of ni, so every fragment offset is an immediate.
 //
 // Configs: 128x128 (4 waves, 64x64 each, 2 blocks/CU), 256x128 (8 waves,
-// 128x32), 256x256 (8 waves, 128x64).  (A 4-wave 256x256 with 128x128 per wave
+// 4x2 of 64x64), 256x256 (8 waves, 128x64).  (A 4-wave 256x256 with 128x128 per wave
 // needs 256 accumulator AGPRs plus > 256 VGPRs and spills: not built.)
 // ---------------------------------------------------------------------------
 template <typename T, int BM, int BN, int WGM, int WGN, int EPI, int ACT>
@@ -785,7 +785,7 @@ hipError_t launch_tile(const GemmParams& p, hipStream_t s) {
     if (!pipe) return hipErrorInvalidValue;
     switch (tile) {
       case TILE_256x256: return launch_pipe<T, 256, 256, 2, 4, EPI, ACT>(p, s);
-      case TILE_256x128: return launch_pipe<T, 256, 128, 2, 4, EPI, ACT>(p, s);
+      case TILE_256x128: return launch_pipe<T, 256, 128, 4, 2, EPI, ACT>(p, s);
       case TILE_128x64_PIPE: return launch_pipe<T, 128, 64, 2, 2, EPI, ACT>(p, s);
       case TILE_64x128_PIPE: return launch_pipe<T, 64, 128, 2, 2, EPI, ACT>(p, s);
       default: return launch_pipe<T, 128, 128, 2, 2, EPI, ACT>(p, s);
@@ -794,7 +794,7 @@ hipError_t launch_tile(const GemmParams& p, hipStream_t s) {
   if (pipe) {
     switch (tile) {
       case TILE_256x256: return launch_pipe<T, 256, 256, 2, 4, EPI, ACT>(p, s);
-      case TILE_256x128: return launch_pipe<T, 256, 128, 2, 4, EPI, ACT>(p, s);
+      case TILE_256x128: return launch_pipe<T, 256, 128, 4, 2, EPI, ACT>(p, s);
       case TILE_128x128_PIPE: return launch_pipe<T, 128, 128, 2, 2, EPI, ACT>(p, s);
       case TILE_128x64_PIPE: return launch_pipe<T, 128, 64, 2, 2, EPI, ACT>(p, s);
       case TILE_64x128_PIPE: return launch_pipe<T, 64, 128, 2, 2, EPI, ACT>(p, s);

@@ -44,7 +44,7 @@ struct GemmParams {
 enum GemmTile {
   TILE_AUTO = 0,
   TILE_128x128 = 1,       // gemm_bt_kernel: 4 waves, 64 KiB LDS, 2 blocks / CU
-  TILE_256x128 = 2,       // gemm_pipe_kernel: 8 waves, 96 KiB LDS
+  TILE_256x128 = 2,       // gemm_pipe_kernel: 8 waves (4x2, 64x64 each), 96 KiB LDS
   TILE_256x256 = 3,       // gemm_pipe_kernel: 8 waves, 128 KiB LDS
   TILE_128x128_PIPE = 4,  // gemm_pipe_kernel: 4 waves, 64 KiB LDS, 2 blocks / CU
   TILE_128x64_PIPE = 5,   // gemm_pipe_kernel: 4 waves (64x32 each), 48 KiB LDS, 3 blocks / CU
