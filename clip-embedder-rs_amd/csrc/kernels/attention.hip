@@ -357,7 +357,8 @@ __global__ __launch_bounds__(256, 2) void flash_attn_kernel(const T* __restrict_
             s[qi][t][j] = e;
             sum += e;
           }
-        sum = xsum32(xsum16(sum));
+        // per-lane partial row sums (this lane's keys); the 4 lanes of a query are added
+        // once after the last tile (corr is the same in all 4: the max is reduced per tile)
         l[qi] = l[qi] * corr + sum;
         m[qi] = mn;
 #pragma unroll
@@ -401,8 +402,9 @@ __global__ __launch_bounds__(256, 2) void flash_attn_kernel(const T* __restrict_
 #pragma unroll
   for (int qi = 0; qi < 2; ++qi) {
     const int q = q0 + qi * 16 + fr;
+    const float lsum = xsum32(xsum16(l[qi]));  // all lanes (cross-lane), before the row mask
     if (q >= N) continue;
-    const float inv = 1.0f / l[qi];
+    const float inv = 1.0f / lsum;
     T* dst = out + ((long)b * N + q) * D + (long)h * HD;
 #pragma unroll
     for (int ni = 0; ni < HV / 16; ++ni) {
