@@ -48,18 +48,25 @@ MODEL_CONFIG = {"logit_scale": 100.0, "logit_bias": 0.0, "activation_function": 
                 "tokenizer_needs_lowercase": False, "pad_id": 0, "vocab_size": 49408}
 
 # Algorithmic work per unit: 2 x MAC over all matmuls.
-def vit_flops(B):
+# The engine prunes the last layer to the pooled token after attention (engine.hip trunk,
+# CLIPGPU_PRUNE_LAST, bit-identical embeddings): `executed` counts the MFMA work that runs.
+PRUNE_LAST = os.environ.get("CLIPGPU_PRUNE_LAST", "1") != "0"
+
+
+def vit_flops(B, executed=False):
     S, P, D, L, M, E = 224, 32, 768, 12, 3072, 512
     g2 = (S // P) ** 2
     N = g2 + 1
     patch = 2 * B * g2 * D * 3 * P * P
     per_layer = 2 * B * N * (3 * D * D + D * D + 2 * D * M) + 2 * 2 * B * N * N * D
-    return patch + L * per_layer + 2 * B * D * E
+    pruned = 2 * B * (N - 1) * (D * D + 2 * D * M) if executed and PRUNE_LAST else 0
+    return patch + L * per_layer + 2 * B * D * E - pruned
 
 
-def text_flops(B, T=77):
+def text_flops(B, T=77, executed=False):
     D, L, M, E = 512, 12, 2048, 512
-    return L * (2 * B * T * (3 * D * D + D * D + 2 * D * M) + 2 * 2 * B * T * T * D) + 2 * B * D * E
+    pruned = 2 * B * (T - 1) * (D * D + 2 * D * M) if executed and PRUNE_LAST else 0
+    return L * (2 * B * T * (3 * D * D + D * D + 2 * D * M) + 2 * 2 * B * T * T * D) + 2 * B * D * E - pruned
 
 
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md chip table)
@@ -200,12 +207,14 @@ def main():
     _, (fc_ms, fc_n) = timed(vision_step, max(3, args.steps // 2), 1, ve, "c_fc")
 
     # roofline of the dominant kernel: c_fc GEMM (+QuickGELU epilogue), M=rows per launch,
-    # N=3072, K=768; fc_n counts launches (12 layers x lanes per step)
-    fc_rows_per_launch = B_VISION * 50 * 12 * max(3, args.steps // 2) / max(fc_n, 1)
+    # N=3072, K=768; fc_n counts the full-row launches (12 layers, or 11 when the last one
+    # is pruned to the pooled rows and profiled as "last_layer", x lanes per step)
+    fc_layers = 11 if PRUNE_LAST else 12
+    fc_rows_per_launch = B_VISION * 50 * fc_layers * max(3, args.steps // 2) / max(fc_n, 1)
     fc_flops = 2.0 * fc_rows_per_launch * 3072 * 768
     fc_avg_s = (fc_ms / 1e3) / max(fc_n, 1)
     achieved = fc_flops / fc_avg_s / 1e12
-    whole_tflops = vit_flops(B_VISION) * args.steps / dt / 1e12 / 1.0
+    whole_tflops = vit_flops(B_VISION, executed=True) * args.steps / dt / 1e12 / 1.0
 
     # The fp8 (MX) engine of the same workload beside the bf16 value (BASELINE configs[4]'s
     # weight path on the bench model): throughput and the cosine of its embeddings to the
@@ -242,7 +251,7 @@ def main():
         text = {"metric": "texts/sec embedding, ViT-B/32 text tower, batch 1024 x 77 tokens",
                 "value": round(world * B_TEXT * tsteps / tdt, 1), "unit": "texts/s",
                 "ms_per_step": round(tdt * 1e3 / tsteps, 3),
-                "mfma_tflops": round(text_flops(B_TEXT) * world * tsteps / tdt / 1e12 / world, 1)}
+                "mfma_tflops": round(text_flops(B_TEXT, executed=True) * world * tsteps / tdt / 1e12 / world, 1)}
         te.close()
 
     cpu = None
@@ -274,6 +283,7 @@ def main():
             "gemm_tiles": gemm_tiles,
             "gemm_tiles_env": ",".join(str(t) for t in tiles),
             "whole_forward_mfma_tflops_per_gpu": round(whole_tflops, 1),
+            "last_layer_pruned": PRUNE_LAST,
             "text": text,
             "fp8": fp8_info,
             "cpu_baseline": cpu,

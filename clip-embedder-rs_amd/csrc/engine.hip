@@ -134,9 +134,9 @@ struct GraphCache {
 namespace clipgpu {
 // Live per-kernel-class timing with HIP events recorded on the launch stream
 // (clipgpu_profile_*; bench.py's roofline.achieved).  Off by default.
-enum ProfCat { PC_PATCH = 0, PC_STEM, PC_QKV, PC_ATTN, PC_OUT_PROJ, PC_LN, PC_C_FC, PC_C_PROJ, PC_HEAD, PC_N };
+enum ProfCat { PC_PATCH = 0, PC_STEM, PC_QKV, PC_ATTN, PC_OUT_PROJ, PC_LN, PC_C_FC, PC_C_PROJ, PC_HEAD, PC_TAIL, PC_N };
 static const char* kProfNames[PC_N] = {"patch_embed", "stem_ln", "qkv", "attention", "out_proj",
-                                       "layernorm", "c_fc", "c_proj", "head"};
+                                       "layernorm", "c_fc", "c_proj", "head", "last_layer"};
 struct Profiler {
   unsigned mask = 0;
   std::vector<hipEvent_t> pool;
@@ -165,6 +165,7 @@ struct clipgpu_engine {
   int tuned_rows = 0;
   int lanes = 1;  // concurrent sub-batches per device (CLIPGPU_LANES, default 2)
   bool graphs = true;  // replay forwards as hipGraphs (CLIPGPU_GRAPHS=0 disables)
+  bool prune = true;   // last layer on the pooled rows only (CLIPGPU_PRUNE_LAST=0 disables; see trunk)
   // K-slices of the N = width GEMMs (out_proj, c_proj): CLIPGPU_GEMM_SPLIT=1 -> 2, else 1.
   // Fixed per engine, independent of the batch and lane split, so outputs stay
   // bit-identical across both; the second slice's partial is added by the next LayerNorm.
@@ -585,33 +586,72 @@ MxGemmParams site_gemm_mx(const clipgpu_engine& e, const Replica& r, const Layer
   return g;
 }
 
-// The transformer trunk shared by both towers: L x [LN1 -> QKV -> MHA -> out+res ->
-// LN2 -> fc1+act -> fc2+res], with h already holding ln_1(x) of layer 0.
-void trunk(const clipgpu_engine& e, const Replica& r, int B, int causal, hipStream_t st) {
+// Residual rows the head pools from: x at token pos(b) of each sequence (tokens = T), or the
+// compact [B][D] rows the pruned last layer leaves (tokens = 1, pos 0).
+struct PoolSrc {
+  const float* x;
+  int tokens;
+  const int64_t* ids;
+};
+
+// Last-layer pruning.  The CLIP heads read one token per sequence (CLS, or the EOT argmax
+// for text), and after the last layer's attention every op is row-local (out_proj, ln_2,
+// c_fc, c_proj), so that layer's tail runs on the pooled rows only: attention still reads
+// every token's K/V, then the pooled token's residual row and attention output are gathered
+// to a compact [B][D] pair and out_proj .. c_proj run at M = B.  Each kept row goes through
+// the same kernels with the same K-ordered sums, so the embeddings are bit-identical to the
+// full last layer (test_last_layer_pruning_is_bit_exact).  Off with CLIPGPU_PRUNE_LAST=0; not
+// for the SigLIP MAP head (pools every token) or split-K engines (slab rows are per token).
+// The compact pair lives in the tail of `big`, past the M = B MLP hidden.
+inline size_t prune_off_x(const TowerSpec& s, int B) { return align256((size_t)B * mlp_pad(s) * 2); }
+inline size_t prune_off_h(const TowerSpec& s, int B) {
+  return prune_off_x(s, B) + align256((size_t)B * s.width * 4);
+}
+inline bool prune_last(const clipgpu_engine& e, int B) {
   const TowerSpec& s = e.spec;
-  const int T = s.tokens(), rows = B * T, D = s.width;
-  const bool tuned = 2 * rows > e.tuned_rows;
+  return e.prune && e.ksplit < 2 && s.family != FAMILY_SIGLIP && s.layers > 0 &&
+         prune_off_h(s, B) + (size_t)B * s.width * 2 <= (size_t)B * s.tokens() * big_wide(s) * 2;
+}
+
+// The transformer trunk shared by both towers: L x [LN1 -> QKV -> MHA -> out+res ->
+// LN2 -> fc1+act -> fc2+res], with h already holding ln_1(x) of layer 0.  ids: the text
+// tower's token ids (pooled-token choice when the last layer is pruned), nullptr for CLS.
+PoolSrc trunk(const clipgpu_engine& e, const Replica& r, int B, int causal, const int64_t* ids, hipStream_t st) {
+  const TowerSpec& s = e.spec;
+  const int T = s.tokens(), D = s.width;
+  const bool prune = prune_last(e, B);
   for (int l = 0; l < s.layers; ++l) {
     const LayerW& L = r.w.layers[l];
+    const bool compact = prune && l + 1 == s.layers;
+    Replica c = r;  // the buffers the tail of this layer runs on
+    int rows = B * T;
     auto gemm = [&](int site, int cat, const char* what) {
-      ProfScope ps(e, cat, st, /*gemm=*/true);
+      ProfScope ps(e, rows == B * T ? cat : PC_TAIL, st, /*gemm=*/true);
+      const bool tuned = 2 * rows > e.tuned_rows;
       if (e.mx && site != GS_OUT) {
-        MxGemmParams g = site_gemm_mx(e, r, L, site, rows);
+        MxGemmParams g = site_gemm_mx(e, c, L, site, rows);
         g.tile = tuned ? e.tile[site] : MX_TILE_AUTO;
         check(launch_gemm_mx(e.dt, site_epi_mx(site), site == GS_FC ? s.act : ACT_NONE, g, st), what);
         return;
       }
-      GemmParams g = site_gemm(e, r, L, site, rows);
+      GemmParams g = site_gemm(e, c, L, site, rows);
       g.tile = tuned ? e.tile[site] : TILE_AUTO;
       check(launch_gemm(e.dt, A_ROWS, site_epi(site), site == GS_FC ? s.act : ACT_NONE, g, st), what);
     };
     gemm(GS_QKV, PC_QKV, "qkv gemm");
     { ProfScope ps(e, PC_ATTN, st);
       check(launch_attention(e.dt, r.big, r.h, B, T, s.heads, D, causal, st), "attention"); }
+    if (compact) {  // pooled rows only from here on (QKV in `big` is dead after attention)
+      c.x = (float*)((char*)r.big + prune_off_x(s, B));
+      c.h = (char*)r.big + prune_off_h(s, B);
+      rows = B;
+      ProfScope ps(e, PC_TAIL, st);
+      check(launch_gather_pooled(r.x, r.h, ids, T, c.x, c.h, B, D, st), "gather pooled rows");
+    }
     gemm(GS_OUT, PC_OUT_PROJ, "out_proj gemm");
-    { ProfScope ps(e, PC_LN, st);
-      check(launch_ln_rows_add(e.dt, r.x, site_split(e, GS_OUT) ? r.slab : nullptr, L.ln2_w, L.ln2_b, s.ln_eps, r.h,
-                               rows, D, st, r.hs), "ln_2"); }
+    { ProfScope ps(e, compact ? PC_TAIL : PC_LN, st);
+      check(launch_ln_rows_add(e.dt, c.x, site_split(e, GS_OUT) ? c.slab : nullptr, L.ln2_w, L.ln2_b, s.ln_eps, c.h,
+                               rows, D, st, c.hs), "ln_2"); }
     gemm(GS_FC, PC_C_FC, "c_fc gemm");
     gemm(GS_PROJ, PC_C_PROJ, "c_proj gemm");
     if (l + 1 < s.layers) {  // (the last c_proj's slab is added by the head's first LayerNorm)
@@ -619,7 +659,9 @@ void trunk(const clipgpu_engine& e, const Replica& r, int B, int causal, hipStre
       check(launch_ln_rows_add(e.dt, r.x, site_split(e, GS_PROJ) ? r.slab : nullptr, r.w.layers[l + 1].ln1_w,
                                r.w.layers[l + 1].ln1_b, s.ln_eps, r.h, rows, D, st, r.hs), "ln_1");
     }
+    if (compact) return PoolSrc{c.x, 1, nullptr};
   }
+  return PoolSrc{r.x, T, ids};
 }
 
 // Times each candidate tile on every trunk GEMM site at max_batch rows (workspace
@@ -708,11 +750,11 @@ void autotune_tiles(clipgpu_engine& e, Replica& r) {
   (void)hipEventDestroy(b);
 }
 
-void head(const clipgpu_engine& e, const Replica& r, int B, const int64_t* ids, float* d_out, hipStream_t st) {
+void head(const clipgpu_engine& e, const Replica& r, int B, const PoolSrc& src, float* d_out, hipStream_t st) {
   const TowerSpec& s = e.spec;
   const int D = s.width, E = s.embed_dim;
   ProfScope ps(e, PC_HEAD, st);
-  check(launch_pool_ln(e.dt, r.x, site_split(e, GS_PROJ) ? r.slab : nullptr, ids, s.tokens(), r.w.lnpost_w,
+  check(launch_pool_ln(e.dt, src.x, site_split(e, GS_PROJ) ? r.slab : nullptr, src.ids, src.tokens, r.w.lnpost_w,
                        r.w.lnpost_b, s.ln_eps, r.pooled, B, D, st), "pool+ln");
   check(launch_gemm(e.dt, A_ROWS, EPI_STORE32, ACT_NONE, rows_gemm(r.pooled, D, r.w.proj_t, nullptr, r.emb, E, B, E, D), st), "proj gemm");
   check(launch_l2norm(r.emb, d_out, B, E, st), "l2norm");
@@ -762,7 +804,7 @@ void vision_forward(const clipgpu_engine& e, const Replica& r, const void* pixel
       check(launch_ln_rows(e.dt, r.x, r.w.layers[0].ln1_w, r.w.layers[0].ln1_b, s.ln_eps, r.h, B * s.tokens(), D, st,
                            r.hs),
             "ln_1"); }
-    trunk(e, r, B, 0, st);
+    trunk(e, r, B, 0, nullptr, st);
     head_map(e, r, B, d_out, st);
     return;
   }
@@ -772,8 +814,7 @@ void vision_forward(const clipgpu_engine& e, const Replica& r, const void* pixel
                                r.w.layers[0].ln1_b, s.ln_eps, r.h, B, s.tokens(), D, st, r.hs),
         "embed+ln_pre");
   }
-  trunk(e, r, B, 0, st);
-  head(e, r, B, nullptr, d_out, st);
+  head(e, r, B, trunk(e, r, B, 0, nullptr, st), d_out, st);
 }
 
 void text_forward(const clipgpu_engine& e, const Replica& r, const int64_t* d_ids, int B, float* d_out,
@@ -785,8 +826,7 @@ void text_forward(const clipgpu_engine& e, const Replica& r, const int64_t* d_id
                              r.x, r.h, B, s.context_length, s.width, s.vocab_size, st, r.hs),
         "token embed+ln_1");
   }
-  trunk(e, r, B, 1, st);
-  head(e, r, B, d_ids, d_out, st);
+  head(e, r, B, trunk(e, r, B, 1, d_ids, st), d_out, st);
 }
 
 // The replica's workspace seen from batch row b0: every activation buffer is
@@ -1299,6 +1339,7 @@ int clipgpu_create(const char* model_dir, int tower, const int* device_ids, int 
     if (const char* ln = getenv("CLIPGPU_LANES")) e->lanes = std::max(1, std::min(4, atoi(ln)));
     else e->lanes = 2;
     if (const char* gr = getenv("CLIPGPU_GRAPHS")) e->graphs = gr[0] != '0';
+    if (const char* pl = getenv("CLIPGPU_PRUNE_LAST")) e->prune = pl[0] != '0';
     const TowerSpec& s = e->spec;
     if (const char* sp = getenv("CLIPGPU_GEMM_SPLIT")) e->ksplit = sp[0] == '1' ? 2 : 1;
     if (s.heads <= 0 || s.width % s.heads || s.width % 64)

@@ -776,8 +776,99 @@ hipError_t launch_pipe(const GemmParams& p, hipStream_t s) {
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// Skinny GEMM (M <= SKINNY_MAX_M; the pruned last layer at M = batch, the heads' projections).
+// A 128-row tile there leaves most CUs idle and runs K/64 dependent K-steps, each paying an
+// L2/HBM round trip (c_proj at M = 128: 6 tiles, 48 steps, 53 us).  Instead one wave owns one
+// 16x16 output block and streams its W rows and A rows straight from global memory (both
+// L2-resident at these sizes), U = 8 k-chunks of loads in flight ahead of the MFMAs.
+// Operand roles, the k -> lane assignment (lane (fr, fq) holds k = 32c + 8fq .. +7 of row fr)
+// and the K order of the MFMA chain are those of the tiled kernels, and the epilogue does the
+// same float ops, so every output element is bit-identical to theirs
+// (test_skinny_gemm_is_bit_exact, test_last_layer_pruning_is_bit_exact).
+constexpr int SKINNY_MAX_M = 256;
+constexpr int SKINNY_U = 8;
+
+template <typename T, int EPI, int ACT>
+__global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmParams p) {
+  typedef typename Vec8<T>::type V8;
+  constexpr int U = SKINNY_U;
+  const int lane = threadIdx.x & 63;
+  const int wid = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int nTn = p.N >> 4;
+  const int tm = wid / nTn, tn = wid - tm * nTn;  // a block's 4 waves share the A rows
+  if (tm * 16 >= p.M) return;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int m = tm * 16 + fr;
+  const T* a = (const T*)p.A + (long)min(m, p.M - 1) * p.lda + fq * 8;
+  const T* w = (const T*)p.W + (long)(tn * 16 + fr) * p.ldw + fq * 8;
+  const int nc = p.K >> 5;
+  V8 wa[U], aa[U], wb[U], ab[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    wa[u] = *(const V8*)(w + u * 32);
+    aa[u] = *(const V8*)(a + u * 32);
+  }
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int c0 = 0; c0 < nc; c0 += U) {
+    if (c0 + U < nc) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        wb[u] = *(const V8*)(w + (c0 + U + u) * 32);
+        ab[u] = *(const V8*)(a + (c0 + U + u) * 32);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc = mfma_16x16x32(wa[u], aa[u], acc);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      wa[u] = wb[u];
+      aa[u] = ab[u];
+    }
+  }
+  if (m >= p.M) return;
+  const int n = tn * 16 + fq * 4;
+  f32x4 bias = {0.f, 0.f, 0.f, 0.f};
+  if (p.bias != nullptr) bias = *(const f32x4*)(p.bias + n);
+  float v[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) v[j] = acc[j] + bias[j];
+  if constexpr (EPI == EPI_STORE16) {
+    typename Vec4<T>::type o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = to16<T>(apply_act<ACT>(v[j]));
+    *(typename Vec4<T>::type*)((T*)p.out + (long)m * p.ldo + n) = o;
+  } else {
+    float* o = (float*)p.out + (long)m * p.ldo + n;
+    float4 r = make_float4(v[0], v[1], v[2], v[3]);
+    if constexpr (EPI == EPI_RESID) {
+      const float4 x = *(const float4*)o;
+      r.x += x.x; r.y += x.y; r.z += x.z; r.w += x.w;
+    }
+    *(float4*)o = r;
+  }
+}
+
+// Shapes the skinny kernel takes: A_ROWS operands, 16-aligned N, K a multiple of 32*U,
+// 16-byte aligned rows, no split-K.
+inline bool skinny_ok(const GemmParams& p) {
+  return p.M > 0 && p.M <= SKINNY_MAX_M && p.N % 16 == 0 && p.K % (32 * SKINNY_U) == 0 && p.lda % 8 == 0 &&
+         p.ldw % 8 == 0 && p.ldo % 4 == 0 && p.ksplit <= 1 && !(p.diag & 2);
+}
+
+template <typename T, int EPI, int ACT>
+hipError_t launch_skinny(const GemmParams& p, hipStream_t s) {
+  const long waves = (long)((p.M + 15) / 16) * (p.N / 16);
+  gemm_launch(gemm_skinny_kernel<T, EPI, ACT>, (int)((waves + 3) / 4), 256, s, p);
+  return hipGetLastError();
+}
+
 template <typename T, int EPI, int ACT>
 hipError_t launch_tile(const GemmParams& p, hipStream_t s) {
+  if constexpr (EPI != EPI_PATCH) {
+    if ((p.tile == TILE_AUTO || p.tile == TILE_SKINNY) && skinny_ok(p)) return launch_skinny<T, EPI, ACT>(p, s);
+  }
+  if (p.tile == TILE_SKINNY) return hipErrorInvalidValue;
   const int tile = p.tile == TILE_AUTO ? pick_gemm_tile(p.M, p.N, p.K) : p.tile;
   // software-pipelined kernel: K >= 128, 16-byte-aligned 16-bit output rows (diag bit 1: legacy, stamp builds)
   const bool pipe = p.K >= 2 * BK && !(p.diag & 2) && (EPI != EPI_STORE16 || p.ldo % 8 == 0);

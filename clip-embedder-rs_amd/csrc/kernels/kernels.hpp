@@ -49,7 +49,8 @@ enum GemmTile {
   TILE_128x128_PIPE = 4,  // gemm_pipe_kernel: 4 waves, 64 KiB LDS, 2 blocks / CU
   TILE_128x64_PIPE = 5,   // gemm_pipe_kernel: 4 waves (64x32 each), 48 KiB LDS, 3 blocks / CU
   TILE_64x128_PIPE = 6,   // gemm_pipe_kernel: 4 waves (32x64 each), 48 KiB LDS, 3 blocks / CU
-  TILE_LAST = TILE_64x128_PIPE,
+  TILE_LAST = TILE_64x128_PIPE,  // (last of the tiled kernels: the range the tuners and pins take)
+  TILE_SKINNY = 7,        // gemm_skinny_kernel: one wave per 16x16 block, M <= 256 (TILE_AUTO's pick there)
 };
 int pick_gemm_tile(int M, int N, int K);
 int device_cus();  // CUs of the current device (cached)
@@ -100,6 +101,11 @@ hipError_t launch_text_embed_ln(DType dt, const int64_t* ids, const float* tok, 
 hipError_t launch_pool_ln(DType dt, const float* x, const float* slab, const int64_t* ids, int tokens,
                           const float* w, const float* b, float eps, void* out16, int B, int D,
                           hipStream_t s);
+
+// Last-layer compaction: xc[b] = x[b*tokens + pos(b)] (f32) and hc[b] = h[same row] (16-bit),
+// pos as launch_pool_ln picks it.  x / h and xc / hc must not overlap.
+hipError_t launch_gather_pooled(const float* x, const void* h16, const int64_t* ids, int tokens, float* xc,
+                                void* hc16, int B, int D, hipStream_t s);
 
 // Patch rows of the patch-embedding conv: out[b*G*G + p][k] (16-bit, row stride Kp) from
 // normalised f32 NCHW (src = A_IMG_F32) or u8 NHWC normalised with mean/std (A_IMG_U8);

@@ -200,6 +200,25 @@ __global__ __launch_bounds__(256) void text_embed_ln_kernel(const int64_t* __res
   store_ln_out(h, qs, row, D, y, lane);
 }
 
+// Token pooled for sequence bi: 0 (CLS, ids == nullptr) or the first index of the maximum
+// id (torch argmax; EOT is the largest id).  Wave-uniform.
+__device__ inline int pooled_token(const int64_t* __restrict__ ids, int bi, int tokens, int lane) {
+  if (ids == nullptr) return 0;
+  long best = -1;
+  int bidx = 0x7fffffff;
+  for (int t = lane; t < tokens; t += 64) {
+    const long v = ids[(long)bi * tokens + t];
+    if (v > best) { best = v; bidx = t; }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const long ov = __shfl_xor(best, o, 64);
+    const int oi = __shfl_xor(bidx, o, 64);
+    if (ov > best || (ov == best && oi < bidx)) { best = ov; bidx = oi; }
+  }
+  return bidx;
+}
+
 template <typename T, int NV>
 __global__ __launch_bounds__(256) void pool_ln_kernel(const float* __restrict__ x, const float* __restrict__ slab,
                                                       const int64_t* __restrict__ ids, int tokens, const float* w,
@@ -207,22 +226,7 @@ __global__ __launch_bounds__(256) void pool_ln_kernel(const float* __restrict__ 
   const int bi = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (bi >= B) return;
   const int D4 = D >> 2;
-  int src = 0;
-  if (ids != nullptr) {  // first index of the maximum id (torch argmax; EOT is the largest id)
-    long best = -1;
-    int bidx = 0x7fffffff;
-    for (int t = lane; t < tokens; t += 64) {
-      const long v = ids[(long)bi * tokens + t];
-      if (v > best) { best = v; bidx = t; }
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const long ov = __shfl_xor(best, o, 64);
-      const int oi = __shfl_xor(bidx, o, 64);
-      if (ov > best || (ov == best && oi < bidx)) { best = ov; bidx = oi; }
-    }
-    src = bidx;
-  }
+  const int src = pooled_token(ids, bi, tokens, lane);
   Row<NV> r, y, g, bb;
   load_row(x + ((long)bi * tokens + src) * D, D4, lane, r);
   load_row(w, D4, lane, g);
@@ -234,6 +238,24 @@ __global__ __launch_bounds__(256) void pool_ln_kernel(const float* __restrict__ 
   }
   layer_norm_regs(r, y, g, bb, eps, D, lane);
   store_row16(out + (long)bi * D, y, D4, lane);
+}
+
+// Last-layer compaction: the pooled token's residual row x and attention-output row h
+// (16-bit, raw bits) of each sequence, copied to row bi of xc / hc.  One wave per sequence.
+__global__ __launch_bounds__(256) void gather_pooled_kernel(const float* __restrict__ x,
+                                                            const uint16_t* __restrict__ h,
+                                                            const int64_t* __restrict__ ids, int tokens,
+                                                            float* __restrict__ xc, uint16_t* __restrict__ hc, int B,
+                                                            int D) {
+  const int bi = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (bi >= B) return;
+  const long src = (long)bi * tokens + pooled_token(ids, bi, tokens, lane);
+  const float4* xs = (const float4*)(x + src * D);
+  float4* xd = (float4*)(xc + (long)bi * D);
+  for (int i = lane; i < D / 4; i += 64) xd[i] = xs[i];
+  const uint2* hs = (const uint2*)(h + src * D);
+  uint2* hd = (uint2*)(hc + (long)bi * D);
+  for (int i = lane; i < D / 4; i += 64) hd[i] = hs[i];
 }
 
 __global__ __launch_bounds__(256) void l2norm_kernel(const float* __restrict__ in, float* __restrict__ out, int B,
@@ -319,6 +341,14 @@ hipError_t launch_text_embed_ln(DType dt, const int64_t* ids, const float* tok, 
     CLIPGPU_ROW_LAUNCH(text_embed_ln_kernel, _Float16, rows_grid(rows), D, ids, tok, pos, ln1_w, ln1_b, eps, x, (_Float16*)h,
                        qs, rows, T, D, vocab);
   }
+  return hipGetLastError();
+}
+
+hipError_t launch_gather_pooled(const float* x, const void* h16, const int64_t* ids, int tokens, float* xc,
+                                void* hc16, int B, int D, hipStream_t s) {
+  if (D % 4 || D <= 0 || B <= 0 || tokens <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(gather_pooled_kernel, rows_grid(B), dim3(256), 0, s, x, (const uint16_t*)h16, ids, tokens, xc,
+                     (uint16_t*)hc16, B, D);
   return hipGetLastError();
 }
 

@@ -108,7 +108,7 @@ class Engine:
 
 
 PROFILE_CATEGORIES = ["patch_embed", "stem_ln", "qkv", "attention", "out_proj", "layernorm", "c_fc",
-                      "c_proj", "head"]
+                      "c_proj", "head", "last_layer"]
 
 
 def profile_enable(engine: "Engine", categories) -> None:

@@ -163,7 +163,8 @@ int clipgpu_similarity_device(const float* d_img, int64_t n_img, const float* d_
 /* ---- live kernel timing -------------------------------------------------------------------
  * Records HIP events around every launch whose category bit is set in `mask` (on the launch
  * stream), for the device-resident entry points.  Categories: 0 patch_embed, 1 stem_ln, 2 qkv,
- * 3 attention, 4 out_proj, 5 layernorm, 6 c_fc, 7 c_proj, 8 head.  enable() resets totals;
+ * 3 attention, 4 out_proj, 5 layernorm, 6 c_fc, 7 c_proj, 8 head, 9 last_layer (the pruned
+ * last layer's gather, out_proj, ln_2, c_fc and c_proj at M = batch).  enable() resets totals;
  * read() waits for the recorded events and returns the summed ms and launch count.  While a
  * mask is set, a batch's concurrent sub-batch lanes run one after another on the launch
  * stream (same launches, no overlap), so each event pair times one kernel alone. */

@@ -98,6 +98,28 @@ def test_gemm_residual(dtype, tile):
     assert np.abs(out - ref).max() < 1e-4
 
 
+@pytest.mark.parametrize("mode,act", [(0, 1), (0, 2), (1, 0), (2, 0)])
+@pytest.mark.parametrize("M,N,K", [(1, 512, 768), (5, 64, 256), (77, 768, 768), (128, 3072, 768),
+                                   (128, 768, 3072), (200, 2304, 1024), (256, 512, 768)])
+def test_skinny_gemm_is_bit_exact(mode, act, M, N, K, monkeypatch):
+    """The skinny kernel (TILE_AUTO's pick at M <= 256: the pruned last layer and the heads)
+    gives the same bits as the tiled kernels: same MFMA operand roles, k -> lane assignment
+    and K order, same epilogue float ops.  Also within the f32-accumulation bound of fp64."""
+    rng = np.random.default_rng(M * 13 + N + K + mode)
+    A = round16(rng.standard_normal((M, K)), BF16)
+    W = round16(rng.standard_normal((N, K)) / np.sqrt(K), BF16)
+    bias = rng.standard_normal(N).astype(np.float32)
+    resid = rng.standard_normal((M, N)).astype(np.float32) if mode == 1 else None
+    outs = []
+    for t in ["7", "1", "4"]:
+        monkeypatch.setenv("CLIPGPU_TEST_TILE", t)
+        outs.append(run_gemm(BF16, mode, act, A, W, bias, resid))
+    assert np.array_equal(outs[0], outs[1]) and np.array_equal(outs[0], outs[2])
+    if mode == 2:
+        ref = A.astype(np.float64) @ W.T.astype(np.float64) + bias
+        assert np.all(np.abs(outs[0] - ref) <= 3e-5 * (np.abs(A) @ np.abs(W).T) + 1e-6)
+
+
 @pytest.mark.parametrize("ks", [2, 3])
 @pytest.mark.parametrize("mode,M,N,K", [(1, 6400, 768, 3072), (1, 1513, 640, 256), (2, 3000, 520, 384),
                                         (1, 8300, 2056, 768)])

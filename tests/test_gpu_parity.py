@@ -279,6 +279,38 @@ def test_concurrent_lanes_are_bit_exact(tower, monkeypatch):
     check_rows(outs[-1][:4], ref)
 
 
+@pytest.mark.parametrize("cfg", [VIT_B_32_CFG, TINY_CFG])
+@pytest.mark.parametrize("dtype", ["bf16", "fp8"])
+@pytest.mark.parametrize("tower", [0, 1])
+def test_last_layer_pruning_is_bit_exact(cfg, dtype, tower, monkeypatch):
+    """The last layer run on the pooled rows only (CLS / EOT argmax gathered after attention,
+    engine.hip trunk) gives the same bits as the full last layer: every op after attention is
+    row-local and each kept row goes through the same kernels.  Random EOT positions, two
+    lanes, and a batch whose rows-per-lane exceed the token count (gather sources and
+    destinations interleave)."""
+    if dtype == "fp8" and cfg is TINY_CFG:
+        pytest.skip("fp8 engines need MX-sized widths")
+    v, t = specs(cfg)
+    B = 37
+    if tower == 0:
+        data = normalized_pixels(weights.synth_images_u8(43, B, v.image_size), OPENAI_MEAN, OPENAI_STD)
+    else:
+        data = weights.synth_token_ids(43, B, t.context_length, t.vocab_size, t.vocab_size - 2,
+                                       t.vocab_size - 1, random_eot=True)
+    monkeypatch.setenv("CLIPGPU_LANES", "2")
+    outs = {}
+    for prune in ["0", "1"]:
+        monkeypatch.setenv("CLIPGPU_PRUNE_LAST", prune)
+        e = engine(cfg, tower, dtype=dtype, max_batch=B)
+        outs[prune] = e.embed_pixels(data) if tower == 0 else e.embed_tokens(data)
+        outs[prune + "s"] = e.embed_pixels(data[:3]) if tower == 0 else e.embed_tokens(data[:3])
+    assert np.array_equal(outs["0"], outs["1"])
+    assert np.array_equal(outs["0s"], outs["1s"])
+    if dtype == "bf16":
+        ref = oracle_vision(cfg, 1234, data[:4]) if tower == 0 else oracle_text(cfg, 1234, data[:4])
+        check_rows(outs["1"][:4], ref)
+
+
 @pytest.mark.parametrize("external", [False, True])
 def test_onnx_model_folder_matches_seeded_weights(tmp_path, external):
     """A model folder in the reference's own format (visual.onnx / text.onnx from a

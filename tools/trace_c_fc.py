@@ -6,7 +6,9 @@ Usage: python tools/trace_c_fc.py KERNEL_TRACE_CSV STEPS WARMUP
 The vision c_fc launches are the QuickGELU GEMM dispatches (gemm_{bt,pipe}_kernel<..., EPI 0,
 ACT 1>) up to the vision leg's last head kernel (the text engine's autotune follows it).  In launch order: autotune (candidate tiles x 5
 launches), warmup, timed loop (lanes concurrent), profiling warmup + profiling pass (lanes
-serialized) -- 12 layers x 2 lanes c_fc launches per step.  The profiling-pass mean is what
+serialized) -- 12 layers x 2 lanes c_fc launches per step.  With the last layer pruned to the
+pooled rows (CLIPGPU_PRUNE_LAST, default on) one launch per lane and step runs at M = 128 rows;
+those (under a fifth of the median) are dropped from the means.  The profiling-pass mean is what
 bench.py's HIP events report as roofline.avg_launch_us; this prints it from the trace so the
 two can be compared.
 """
@@ -28,4 +30,6 @@ n_prof = max(3, steps // 2) * per
 segs = [("timed (lanes concurrent)", d[-(n_prof + per + steps * per):-(n_prof + per)]),
         ("profiling pass (lanes serialized)", d[-n_prof:])]
 for name, x in segs:
+    cut = statistics.median(x) / 5
+    x = [v for v in x if v >= cut]
     print(f"{name:36s} launches {len(x):4d}  mean {statistics.mean(x):8.2f} us  median {statistics.median(x):8.2f} us")
