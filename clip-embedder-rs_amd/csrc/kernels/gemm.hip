@@ -781,7 +781,7 @@ hipError_t launch_pipe(const GemmParams& p, hipStream_t s) {
 // A 128-row tile there leaves most CUs idle and runs K/64 dependent K-steps, each paying an
 // L2/HBM round trip (c_proj at M = 128: 6 tiles, 48 steps, 53 us).  Instead one wave owns one
 // 16x16 output block and streams its W rows and A rows straight from global memory (both
-// L2-resident at these sizes), U = 8 k-chunks of loads in flight ahead of the MFMAs.
+// L2-resident at these sizes), two batches of U = 8 k-chunks of loads in flight ahead of the MFMAs.
 // Operand roles, the k -> lane assignment (lane (fr, fq) holds k = 32c + 8fq .. +7 of row fr)
 // and the K order of the MFMA chain are those of the tiled kernels, and the epilogue does the
 // same float ops, so every output element is bit-identical to theirs
@@ -803,27 +803,29 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmParams p) {
   const T* a = (const T*)p.A + (long)min(m, p.M - 1) * p.lda + fq * 8;
   const T* w = (const T*)p.W + (long)(tn * 16 + fr) * p.ldw + fq * 8;
   const int nc = p.K >> 5;
-  V8 wa[U], aa[U], wb[U], ab[U];
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    wa[u] = *(const V8*)(w + u * 32);
-    aa[u] = *(const V8*)(a + u * 32);
-  }
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  for (int c0 = 0; c0 < nc; c0 += U) {
-    if (c0 + U < nc) {
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        wb[u] = *(const V8*)(w + (c0 + U + u) * 32);
-        ab[u] = *(const V8*)(a + (c0 + U + u) * 32);
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) acc = mfma_16x16x32(wa[u], aa[u], acc);
+  // three register batches of U k-chunks: the loads of batch i+2 are issued before the
+  // MFMAs of batch i, so two batches of L2 / HBM latency are covered
+  V8 w0[U], a0[U], w1[U], a1[U], w2[U], a2[U];
+  auto load = [&](V8(&wv)[U], V8(&av)[U], int c) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      wa[u] = wb[u];
-      aa[u] = ab[u];
+      wv[u] = *(const V8*)(w + (c + u) * 32);
+      av[u] = *(const V8*)(a + (c + u) * 32);
+    }
+  };
+  load(w0, a0, 0);
+  if (U < nc) load(w1, a1, U);
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int c0 = 0; c0 < nc; c0 += U) {
+    if (c0 + 2 * U < nc) load(w2, a2, c0 + 2 * U);
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc = mfma_16x16x32(w0[u], a0[u], acc);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      w0[u] = w1[u];
+      a0[u] = a1[u];
+      w1[u] = w2[u];
+      a1[u] = a2[u];
     }
   }
   if (m >= p.M) return;
