@@ -166,6 +166,7 @@ struct clipgpu_engine {
   int lanes = 1;  // concurrent sub-batches per device (CLIPGPU_LANES, default 2)
   bool graphs = true;  // replay forwards as hipGraphs (CLIPGPU_GRAPHS=0 disables)
   bool prune = true;   // last layer on the pooled rows only (CLIPGPU_PRUNE_LAST=0 disables; see trunk)
+  bool trim = true;    // host-ids text batches run on their first max(EOT)+1 tokens (CLIPGPU_TRIM_TEXT=0)
   // K-slices of the N = width GEMMs (out_proj, c_proj): CLIPGPU_GEMM_SPLIT=1 -> 2, else 1.
   // Fixed per engine, independent of the batch and lane split, so outputs stay
   // bit-identical across both; the second slice's partial is added by the next LayerNorm.
@@ -607,19 +608,21 @@ inline size_t prune_off_x(const TowerSpec& s, int B) { return align256((size_t)B
 inline size_t prune_off_h(const TowerSpec& s, int B) {
   return prune_off_x(s, B) + align256((size_t)B * s.width * 4);
 }
-inline bool prune_last(const clipgpu_engine& e, int B) {
+inline bool prune_last(const clipgpu_engine& e, int B, int T) {
   const TowerSpec& s = e.spec;
   return e.prune && e.ksplit < 2 && s.family != FAMILY_SIGLIP && s.layers > 0 &&
-         prune_off_h(s, B) + (size_t)B * s.width * 2 <= (size_t)B * s.tokens() * big_wide(s) * 2;
+         prune_off_h(s, B) + (size_t)B * s.width * 2 <= (size_t)B * T * big_wide(s) * 2;
 }
 
 // The transformer trunk shared by both towers: L x [LN1 -> QKV -> MHA -> out+res ->
 // LN2 -> fc1+act -> fc2+res], with h already holding ln_1(x) of layer 0.  ids: the text
 // tower's token ids (pooled-token choice when the last layer is pruned), nullptr for CLS.
-PoolSrc trunk(const clipgpu_engine& e, const Replica& r, int B, int causal, const int64_t* ids, hipStream_t st) {
+// T: tokens per sequence (the text tower's trimmed length, else the tower's own).
+PoolSrc trunk(const clipgpu_engine& e, const Replica& r, int B, int causal, const int64_t* ids, hipStream_t st,
+              int T) {
   const TowerSpec& s = e.spec;
-  const int T = s.tokens(), D = s.width;
-  const bool prune = prune_last(e, B);
+  const int D = s.width;
+  const bool prune = prune_last(e, B, T);
   for (int l = 0; l < s.layers; ++l) {
     const LayerW& L = r.w.layers[l];
     const bool compact = prune && l + 1 == s.layers;
@@ -804,7 +807,7 @@ void vision_forward(const clipgpu_engine& e, const Replica& r, const void* pixel
       check(launch_ln_rows(e.dt, r.x, r.w.layers[0].ln1_w, r.w.layers[0].ln1_b, s.ln_eps, r.h, B * s.tokens(), D, st,
                            r.hs),
             "ln_1"); }
-    trunk(e, r, B, 0, nullptr, st);
+    trunk(e, r, B, 0, nullptr, st, s.tokens());
     head_map(e, r, B, d_out, st);
     return;
   }
@@ -814,19 +817,23 @@ void vision_forward(const clipgpu_engine& e, const Replica& r, const void* pixel
                                r.w.layers[0].ln1_b, s.ln_eps, r.h, B, s.tokens(), D, st, r.hs),
         "embed+ln_pre");
   }
-  head(e, r, B, trunk(e, r, B, 0, nullptr, st), d_out, st);
+  head(e, r, B, trunk(e, r, B, 0, nullptr, st, s.tokens()), d_out, st);
 }
 
+// T: tokens per sequence in d_ids ([B][T]): the context length, or a trimmed length (every
+// sequence's EOT inside the first T tokens, clipgpu_embed_tokens) -- causal attention makes
+// the tokens after a sequence's EOT invisible to its pooled row.
 void text_forward(const clipgpu_engine& e, const Replica& r, const int64_t* d_ids, int B, float* d_out,
-                  hipStream_t st) {
+                  hipStream_t st, int T = 0) {
   const TowerSpec& s = e.spec;
+  if (T <= 0) T = s.context_length;
   {
   ProfScope ps(e, PC_STEM, st);
   check(launch_text_embed_ln(e.dt, d_ids, r.w.tok, r.w.pos, r.w.layers[0].ln1_w, r.w.layers[0].ln1_b, s.ln_eps,
-                             r.x, r.h, B, s.context_length, s.width, s.vocab_size, st, r.hs),
+                             r.x, r.h, B, T, s.width, s.vocab_size, st, r.hs),
         "token embed+ln_1");
   }
-  head(e, r, B, trunk(e, r, B, 1, d_ids, st), d_out, st);
+  head(e, r, B, trunk(e, r, B, 1, d_ids, st, T), d_out, st);
 }
 
 // The replica's workspace seen from batch row b0: every activation buffer is
@@ -1028,7 +1035,7 @@ void par_memcpy(void* dst, const void* src, size_t n) {
 // so the host copy of sub-chunk j+1 and its H2D overlap the forward of sub-chunk j.  A slot
 // is reused after its previous sub-chunk's D2H event, whose rows are then copied out.
 void run_host_shard(clipgpu_engine& e, Replica& r, InKind kind, const void* in, size_t in_row_bytes, int64_t b0,
-                    int64_t b1, const float* mean, const float* stdv, float* out) {
+                    int64_t b1, const float* mean, const float* stdv, float* out, int tokens = 0) {
   HIP_CHECK(hipSetDevice(r.device));
   const int E = e.spec.embed_dim, L = e.lanes;
   const int S = (e.max_batch + L - 1) / L;  // rows per slot
@@ -1054,10 +1061,10 @@ void run_host_shard(clipgpu_engine& e, Replica& r, InKind kind, const void* in, 
     const Replica v = lane_view(e, r, k * S);
     run_graph(e, r,
               {(uint64_t)(10 + kind), (uint64_t)k, (uint64_t)n, fbits(mean, 0), fbits(mean, 1), fbits(mean, 2),
-               fbits(stdv, 0), fbits(stdv, 1), fbits(stdv, 2)},
+               fbits(stdv, 0), fbits(stdv, 1), fbits(stdv, 2), (uint64_t)tokens},
               st, [&](hipStream_t gs) {
                 if (kind == IN_IDS)
-                  text_forward(e, v, (const int64_t*)din, n, dout, gs);
+                  text_forward(e, v, (const int64_t*)din, n, dout, gs, tokens);
                 else
                   vision_forward(e, v, din, kind == IN_F32 ? A_IMG_F32 : A_IMG_U8, mean, stdv, n, dout, gs);
               });
@@ -1070,10 +1077,10 @@ void run_host_shard(clipgpu_engine& e, Replica& r, InKind kind, const void* in, 
 }
 
 void run_host(clipgpu_engine& e, InKind kind, const void* in, size_t in_row_bytes, int64_t B, const float* mean,
-              const float* stdv, float* out) {
+              const float* stdv, float* out, int tokens = 0) {
   const int G = (int)e.reps.size();
   if (G == 1) {
-    run_host_shard(e, e.reps[0], kind, in, in_row_bytes, 0, B, mean, stdv, out);
+    run_host_shard(e, e.reps[0], kind, in, in_row_bytes, 0, B, mean, stdv, out, tokens);
     return;
   }
   // Contiguous row blocks, rank order == input order.
@@ -1085,7 +1092,7 @@ void run_host(clipgpu_engine& e, InKind kind, const void* in, size_t in_row_byte
     if (b0 == b1) continue;
     th.emplace_back([&, g, b0, b1]() {
       try {
-        run_host_shard(e, e.reps[g], kind, in, in_row_bytes, b0, b1, mean, stdv, out);
+        run_host_shard(e, e.reps[g], kind, in, in_row_bytes, b0, b1, mean, stdv, out, tokens);
       } catch (const ClipErr& ex) {
         codes[g] = ex.code;
         errs[g] = ex.what();
@@ -1340,6 +1347,7 @@ int clipgpu_create(const char* model_dir, int tower, const int* device_ids, int 
     else e->lanes = 2;
     if (const char* gr = getenv("CLIPGPU_GRAPHS")) e->graphs = gr[0] != '0';
     if (const char* pl = getenv("CLIPGPU_PRUNE_LAST")) e->prune = pl[0] != '0';
+    if (const char* tt = getenv("CLIPGPU_TRIM_TEXT")) e->trim = tt[0] != '0';
     const TowerSpec& s = e->spec;
     if (const char* sp = getenv("CLIPGPU_GEMM_SPLIT")) e->ksplit = sp[0] == '1' ? 2 : 1;
     if (s.heads <= 0 || s.width % s.heads || s.width % 64)
@@ -1446,8 +1454,31 @@ int clipgpu_embed_tokens(clipgpu_engine* e, const int64_t* ids, const int64_t* m
     for (int64_t i = 0; i < B * T; ++i)
       if (ids[i] < 0 || ids[i] >= e->spec.vocab_size)
         throw ClipErr(CLIPGPU_ERR_INVALID, "Inference error: token id " + std::to_string(ids[i]) + " out of range");
+    // Sequence trimming: the pooled row of a sequence is its first argmax (EOT) token and
+    // attention is causal, so tokens past the batch's last EOT never reach an embedding.
+    // The batch runs on its first Tc = max(EOT index) + 1 tokens (at least 16), bit-identical
+    // (test_text_trim_is_bit_exact).  CLIPGPU_TRIM_TEXT=0 disables.
+    int64_t Tc = T;
+    if (e->trim) {
+      Tc = 1;
+      for (int64_t b = 0; b < B && Tc < T; ++b) {
+        const int64_t* row = ids + b * T;
+        int64_t best = 0;
+        for (int64_t t = 1; t < T; ++t)
+          if (row[t] > row[best]) best = t;
+        Tc = std::max<int64_t>(Tc, best + 1);
+      }
+      Tc = std::min<int64_t>(T, std::max<int64_t>(Tc, 16));
+    }
+    std::vector<int64_t> trimmed;
+    const int64_t* src = ids;
+    if (Tc < T) {
+      trimmed.resize((size_t)(B * Tc));
+      for (int64_t b = 0; b < B; ++b) std::memcpy(&trimmed[(size_t)(b * Tc)], ids + b * T, (size_t)Tc * 8);
+      src = trimmed.data();
+    }
     std::lock_guard<std::mutex> lk(e->mu);
-    run_host(*e, IN_IDS, ids, (size_t)T * 8, B, nullptr, nullptr, out);
+    run_host(*e, IN_IDS, src, (size_t)Tc * 8, B, nullptr, nullptr, out, (int)Tc);
   });
 }
 

@@ -311,6 +311,31 @@ def test_last_layer_pruning_is_bit_exact(cfg, dtype, tower, monkeypatch):
         check_rows(outs["1"][:4], ref)
 
 
+@pytest.mark.parametrize("cfg,max_eot", [(VIT_B_32_CFG, 9), (VIT_B_32_CFG, 30), (VIT_B_32_CFG, 76), (TINY_CFG, 5)])
+def test_text_trim_is_bit_exact(cfg, max_eot, monkeypatch):
+    """Host-ids text batches run on their first max(EOT) + 1 tokens (at least 16;
+    clipgpu_embed_tokens): causal attention keeps the tokens after a sequence's EOT away from
+    its pooled row, so the embeddings equal the full-context run bit for bit.  Short captions
+    (EOT at 2..max_eot, zero padding after), a batch over two lanes and several slots."""
+    _, t = specs(cfg)
+    B = 37
+    rng = np.random.default_rng(max_eot)
+    ids = np.zeros((B, t.context_length), np.int64)
+    ids[:, 0] = t.vocab_size - 2
+    eot = rng.integers(2, max_eot + 1, B)
+    eot[0] = max_eot
+    for b in range(B):
+        ids[b, 1:eot[b]] = rng.integers(1, t.vocab_size - 3, eot[b] - 1)
+        ids[b, eot[b]] = t.vocab_size - 1
+    outs = {}
+    for trim in ["0", "1"]:
+        monkeypatch.setenv("CLIPGPU_TRIM_TEXT", trim)
+        e = engine(cfg, 1, max_batch=16)
+        outs[trim] = e.embed_tokens(ids)
+    assert np.array_equal(outs["0"], outs["1"])
+    check_rows(outs["1"][:4], oracle_text(cfg, 1234, ids[:4]))
+
+
 @pytest.mark.parametrize("external", [False, True])
 def test_onnx_model_folder_matches_seeded_weights(tmp_path, external):
     """A model folder in the reference's own format (visual.onnx / text.onnx from a
