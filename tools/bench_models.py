@@ -91,6 +91,35 @@ def host_leg(B=256, steps=6, warmup=2):
     e.close()
 
 
+def captions_leg(B=1024, steps=6, warmup=2):
+    """ViT-B/32 text from host token ids at caption lengths (EOT at 8..24, zero padding to
+    77): sequence trimming (clipgpu_embed_tokens runs the batch on its first max(EOT)+1
+    tokens) on vs off (CLIPGPU_TRIM_TEXT=0).  Host buffers: H2D/D2H inside the timing."""
+    d = model_dir(VIT_B_32_CFG)
+    rng = np.random.default_rng(0)
+    V = 49408
+    ids = np.zeros((B, 77), np.int64)
+    ids[:, 0] = V - 2
+    eot = rng.integers(8, 25, B)
+    for b in range(B):
+        ids[b, 1:eot[b]] = rng.integers(1, V - 3, eot[b] - 1)
+        ids[b, eot[b]] = V - 1
+    res = {}
+    for trim in ("1", "0"):
+        os.environ["CLIPGPU_TRIM_TEXT"] = trim
+        e = Engine(d, 1, [0], "bf16", B)
+        dt = timed(lambda: e.embed_tokens(ids), steps, warmup)
+        res[trim] = e.embed_tokens(ids)
+        print(json.dumps({"measure": "b32_text_captions_" + ("trimmed" if trim == "1" else "full77"), "batch": B,
+                          "max_eot": int(eot.max()), "units_per_s": round(B / dt, 1),
+                          "ms_per_step": round(dt * 1e3, 3),
+                          "input": "host token ids (pinned staging + H2D/D2H inside the timing)"}), flush=True)
+        e.close()
+    os.environ.pop("CLIPGPU_TRIM_TEXT")
+    print(json.dumps({"measure": "b32_text_captions_bit_equal", "value": bool(np.array_equal(res["1"], res["0"]))}),
+          flush=True)
+
+
 def photos_leg(B=256, H=480, W=640, steps=4, warmup=1):
     """Decoded 640x480 photos -> embeddings (a3-a7 + forward, BASELINE configs[1] model): the
     reference's CPU resize path restated (host C++ preprocess_batch thread pool + embed_pixels)
@@ -168,6 +197,8 @@ if __name__ == "__main__":
     which = sys.argv[1:] or ["host", "photos", "similarity", "latency", "so400m", "h14"]
     if "host" in which:
         host_leg()
+    if "captions" in which:
+        captions_leg()
     if "photos" in which:
         photos_leg()
     if "similarity" in which:
