@@ -881,6 +881,7 @@ hipError_t launch_tile(const GemmParams& p, hipStream_t s) {
       case TILE_256x128: return launch_pipe<T, 256, 128, 4, 2, EPI, ACT>(p, s);
       case TILE_128x64_PIPE: return launch_pipe<T, 128, 64, 2, 2, EPI, ACT>(p, s);
       case TILE_64x128_PIPE: return launch_pipe<T, 64, 128, 2, 2, EPI, ACT>(p, s);
+      case TILE_160x128_PIPE: return launch_pipe<T, 160, 128, 2, 2, EPI, ACT>(p, s);
       default: return launch_pipe<T, 128, 128, 2, 2, EPI, ACT>(p, s);
     }
   }
@@ -891,6 +892,7 @@ hipError_t launch_tile(const GemmParams& p, hipStream_t s) {
       case TILE_128x128_PIPE: return launch_pipe<T, 128, 128, 2, 2, EPI, ACT>(p, s);
       case TILE_128x64_PIPE: return launch_pipe<T, 128, 64, 2, 2, EPI, ACT>(p, s);
       case TILE_64x128_PIPE: return launch_pipe<T, 64, 128, 2, 2, EPI, ACT>(p, s);
+      case TILE_160x128_PIPE: return launch_pipe<T, 160, 128, 2, 2, EPI, ACT>(p, s);
       default: break;
     }
   }
