@@ -27,6 +27,7 @@
 // epilogue stores).  M and N tails: clamped source rows + masked stores; K must
 // be a multiple of 64.
 #include <algorithm>
+#include <cstdlib>
 #include <utility>
 
 #include <hip/hip_ext.h>
@@ -400,7 +401,11 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
 // 4x2 of 64x64), 256x256 (8 waves, 128x64).  (A 4-wave 256x256 with 128x128 per wave
 // needs 256 accumulator AGPRs plus > 256 VGPRs and spills: not built.)
 // ---------------------------------------------------------------------------
-template <typename T, int BM, int BN, int WGM, int WGN, int EPI, int ACT>
+// NS: LDS stages.  2 = the schedule above.  3 (K-long GEMMs that fit in one round of blocks,
+// launch_pipe): phase1 of step g issues the DMA of step g+3 into g's buffer, and the wait
+// before the barrier lets the DMA of step g+2 stay in flight, so each DMA has two K-steps to
+// land instead of one (c_proj at K = 3072 with one block per CU was bound by that latency).
+template <typename T, int BM, int BN, int WGM, int WGN, int EPI, int ACT, int NS = 2>
 __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_pipe_kernel(GemmParams p) {
   typedef typename Vec8<T>::type V8;
   constexpr int NW = WGM * WGN;
@@ -411,7 +416,8 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_pipe_kernel(GemmParams 
   constexpr bool SPREAD = MI * NI >= 32;
   static_assert(A_INSTR >= 1 && B_INSTR >= 1 && MI >= 1 && BN <= 256, "bad tile");
   static_assert(NI == 2 || NI == 4 || NI == 8, "column permutation needs NI in {2,4,8}");
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + 2048];
+  static_assert(NS == 2 || NS == 3, "2 or 3 LDS stages");
+  __shared__ __attribute__((aligned(16))) char smem[NS * STAGE + 2048];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -477,7 +483,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_pipe_kernel(GemmParams 
   }
   auto dma_piece = [&](auto jc) {  // W pieces first, then A pieces
     constexpr int j = decltype(jc)::value;
-    char* const st = smem + (d_g & 1) * STAGE;
+    char* const st = smem + (d_g % NS) * STAGE;
     if constexpr (j < B_INSTR) {
       glds16(Wb + (size_t)d_kt * (BK * 2) + woff[j], st + A_BYTES + (wave * B_INSTR + j) * 1024);
     } else {
@@ -488,7 +494,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_pipe_kernel(GemmParams 
   auto dma_bias = [&]() {  // the tile's bias slice, with its first K-step (tile-parity buffer)
     if (p.bias != nullptr && wave == 0 && d_kt == 0) {
       const int n = min(d_n0 + lane * 4, ((p.N - 1) / 4) * 4);
-      glds16(p.bias + n, smem + 2 * STAGE + (d_ti & 1) * 1024);
+      glds16(p.bias + n, smem + NS * STAGE + (d_ti & 1) * 1024);
     }
   };
   auto dma_advance = [&]() {
@@ -603,7 +609,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_pipe_kernel(GemmParams 
       return;
     }
     if (p.bias != nullptr) {
-      const uint32_t ba = lds0 + 2 * STAGE + bpar * 1024 + (wn + fq * (4 * NI)) * 4;
+      const uint32_t ba = lds0 + NS * STAGE + bpar * 1024 + (wn + fq * (4 * NI)) * 4;
       static_for<NI>([&](auto ni) { ds_read_b128<(int)ni * 16>(bias[ni], ba); });
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
@@ -712,6 +718,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_pipe_kernel(GemmParams 
   vm_wait<0>();
   __builtin_amdgcn_s_barrier();
   dma_step();
+  if constexpr (NS == 3) dma_step();
   read_b(b0, lds0 + offB[0]);
   read_a(a0, lds0 + offA[0]);
   lgkm_wait_all(a0, b0);
@@ -726,14 +733,17 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_pipe_kernel(GemmParams 
     GEMM_STAMP(2 + ti * 4);
     for (int kt = 0; kt < nk; ++kt, ++g) {
       if (kt + 1 == nk) GEMM_STAMP(3 + ti * 4);
-      const uint32_t buf = lds0 + (g & 1) * STAGE;
+      const uint32_t buf = lds0 + (g % NS) * STAGE;
       if (kt == 0) phase0(std::true_type{}, buf);
       else phase0(std::false_type{}, buf);
-      if (after_full_epi) vm_wait<(EPI_VM < 63 ? EPI_VM : 63)>();
-      else vm_wait<0>();
+      // the DMA of step g+1 has landed once at most the later ops are outstanding: the
+      // DMA of step g+2 (3 stages), then the epilogue's stores and loads
+      constexpr int AHEAD = NS == 3 ? NP : 0;
+      if (after_full_epi) vm_wait<(EPI_VM + AHEAD < 63 ? EPI_VM + AHEAD : 63)>();
+      else vm_wait<AHEAD>();
       after_full_epi = false;
       __builtin_amdgcn_s_barrier();
-      phase1(kt + 1 < nk, lds0 + ((g + 1) & 1) * STAGE);
+      phase1(kt + 1 < nk, lds0 + ((g + 1) % NS) * STAGE);
       if (ti == 0 && kt + 1 < nk) GEMM_STAMP(34 + kt);
     }
     GEMM_STAMP(4 + ti * 4);
@@ -742,7 +752,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_pipe_kernel(GemmParams 
     after_full_epi = slice == 0 && m0 + BM <= p.M && n0 + BN <= p.N;
     if (!after_full_epi) vm_wait<0>();
     if (t + t_stride < t_end) {  // the next tile's step 0 landed at the last barrier
-      const uint32_t buf = lds0 + (g & 1) * STAGE;
+      const uint32_t buf = lds0 + (g % NS) * STAGE;
       read_b(b0, buf + offB[0]);
       read_a(a0, buf + offA[0]);
       lgkm_wait_all(a0, b0);
@@ -750,6 +760,15 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_pipe_kernel(GemmParams 
     GEMM_STAMP(5 + ti * 4);
   }
   GEMM_STAMP_REAL(63);
+}
+
+// CLIPGPU_GEMM_PIPE3=1 enables the 3-stage schedule (off by default).  Alone it is a little
+// faster (ViT-B/32 c_proj 49.7 -> 48.3 us), but its 110 KiB of LDS per block keeps the other
+// lane's blocks off the CU, and the concurrent-lane forward measured 83.7k vs 85.5k img/s
+// (profiles/r01_v19_pipe3_ab.txt).
+inline bool pipe3_enabled() {
+  const char* e = getenv("CLIPGPU_GEMM_PIPE3");
+  return e && e[0] == '1';
 }
 
 template <typename T, int BM, int BN, int WGM, int WGN, int EPI, int ACT>
@@ -767,10 +786,23 @@ template <typename T, int BM, int BN, int WGM, int WGN, int EPI, int ACT>
 hipError_t launch_pipe(const GemmParams& p, hipStream_t s) {
   const int nTn = (p.N + BN - 1) / BN, nTm = (p.M + BM - 1) / BM;
   const int ntiles = nTn * nTm * (p.ksplit > 1 ? p.ksplit : 1);
-  // resident blocks per CU: by LDS (2 stages + 2 KiB bias) and the 8-wave tiles' registers
-  const int lds = 2 * (BM + BN) * BK * 2 + 2048;
-  const int per_cu = WGM * WGN == 8 ? 1 : std::min(3, (160 * 1024) / lds);
-  const int resident = device_cus() * per_cu;
+  // resident blocks per CU: by LDS (stages + 2 KiB bias) and the 8-wave tiles' registers
+  auto per_cu = [&](int ns) {
+    const int lds = ns * (BM + BN) * BK * 2 + 2048;
+    return WGM * WGN == 8 ? 1 : std::min(3, (160 * 1024) / lds);
+  };
+  // 3 stages for K-long GEMMs whose tiles fit in one round of 3-stage blocks: there the
+  // K-step is DMA-latency-bound and the extra stage costs no occupancy (>= 3 K-steps per
+  // unit keep the bias double buffer safe)
+  constexpr bool FITS3 = 3 * (BM + BN) * BK * 2 + 2048 <= 160 * 1024;
+  if constexpr (FITS3) {
+    const int nk = p.K / BK / (p.ksplit > 1 ? p.ksplit : 1);
+    if (pipe3_enabled() && p.K >= 1024 && nk >= 3 && ntiles <= device_cus() * per_cu(3)) {
+      gemm_launch(gemm_pipe_kernel<T, BM, BN, WGM, WGN, EPI, ACT, 3>, ntiles, WGM * WGN * 64, s, p);
+      return hipGetLastError();
+    }
+  }
+  const int resident = device_cus() * per_cu(2);
   const int grid = ntiles <= resident ? ntiles : resident;
   gemm_launch(gemm_pipe_kernel<T, BM, BN, WGM, WGN, EPI, ACT>, grid, WGM * WGN * 64, s, p);
   return hipGetLastError();

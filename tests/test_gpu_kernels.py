@@ -98,6 +98,30 @@ def test_gemm_residual(dtype, tile):
     assert np.abs(out - ref).max() < 1e-4
 
 
+@pytest.mark.parametrize("mode,act", [(0, 1), (1, 0), (2, 0)])
+@pytest.mark.parametrize("M,N,K,tiles", [(1000, 768, 3072, "4,2,5,6,7"), (6400, 768, 3072, "7,5"),
+                                         (2600, 520, 1024, "4,7,2"), (333, 2304, 1280, "4,6")])
+def test_gemm_three_stage_pipeline_is_bit_exact(mode, act, M, N, K, tiles, monkeypatch):
+    """K >= 1024 launches whose tiles fit in one round of blocks run the 3-stage LDS
+    pipeline (DMA two K-steps ahead): same bits as the 2-stage schedule
+    (CLIPGPU_GEMM_PIPE3=0), M / N tails, residual epilogue."""
+    rng = np.random.default_rng(M + N + K + mode)
+    A = round16(rng.standard_normal((M, K)), BF16)
+    W = round16(rng.standard_normal((N, K)) / np.sqrt(K), BF16)
+    bias = rng.standard_normal(N).astype(np.float32)
+    resid = rng.standard_normal((M, N)).astype(np.float32) if mode == 1 else None
+    for t in tiles.split(","):
+        monkeypatch.setenv("CLIPGPU_TEST_TILE", t)
+        outs = []
+        for p3 in ("1", "0"):
+            monkeypatch.setenv("CLIPGPU_GEMM_PIPE3", p3)
+            outs.append(run_gemm(BF16, mode, act, A, W, bias, resid))
+        assert np.array_equal(outs[0], outs[1]), t
+    if mode == 2:
+        ref = A.astype(np.float64) @ W.T.astype(np.float64) + bias
+        assert np.all(np.abs(outs[0] - ref) <= 3e-5 * (np.abs(A) @ np.abs(W).T) + 1e-6)
+
+
 @pytest.mark.parametrize("mode,act", [(0, 1), (0, 2), (1, 0), (2, 0)])
 @pytest.mark.parametrize("M,N,K", [(1, 512, 768), (5, 64, 256), (77, 768, 768), (128, 3072, 768),
                                    (128, 768, 3072), (200, 2304, 1024), (256, 512, 768)])
