@@ -87,7 +87,9 @@ int clipgpu_embed_u8(clipgpu_engine* e, const uint8_t* nhwc, int64_t B, int64_t 
  * Replaces session.run(input_ids [, attention_mask]) in TextEmbedder::embed_texts
  * (src/text.rs:148-169).  ids: [B,T] int64; mask may be NULL (the exported text graph has
  * no mask input, pull_onnx.py:296-302; it is accepted and ignored, as the reference does
- * when the graph lacks "attention_mask", src/text.rs:156-161). */
+ * when the graph lacks "attention_mask", src/text.rs:156-161).  The batch runs on its first
+ * max(EOT index)+1 tokens (at least 16; bit-identical to the full context under causal
+ * attention and argmax pooling; CLIPGPU_TRIM_TEXT=0 disables). */
 int clipgpu_embed_tokens(clipgpu_engine* e, const int64_t* ids, const int64_t* mask, int64_t B, int64_t T,
                          float* out);
 
