@@ -737,10 +737,16 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_pipe_kernel(GemmParams 
       if (kt == 0) phase0(std::true_type{}, buf);
       else phase0(std::false_type{}, buf);
       // the DMA of step g+1 has landed once at most the later ops are outstanding: the
-      // DMA of step g+2 (3 stages), then the epilogue's stores and loads
-      constexpr int AHEAD = NS == 3 ? NP : 0;
-      if (after_full_epi) vm_wait<(EPI_VM + AHEAD < 63 ? EPI_VM + AHEAD : 63)>();
-      else vm_wait<AHEAD>();
+      // DMA of step g+2 (3 stages, if there is such a step), then the epilogue's stores
+      // and loads
+      constexpr int EW = EPI_VM < 63 ? EPI_VM : 63;
+      if (NS == 3 && g + 2 < total) {
+        if (after_full_epi) vm_wait<(EPI_VM + NP < 63 ? EPI_VM + NP : 63)>();
+        else vm_wait<NP>();
+      } else {
+        if (after_full_epi) vm_wait<EW>();
+        else vm_wait<0>();
+      }
       after_full_epi = false;
       __builtin_amdgcn_s_barrier();
       phase1(kt + 1 < nk, lds0 + ((g + 1) % NS) * STAGE);

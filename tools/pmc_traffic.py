@@ -19,7 +19,7 @@ import re
 import statistics
 import sys
 
-C_FC = re.compile(r"gemm_(bt|pipe)_kernelIDF16bLi\d+ELi\d+ELi\d+ELi\d+ELi0ELi1EEEv")
+C_FC = re.compile(r"gemm_(bt|pipe)_kernelIDF16bLi\d+ELi\d+ELi\d+ELi\d+ELi0ELi1E(?:Li\dE)?EEv")
 
 
 def per_launch_kb(d, counter):

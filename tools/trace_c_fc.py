@@ -22,7 +22,7 @@ rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]
 text0 = next((i for i, r in enumerate(rows) if "text_embed_ln" in r["Kernel_Name"]), len(rows))
 # the vision leg ends with its last head kernel (l2norm) before the text engine's autotune
 vis_end = max(i for i, r in enumerate(rows[:text0]) if "l2norm_kernel" in r["Kernel_Name"]) + 1
-fc_re = re.compile(r"gemm_(bt|pipe)_kernelIDF16bLi\d+ELi\d+ELi\d+ELi\d+ELi0ELi1EEEv")
+fc_re = re.compile(r"gemm_(bt|pipe)_kernelIDF16bLi\d+ELi\d+ELi\d+ELi\d+ELi0ELi1E(?:Li\dE)?EEv")
 fc = [r for r in rows[:vis_end] if fc_re.search(r["Kernel_Name"])]
 d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in fc]
 import os
