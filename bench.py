@@ -189,7 +189,8 @@ def main():
     tiles = (ctypes.c_int * 4)()
     _lib.check(_lib.lib().clipgpu_test_engine_tiles(ve._h, tiles))
     tile_names = {0: "heuristic", 1: "128x128", 2: "256x128", 3: "256x256", 4: "128x128pipe", 5: "128x64pipe",
-                  6: "64x128pipe", 7: "160x128pipe"}
+                  6: "64x128pipe", 7: "160x128pipe",
+                  8: "160x64pipe"}
     mx_names = {0: "heuristic", 2: "mx256x128", 3: "mx128x128"}  # fp8 engines: QKV / c_fc / c_proj sites
     fp8 = args.dtype == "fp8"
     gemm_tiles = {site: (mx_names if fp8 and site != "out_proj" else tile_names)[t]

@@ -920,6 +920,7 @@ hipError_t launch_tile(const GemmParams& p, hipStream_t s) {
       case TILE_128x64_PIPE: return launch_pipe<T, 128, 64, 2, 2, EPI, ACT>(p, s);
       case TILE_64x128_PIPE: return launch_pipe<T, 64, 128, 2, 2, EPI, ACT>(p, s);
       case TILE_160x128_PIPE: return launch_pipe<T, 160, 128, 2, 2, EPI, ACT>(p, s);
+      case TILE_160x64_PIPE: return launch_pipe<T, 160, 64, 2, 2, EPI, ACT>(p, s);
       default: return launch_pipe<T, 128, 128, 2, 2, EPI, ACT>(p, s);
     }
   }
@@ -931,6 +932,7 @@ hipError_t launch_tile(const GemmParams& p, hipStream_t s) {
       case TILE_128x64_PIPE: return launch_pipe<T, 128, 64, 2, 2, EPI, ACT>(p, s);
       case TILE_64x128_PIPE: return launch_pipe<T, 64, 128, 2, 2, EPI, ACT>(p, s);
       case TILE_160x128_PIPE: return launch_pipe<T, 160, 128, 2, 2, EPI, ACT>(p, s);
+      case TILE_160x64_PIPE: return launch_pipe<T, 160, 64, 2, 2, EPI, ACT>(p, s);
       default: break;
     }
   }

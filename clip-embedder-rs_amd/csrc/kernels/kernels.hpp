@@ -51,8 +51,10 @@ enum GemmTile {
   TILE_64x128_PIPE = 6,   // gemm_pipe_kernel: 4 waves (32x64 each), 48 KiB LDS, 3 blocks / CU
   TILE_160x128_PIPE = 7,  // gemm_pipe_kernel: 4 waves (80x64 each), 74 KiB LDS, 2 blocks / CU: M = 6400
                           // (a 128-image lane of ViT-B/32) is 40 row tiles, 960 tiles = 1.9 rounds of 512
-  TILE_LAST = TILE_160x128_PIPE,  // (last of the tiled kernels: the range the tuners and pins take)
-  TILE_SKINNY = 8,        // gemm_skinny_kernel: one wave per 16x16 block, M <= 256 (TILE_AUTO's pick there)
+  TILE_160x64_PIPE = 8,   // gemm_pipe_kernel: 4 waves (80x32 each), 58 KiB LDS, 2 blocks / CU: the N = 768
+                          // GEMMs at M = 6400 are 480 tiles, one round with two blocks on most CUs
+  TILE_LAST = TILE_160x64_PIPE,  // (last of the tiled kernels: the range the tuners and pins take)
+  TILE_SKINNY = 9,        // gemm_skinny_kernel: one wave per 16x16 block, M <= 256 (TILE_AUTO's pick there)
 };
 int pick_gemm_tile(int M, int N, int K);
 int device_cus();  // CUs of the current device (cached)
