@@ -140,6 +140,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f16", "fp8"])
     ap.add_argument("--no-fp8", action="store_true", help="skip the fp8 side measurement")
+    ap.add_argument("--breakdown", action="store_true", help="per-kernel-class ms per step (serialized lanes)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -217,6 +218,25 @@ def main():
     achieved = fc_flops / fc_avg_s / 1e12
     whole_tflops = vit_flops(B_VISION, executed=True) * args.steps / dt / 1e12 / 1.0
 
+    # Per-kernel-class time per step (lanes serialized, no graph): where the step goes.
+    breakdown = None
+    if args.breakdown:
+        from open_clip_inference.engine import PROFILE_CATEGORIES
+        bsteps = max(3, args.steps // 2)
+        for _ in range(2):
+            vision_step()
+        profile_enable(ve, PROFILE_CATEGORIES)
+        torch.cuda.synchronize()
+        for _ in range(bsteps):
+            vision_step()
+        torch.cuda.synchronize()
+        breakdown = {}
+        for c in PROFILE_CATEGORIES:
+            ms, n = profile_read(ve, c)
+            if n:
+                breakdown[c] = {"ms_per_step": round(ms / bsteps, 4), "launches_per_step": n // bsteps}
+        profile_enable(ve, [])
+
     # The fp8 (MX) engine of the same workload beside the bf16 value (BASELINE configs[4]'s
     # weight path on the bench model): throughput and the cosine of its embeddings to the
     # bf16 engine's on the same input (the fp8 path is lossy).  Not `value`.
@@ -285,6 +305,7 @@ def main():
             "gemm_tiles_env": ",".join(str(t) for t in tiles),
             "whole_forward_mfma_tflops_per_gpu": round(whole_tflops, 1),
             "last_layer_pruned": PRUNE_LAST,
+            **({"breakdown_serialized": breakdown} if breakdown is not None else {}),
             "text": text,
             "fp8": fp8_info,
             "cpu_baseline": cpu,

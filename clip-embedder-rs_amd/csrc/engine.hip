@@ -116,12 +116,17 @@ struct Replica {
 // Replayable forwards: one hipGraphExec per (entry point, input / output buffers, batch,
 // normalisation constants).  A forward is ~90 dependent launches per lane; replaying it
 // as one graph removes the per-launch host cost and most inter-kernel dispatch gaps.
+// Bounded: at kMax entries the least recently replayed one is destroyed, after every stream of
+// the replica (the capture stream and the lane streams a host-path slot replays on) has drained,
+// since any of them may still be running it.
 struct GraphCache {
   struct Entry {
     std::vector<uint64_t> key;
     hipGraphExec_t exec;
+    uint64_t last_use;
   };
   std::vector<Entry> entries;
+  uint64_t clock = 0;
   static constexpr size_t kMax = 32;
   void clear() {
     for (auto& en : entries) (void)hipGraphExecDestroy(en.exec);
@@ -173,6 +178,7 @@ struct clipgpu_engine {
   // Off by default: measured slower at ViT-B/32 lane sizes (profiles/r01_v6_split_sweep.txt:
   // the extra f32 slab round trip costs more than the better CU fill returns).
   int ksplit = 1;
+  int pipe3 = 0;  // CLIPGPU_GEMM_PIPE3=1: 3-stage LDS schedule for K-long one-round GEMMs (GemmParams::pipe3)
   clipgpu::TowerSpec spec;
   clipgpu::PreprocessCfg pre;
   clipgpu::DType dt = clipgpu::DT_BF16;
@@ -558,6 +564,7 @@ GemmParams site_gemm(const clipgpu_engine& e, const Replica& r, const LayerW& L,
     g.ksplit = e.ksplit;
     g.slab = r.slab;
   }
+  g.pipe3 = e.pipe3;
   return g;
 }
 
@@ -905,17 +912,28 @@ void run_graph(const clipgpu_engine& e, const Replica& r, const std::vector<uint
   hipStream_t gs = own ? st : r.stream;
   GraphCache& gc = *r.graphs;
   hipGraphExec_t exec = nullptr;
+  ++gc.clock;
   for (auto& en : gc.entries)
-    if (en.key == key) exec = en.exec;
+    if (en.key == key) {
+      exec = en.exec;
+      en.last_use = gc.clock;
+    }
+  if (!exec && gc.entries.size() >= GraphCache::kMax) {  // evict the least recently used graph
+    HIP_CHECK(hipStreamSynchronize(r.stream));
+    for (int i = 0; i < 4; ++i)
+      if (r.lane[i]) HIP_CHECK(hipStreamSynchronize(r.lane[i]));
+    if (!own) HIP_CHECK(hipStreamSynchronize(st));
+    size_t lru = 0;
+    for (size_t i = 1; i < gc.entries.size(); ++i)
+      if (gc.entries[i].last_use < gc.entries[lru].last_use) lru = i;
+    (void)hipGraphExecDestroy(gc.entries[lru].exec);
+    gc.entries.erase(gc.entries.begin() + (long)lru);
+  }
   if (!own) {
     HIP_CHECK(hipEventRecord(r.gin, st));
     HIP_CHECK(hipStreamWaitEvent(gs, r.gin, 0));
   }
   if (!exec) {
-    if (gc.entries.size() >= GraphCache::kMax) {
-      HIP_CHECK(hipStreamSynchronize(gs));
-      gc.clear();
-    }
     hipGraph_t g = nullptr;
     HIP_CHECK(hipStreamBeginCapture(gs, hipStreamCaptureModeRelaxed));
     try {
@@ -929,7 +947,7 @@ void run_graph(const clipgpu_engine& e, const Replica& r, const std::vector<uint
     const hipError_t ie = hipGraphInstantiate(&exec, g, nullptr, nullptr, 0);
     (void)hipGraphDestroy(g);
     HIP_CHECK(ie);
-    gc.entries.push_back({key, exec});
+    gc.entries.push_back({key, exec, gc.clock});
   }
   HIP_CHECK(hipGraphLaunch(exec, gs));
   if (!own) {
@@ -1349,7 +1367,9 @@ int clipgpu_create(const char* model_dir, int tower, const int* device_ids, int 
     if (const char* pl = getenv("CLIPGPU_PRUNE_LAST")) e->prune = pl[0] != '0';
     if (const char* tt = getenv("CLIPGPU_TRIM_TEXT")) e->trim = tt[0] != '0';
     const TowerSpec& s = e->spec;
+    if (!s.unsupported.empty()) throw ClipErr(CLIPGPU_ERR_CONFIG, s.unsupported);
     if (const char* sp = getenv("CLIPGPU_GEMM_SPLIT")) e->ksplit = sp[0] == '1' ? 2 : 1;
+    if (const char* p3 = getenv("CLIPGPU_GEMM_PIPE3")) e->pipe3 = p3[0] == '1' ? 1 : 0;
     if (s.heads <= 0 || s.width % s.heads || s.width % 64)
       throw ClipErr(CLIPGPU_ERR_CONFIG, "Configuration error: width must be a multiple of 64 and of heads");
     const int hd = s.width / s.heads;
@@ -1456,7 +1476,8 @@ int clipgpu_embed_tokens(clipgpu_engine* e, const int64_t* ids, const int64_t* m
         throw ClipErr(CLIPGPU_ERR_INVALID, "Inference error: token id " + std::to_string(ids[i]) + " out of range");
     // Sequence trimming: the pooled row of a sequence is its first argmax (EOT) token and
     // attention is causal, so tokens past the batch's last EOT never reach an embedding.
-    // The batch runs on its first Tc = max(EOT index) + 1 tokens (at least 16), bit-identical
+    // The batch runs on its first Tc = max(EOT index) + 1 tokens, rounded up to a multiple of 16,
+    // bit-identical
     // (test_text_trim_is_bit_exact).  CLIPGPU_TRIM_TEXT=0 disables.
     int64_t Tc = T;
     if (e->trim) {
@@ -1468,7 +1489,9 @@ int clipgpu_embed_tokens(clipgpu_engine* e, const int64_t* ids, const int64_t* m
           if (row[t] > row[best]) best = t;
         Tc = std::max<int64_t>(Tc, best + 1);
       }
-      Tc = std::min<int64_t>(T, std::max<int64_t>(Tc, 16));
+      // rounded up to a multiple of 16 (the causal key tiles are 16 wide, so any Tc past the
+      // last EOT gives the same bits): at most ceil(T / 16) lengths reach the graph cache
+      Tc = std::min<int64_t>(T, std::max<int64_t>((Tc + 15) / 16 * 16, 16));
     }
     std::vector<int64_t> trimmed;
     const int64_t* src = ids;

@@ -117,6 +117,29 @@ OpenClipConfig load_open_clip_config(const std::string& path) {
   ts.mlp_width = (int)(ts.width * getd(t, "mlp_ratio", 4.0));
   ts.embed_dim = c.embed_dim;
   ts.act = act_from(*mc, t);
+  // The text engine builds open_clip's TextTransformer as CLIP exports it: causal mask,
+  // argmax (EOT) pooling, linear projection without bias.  Host-side sequence trimming and
+  // last-layer pruning both rely on the causal mask + argmax pooling, so any other form (e.g.
+  // SigLIP's text_cfg: no_causal_mask, pool_type "last", proj_bias) is refused, not mis-run.
+  auto text_flag = [&](const char* key) {
+    const json::Value* f = t->get(key);
+    return f && !f->is_null() && f->as_bool(false);
+  };
+  auto text_str = [&](const char* key, const char* dflt) {
+    const json::Value* f = t->get(key);
+    return (f && !f->is_null()) ? f->as_str(dflt) : std::string(dflt);
+  };
+  if (text_flag("no_causal_mask"))
+    ts.unsupported = "Configuration error: text_cfg.no_causal_mask is not supported (causal text tower only)";
+  else if (text_str("pool_type", "argmax") != "argmax")
+    ts.unsupported = "Configuration error: text_cfg.pool_type '" + text_str("pool_type", "") +
+                     "' is not supported (argmax / EOT pooling only)";
+  else if (text_str("proj_type", "linear") != "linear")
+    ts.unsupported = "Configuration error: text_cfg.proj_type '" + text_str("proj_type", "") + "' is not supported";
+  else if (text_flag("proj_bias") || text_flag("embed_cls"))
+    ts.unsupported = "Configuration error: text_cfg.proj_bias / embed_cls are not supported";
+  else if (t->get("hf_model_name") && !t->get("hf_model_name")->is_null())
+    ts.unsupported = "Configuration error: HF text towers (text_cfg.hf_model_name) are not supported";
 
   const json::Value* pc = root->get("preprocess_cfg");
   if (!pc) throw std::runtime_error("Configuration error: preprocess_cfg missing");

@@ -47,6 +47,9 @@ struct TowerSpec {
   int tokens() const { return tower == TOWER_VISION ? grid() * grid() + (cls() ? 1 : 0) : context_length; }
   // text
   int context_length = 0, vocab_size = 0;
+  // Non-empty: the config asks for a tower form the engine does not build (clipgpu_create fails
+  // with this message; the other tower of the same folder still loads).
+  std::string unsupported;
 };
 
 struct OpenClipConfig {

@@ -768,14 +768,10 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_pipe_kernel(GemmParams 
   GEMM_STAMP_REAL(63);
 }
 
-// CLIPGPU_GEMM_PIPE3=1 enables the 3-stage schedule (off by default).  Alone it is a little
-// faster (ViT-B/32 c_proj 49.7 -> 48.3 us), but its 110 KiB of LDS per block keeps the other
-// lane's blocks off the CU, and the concurrent-lane forward measured 83.7k vs 85.5k img/s
-// (profiles/r01_v19_pipe3_ab.txt).
-inline bool pipe3_enabled() {
-  const char* e = getenv("CLIPGPU_GEMM_PIPE3");
-  return e && e[0] == '1';
-}
+// GemmParams::pipe3 = 1 (CLIPGPU_GEMM_PIPE3=1 at engine creation) enables the 3-stage schedule
+// (off by default).  Alone it is a little faster (ViT-B/32 c_proj 49.7 -> 48.3 us), but its
+// 110 KiB of LDS per block keeps the other lane's blocks off the CU, and the concurrent-lane
+// forward measured 83.7k vs 85.5k img/s (profiles/r01_v19_pipe3_ab.txt).
 
 template <typename T, int BM, int BN, int WGM, int WGN, int EPI, int ACT>
 hipError_t launch_cfg(const GemmParams& p, hipStream_t s) {
@@ -803,7 +799,7 @@ hipError_t launch_pipe(const GemmParams& p, hipStream_t s) {
   constexpr bool FITS3 = 3 * (BM + BN) * BK * 2 + 2048 <= 160 * 1024;
   if constexpr (FITS3) {
     const int nk = p.K / BK / (p.ksplit > 1 ? p.ksplit : 1);
-    if (pipe3_enabled() && p.K >= 1024 && nk >= 3 && ntiles <= device_cus() * per_cu(3)) {
+    if (p.pipe3 == 1 && p.K >= 1024 && nk >= 3 && ntiles <= device_cus() * per_cu(3)) {
       gemm_launch(gemm_pipe_kernel<T, BM, BN, WGM, WGN, EPI, ACT, 3>, ntiles, WGM * WGN * 64, s, p);
       return hipGetLastError();
     }

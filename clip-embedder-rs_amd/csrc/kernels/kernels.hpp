@@ -38,6 +38,8 @@ struct GemmParams {
                              // epilogue, slice s >= 1 stores its f32 partial to slab[(s-1)*M*ldo + m*ldo + n]
   float* slab;
   int diag;                  // stamp build only: bit 0 = skip epilogue stores (timing experiments)
+  int pipe3;                 // 1: K-long GEMMs that fit in one round of blocks take the 3-stage LDS schedule
+                             // (the engine reads CLIPGPU_GEMM_PIPE3 once at creation)
 };
 
 // Tile configurations of the MFMA GEMM.
@@ -54,7 +56,8 @@ enum GemmTile {
   TILE_160x64_PIPE = 8,   // gemm_pipe_kernel: 4 waves (80x32 each), 58 KiB LDS, 2 blocks / CU: the N = 768
                           // GEMMs at M = 6400 are 480 tiles, one round with two blocks on most CUs
   TILE_LAST = TILE_160x64_PIPE,  // (last of the tiled kernels: the range the tuners and pins take)
-  TILE_SKINNY = 9,        // gemm_skinny_kernel: one wave per 16x16 block, M <= 256 (TILE_AUTO's pick there)
+  TILE_SKINNY = 100,      // gemm_skinny_kernel: one wave per 16x16 block, M <= 256 (TILE_AUTO's pick there);
+                          // a fixed id outside the tunable range, so new tiles append without renumbering
 };
 int pick_gemm_tile(int M, int N, int K);
 int device_cus();  // CUs of the current device (cached)

@@ -36,10 +36,16 @@ DType dt_of(int dtype) {
   return dtype == CLIPGPU_DTYPE_BF16 ? DT_BF16 : DT_F16;
 }
 
-// CLIPGPU_TEST_TILE=1|2|3 forces a GEMM tile in clipgpu_test_gemm (tile-config coverage).
+// CLIPGPU_TEST_TILE forces a GEMM tile in clipgpu_test_gemm (tile-config coverage): a GemmTile
+// id (kernels.hpp: 0 auto, 1..TILE_LAST the tiled kernels, 100 skinny); the MX hooks take MxTile ids.
+// CLIPGPU_GEMM_PIPE3=1 selects the 3-stage schedule for the hooks' launches (read per call).
 int tile_override() {
   const char* e = getenv("CLIPGPU_TEST_TILE");
   return e ? atoi(e) : 0;
+}
+int pipe3_override() {
+  const char* e = getenv("CLIPGPU_GEMM_PIPE3");
+  return e && e[0] == '1' ? 1 : 0;
 }
 // K-slices for the f32-epilogue GEMM hooks (CLIPGPU_TEST_KSPLIT, default 1).
 int ksplit_override() {
@@ -88,6 +94,7 @@ int clipgpu_test_gemm(int dtype, int mode, int act, int64_t M, int64_t N, int64_
     if (bias) up(dB.p, bias, N * 4);
     GemmParams g{};
     g.tile = tile_override();
+    g.pipe3 = pipe3_override();
     g.A = dA.p; g.lda = K; g.W = dW.p; g.ldw = K; g.bias = bias ? dB.as<float>() : nullptr;
     g.out = dO.p; g.ldo = N; g.M = (int)M; g.N = (int)N; g.K = (int)K;
     int epi = EPI_STORE16;
@@ -167,6 +174,7 @@ int clipgpu_test_patch_embed(int dtype, int mode, int64_t B, int64_t S, int64_t 
     g.cls = 1;
     g.G = (int)G; g.pos = dpos.as<float>();
     g.tile = tile_override();
+    g.pipe3 = pipe3_override();
     TCHECK(launch_gemm(dt, A_ROWS, EPI_PATCH, 0, g, nullptr));
     TCHECK(hipDeviceSynchronize());
     down(x_out, dx.p, B * tokens * D * 4);
@@ -242,6 +250,7 @@ int clipgpu_test_gemm_bench(int dtype, int epi, int act, int64_t M, int64_t N, i
     GemmParams g{};
     g.A = dA.p; g.lda = K; g.W = dW.p; g.ldw = K; g.bias = dB.as<float>();
     g.out = dO.p; g.ldo = N; g.M = (int)M; g.N = (int)N; g.K = (int)K; g.tile = tile;
+    g.pipe3 = pipe3_override();
     const int e = epi == 1 ? EPI_RESID : (epi == 2 ? EPI_STORE32 : EPI_STORE16);
     const int ks = e == EPI_STORE16 ? 1 : ksplit_override();
     DevBuf dS(ks > 1 ? (size_t)(ks - 1) * M * N * 4 : 4);

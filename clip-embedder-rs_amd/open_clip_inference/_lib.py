@@ -25,6 +25,7 @@ DTYPE_FP8 = 2  # MX-fp8 trunk GEMMs (BASELINE configs[4] "fp8 MFMA weight path")
 _PROTOS = [
     ("clipgpu_last_error", c_char_p, []),
     ("clipgpu_abi_version", c_int, []),
+    ("clipgpu_build_source_hash", c_char_p, []),
     ("clipgpu_create", c_int, [c_char_p, c_int, POINTER(c_int), c_int, c_int, c_int, POINTER(c_void_p)]),
     ("clipgpu_destroy", None, [c_void_p]),
     ("clipgpu_embed_dim", c_int, [c_void_p]),
@@ -47,6 +48,7 @@ _PROTOS = [
     ("clipgpu_tokenizer_vocab_size", c_int64, [c_void_p]),
     ("clipgpu_similarity", c_int, [c_int, c_void_p, c_int64, c_void_p, c_int64, c_int64, c_float, c_float, c_int, c_int, c_void_p]),
     ("clipgpu_similarity_device", c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int64, c_float, c_float, c_int, c_int, c_void_p, c_void_p]),
+    ("clipgpu_facade_scores", c_int, [c_void_p, c_int64, c_void_p, c_int64, c_float, c_float, c_int, c_void_p]),
     ("clipgpu_profile_enable", c_int, [c_void_p, ctypes.c_uint]),
     ("clipgpu_profile_read", c_int, [c_void_p, c_int, POINTER(c_double), POINTER(c_int64)]),
     ("clipgpu_profile_category_name", c_char_p, [c_int]),
@@ -86,8 +88,22 @@ def lib():
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
+        _check_provenance(L)
         _lib = L
     return _lib
+
+
+def _check_provenance(L) -> None:
+    """The library must have been built from the sources next to it (binary provenance)."""
+    from ._source_hash import source_hash
+    fn = L.clipgpu_build_source_hash
+    fn.restype = c_char_p
+    fn.argtypes = []
+    built = fn().decode()
+    here = source_hash(os.path.dirname(_HERE))
+    if built != here:
+        raise ClipError(f"stale native library {LIB_PATH}: built from sources {built[:12]}, the tree has "
+                        f"{here[:12]}; rebuild with `make -C clip-embedder-rs_amd` (__graft_entry__.build())")
 
 
 def check(rc: int) -> None:

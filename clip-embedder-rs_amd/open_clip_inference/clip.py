@@ -49,25 +49,35 @@ class Clip:
         bias = 0.0 if mc.logit_bias is None else mc.logit_bias
         return np.float32(scale), np.float32(bias)
 
-    def _probs(self, logits: np.ndarray) -> np.ndarray:
+    def _activation(self) -> str:
         act = self.text.model_config.activation_function or "softmax"
-        if act == "sigmoid":
-            return np.array([self.sigmoid(float(l)) for l in logits], np.float32)
-        return self.softmax(logits)
+        return "sigmoid" if act == "sigmoid" else "softmax"
+
+    def _scores(self, embs: np.ndarray, query: np.ndarray, activation: str) -> np.ndarray:
+        """logits = embs . query, mul_add(scale, bias), then the activation -- the reference's
+        f32 arithmetic bit for bit (clipgpu_facade_scores, csrc/host/facade.cpp)."""
+        from ._lib import check, lib
+        from .engine import SIM_ACTIVATIONS
+        e = np.ascontiguousarray(embs, dtype=np.float32)
+        q = np.ascontiguousarray(query, dtype=np.float32).reshape(-1)
+        if e.ndim != 2 or e.shape[1] != q.shape[0]:
+            from .error import ShapeError
+            raise ShapeError(f"Shape error: {e.shape} . {q.shape}")
+        scale, bias = self._scale_bias()
+        out = np.empty(e.shape[0], np.float32)
+        check(lib().clipgpu_facade_scores(e.ctypes.data, e.shape[0], q.ctypes.data, e.shape[1], float(scale),
+                                          float(bias), SIM_ACTIVATIONS[activation], out.ctypes.data))
+        return out
 
     def compare(self, image, text: str) -> float:  # src/clip.rs:79-90
         v = self.vision.embed_image(image)
         t = self.text.embed_text(text)
-        sim = np.float32(np.dot(v, t))
-        scale, bias = self._scale_bias()
-        return float(np.float32(sim * scale + bias))
+        return float(self._scores(v[None], t, "logits")[0])
 
     def classify(self, image, labels: Sequence[str]) -> List[Tuple[str, float]]:  # src/clip.rs:92-132
         v = self.vision.embed_image(image)
         t = self.text.embed_texts(labels)
-        scale, bias = self._scale_bias()
-        logits = (t @ v).astype(np.float32) * scale + bias
-        probs = self._probs(logits)
+        probs = self._scores(t, v, self._activation())
         res = [(str(l), float(p)) for l, p in zip(labels, probs)]
         res.sort(key=lambda x: -x[1])  # stable, descending (sort_by partial_cmp)
         return res
@@ -75,9 +85,7 @@ class Clip:
     def rank_images(self, images, text: str) -> List[Tuple[int, float]]:  # src/clip.rs:134-170
         v = self.vision.embed_images(images)
         t = self.text.embed_text(text)
-        scale, bias = self._scale_bias()
-        logits = (v @ t).astype(np.float32) * scale + bias
-        probs = self._probs(logits)
+        probs = self._scores(v, t, self._activation())
         res = [(i, float(p)) for i, p in enumerate(probs)]
         res.sort(key=lambda x: -x[1])
         return res
@@ -113,12 +121,21 @@ class Clip:
         return out
 
     @staticmethod
-    def softmax(logits) -> np.ndarray:  # src/clip.rs:172-179
-        x = np.asarray(logits, np.float32)
-        m = np.float32(-np.inf) if x.size == 0 else x.max()
-        e = np.exp(x - m).astype(np.float32)
-        return (e / e.sum(dtype=np.float32)).astype(np.float32)
+    def softmax(logits) -> np.ndarray:  # src/clip.rs:172-179 (f32, sequential sum; facade.cpp)
+        from ._lib import check, lib
+        x = np.ascontiguousarray(logits, dtype=np.float32).reshape(-1)
+        if x.size == 0:
+            return x.copy()
+        one = np.ones(1, np.float32)  # logits = x[i] * 1 (exact) .mul_add(1, 0) (exact)
+        out = np.empty(x.size, np.float32)
+        check(lib().clipgpu_facade_scores(x.ctypes.data, x.size, one.ctypes.data, 1, 1.0, 0.0, 0, out.ctypes.data))
+        return out
 
     @staticmethod
     def sigmoid(logit: float) -> float:  # src/clip.rs:181-185
-        return float(np.float32(1.0) / (np.float32(1.0) + np.exp(np.float32(-logit))))
+        from ._lib import check, lib
+        x = np.array([logit], np.float32)
+        one = np.ones(1, np.float32)
+        out = np.empty(1, np.float32)
+        check(lib().clipgpu_facade_scores(x.ctypes.data, 1, one.ctypes.data, 1, 1.0, 0.0, 1, out.ctypes.data))
+        return float(out[0])

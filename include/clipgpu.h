@@ -52,6 +52,9 @@ typedef struct clipgpu_tokenizer clipgpu_tokenizer; /* CLIP BPE tokenizer (== to
 /* Thread-local message for the last failed call on this thread ("" if none). */
 const char* clipgpu_last_error(void);
 int clipgpu_abi_version(void);
+/* sha256 fingerprint of the sources this library was built from (binary provenance; the
+ * Python host refuses a library whose fingerprint differs from its tree's). */
+const char* clipgpu_build_source_hash(void);
 
 /* ---- engine lifecycle ----------------------------------------------------------------
  * Replaces OnnxSession::new (src/onnx.rs:13-30) as called by VisionEmbedder::from_local_dir
@@ -161,6 +164,19 @@ int clipgpu_similarity(int device, const float* img, int64_t n_img, const float*
 int clipgpu_similarity_device(const float* d_img, int64_t n_img, const float* d_txt, int64_t n_txt, int64_t E,
                               float logit_scale, float logit_bias, int activation, int axis, float* d_out,
                               void* stream);
+
+/* ---- Clip facade scores on the host, the reference's f32 arithmetic bit for bit -----------
+ * src/clip.rs:79-185 as the crate computes it (ndarray 0.17 without BLAS, Cargo.toml:14):
+ * out[i] = unrolled_dot(embs[i], query).mul_add(logit_scale, logit_bias) -- ndarray's
+ * eight-accumulator numeric_util::unrolled_dot, one fused multiply-add -- then
+ *   CLIPGPU_SIM_SOFTMAX: max (f32::max fold) -> exp(x - max) -> sequential f32 sum -> x / sum
+ *     over the n scores (classify :92-132 with embs = label embeddings, query = the image;
+ *     rank_images :134-170 with embs = image embeddings, query = the text);
+ *   CLIPGPU_SIM_SIGMOID: 1 / (1 + exp(-l)) (:181-185);  CLIPGPU_SIM_LOGITS: the logits (compare,
+ *     :79-90, n = 1).
+ * embs [n][E], query [E], out [n] f32; no GPU involved.  n == 0 -> "Empty batch". */
+int clipgpu_facade_scores(const float* embs, int64_t n, const float* query, int64_t E, float logit_scale,
+                          float logit_bias, int activation, float* out);
 
 /* ---- live kernel timing -------------------------------------------------------------------
  * Records HIP events around every launch whose category bit is set in `mask` (on the launch

@@ -17,7 +17,8 @@ extern "C" {
 
 /* out[M][N] = act(A[M][K] . W[N][K]^T + bias[N]) (act: 0 none, 1 quick_gelu, 2 gelu, 3 gelu_tanh).
  * mode 0: 16-bit output (returned as f32); mode 1: residual (out = resid + ...); mode 2: f32 output.
- * bias and resid may be NULL. */
+ * bias and resid may be NULL.  CLIPGPU_TEST_TILE = a GemmTile id (kernels.hpp: 0 auto, 1..8 the tiled
+ * kernels, 100 skinny) forces the tile; CLIPGPU_GEMM_PIPE3=1 the 3-stage schedule. */
 int clipgpu_test_gemm(int dtype, int mode, int act, int64_t M, int64_t N, int64_t K, const float* A,
                       const float* W, const float* bias, const float* resid, float* out);
 
@@ -72,7 +73,7 @@ int clipgpu_test_layernorm_mx(int64_t rows, int64_t D, float eps, const float* x
 /* MX-fp8 GEMM on given MX operands A (Aq [M][K], As [M][K/32]) and W (Wq [N][K], Ws [N][K/32]):
  * mode 0: act(A.W^T + bias) as 16-bit (returned as f32 in out); 1: out = resid + A.W^T + bias (f32);
  * 2: f32 A.W^T + bias; 3: MX-fp8 of act(A.W^T + bias) into outq [M][N] / outs [M][N/32].
- * K % 128 == 0, N % 32 == 0; CLIPGPU_TEST_TILE picks the tile (0 auto, 2 256x128, 3 128x128). */
+ * K % 128 == 0, N % 32 == 0; CLIPGPU_TEST_TILE picks the MxTile (0 auto, 2 256x128, 3 128x128). */
 int clipgpu_test_gemm_mx(int dtype, int mode, int act, int64_t M, int64_t N, int64_t K, const uint8_t* Aq,
                          const uint8_t* As, const uint8_t* Wq, const uint8_t* Ws, const float* bias,
                          const float* resid, float* out, uint8_t* outq, uint8_t* outs);

@@ -132,3 +132,44 @@ def test_param_inventory_matches_oracle(cfg_name):
             _lib.check(_lib.lib().clipgpu_test_read_weights(d.encode(), tower, name.encode(), out.ctypes.data,
                                                             out.size))
             assert np.array_equal(out, ref.ravel()), name
+
+
+@pytest.mark.parametrize("extra,msg", [({"no_causal_mask": True}, "no_causal_mask"),
+                                       ({"pool_type": "last"}, "pool_type 'last'"),
+                                       ({"proj_type": "mlp"}, "proj_type 'mlp'"),
+                                       ({"proj_bias": True}, "proj_bias"),
+                                       ({"hf_model_name": "google/siglip"}, "hf_model_name")])
+def test_unsupported_text_tower_forms_are_refused(extra, msg):
+    """The text engine's trimming and last-layer pruning assume open_clip's causal,
+    argmax-pooled text tower: any other text_cfg form (SigLIP's, HF towers) is a Configuration
+    error at clipgpu_create, raised before any device call (runs on CPU)."""
+    import json
+    from open_clip_inference import _lib
+    from open_clip_inference.engine import Engine
+    from open_clip_inference.error import ConfigError
+    cfg = json.loads(json.dumps(TINY_CFG))
+    cfg["model_cfg"]["text_cfg"].update(extra)
+    d = make_model_dir(cfg)
+    with pytest.raises(ConfigError, match=msg):
+        Engine(d, _lib.TOWER_TEXT, [0], "bf16", 8)
+    # the default form passes the check (and then fails only for want of a GPU here)
+    d = make_model_dir(TINY_CFG)
+    try:
+        Engine(d, _lib.TOWER_TEXT, [0], "bf16", 8).close()
+    except ConfigError as e:  # pragma: no cover
+        raise AssertionError(e)
+    except Exception:
+        pass
+
+
+def test_library_provenance_is_checked(monkeypatch):
+    """The loader refuses a library built from sources other than the tree's (a stale
+    lib/libclipgpu.so travels with the tree to the GPU box)."""
+    from open_clip_inference import _lib, _source_hash
+    from open_clip_inference.error import ClipError
+    L = _lib.lib()
+    assert L.clipgpu_build_source_hash().decode() == _source_hash.source_hash(os.path.dirname(os.path.dirname(
+        os.path.abspath(_lib.__file__))))
+    monkeypatch.setattr(_source_hash, "source_hash", lambda d: "0" * 64)
+    with pytest.raises(ClipError, match="stale native library"):
+        _lib._check_provenance(L)

@@ -109,6 +109,43 @@ def test_clip_facade_and_integration_shape(model):
     assert clip.get_model_config().logit_scale == 100.0
 
 
+def test_clip_classify_vit_b32_dims():
+    """BASELINE configs[0] plumbing at the north-star model's dims (ViT-B/32-224 vision, 12 x 512
+    text tower, 77-token context): Clip.classify(cat_face, three labels) as
+    tests/integration_test.rs:16-29 calls it, against the oracle chain (preprocess_ref ->
+    clip_ref, tokenizer_ref -> clip_ref -> facade_ref).  Seeded weights, so the semantic
+    p > 0.99 assertion is replaced by agreement with the oracle facade."""
+    from open_clip_inference import Clip
+    from oracle.model_spec import VIT_B_32_CFG
+    with open(TOKJ, encoding="utf-8") as f:
+        tj = f.read()
+    cfg = json.loads(json.dumps(VIT_B_32_CFG))
+    d = make_model_dir(cfg, seed=1234, tokenizer_json=tj, model_config=OPENAI_MODEL_CONFIG)
+    clip = Clip.from_local_dir(d).build()
+    cat = images()[0]
+    labels = ["A photo of a cat", "A photo of a dog", "A photo of a beignet"]
+    res = clip.classify(cat, labels)
+    v = vision_spec_from_cfg(cfg["model_cfg"])
+    t = text_spec_from_cfg(cfg["model_cfg"])
+    px = preprocess_ref.preprocess(cat, v.image_size, OPENAI_MEAN, OPENAI_STD)[None]
+    img_ref = clip_ref.encode_image(weights.vision_weights(v, 1234), v, px)
+    tok = ClipTokenizerRef(TOKJ, t.context_length, 0)
+    ids = np.array([tok.encode(x)[0] for x in labels], np.int64)
+    txt_ref = clip_ref.encode_text(weights.text_weights(t, 1234), t, ids)
+    img = clip.vision.embed_image(cat)
+    txt = clip.text.embed_texts(labels)
+    assert clip_ref.cosine_rows(img[None], img_ref).min() >= COS_TOL
+    assert clip_ref.cosine_rows(txt, txt_ref).min() >= COS_TOL
+    ref = facade_ref.classify(img_ref[0], txt_ref, labels, 100.0, 0.0)
+    assert sorted(l for l, _ in res) == sorted(labels)
+    assert abs(sum(p for _, p in res) - 1) < 1e-5
+    # logit_scale 100 amplifies the <= 1e-4 cosine gap of each embedding: compare at 0.05
+    assert np.allclose([p for _, p in sorted(res)], [p for _, p in sorted(ref)], atol=0.05)
+    # and the facade on the engine's own embeddings is the reference's arithmetic exactly
+    exact = facade_ref.classify_f32_exact(img, txt, labels, 100.0, 0.0)
+    assert [(l, np.float32(p)) for l, p in res] == [(l, np.float32(p)) for l, p in exact]
+
+
 def test_duplicate_and_multi_replica_handle(model):
     """duplicate() gives an independent handle; a handle with devices [0, 0] exercises the
     multi-device row-sharding path (two replicas, two host workers) on one GPU."""

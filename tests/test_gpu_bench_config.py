@@ -1,0 +1,97 @@
+"""The exact configurations `bench.py` measures, checked against the fp64 oracle.
+
+`bench.py`'s headline (BASELINE.json configs[1]) and its text leg (configs[2]) run engines
+built exactly as the bench builds them: the bench's own model folder and seeded inputs,
+max_batch 256 / 1024, the default lane split (2), the default two-pass tile autotune, the
+hipGraph-replayed device entry point on the caller's stream.  Sampled rows cover both lanes
+and the lane boundary; every row of the batch is checked for unit norm, and a second replay
+must give the same bits.  Tolerance: cosine >= 0.9999 per row (north_star, tests/helpers.py).
+"""
+import numpy as np
+import pytest
+
+from oracle import clip_ref, weights
+from oracle.model_spec import VIT_B_32_CFG, text_spec_from_cfg, vision_spec_from_cfg
+from tests.helpers import COS_TOL
+
+pytestmark = pytest.mark.gpu
+
+VISION_ROWS = [0, 1, 63, 126, 127, 128, 129, 191, 254, 255]
+TEXT_ROWS = [0, 1, 255, 510, 511, 512, 513, 767, 1022, 1023]
+
+
+@pytest.fixture(scope="module")
+def bench_mod():
+    import bench
+    assert bench.CFG["model_cfg"] == VIT_B_32_CFG["model_cfg"]
+    return bench
+
+
+def _tiles(engine):
+    from ctypes import c_int
+    from open_clip_inference import _lib
+    t = (c_int * 4)()
+    _lib.check(_lib.lib().clipgpu_test_engine_tiles(engine._h, t))
+    return list(t)
+
+
+def test_bench_vision_config_matches_oracle(bench_mod, monkeypatch):
+    import torch
+    from open_clip_inference import _lib
+    from open_clip_inference.engine import Engine
+    for var in ("CLIPGPU_LANES", "CLIPGPU_GEMM_TILES", "CLIPGPU_GEMM_AUTOTUNE", "CLIPGPU_TUNE_FORWARD",
+                "CLIPGPU_PRUNE_LAST", "CLIPGPU_GRAPHS", "CLIPGPU_GEMM_SPLIT"):
+        monkeypatch.delenv(var, raising=False)
+    B = bench_mod.B_VISION
+    dev = torch.device("cuda", 0)
+    ve = Engine(bench_mod.make_model_dir(), _lib.TOWER_VISION, [0], "bf16", B)
+    px, _ = bench_mod.synth_inputs(0, dev)
+    out = torch.empty((B, 512), device=dev, dtype=torch.float32)
+    s = torch.cuda.current_stream(dev)
+    ve.embed_pixels_device(px.data_ptr(), B, out.data_ptr(), s.cuda_stream)
+    torch.cuda.synchronize()
+    first = out.cpu().numpy()
+    out.zero_()
+    ve.embed_pixels_device(px.data_ptr(), B, out.data_ptr(), s.cuda_stream)  # graph replay
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    assert np.array_equal(first, got)
+    assert np.all(np.abs(np.linalg.norm(got, axis=1) - 1) < 1e-5)
+    v = vision_spec_from_cfg(VIT_B_32_CFG["model_cfg"])
+    ref = clip_ref.encode_image(weights.vision_weights(v, 1234), v, px[VISION_ROWS].cpu().numpy())
+    cos = clip_ref.cosine_rows(got[VISION_ROWS], ref)
+    print("bench vision tiles", _tiles(ve), "cos min", float(cos.min()))
+    assert cos.min() >= COS_TOL, (cos.min(), _tiles(ve))
+    ve.close()
+
+
+def test_bench_text_config_matches_oracle(bench_mod, monkeypatch):
+    import torch
+    from open_clip_inference import _lib
+    from open_clip_inference.engine import Engine
+    for var in ("CLIPGPU_LANES", "CLIPGPU_GEMM_TILES", "CLIPGPU_GEMM_AUTOTUNE", "CLIPGPU_TUNE_FORWARD",
+                "CLIPGPU_PRUNE_LAST", "CLIPGPU_GRAPHS", "CLIPGPU_GEMM_SPLIT"):
+        monkeypatch.delenv(var, raising=False)
+    B = bench_mod.B_TEXT
+    dev = torch.device("cuda", 0)
+    te = Engine(bench_mod.make_model_dir(), _lib.TOWER_TEXT, [0], "bf16", B)
+    _, ids = bench_mod.synth_inputs(0, dev)
+    out = torch.empty((B, 512), device=dev, dtype=torch.float32)
+    s = torch.cuda.current_stream(dev)
+    te.embed_tokens_device(ids.data_ptr(), B, out.data_ptr(), s.cuda_stream)
+    torch.cuda.synchronize()
+    first = out.cpu().numpy()
+    te.embed_tokens_device(ids.data_ptr(), B, out.data_ptr(), s.cuda_stream)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    assert np.array_equal(first, got)
+    assert np.all(np.abs(np.linalg.norm(got, axis=1) - 1) < 1e-5)
+    t = text_spec_from_cfg(VIT_B_32_CFG["model_cfg"])
+    ref = clip_ref.encode_text(weights.text_weights(t, 1234), t, ids[TEXT_ROWS].cpu().numpy())
+    cos = clip_ref.cosine_rows(got[TEXT_ROWS], ref)
+    print("bench text tiles", _tiles(te), "cos min", float(cos.min()))
+    assert cos.min() >= COS_TOL, (cos.min(), _tiles(te))
+    # the host entry point (trimming off: full-length rows) gives the same bits as the device one
+    host = te.embed_tokens(ids[:64].cpu().numpy())
+    assert np.array_equal(host, got[:64])
+    te.close()

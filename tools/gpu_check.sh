@@ -27,6 +27,11 @@ for s in $STEPS; do
       run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
     bench)
       run bench 600 python bench.py --steps 20 --warmup 5 || exit $? ;;
+    breakdown)
+      run breakdown 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-fp8 --no-text --breakdown || exit $? ;;
+    vtrace)  # kernel trace of the vision leg alone (per-kernel durations of the timed steps)
+      run vtrace 300 rocprofv3 --kernel-trace --stats -d gpurun_out/vtrace -o run --output-format csv -- \
+          python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-fp8 --no-text || exit $? ;;
     prof)
       run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
           python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline || exit $?
