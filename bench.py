@@ -11,7 +11,9 @@ with f32 accumulation / residual stream / LayerNorm / softmax.
 
 Also reported: texts/s for configs[2] (text tower, batch 1024 x 77 tokens);
 roofline of the dominant kernel (c_fc GEMM) from HIP events on the launch stream;
-CPU baseline = the numpy oracle (fp32 port) on a bounded sample on rank 0.
+end-to-end legs through the host-buffer entry points (PCIe included; N = 1);
+CPU baseline = the fp32 torch CPU port of the same graphs (oracle/torch_cpu.py) on a bounded
+sample of the same inputs on rank 0, which also checks the GPU rows (cosine).
 
 Launch: python bench.py [--gpus 1 --steps K --warmup W]   (N > 1: torch.distributed.run)
 """
@@ -95,40 +97,94 @@ def synth_inputs(rank, device):
     return px.to(device), ids.to(device)
 
 
-def cpu_baseline(target_s=20.0):
-    """Numpy oracle (fp32 port of the reference graph) on a bounded sample."""
-    from oracle import clip_ref, weights
-    from oracle.model_spec import vision_spec_from_cfg
+def host_info():
+    """Host cores as the CPU leg sees them (the GPU box's CPU share, not the machine's count)."""
+    model = ""
     try:
-        from threadpoolctl import threadpool_info
-        cores = max([int(i.get("num_threads", 1)) for i in threadpool_info()] or [1])
-    except Exception:
-        cores = os.cpu_count() or 1
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"nproc_affinity": len(os.sched_getaffinity(0)), "cpu_count": os.cpu_count(), "cpu_model": model,
+            "torch_threads": torch.get_num_threads(), "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS")}
+
+
+def cpu_baseline(px_host, ids_host, gpu_vision, gpu_text, fp8_vision=None, target_s=12.0):
+    """The CPU leg (rank 0, N = 1): the reference's graphs in fp32 on torch's CPU kernels
+    (oracle/torch_cpu.py -- the closest buildable proxy of the reference's ONNX Runtime CPU path,
+    src/onnx.rs:18-22), all host threads torch has, on the bench's own inputs: a bounded sample
+    of the vision batch and of the text batch.  Its embeddings also check the GPU rows of the
+    same inputs (cosine), which ties the timed numbers to a correctness check."""
+    from oracle import torch_cpu, weights
+    from oracle.model_spec import text_spec_from_cfg, vision_spec_from_cfg
     v = vision_spec_from_cfg(CFG["model_cfg"])
-    P = {k: a.astype(np.float32) for k, a in weights.vision_weights(v, 1234).items()}
-    rng = np.random.default_rng(0)
-    px = rng.standard_normal((4, 3, 224, 224)).astype(np.float32)
-    clip_ref.encode_image(P, v, px[:1], dtype=np.float32)  # warm
-    t0 = time.perf_counter()
-    clip_ref.encode_image(P, v, px, dtype=np.float32)
-    per_img = (time.perf_counter() - t0) / 4
-    n = int(max(16, min(1024, target_s / max(per_img, 1e-6)))) // 16 * 16
-    px = rng.standard_normal((n, 3, 224, 224)).astype(np.float32)
-    t0 = time.perf_counter()
-    for i in range(0, n, 16):
-        clip_ref.encode_image(P, v, px[i:i + 16], dtype=np.float32)
-    dt = time.perf_counter() - t0
-    return {"value": round(n / dt, 2), "unit": "images/s", "cores": cores, "kind": "port",
-            "sample": f"{n} synthetic 224x224 images, ViT-B/32 vision tower, numpy fp32 oracle "
-                      f"(oracle/clip_ref.py), batches of 16, {dt:.1f} s"}
+    t = text_spec_from_cfg(CFG["model_cfg"])
+    vm = torch_cpu.VisionCPU(weights.vision_weights(v, 1234), v)
+    tm = torch_cpu.TextCPU(weights.text_weights(t, 1234), t)
+
+    def run(model, data, budget, chunk):
+        model(data[:2])  # warm
+        t0 = time.perf_counter()
+        model(data[:chunk])
+        per = (time.perf_counter() - t0) / chunk
+        n = int(min(len(data), max(chunk, budget / max(per, 1e-9)))) // chunk * chunk
+        outs = []
+        t0 = time.perf_counter()
+        for i in range(0, n, chunk):
+            outs.append(model(data[i:i + chunk]))
+        return np.concatenate(outs), time.perf_counter() - t0
+
+    def cos_min(a, b):
+        a = np.asarray(a, np.float64)
+        b = np.asarray(b, np.float64)
+        return float(((a * b).sum(1) / (np.linalg.norm(a, axis=1) * np.linalg.norm(b, axis=1))).min())
+
+    ve, vdt = run(vm, px_host, target_s, 32)
+    te, tdt = run(tm, ids_host, target_s, 128)
+    cores = torch.get_num_threads()
+    res = {"value": round(len(ve) / vdt, 2), "unit": "images/s", "cores": cores, "kind": "port",
+           "sample": f"{len(ve)} of the bench's 256 synthetic 224x224 images (batches of 32), ViT-B/32 vision tower, "
+                     f"fp32 torch CPU port of the graph (oracle/torch_cpu.py), {cores} threads, {vdt:.1f} s",
+           "host": host_info(),
+           "text": {"value": round(len(te) / tdt, 2), "unit": "texts/s",
+                    "sample": f"{len(te)} of the bench's 1024 x 77-token sequences (batches of 128), {tdt:.1f} s"},
+           "gpu_vs_cpu_cos_min": {"vision_bf16": cos_min(gpu_vision[:len(ve)], ve),
+                                  "text_bf16": cos_min(gpu_text[:len(te)], te) if gpu_text is not None else None}}
+    if fp8_vision is not None:
+        res["gpu_vs_cpu_cos_min"]["vision_fp8"] = cos_min(fp8_vision[:len(ve)], ve)
+    return res
 
 
 def load_traffic():
+    """HBM bytes per c_fc launch: NOT measured in this run -- read from the committed PMC summary
+    (separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench, gfx950 FETCH_SIZE x2
+    correction, tools/pmc_traffic.py); its `source` names the run it came from."""
     p = os.path.join(ROOT, "profiles", "pmc_c_fc.json")
     if os.path.exists(p):
         with open(p) as f:
-            return json.load(f).get("hbm_bytes_per_launch")
-    return None
+            d = json.load(f)
+        return d.get("hbm_bytes_per_launch"), "profiles/pmc_c_fc.json: " + d.get("source", "rocprofv3 PMC passes")
+    return None, None
+
+
+def host_leg(engine, kind, host, steps):
+    """Host-buffer throughput through the C ABI (pinned staging + H2D + forward + D2H, PCIe
+    included), units per second over `steps` calls after one warm call."""
+    call = {"u8": lambda: engine.embed_u8(host, CFG["preprocess_cfg"]["mean"], CFG["preprocess_cfg"]["std"]),
+            "f32": lambda: engine.embed_pixels(host),
+            "tokens": lambda: engine.embed_tokens(host)}[kind]
+    call()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        call()
+    dt = time.perf_counter() - t0
+    entry = {"u8": "clipgpu_embed_u8 (u8 NHWC [256,224,224,3])", "f32": "clipgpu_embed_pixels (f32 NCHW [256,3,224,224])",
+             "tokens": "clipgpu_embed_tokens (i64 ids [1024,77], full-length rows: no trimming)"}[kind]
+    return {"value": round(len(host) * steps / dt, 1), "unit": "texts/s" if kind == "tokens" else "images/s",
+            "ms_per_call": round(dt * 1e3 / steps, 3), "entry": entry}
 
 
 def main():
@@ -141,6 +197,7 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f16", "fp8"])
     ap.add_argument("--no-fp8", action="store_true", help="skip the fp8 side measurement")
     ap.add_argument("--breakdown", action="store_true", help="per-kernel-class ms per step (serialized lanes)")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the host-buffer (PCIe-inclusive) legs")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -241,6 +298,7 @@ def main():
     # weight path on the bench model): throughput and the cosine of its embeddings to the
     # bf16 engine's on the same input (the fp8 path is lossy).  Not `value`.
     fp8_info = None
+    fout_host = None
     if world == 1 and not fp8 and not args.no_fp8:
         fe = Engine(mdir, _lib.TOWER_VISION, [local], "fp8", B_VISION)
         fout = torch.empty_like(out)
@@ -251,13 +309,20 @@ def main():
         vision_step()
         torch.cuda.synchronize()
         cos = torch.nn.functional.cosine_similarity(fout, out, dim=1)
+        fout_host = fout.cpu().numpy()
+        f_tflops = vit_flops(B_VISION, executed=True) * args.steps / fdt / 1e12
         fp8_info = {"value": round(B_VISION * args.steps / fdt, 1), "unit": "images/s",
                     "ms_per_step": round(fdt * 1e3 / args.steps, 3),
+                    "whole_forward_tflops": round(f_tflops, 1),
+                    "frac_of_mx_fp8_peak": round(f_tflops / (2 * PEAK_BF16_TFLOPS), 4),
                     "cos_vs_bf16_min": round(float(cos.min()), 6), "cos_vs_bf16_mean": round(float(cos.mean()), 6),
-                    "note": "MX-fp8 QKV/c_fc/c_proj (e4m3 + E8M0 per 32, v_mfma_scale_f32_32x32x64_f8f6f4)"}
+                    "note": "MX-fp8 QKV/c_fc/c_proj (e4m3 + E8M0 per 32, v_mfma_scale_f32_32x32x64_f8f6f4); "
+                            "frac against the 5 PF block-scaled MX peak (the mix also runs bf16 GEMMs); "
+                            "cosine vs the fp32 CPU port in cpu_baseline.gpu_vs_cpu_cos_min.vision_fp8"}
         fe.close()
 
     text = None
+    tout_host = None
     if not args.no_text:
         te = Engine(mdir, _lib.TOWER_TEXT, [local], args.dtype, B_TEXT)
         tout = torch.empty((B_TEXT, 512), device=dev, dtype=torch.float32)
@@ -273,12 +338,31 @@ def main():
                 "value": round(world * B_TEXT * tsteps / tdt, 1), "unit": "texts/s",
                 "ms_per_step": round(tdt * 1e3 / tsteps, 3),
                 "mfma_tflops": round(text_flops(B_TEXT, executed=True) * world * tsteps / tdt / 1e12 / world, 1)}
+        text["frac_of_peak"] = round(text["mfma_tflops"] / PEAK_BF16_TFLOPS, 4)
+        tout_host = tout.cpu().numpy()
+        if world == 1 and not args.no_e2e:
+            text_e2e = host_leg(te, "tokens", ids.cpu().numpy(), max(3, args.steps // 4))
         te.close()
+
+    # End-to-end legs (host buffers in, host embeddings out, PCIe included; not `value`): the
+    # reference's embed_images / embed_texts hand host arrays to the session (src/vision.rs:102-113,
+    # src/text.rs:150-166); here through the C ABI's host entry points with pinned-staging overlap.
+    e2e = None
+    if world == 1 and not args.no_e2e:
+        g = torch.Generator(device="cpu").manual_seed(1000 + rank)
+        u8_host = torch.randint(0, 256, (B_VISION, 224, 224, 3), dtype=torch.uint8, generator=g).numpy()
+        e2e = {"vision_u8_host": host_leg(ve, "u8", u8_host, max(3, args.steps // 4)),
+               "vision_f32_host": host_leg(ve, "f32", px.cpu().numpy(), max(3, args.steps // 4))}
+        if text is not None:
+            e2e["text_ids_host"] = text_e2e
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline()
+        vision_step()
+        torch.cuda.synchronize()
+        cpu = cpu_baseline(px.cpu().numpy(), ids.cpu().numpy(), out.cpu().numpy(), tout_host, fout_host)
 
+    traffic, traffic_src = load_traffic() if not fp8 else (None, None)
     if rank == 0:
         line = {
             "metric": "images/sec embedding, ViT-B/32-224 vision tower, batch 256 per GPU",
@@ -299,14 +383,17 @@ def main():
                        "parallelism": f"dp{world}, {os.environ.get('CLIPGPU_LANES', '2')} concurrent sub-batch lanes/GPU" + (" + RCCL all-gather of [B,512] embeddings" if world > 1 else "")},
             "roofline": {"bound": "mfma", "kernel": f"c_fc GEMM ({int(fc_rows_per_launch)}x3072x768, +QuickGELU, tile {gemm_tiles['c_fc']})",
                          "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
-                         "frac": round(achieved / peak, 4), "traffic": load_traffic() if not fp8 else None,
+                         "frac": round(achieved / peak, 4), "traffic": traffic,
+                         "traffic_source": traffic_src,
                          "launches_timed": fc_n, "avg_launch_us": round(fc_avg_s * 1e6, 2)},
             "gemm_tiles": gemm_tiles,
             "gemm_tiles_env": ",".join(str(t) for t in tiles),
             "whole_forward_mfma_tflops_per_gpu": round(whole_tflops, 1),
+            "whole_forward_frac_of_peak": round(whole_tflops / PEAK_BF16_TFLOPS, 4),
             "last_layer_pruned": PRUNE_LAST,
             **({"breakdown_serialized": breakdown} if breakdown is not None else {}),
             "text": text,
+            "end_to_end": e2e,
             "fp8": fp8_info,
             "cpu_baseline": cpu,
         }

@@ -88,3 +88,22 @@ def test_so400m_siglip2_spec():
     assert (v.patch_size, v.width, v.layers, v.heads, v.mlp_width, v.tokens, v.head_dim) == \
         (16, 1152, 27, 16, 4304, 576, 72)
     assert v.act == "gelu_tanh" and v.ln_eps == 1e-6 and v.embed_dim == 1152
+
+
+@pytest.mark.parametrize("cfg_name", ["TINY_CFG", "VIT_B_32_CFG"])
+def test_torch_cpu_port_matches_oracle(cfg_name):
+    """oracle/torch_cpu.py (the fp32 CPU baseline bench.py times) computes the fp64 oracle's
+    embeddings to fp32 accuracy."""
+    from oracle import model_spec, torch_cpu
+    from oracle.model_spec import text_spec_from_cfg, vision_spec_from_cfg
+    cfg = getattr(model_spec, cfg_name)
+    v = vision_spec_from_cfg(cfg["model_cfg"])
+    t = text_spec_from_cfg(cfg["model_cfg"])
+    Pv = weights.vision_weights(v, 5)
+    Pt = weights.text_weights(t, 5)
+    px = np.random.default_rng(3).standard_normal((2, 3, v.image_size, v.image_size)).astype(np.float32)
+    ids = weights.synth_token_ids(4, 3, t.context_length, t.vocab_size, t.vocab_size - 2, t.vocab_size - 1,
+                                  random_eot=True)
+    cv = clip_ref.cosine_rows(torch_cpu.VisionCPU(Pv, v)(px), clip_ref.encode_image(Pv, v, px))
+    ct = clip_ref.cosine_rows(torch_cpu.TextCPU(Pt, t)(ids), clip_ref.encode_text(Pt, t, ids))
+    assert cv.min() > 0.999999 and ct.min() > 0.999999, (cv, ct)

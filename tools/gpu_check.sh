@@ -28,10 +28,10 @@ for s in $STEPS; do
     bench)
       run bench 600 python bench.py --steps 20 --warmup 5 || exit $? ;;
     breakdown)
-      run breakdown 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-fp8 --no-text --breakdown || exit $? ;;
+      run breakdown 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-fp8 --no-text --no-e2e --breakdown || exit $? ;;
     vtrace)  # kernel trace of the vision leg alone (per-kernel durations of the timed steps)
       run vtrace 300 rocprofv3 --kernel-trace --stats -d gpurun_out/vtrace -o run --output-format csv -- \
-          python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-fp8 --no-text || exit $? ;;
+          python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-fp8 --no-text --no-e2e || exit $? ;;
     prof)
       run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
           python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline || exit $?
@@ -41,10 +41,10 @@ for s in $STEPS; do
       export CLIPGPU_GEMM_TILES=$(python3 -c "import json;print([json.loads(l) for l in open('gpurun_out/bench.log') if l.startswith('{')][-1]['gemm_tiles_env'])") || exit 1
       for C in FETCH_SIZE WRITE_SIZE; do
         run pmc_$C 600 rocprofv3 --pmc $C --output-format csv -d gpurun_out/pmc_bench/$C -o run -- \
-            python3 bench.py --steps 3 --warmup 1 --no-text --no-cpu-baseline --no-fp8 || exit $?
+            python3 bench.py --steps 3 --warmup 1 --no-text --no-cpu-baseline --no-fp8 --no-e2e || exit $?
       done
       python3 tools/pmc_traffic.py gpurun_out/pmc_bench/FETCH_SIZE gpurun_out/pmc_bench/WRITE_SIZE \
-          gpurun_out/pmc_c_fc.json || exit $?
+          gpurun_out/pmc_c_fc.json 6400 "${PMC_LABEL:-this run}: --pmc FETCH_SIZE and --pmc WRITE_SIZE passes of bench.py --no-text, tiles $CLIPGPU_GEMM_TILES" || exit $?
       unset CLIPGPU_GEMM_TILES ;;
   esac
 done

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """HBM traffic per launch of the bench's roofline kernel from two rocprofv3 --pmc passes.
 
-Usage: python tools/pmc_traffic.py FETCH_DIR WRITE_DIR OUT_JSON [ROWS_PER_LAUNCH]
+Usage: python tools/pmc_traffic.py FETCH_DIR WRITE_DIR OUT_JSON [ROWS_PER_LAUNCH [SOURCE_LABEL]]
 
 FETCH_DIR / WRITE_DIR hold `rocprofv3 --pmc FETCH_SIZE` and `--pmc WRITE_SIZE`
 counter_collection CSVs of the same `bench.py --no-text` command (separate passes: the
@@ -48,6 +48,7 @@ def main():
         "fetch_dispatches": nf, "write_dispatches": nw,
         "hbm_read_bytes_per_launch": read_b, "hbm_write_bytes_per_launch": write_b,
         "hbm_bytes_per_launch": read_b + write_b,
+        "source": sys.argv[5] if len(sys.argv) > 5 else "rocprofv3 --pmc passes of bench.py",
         "compulsory_bytes_per_launch": compulsory,
         "correction": "FETCH_SIZE x2 (gfx950 wide streaming reads), KB x 1024; WRITE_SIZE as reported",
     }
