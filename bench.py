@@ -35,7 +35,7 @@ sys.path.insert(0, os.path.join(ROOT, "clip-embedder-rs_amd"))
 
 from open_clip_inference import _lib  # noqa: E402
 from open_clip_inference.engine import Engine, profile_enable, profile_read  # noqa: E402
-from open_clip_inference.parallel import all_gather_rows  # noqa: E402
+from open_clip_inference.parallel import init_engine_comm  # noqa: E402
 
 # ViT-B/32 (open_clip timm/vit_base_patch32_clip_224.openai)
 CFG = {
@@ -198,44 +198,63 @@ def main():
     ap.add_argument("--no-fp8", action="store_true", help="skip the fp8 side measurement")
     ap.add_argument("--breakdown", action="store_true", help="per-kernel-class ms per step (serialized lanes)")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-buffer (PCIe-inclusive) legs")
+    ap.add_argument("--gather", action="store_true",
+                    help="N = 1: run the data-parallel path anyway (gloo control plane, the engine's RCCL "
+                         "communicator, gathered entry points) -- a one-GPU rehearsal of N > 1")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # dp: the data-parallel path (every N > 1 run; --gather rehearses it at N = 1 on one GPU)
+    dp = world > 1 or args.gather
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # control plane only (barriers, max-over-ranks timing, the RCCL unique id); the data path's
+        # collective is the engine's own RCCL communicator (clipgpu_comm_init_rank)
+        dist.init_process_group("gloo")
+    elif dp:
+        import socket
+        sk = socket.socket()
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+        sk.close()
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
     mdir = make_model_dir()
     ve = Engine(mdir, _lib.TOWER_VISION, [local], args.dtype, B_VISION)
+    if dp:
+        init_engine_comm(ve)
     px, ids = synth_inputs(rank, dev)
-    out = torch.empty((B_VISION, 512), device=dev, dtype=torch.float32)
+    out_full = torch.empty((world * B_VISION, 512), device=dev, dtype=torch.float32)
+    out = out_full[rank * B_VISION:(rank + 1) * B_VISION]  # this rank's rows
     stream = torch.cuda.current_stream(dev)
 
     def vision_step():
-        ve.embed_pixels_device(px.data_ptr(), B_VISION, out.data_ptr(), stream.cuda_stream)
-        if world > 1:  # one RCCL all-gather of the [256, 512] embedding rows, rank order
-            all_gather_rows(out, world * B_VISION)
+        if dp:  # forward of this rank's 256 rows + one RCCL all-gather of [world*256, 512]
+            ve.embed_pixels_gather_device([px.data_ptr()], [B_VISION] * world, [out_full.data_ptr()],
+                                          [stream.cuda_stream])
+        else:
+            ve.embed_pixels_device(px.data_ptr(), B_VISION, out.data_ptr(), stream.cuda_stream)
 
     def timed(step, steps, warmup, prof_engine=None, prof_cat=None):
         for _ in range(warmup):
             step()
         if prof_engine is not None:
             profile_enable(prof_engine, [prof_cat])
-        if world > 1:
+        if dp:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(steps):
             step()
         torch.cuda.synchronize()
-        if world > 1:
+        if dp:
             dist.barrier()
         dt = time.perf_counter() - t0
-        if world > 1:
-            t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        if dp:
+            t = torch.tensor([dt], dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             dt = float(t.item())
         prof = None
@@ -325,12 +344,17 @@ def main():
     tout_host = None
     if not args.no_text:
         te = Engine(mdir, _lib.TOWER_TEXT, [local], args.dtype, B_TEXT)
-        tout = torch.empty((B_TEXT, 512), device=dev, dtype=torch.float32)
+        if dp:
+            init_engine_comm(te)
+        tout_full = torch.empty((world * B_TEXT, 512), device=dev, dtype=torch.float32)
+        tout = tout_full[rank * B_TEXT:(rank + 1) * B_TEXT]
 
         def text_step():
-            te.embed_tokens_device(ids.data_ptr(), B_TEXT, tout.data_ptr(), stream.cuda_stream)
-            if world > 1:
-                all_gather_rows(tout, world * B_TEXT)
+            if dp:
+                te.embed_tokens_gather_device([ids.data_ptr()], [B_TEXT] * world, [tout_full.data_ptr()],
+                                              [stream.cuda_stream])
+            else:
+                te.embed_tokens_device(ids.data_ptr(), B_TEXT, tout.data_ptr(), stream.cuda_stream)
 
         tsteps = max(3, args.steps // 2)
         tdt, _ = timed(text_step, tsteps, max(1, args.warmup // 2))
@@ -380,7 +404,7 @@ def main():
             "config": {"workload": "BASELINE.json configs[1]: ViT-B/32-224 VisionEmbedder, batch 256 "
                                    "synthetic 224x224 per GPU, device-resident input",
                        "global_batch": world * B_VISION, "seq_len": 50,
-                       "parallelism": f"dp{world}, {os.environ.get('CLIPGPU_LANES', '2')} concurrent sub-batch lanes/GPU" + (" + RCCL all-gather of [B,512] embeddings" if world > 1 else "")},
+                       "parallelism": f"dp{world}, {os.environ.get('CLIPGPU_LANES', '2')} concurrent sub-batch lanes/GPU" + (" + the engine's RCCL all-gather (ncclAllGather in the C ABI) of the [B,512] embeddings on every rank" if dp else "")},
             "roofline": {"bound": "mfma", "kernel": f"c_fc GEMM ({int(fc_rows_per_launch)}x3072x768, +QuickGELU, tile {gemm_tiles['c_fc']})",
                          "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
                          "frac": round(achieved / peak, 4), "traffic": traffic,
@@ -399,7 +423,7 @@ def main():
         }
         print(json.dumps(line), flush=True)
     ve.close()
-    if world > 1:
+    if dp:
         dist.destroy_process_group()
 
 

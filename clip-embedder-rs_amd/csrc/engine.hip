@@ -9,6 +9,7 @@
 // hipGraph.  Multi-device handles shard the batch into contiguous row blocks,
 // one host worker thread and one stream per device.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <atomic>
 #include <cstdio>
@@ -33,6 +34,13 @@
 #include "kernels/kernels.hpp"
 
 namespace clipgpu {
+
+#define NCCL_CHECK(expr)                                                                            \
+  do {                                                                                              \
+    ncclResult_t _r = (expr);                                                                       \
+    if (_r != ncclSuccess)                                                                          \
+      throw ClipErr(CLIPGPU_ERR_DEVICE, std::string("RCCL error: ") + ncclGetErrorString(_r) + " (" #expr ")"); \
+  } while (0)
 
 #define HIP_CHECK(expr)                                                                             \
   do {                                                                                              \
@@ -111,6 +119,10 @@ struct Replica {
   // shared by the lane views.
   struct GraphCache* graphs = nullptr;
   hipEvent_t gin = nullptr, gout = nullptr;  // fork / join around a graph launched for a caller stream
+  // RCCL communicator of this replica's rank (the one collective, an all-gather of
+  // the embedding rows over xGMI): ncclCommInitAll over a multi-device handle's devices, or
+  // ncclCommInitRank for one-process-per-GPU deployments (clipgpu_comm_init_rank).
+  ncclComm_t comm = nullptr;
 };
 
 // Replayable forwards: one hipGraphExec per (entry point, input / output buffers, batch,
@@ -189,6 +201,8 @@ struct clipgpu_engine {
   int max_batch = 0;
   size_t in_bytes_per_row = 0;
   std::vector<clipgpu::Replica> reps;
+  // Communicator geometry: comm_nranks ranks in all; replica i is rank comm_rank0 + i.
+  int comm_nranks = 0, comm_rank0 = 0;
   std::mutex mu;  // one call per handle at a time (src/vision.rs:107 write lock)
 };
 
@@ -1295,9 +1309,54 @@ void run_sharded(clipgpu_engine& e, int64_t B, F shard) {
     if (codes[g]) throw ClipErr(codes[g], "device " + std::to_string(e.reps[g].device) + ": " + errs[g]);
 }
 
+// ---- sharded forward + the RCCL all-gather of the embedding rows ----------
+// Every rank embeds its own contiguous block of rows[rank] rows into its slot of a [sum rows][E]
+// output on its device, then one collective leaves the whole matrix, in rank order, on every
+// rank: an in-place ncclAllGather when all blocks are equal, else (ragged blocks) one in-place
+// ncclBroadcast per non-empty block inside a group.  `local` is replica i = rank rank0 + i.
+template <typename Fwd>
+void sharded_gather(clipgpu_engine& e, const int64_t* rows, float* const* d_out, void* const* streams, Fwd fwd) {
+  const int nr = e.comm_nranks, E = e.spec.embed_dim, G = (int)e.reps.size();
+  if (nr <= 0) throw ClipErr(CLIPGPU_ERR_INVALID, "no communicator: create the handle over distinct devices "
+                                                  "or call clipgpu_comm_init_rank first");
+  std::vector<int64_t> off((size_t)nr + 1, 0);
+  bool equal = true;
+  for (int r = 0; r < nr; ++r) {
+    if (rows[r] < 0) throw ClipErr(CLIPGPU_ERR_INVALID, "negative row count");
+    off[r + 1] = off[r] + rows[r];
+    equal = equal && rows[r] == rows[0];
+  }
+  if (off[nr] == 0) throw ClipErr(CLIPGPU_ERR_INVALID, "Empty batch");
+  std::vector<hipStream_t> sts((size_t)G);
+  for (int i = 0; i < G; ++i) {
+    Replica& r = e.reps[i];
+    if (!d_out[i]) throw ClipErr(CLIPGPU_ERR_INVALID, "NULL buffer");
+    sts[i] = streams && streams[i] ? (hipStream_t)streams[i] : r.stream;
+    const int rank = e.comm_rank0 + i;
+    HIP_CHECK(hipSetDevice(r.device));
+    for (int64_t c0 = 0; c0 < rows[rank]; c0 += e.max_batch)
+      fwd(r, i, c0, (int)std::min<int64_t>(e.max_batch, rows[rank] - c0), d_out[i] + (off[rank] + c0) * E, sts[i]);
+  }
+  NCCL_CHECK(ncclGroupStart());
+  for (int i = 0; i < G; ++i) {
+    Replica& r = e.reps[i];
+    const int rank = e.comm_rank0 + i;
+    if (equal) {
+      NCCL_CHECK(ncclAllGather(d_out[i] + off[rank] * E, d_out[i], (size_t)rows[rank] * E, ncclFloat, r.comm, sts[i]));
+    } else {
+      for (int q = 0; q < nr; ++q)
+        if (rows[q] > 0)
+          NCCL_CHECK(ncclBroadcast(d_out[i] + off[q] * E, d_out[i] + off[q] * E, (size_t)rows[q] * E, ncclFloat, q,
+                                   r.comm, sts[i]));
+    }
+  }
+  NCCL_CHECK(ncclGroupEnd());
+}
+
 void destroy_replica(Replica& r) {
   (void)hipSetDevice(r.device);
   if (r.stream) (void)hipStreamSynchronize(r.stream);
+  if (r.comm) (void)ncclCommDestroy(r.comm);
   if (r.arena) (void)hipFree(r.arena);
   if (r.work) (void)hipFree(r.work);
   if (r.pin_in) (void)hipHostFree(r.pin_in);
@@ -1412,6 +1471,19 @@ int clipgpu_create(const char* model_dir, int tower, const int* device_ids, int 
         autotune_tiles(*e, r);
         tune_forward(*e, r);
       }
+    }
+    // A multi-device handle gets one communicator over its devices (ncclCommInitAll; rank i =
+    // device_ids[i]) when they are distinct (RCCL refuses two ranks on one GPU; a handle that
+    // lists a device twice keeps the host-buffer sharding and has no collective entry points).
+    bool distinct = devs.size() > 1;
+    for (size_t i = 0; i < devs.size() && distinct; ++i)
+      for (size_t j = i + 1; j < devs.size(); ++j) distinct = distinct && devs[i] != devs[j];
+    if (distinct) {
+      std::vector<ncclComm_t> comms(devs.size());
+      NCCL_CHECK(ncclCommInitAll(comms.data(), (int)devs.size(), devs.data()));
+      for (size_t i = 0; i < devs.size(); ++i) e->reps[i].comm = comms[i];
+      e->comm_nranks = (int)devs.size();
+      e->comm_rank0 = 0;
     }
     *out = e.release();
   });
@@ -1605,6 +1677,73 @@ int clipgpu_embed_tokens_device(clipgpu_engine* e, const int64_t* d_ids, int64_t
     HIP_CHECK(hipSetDevice(r.device));
     run_graph(*e, r, {3, (uint64_t)d_ids, (uint64_t)d_out, (uint64_t)B}, stream ? (hipStream_t)stream : r.stream,
               [&](hipStream_t gs) { text_forward_lanes(*e, r, d_ids, (int)B, d_out, gs); });
+  });
+}
+
+int clipgpu_comm_unique_id(uint8_t* id) {
+  return guarded([&]() {
+    if (!id) throw ClipErr(CLIPGPU_ERR_INVALID, "NULL id");
+    ncclUniqueId u;
+    NCCL_CHECK(ncclGetUniqueId(&u));
+    std::memcpy(id, u.internal, NCCL_UNIQUE_ID_BYTES);
+  });
+}
+
+int clipgpu_comm_init_rank(clipgpu_engine* e, const uint8_t* id, int nranks, int rank) {
+  return guarded([&]() {
+    if (!e || !id) throw ClipErr(CLIPGPU_ERR_INVALID, "NULL argument");
+    if (e->reps.size() != 1) throw ClipErr(CLIPGPU_ERR_INVALID, "clipgpu_comm_init_rank needs a one-device handle");
+    if (nranks < 1 || rank < 0 || rank >= nranks) throw ClipErr(CLIPGPU_ERR_INVALID, "bad nranks / rank");
+    std::lock_guard<std::mutex> lk(e->mu);
+    Replica& r = e->reps[0];
+    if (r.comm) throw ClipErr(CLIPGPU_ERR_INVALID, "the handle already has a communicator");
+    ncclUniqueId u;
+    std::memcpy(u.internal, id, NCCL_UNIQUE_ID_BYTES);
+    HIP_CHECK(hipSetDevice(r.device));
+    NCCL_CHECK(ncclCommInitRank(&r.comm, nranks, u, rank));
+    e->comm_nranks = nranks;
+    e->comm_rank0 = rank;
+  });
+}
+
+int clipgpu_comm_info(const clipgpu_engine* e, int* nranks, int* rank0) {
+  return guarded([&]() {
+    if (!e || !nranks || !rank0) throw ClipErr(CLIPGPU_ERR_INVALID, "NULL argument");
+    *nranks = e->comm_nranks;
+    *rank0 = e->comm_rank0;
+  });
+}
+
+int clipgpu_embed_pixels_gather_device(clipgpu_engine* e, const float* const* d_nchw, const int64_t* rows,
+                                       float* const* d_out, void* const* streams) {
+  return guarded([&]() {
+    need_tower(e, TOWER_VISION);
+    if (!d_nchw || !rows || !d_out) throw ClipErr(CLIPGPU_ERR_INVALID, "NULL buffer");
+    std::lock_guard<std::mutex> lk(e->mu);
+    const size_t row_bytes = (size_t)3 * e->spec.image_size * e->spec.image_size * 4;
+    sharded_gather(*e, rows, d_out, streams, [&](Replica& r, int i, int64_t c0, int n, float* dst, hipStream_t st) {
+      if (!d_nchw[i]) throw ClipErr(CLIPGPU_ERR_INVALID, "NULL buffer");
+      const float* src = (const float*)((const char*)d_nchw[i] + c0 * row_bytes);
+      run_graph(*e, r, {1, (uint64_t)src, (uint64_t)dst, (uint64_t)n}, st, [&](hipStream_t gs) {
+        vision_forward_lanes(*e, r, src, A_IMG_F32, nullptr, nullptr, n, dst, gs);
+      });
+    });
+  });
+}
+
+int clipgpu_embed_tokens_gather_device(clipgpu_engine* e, const int64_t* const* d_ids, const int64_t* rows,
+                                       float* const* d_out, void* const* streams) {
+  return guarded([&]() {
+    need_tower(e, TOWER_TEXT);
+    if (!d_ids || !rows || !d_out) throw ClipErr(CLIPGPU_ERR_INVALID, "NULL buffer");
+    std::lock_guard<std::mutex> lk(e->mu);
+    const int T = e->spec.context_length;
+    sharded_gather(*e, rows, d_out, streams, [&](Replica& r, int i, int64_t c0, int n, float* dst, hipStream_t st) {
+      if (!d_ids[i]) throw ClipErr(CLIPGPU_ERR_INVALID, "NULL buffer");
+      const int64_t* src = d_ids[i] + c0 * T;
+      run_graph(*e, r, {3, (uint64_t)src, (uint64_t)dst, (uint64_t)n}, st,
+                [&](hipStream_t gs) { text_forward_lanes(*e, r, src, n, dst, gs); });
+    });
   });
 }
 

@@ -48,6 +48,11 @@ _PROTOS = [
     ("clipgpu_tokenizer_vocab_size", c_int64, [c_void_p]),
     ("clipgpu_similarity", c_int, [c_int, c_void_p, c_int64, c_void_p, c_int64, c_int64, c_float, c_float, c_int, c_int, c_void_p]),
     ("clipgpu_similarity_device", c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int64, c_float, c_float, c_int, c_int, c_void_p, c_void_p]),
+    ("clipgpu_comm_unique_id", c_int, [c_void_p]),
+    ("clipgpu_comm_init_rank", c_int, [c_void_p, c_void_p, c_int, c_int]),
+    ("clipgpu_comm_info", c_int, [c_void_p, POINTER(c_int), POINTER(c_int)]),
+    ("clipgpu_embed_pixels_gather_device", c_int, [c_void_p, POINTER(c_void_p), POINTER(c_int64), POINTER(c_void_p), POINTER(c_void_p)]),
+    ("clipgpu_embed_tokens_gather_device", c_int, [c_void_p, POINTER(c_void_p), POINTER(c_int64), POINTER(c_void_p), POINTER(c_void_p)]),
     ("clipgpu_facade_scores", c_int, [c_void_p, c_int64, c_void_p, c_int64, c_float, c_float, c_int, c_void_p]),
     ("clipgpu_profile_enable", c_int, [c_void_p, ctypes.c_uint]),
     ("clipgpu_profile_read", c_int, [c_void_p, c_int, POINTER(c_double), POINTER(c_int64)]),

@@ -106,6 +106,42 @@ class Engine:
         check(lib().clipgpu_embed_tokens_device(self.handle, c_void_p(d_ids), B, c_void_p(d_out),
                                                 c_void_p(stream or None)))
 
+    # ---- data-parallel sharding + the RCCL all-gather (include/clipgpu.h) ----------------
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        buf = (ctypes.c_uint8 * 128)()
+        check(lib().clipgpu_comm_unique_id(buf))
+        return bytes(buf)
+
+    def comm_init_rank(self, uid: bytes, nranks: int, rank: int) -> None:
+        if len(uid) != 128:
+            raise ValueError("the unique id is 128 bytes")
+        buf = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
+        check(lib().clipgpu_comm_init_rank(self.handle, buf, int(nranks), int(rank)))
+
+    def comm_info(self):
+        n, r0 = c_int(), c_int()
+        check(lib().clipgpu_comm_info(self.handle, ctypes.byref(n), ctypes.byref(r0)))
+        return n.value, r0.value
+
+    def _gather(self, fn, d_in, rows, d_out, streams):
+        k = len(self.devices)
+        if len(d_in) != k or len(d_out) != k:
+            raise ValueError(f"one input and one output buffer per local device ({k})")
+        ins = (c_void_p * k)(*[c_void_p(p) for p in d_in])
+        outs = (c_void_p * k)(*[c_void_p(p) for p in d_out])
+        rs = (ctypes.c_int64 * len(rows))(*[int(r) for r in rows])
+        sts = (c_void_p * k)(*[c_void_p(s or None) for s in (streams or [0] * k)])
+        check(fn(self.handle, ins, rs, outs, sts))
+
+    def embed_pixels_gather_device(self, d_in, rows, d_out, streams=None) -> None:
+        """Per local device: its rank's block of normalised pixels in, the whole [sum rows][E]
+        embedding matrix (rank order) out -- forward + one RCCL all-gather."""
+        self._gather(lib().clipgpu_embed_pixels_gather_device, d_in, rows, d_out, streams)
+
+    def embed_tokens_gather_device(self, d_in, rows, d_out, streams=None) -> None:
+        self._gather(lib().clipgpu_embed_tokens_gather_device, d_in, rows, d_out, streams)
+
 
 PROFILE_CATEGORIES = ["patch_embed", "stem_ln", "qkv", "attention", "out_proj", "layernorm", "c_fc",
                       "c_proj", "head", "last_layer"]

@@ -165,6 +165,30 @@ int clipgpu_similarity_device(const float* d_img, int64_t n_img, const float* d_
                               float logit_scale, float logit_bias, int activation, int axis, float* d_out,
                               void* stream);
 
+/* ---- data-parallel sharding + the RCCL all-gather (north_star: "batches shard
+ * data-parallel across the 8 GPUs of one node with an RCCL all-gather over xGMI only for the final
+ * embedding matrix").  The reference has no multi-device path: embed_images / embed_texts
+ * (src/vision.rs:100-117, src/text.rs:148-169) keep their signatures; these entry points are
+ * what a multi-GPU caller of them binds.
+ * Communicator: a handle created over n > 1 DISTINCT devices owns one (ncclCommInitAll, rank i =
+ * device_ids[i]); a one-device handle in a one-process-per-GPU deployment joins one with
+ * clipgpu_comm_init_rank (rank 0 calls clipgpu_comm_unique_id and sends the 128 bytes to every
+ * rank out of band; every rank then calls init_rank, collectively).  clipgpu_comm_info gives
+ * (nranks, first rank of this handle); nranks 0 = no communicator.
+ * Gathered forward: rows[nranks] = every rank's block size (identical on every rank); per LOCAL
+ * device i (rank = first rank + i): d_in[i] = that rank's block on device i (f32 NCHW normalised
+ * pixels / i64 ids [rows][T]), d_out[i] = [sum rows][E] f32 on device i, streams[i] (NULL entry or
+ * array: the handle's stream).  Each rank embeds its block into its slot, then one collective
+ * (in-place ncclAllGather for equal blocks; one ncclBroadcast per block otherwise) leaves the
+ * whole matrix in rank order on every device.  Stream-ordered; collective over all ranks. */
+int clipgpu_comm_unique_id(uint8_t* id /* [128] */);
+int clipgpu_comm_init_rank(clipgpu_engine* e, const uint8_t* id /* [128] */, int nranks, int rank);
+int clipgpu_comm_info(const clipgpu_engine* e, int* nranks, int* rank0);
+int clipgpu_embed_pixels_gather_device(clipgpu_engine* e, const float* const* d_nchw, const int64_t* rows,
+                                       float* const* d_out, void* const* streams);
+int clipgpu_embed_tokens_gather_device(clipgpu_engine* e, const int64_t* const* d_ids, const int64_t* rows,
+                                       float* const* d_out, void* const* streams);
+
 /* ---- Clip facade scores on the host, the reference's f32 arithmetic bit for bit -----------
  * src/clip.rs:79-185 as the crate computes it (ndarray 0.17 without BLAS, Cargo.toml:14):
  * out[i] = unrolled_dot(embs[i], query).mul_add(logit_scale, logit_bias) -- ndarray's

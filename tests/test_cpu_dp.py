@@ -73,3 +73,48 @@ def test_shard_ranges_cover_batch_in_order():
             assert rs[0][0] == 0 and rs[-1][1] == B
             assert all(rs[i][1] == rs[i + 1][0] for i in range(world - 1))
             assert max(b - a for a, b in rs) - min(b - a for a, b in rs) <= 1
+
+
+class _FakeEngine:
+    """Records what the RCCL bootstrap hands the C ABI (no GPU here)."""
+
+    def __init__(self, rank):
+        self.rank = rank
+        self.got = None
+
+    def comm_unique_id(self):
+        assert self.rank == 0, "only rank 0 draws the unique id"
+        return bytes(range(128))
+
+    def comm_init_rank(self, uid, nranks, rank):
+        self.got = (uid, nranks, rank)
+
+
+def _comm_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from open_clip_inference.parallel import init_engine_comm, shard_rows
+    e = _FakeEngine(rank)
+    assert init_engine_comm(e) == (world, rank)
+    q.put((rank, e.got, shard_rows(10, world)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_engine_comm_bootstrap_over_the_control_plane(world):
+    """bench.py's N > 1 path: rank 0's 128-byte RCCL unique id reaches every rank over the gloo
+    control plane, and each rank joins with its own rank number (clipgpu_comm_init_rank)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_comm_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = sorted(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for r, (rank, (uid, nranks, rk), rows) in enumerate(got):
+        assert rank == r and rk == r and nranks == world and uid == bytes(range(128))
+        assert sum(rows) == 10 and len(rows) == world

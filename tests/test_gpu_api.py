@@ -252,3 +252,46 @@ def test_classify_many_and_rank_images_many(model):
         one = clip.rank_images(ims, q)
         assert np.allclose(sorted(p for _, p in res), sorted(p for _, p in one), atol=1e-5)
         assert sorted(i for i, _ in res) == list(range(len(ims)))
+
+
+def test_rccl_communicator_and_gathered_entry_points(monkeypatch):
+    """The data-parallel collective inside the C ABI on a one-GPU box: a one-rank RCCL
+    communicator (clipgpu_comm_unique_id + clipgpu_comm_init_rank, as each rank of a
+    one-process-per-GPU deployment does), then the gathered entry points (forward of the rank's
+    block + ncclAllGather, in place) equal the plain device forward bit for bit -- vision and
+    text, a block larger than max_batch (chunked).  A handle listing one device twice has no
+    communicator."""
+    import torch
+    from oracle.model_spec import VIT_B_32_CFG
+    from open_clip_inference import _lib
+    from open_clip_inference.engine import Engine
+    from open_clip_inference.error import InferenceError
+    from tests.helpers import normalized_pixels
+    d = make_model_dir(VIT_B_32_CFG, seed=1234)
+    v = vision_spec_from_cfg(VIT_B_32_CFG["model_cfg"])
+    t = text_spec_from_cfg(VIT_B_32_CFG["model_cfg"])
+    s = torch.cuda.current_stream()
+    for tower in (0, 1):
+        e = Engine(d, tower, [0], "bf16", 16)
+        assert e.comm_info() == (0, 0)
+        B = 40
+        if tower == 0:
+            x = normalized_pixels(weights.synth_images_u8(9, B, v.image_size), OPENAI_MEAN, OPENAI_STD)
+        else:
+            x = weights.synth_token_ids(9, B, t.context_length, t.vocab_size, t.vocab_size - 2, t.vocab_size - 1,
+                                        random_eot=True)
+        d_in = torch.from_numpy(x).cuda()
+        out = torch.full((B, 512), float("nan"), device="cuda")
+        gather = e.embed_pixels_gather_device if tower == 0 else e.embed_tokens_gather_device
+        with pytest.raises(InferenceError, match="no communicator"):
+            gather([d_in.data_ptr()], [B], [out.data_ptr()], [s.cuda_stream])
+        e.comm_init_rank(Engine.comm_unique_id(), 1, 0)
+        assert e.comm_info() == (1, 0)
+        gather([d_in.data_ptr()], [B], [out.data_ptr()], [s.cuda_stream])
+        torch.cuda.synchronize()
+        got = out.cpu().numpy()
+        ref = e.embed_pixels(x) if tower == 0 else e.embed_tokens(x)
+        assert np.array_equal(got, ref)
+        e.close()
+    multi = Engine(d, 0, [0, 0], "bf16", 4)
+    assert multi.comm_info() == (0, 0)
