@@ -198,6 +198,9 @@ struct clipgpu_engine {
   // activations, E8M0 block scales, v_mfma_scale_f32_32x32x64_f8f6f4); attention, out_proj,
   // the stems and heads stay bf16.
   bool mx = false;
+  // The MX sites of an fp8 engine (CLIPGPU_MX_SITES, a subset of "qkv,fc,proj"; c_proj in MX
+  // needs c_fc in MX, whose epilogue quantizes the hidden activations).  Default: all three.
+  bool mx_site[4] = {false, false, false, false};  // indexed by GemmSite (GS_OUT stays bf16)
   int max_batch = 0;
   size_t in_bytes_per_row = 0;
   std::vector<clipgpu::Replica> reps;
@@ -209,6 +212,8 @@ struct clipgpu_engine {
 namespace clipgpu {
 
 namespace {
+
+enum GemmSite { GS_QKV = 0, GS_OUT, GS_FC, GS_PROJ, GS_N };
 
 inline size_t align256(size_t n) { return (n + 255) & ~size_t(255); }
 inline int round64(int n) { return (n + 63) / 64 * 64; }
@@ -404,15 +409,12 @@ void upload_weights(clipgpu_engine& e, Replica& r, const TensorMap& m) {
     L.ln1_w = f32(p + n_ln1w);
     L.ln1_b = f32(p + n_ln1b);
     L.wqkv = L.w1 = L.w2 = nullptr;
-    if (e.mx) {
-      L.mqkv = wmx_pad(p + n_qkvw, 3 * D, D);
-      L.m1 = wmx_pad(p + n_fc1w, mlp_pad(s), D);
-      L.m2 = wmx_pad(p + n_fc2w, D, mlp_pad(s));
-    } else {
-      L.wqkv = w16(p + n_qkvw);
-      L.w1 = w16_pad(p + n_fc1w, mlp_pad(s), D);
-      L.w2 = w16_pad(p + n_fc2w, D, mlp_pad(s));
-    }
+    if (e.mx_site[GS_QKV]) L.mqkv = wmx_pad(p + n_qkvw, 3 * D, D);
+    else L.wqkv = w16(p + n_qkvw);
+    if (e.mx_site[GS_FC]) L.m1 = wmx_pad(p + n_fc1w, mlp_pad(s), D);
+    else L.w1 = w16_pad(p + n_fc1w, mlp_pad(s), D);
+    if (e.mx_site[GS_PROJ]) L.m2 = wmx_pad(p + n_fc2w, D, mlp_pad(s));
+    else L.w2 = w16_pad(p + n_fc2w, D, mlp_pad(s));
     L.bqkv = f32(p + n_qkvb);
     L.wo = w16(p + n_ow);
     L.bo = f32(p + n_ob);
@@ -540,8 +542,6 @@ struct ProfScope {
   }
 };
 
-enum GemmSite { GS_QKV = 0, GS_OUT, GS_FC, GS_PROJ, GS_N };
-
 GemmParams rows_gemm(const void* A, long lda, const void* W, const float* bias, void* out, long ldo, int M, int N,
                      int K) {
   GemmParams g{};
@@ -584,7 +584,14 @@ GemmParams site_gemm(const clipgpu_engine& e, const Replica& r, const LayerW& L,
 
 // fp8 engines: the MX-fp8 GEMM of a trunk site (QKV: LN e4m3 -> 16-bit qkv; c_fc: LN e4m3 ->
 // act -> e4m3 hidden in `big` + scales; c_proj: e4m3 hidden -> residual stream).
-int site_epi_mx(int site) { return site == GS_PROJ ? EPI_RESID : (site == GS_FC ? EPI_STOREQ : EPI_STORE16); }
+// c_fc quantizes its output (EPI_STOREQ) only when c_proj consumes MX; else it stores 16-bit.
+int site_epi_mx(const clipgpu_engine& e, int site) {
+  return site == GS_PROJ ? EPI_RESID : (site == GS_FC && e.mx_site[GS_PROJ] ? EPI_STOREQ : EPI_STORE16);
+}
+// LN output feeding an MX GEMM is written as MX-fp8 (scales in hs), else 16-bit.
+inline uint8_t* ln_q(const clipgpu_engine& e, int consumer_site, uint8_t* hs) {
+  return e.mx_site[consumer_site] ? hs : nullptr;
+}
 
 MxGemmParams site_gemm_mx(const clipgpu_engine& e, const Replica& r, const LayerW& L, int site, int rows) {
   const int D = e.spec.width, MLP = mlp_pad(e.spec);
@@ -652,10 +659,10 @@ PoolSrc trunk(const clipgpu_engine& e, const Replica& r, int B, int causal, cons
     auto gemm = [&](int site, int cat, const char* what) {
       ProfScope ps(e, rows == B * T ? cat : PC_TAIL, st, /*gemm=*/true);
       const bool tuned = 2 * rows > e.tuned_rows;
-      if (e.mx && site != GS_OUT) {
+      if (e.mx_site[site]) {
         MxGemmParams g = site_gemm_mx(e, c, L, site, rows);
         g.tile = tuned ? e.tile[site] : MX_TILE_AUTO;
-        check(launch_gemm_mx(e.dt, site_epi_mx(site), site == GS_FC ? s.act : ACT_NONE, g, st), what);
+        check(launch_gemm_mx(e.dt, site_epi_mx(e, site), site == GS_FC ? s.act : ACT_NONE, g, st), what);
         return;
       }
       GemmParams g = site_gemm(e, c, L, site, rows);
@@ -675,13 +682,13 @@ PoolSrc trunk(const clipgpu_engine& e, const Replica& r, int B, int causal, cons
     gemm(GS_OUT, PC_OUT_PROJ, "out_proj gemm");
     { ProfScope ps(e, compact ? PC_TAIL : PC_LN, st);
       check(launch_ln_rows_add(e.dt, c.x, site_split(e, GS_OUT) ? c.slab : nullptr, L.ln2_w, L.ln2_b, s.ln_eps, c.h,
-                               rows, D, st, c.hs), "ln_2"); }
+                               rows, D, st, ln_q(e, GS_FC, c.hs)), "ln_2"); }
     gemm(GS_FC, PC_C_FC, "c_fc gemm");
     gemm(GS_PROJ, PC_C_PROJ, "c_proj gemm");
     if (l + 1 < s.layers) {  // (the last c_proj's slab is added by the head's first LayerNorm)
       ProfScope ps(e, PC_LN, st);
       check(launch_ln_rows_add(e.dt, r.x, site_split(e, GS_PROJ) ? r.slab : nullptr, r.w.layers[l + 1].ln1_w,
-                               r.w.layers[l + 1].ln1_b, s.ln_eps, r.h, rows, D, st, r.hs), "ln_1");
+                               r.w.layers[l + 1].ln1_b, s.ln_eps, r.h, rows, D, st, ln_q(e, GS_QKV, r.hs)), "ln_1");
     }
     if (compact) return PoolSrc{c.x, 1, nullptr};
   }
@@ -707,7 +714,7 @@ void autotune_tiles(clipgpu_engine& e, Replica& r) {
     for (int i = 0; i < 4; ++i) {
       if (v[i] < TILE_AUTO || v[i] > TILE_LAST) throw ClipErr(CLIPGPU_ERR_INVALID, "bad CLIPGPU_GEMM_TILES entry");
       e.tile[i] = v[i];
-      if (e.mx && i != GS_OUT) e.tile[i] = MX_TILE_AUTO;  // the pins name 16-bit tiles
+      if (e.mx_site[i]) e.tile[i] = MX_TILE_AUTO;  // the pins name 16-bit tiles
     }
     return;
   }
@@ -739,9 +746,9 @@ void autotune_tiles(clipgpu_engine& e, Replica& r) {
   };
   const LayerW& L = r.w.layers[0];
   for (int site = 0; site < GS_N; ++site) {
-    if (e.mx && site != GS_OUT) {  // MX sites: the built MX tiles (same timing loop)
+    if (e.mx_site[site]) {  // MX sites: the built MX tiles (same timing loop)
       MxGemmParams g = site_gemm_mx(e, r, L, site, rows);
-      const int epi = site_epi_mx(site), act = site == GS_FC ? e.spec.act : ACT_NONE;
+      const int epi = site_epi_mx(e, site), act = site == GS_FC ? e.spec.act : ACT_NONE;
       float best = 1e30f;
       for (int t : {MX_TILE_256x128, MX_TILE_128x128}) {
         g.tile = t;
@@ -826,7 +833,7 @@ void vision_forward(const clipgpu_engine& e, const Replica& r, const void* pixel
   if (s.family == FAMILY_SIGLIP) {  // no class token, no pre-norm: x = patches + bias + pos
     { ProfScope ps(e, PC_STEM, st);
       check(launch_ln_rows(e.dt, r.x, r.w.layers[0].ln1_w, r.w.layers[0].ln1_b, s.ln_eps, r.h, B * s.tokens(), D, st,
-                           r.hs),
+                           ln_q(e, GS_QKV, r.hs)),
             "ln_1"); }
     trunk(e, r, B, 0, nullptr, st, s.tokens());
     head_map(e, r, B, d_out, st);
@@ -835,7 +842,7 @@ void vision_forward(const clipgpu_engine& e, const Replica& r, const void* pixel
   {
   ProfScope ps(e, PC_STEM, st);
   check(launch_vision_embed_ln(e.dt, r.x, r.w.cls, r.w.pos, r.w.lnpre_w, r.w.lnpre_b, r.w.layers[0].ln1_w,
-                               r.w.layers[0].ln1_b, s.ln_eps, r.h, B, s.tokens(), D, st, r.hs),
+                               r.w.layers[0].ln1_b, s.ln_eps, r.h, B, s.tokens(), D, st, ln_q(e, GS_QKV, r.hs)),
         "embed+ln_pre");
   }
   head(e, r, B, trunk(e, r, B, 0, nullptr, st, s.tokens()), d_out, st);
@@ -851,7 +858,7 @@ void text_forward(const clipgpu_engine& e, const Replica& r, const int64_t* d_id
   {
   ProfScope ps(e, PC_STEM, st);
   check(launch_text_embed_ln(e.dt, d_ids, r.w.tok, r.w.pos, r.w.layers[0].ln1_w, r.w.layers[0].ln1_b, s.ln_eps,
-                             r.x, r.h, B, T, s.width, s.vocab_size, st, r.hs),
+                             r.x, r.h, B, T, s.width, s.vocab_size, st, ln_q(e, GS_QKV, r.hs)),
         "token embed+ln_1");
   }
   head(e, r, B, trunk(e, r, B, 1, d_ids, st, T), d_out, st);
@@ -1419,6 +1426,24 @@ int clipgpu_create(const char* model_dir, int tower, const int* device_ids, int 
     e->pre = oc.pre;
     e->dt = dtype == CLIPGPU_DTYPE_F16 ? DT_F16 : DT_BF16;  // fp8 engines keep bf16 outside the MX GEMMs
     e->mx = dtype == CLIPGPU_DTYPE_FP8;
+    if (e->mx) {
+      const char* ms = getenv("CLIPGPU_MX_SITES");
+      const std::string sites = ms ? ms : "qkv,fc,proj";
+      auto has = [&](const char* k) {
+        size_t p = 0;
+        while ((p = sites.find(k, p)) != std::string::npos) {
+          const size_t q = p + strlen(k);
+          if ((p == 0 || sites[p - 1] == ',') && (q == sites.size() || sites[q] == ',')) return true;
+          p = q;
+        }
+        return false;
+      };
+      e->mx_site[GS_QKV] = has("qkv");
+      e->mx_site[GS_FC] = has("fc");
+      e->mx_site[GS_PROJ] = has("proj");
+      if (e->mx_site[GS_PROJ] && !e->mx_site[GS_FC])
+        throw ClipErr(CLIPGPU_ERR_INVALID, "CLIPGPU_MX_SITES: proj in MX needs fc in MX");
+    }
     e->max_batch = max_batch;
     if (const char* ln = getenv("CLIPGPU_LANES")) e->lanes = std::max(1, std::min(4, atoi(ln)));
     else e->lanes = 2;
