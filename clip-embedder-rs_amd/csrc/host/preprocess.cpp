@@ -200,6 +200,10 @@ void apply_resize_plan(const ResizePlan& p, const uint8_t* src, uint8_t* dst) {
   }
 }
 
+// resize_image.cpp: resize_with_image (src/vision.rs:200-233), the non-default resize
+void resize_rgb8_image_crate(const uint8_t* rgb, int W, int H, int S, const std::string& interp,
+                             const std::string& mode, uint8_t* out);
+
 namespace {
 
 void resize_rgb8(const uint8_t* rgb, int W, int H, int S, const std::string& interp, const std::string& mode,
@@ -219,11 +223,44 @@ void normalize_pixels(const uint8_t* px, int S, const float* mean, const float* 
   }
 }
 
+// image_crate: resize with resize_with_image (the crate built without `fast_image_resize`)
+// instead of the default resize_with_fast_image_resize (src/vision.rs:149-157).
 void preprocess_one(const uint8_t* rgb, int W, int H, int S, const std::string& interp, const std::string& mode,
-                    const float* mean, const float* stdv, float* out) {
+                    const float* mean, const float* stdv, float* out, bool image_crate = false) {
   std::vector<uint8_t> resized((size_t)S * S * 3);
-  resize_rgb8(rgb, W, H, S, interp, mode, resized.data());
+  if (image_crate) resize_rgb8_image_crate(rgb, W, H, S, interp, mode, resized.data());
+  else resize_rgb8(rgb, W, H, S, interp, mode, resized.data());
   normalize_pixels(resized.data(), S, mean, stdv, out);
+}
+
+void preprocess_batch(const uint8_t* const* images, const int* widths, const int* heights, int64_t n, int size,
+                      const char* interpolation, const char* resize_mode, const float* mean, const float* stdv,
+                      float* out, bool image_crate) {
+  if (n <= 0) throw ClipErr(CLIPGPU_ERR_INVALID, "Empty batch");  // src/vision.rs:121-123
+  if (!images || !widths || !heights || !mean || !stdv || !out) throw ClipErr(CLIPGPU_ERR_INVALID, "NULL buffer");
+  const std::string interp = interpolation ? interpolation : "bicubic";
+  const std::string mode = resize_mode ? resize_mode : "shortest";
+  const size_t per = (size_t)3 * size * size;
+  unsigned nt = std::thread::hardware_concurrency();
+  if (nt == 0) nt = 1;
+  nt = (unsigned)std::min<int64_t>(nt, 16);
+  nt = (unsigned)std::min<int64_t>(nt, n);
+  std::vector<std::thread> th;
+  std::vector<std::string> errs(nt);
+  for (unsigned t = 0; t < nt; ++t) {
+    th.emplace_back([&, t]() {
+      try {
+        for (int64_t i = t; i < n; i += nt)
+          preprocess_one(images[i], widths[i], heights[i], size, interp, mode, mean, stdv, out + i * per,
+                         image_crate);
+      } catch (const std::exception& ex) {
+        errs[t] = ex.what();
+      }
+    });
+  }
+  for (auto& x : th) x.join();
+  for (auto& e : errs)
+    if (!e.empty()) throw ClipErr(CLIPGPU_ERR_INVALID, e);
 }
 
 }  // namespace
@@ -254,30 +291,23 @@ int clipgpu_preprocess_batch(const uint8_t* const* images, const int* widths, co
                              int size, const char* interpolation, const char* resize_mode, const float mean[3],
                              const float stdv[3], float* out) {
   return guarded([&]() {
-    if (n <= 0) throw ClipErr(CLIPGPU_ERR_INVALID, "Empty batch");  // src/vision.rs:121-123
-    if (!images || !widths || !heights || !mean || !stdv || !out) throw ClipErr(CLIPGPU_ERR_INVALID, "NULL buffer");
-    const std::string interp = interpolation ? interpolation : "bicubic";
-    const std::string mode = resize_mode ? resize_mode : "shortest";
-    const size_t per = (size_t)3 * size * size;
-    unsigned nt = std::thread::hardware_concurrency();
-    if (nt == 0) nt = 1;
-    nt = (unsigned)std::min<int64_t>(nt, 16);
-    nt = (unsigned)std::min<int64_t>(nt, n);
-    std::vector<std::thread> th;
-    std::vector<std::string> errs(nt);
-    for (unsigned t = 0; t < nt; ++t) {
-      th.emplace_back([&, t]() {
-        try {
-          for (int64_t i = t; i < n; i += nt)
-            preprocess_one(images[i], widths[i], heights[i], size, interp, mode, mean, stdv, out + i * per);
-        } catch (const std::exception& ex) {
-          errs[t] = ex.what();
-        }
-      });
-    }
-    for (auto& x : th) x.join();
-    for (auto& e : errs)
-      if (!e.empty()) throw ClipErr(CLIPGPU_ERR_INVALID, e);
+    preprocess_batch(images, widths, heights, n, size, interpolation, resize_mode, mean, stdv, out, false);
+  });
+}
+
+int clipgpu_resize_rgb8_image(const uint8_t* rgb, int width, int height, int size, const char* interpolation,
+                              const char* resize_mode, uint8_t* out_rgb) {
+  return guarded([&]() {
+    resize_rgb8_image_crate(rgb, width, height, size, interpolation ? interpolation : "bicubic",
+                            resize_mode ? resize_mode : "shortest", out_rgb);
+  });
+}
+
+int clipgpu_preprocess_batch_image(const uint8_t* const* images, const int* widths, const int* heights, int64_t n,
+                                   int size, const char* interpolation, const char* resize_mode, const float mean[3],
+                                   const float stdv[3], float* out) {
+  return guarded([&]() {
+    preprocess_batch(images, widths, heights, n, size, interpolation, resize_mode, mean, stdv, out, true);
   });
 }
 

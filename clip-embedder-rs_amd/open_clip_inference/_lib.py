@@ -41,6 +41,8 @@ _PROTOS = [
     ("clipgpu_preprocess_rgb8", c_int, [c_void_p, c_int, c_int, c_int, c_char_p, c_char_p, POINTER(c_float), POINTER(c_float), c_void_p]),
     ("clipgpu_resize_rgb8", c_int, [c_void_p, c_int, c_int, c_int, c_char_p, c_char_p, c_void_p]),
     ("clipgpu_preprocess_batch", c_int, [POINTER(c_void_p), POINTER(c_int), POINTER(c_int), c_int64, c_int, c_char_p, c_char_p, POINTER(c_float), POINTER(c_float), c_void_p]),
+    ("clipgpu_resize_rgb8_image", c_int, [c_void_p, c_int, c_int, c_int, c_char_p, c_char_p, c_void_p]),
+    ("clipgpu_preprocess_batch_image", c_int, [POINTER(c_void_p), POINTER(c_int), POINTER(c_int), c_int64, c_int, c_char_p, c_char_p, POINTER(c_float), POINTER(c_float), c_void_p]),
     ("clipgpu_tokenizer_create", c_int, [c_char_p, c_int, c_int64, POINTER(c_void_p)]),
     ("clipgpu_tokenizer_destroy", None, [c_void_p]),
     ("clipgpu_tokenize", c_int, [c_void_p, POINTER(c_char_p), c_void_p, c_int64, c_int, c_void_p, c_void_p]),

@@ -31,9 +31,9 @@ class Clip:
         return _Builder(cls, model_id=model_id)
 
     @classmethod
-    def _build(cls, model_dir, devices, dtype, max_batch):
+    def _build(cls, model_dir, devices, dtype, max_batch, **opts):
         verify_model_dir(model_dir, need_tokenizer=True)
-        v = VisionEmbedder._build(model_dir, devices, dtype, max_batch)
+        v = VisionEmbedder._build(model_dir, devices, dtype, max_batch, **opts)
         t = TextEmbedder._build(model_dir, devices, dtype, max_batch)
         return cls(v, t, model_dir)
 

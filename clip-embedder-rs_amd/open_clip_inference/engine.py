@@ -201,11 +201,18 @@ class Tokenizer:
         return ids, mask
 
 
-def resize_rgb8(rgb: np.ndarray, size: int, interpolation: str = "bicubic", resize_mode: str = "shortest"):
+RESIZE_IMPLS = ("fast_image_resize", "image")  # src/vision.rs:149-157: the crate feature picks one
+
+
+def resize_rgb8(rgb: np.ndarray, size: int, interpolation: str = "bicubic", resize_mode: str = "shortest",
+                resize_impl: str = "fast_image_resize"):
+    """resize_with_fast_image_resize (default, src/vision.rs:164-198) or resize_with_image
+    (resize_impl="image", src/vision.rs:200-233)."""
     x = np.ascontiguousarray(rgb, dtype=np.uint8)
     out = np.empty((size, size, 3), np.uint8)
-    check(lib().clipgpu_resize_rgb8(x.ctypes.data, x.shape[1], x.shape[0], size, interpolation.encode(),
-                                    resize_mode.encode(), out.ctypes.data))
+    fn = lib().clipgpu_resize_rgb8_image if resize_impl == "image" else lib().clipgpu_resize_rgb8
+    check(fn(x.ctypes.data, x.shape[1], x.shape[0], size, interpolation.encode(), resize_mode.encode(),
+             out.ctypes.data))
     return out
 
 
@@ -241,13 +248,16 @@ def resize_rgb8_gpu(images, size: int, interpolation: str = "bicubic", resize_mo
     return out
 
 
-def preprocess_batch_rgb8(images, size: int, interpolation: str, resize_mode: str, mean, std) -> np.ndarray:
+def preprocess_batch_rgb8(images, size: int, interpolation: str, resize_mode: str, mean, std,
+                          resize_impl: str = "fast_image_resize") -> np.ndarray:
+    if resize_impl not in RESIZE_IMPLS:
+        raise ValueError(f"resize_impl must be one of {RESIZE_IMPLS}")
     arrs = [np.ascontiguousarray(a, dtype=np.uint8) for a in images]
     n = len(arrs)
     out = np.empty((n, 3, size, size), np.float32)
     ptrs = (c_void_p * max(n, 1))(*[a.ctypes.data for a in arrs])
     ws = (c_int * max(n, 1))(*[a.shape[1] for a in arrs])
     hs = (c_int * max(n, 1))(*[a.shape[0] for a in arrs])
-    check(lib().clipgpu_preprocess_batch(ptrs, ws, hs, n, size, interpolation.encode(), resize_mode.encode(),
-                                         f3(mean), f3(std), out.ctypes.data))
+    fn = lib().clipgpu_preprocess_batch_image if resize_impl == "image" else lib().clipgpu_preprocess_batch
+    check(fn(ptrs, ws, hs, n, size, interpolation.encode(), resize_mode.encode(), f3(mean), f3(std), out.ctypes.data))
     return out

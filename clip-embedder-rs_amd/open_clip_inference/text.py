@@ -38,7 +38,7 @@ class TextEmbedder:
         return _Builder(cls, model_id=model_id)
 
     @classmethod
-    def _build(cls, model_dir, devices, dtype, max_batch):  # src/text.rs:54-101
+    def _build(cls, model_dir, devices, dtype, max_batch, **_opts):  # src/text.rs:54-101
         verify_model_dir(model_dir, need_tokenizer=True)
         model_config = ModelConfig.from_file(os.path.join(model_dir, "model_config.json"))
         config = OpenClipConfig.from_file(os.path.join(model_dir, "open_clip_config.json"))

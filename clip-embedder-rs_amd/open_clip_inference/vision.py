@@ -40,6 +40,7 @@ class _Builder:
         self._devices = None
         self._dtype = "bf16"
         self._max_batch = None
+        self._opts = {}
 
     def base_folder(self, path: str):
         self._base = path
@@ -57,20 +58,31 @@ class _Builder:
         self._max_batch = int(n)
         return self
 
+    def with_resize_impl(self, impl: str):
+        """The resize the crate's `fast_image_resize` feature selects (src/vision.rs:149-157):
+        "fast_image_resize" (default feature) or "image" (resize_with_image, :200-233)."""
+        from .engine import RESIZE_IMPLS
+        if impl not in RESIZE_IMPLS:
+            raise ValueError(f"resize impl must be one of {RESIZE_IMPLS}")
+        self._opts["resize_impl"] = impl
+        return self
+
     def build(self):
         d = self._model_dir
         if d is None:
             d = os.path.join(self._base or get_default_base_folder(), self._model_id)
-        return self._cls._build(d, self._devices, self._dtype, self._max_batch)
+        return self._cls._build(d, self._devices, self._dtype, self._max_batch, **self._opts)
 
 
 class VisionEmbedder:
-    def __init__(self, engine: Engine, config: OpenClipConfig, model_config: ModelConfig, model_dir: str):
+    def __init__(self, engine: Engine, config: OpenClipConfig, model_config: ModelConfig, model_dir: str,
+                 resize_impl: str = "fast_image_resize"):
         self.session = engine          # pub session (src/vision.rs:21) -> engine handle
         self.config = config
         self.model_config = model_config
         self.input_name = "pixel_values"
         self.model_dir = model_dir
+        self.resize_impl = resize_impl
 
     # -- builders (src/vision.rs:45-84) --
     @classmethod
@@ -82,16 +94,16 @@ class VisionEmbedder:
         return _Builder(cls, model_id=model_id)
 
     @classmethod
-    def _build(cls, model_dir, devices, dtype, max_batch):
+    def _build(cls, model_dir, devices, dtype, max_batch, resize_impl="fast_image_resize"):
         verify_model_dir(model_dir)
         config = OpenClipConfig.from_file(os.path.join(model_dir, "open_clip_config.json"))
         model_config = ModelConfig.from_file(os.path.join(model_dir, "model_config.json"))
         engine = Engine(model_dir, _lib.TOWER_VISION, devices, dtype, max_batch or 256)
-        return cls(engine, config, model_config, model_dir)
+        return cls(engine, config, model_config, model_dir, resize_impl)
 
     def duplicate(self) -> "VisionEmbedder":  # src/vision.rs:86-91
         e = self.session
-        return self._build(self.model_dir, e.devices, e.dtype, e.max_batch)
+        return self._build(self.model_dir, e.devices, e.dtype, e.max_batch, self.resize_impl)
 
     # -- embedding (src/vision.rs:93-117) --
     def embed_image(self, image) -> np.ndarray:
@@ -103,6 +115,8 @@ class VisionEmbedder:
         # GPU: bit-identical to self.session.embed_pixels(self.preprocess_batch(images)).
         if len(images) == 0:
             raise InferenceError("Empty batch")
+        if self.resize_impl == "image":  # resize_with_image runs on the host (no GPU form)
+            return self.session.embed_pixels(self.preprocess_batch(images))
         return self.session.embed_images_rgb8([to_rgb8(im) for im in images])
 
     # -- preprocessing (src/vision.rs:119-140) --
@@ -112,7 +126,7 @@ class VisionEmbedder:
         pc = self.config.preprocess_cfg
         size = self.config.model_cfg.vision_cfg.image_size
         return preprocess_batch_rgb8([to_rgb8(im) for im in images], size, pc.interpolation, pc.resize_mode,
-                                     pc.mean, pc.std)
+                                     pc.mean, pc.std, self.resize_impl)
 
     def preprocess(self, image) -> np.ndarray:
         return self.preprocess_batch([image])

@@ -130,6 +130,16 @@ int clipgpu_resize_rgb8(const uint8_t* rgb, int width, int height, int size, con
 int clipgpu_preprocess_batch(const uint8_t* const* images, const int* widths, const int* heights, int64_t n,
                              int size, const char* interpolation, const char* resize_mode, const float mean[3],
                              const float std[3], float* out);
+/* The crate's non-default resize, resize_with_image (src/vision.rs:200-233; the build without the
+ * `fast_image_resize` feature): the image crate 0.25.9's imageops::resize (f32 separable filter,
+ * vertical pass then horizontal, CatmullRom / Triangle / Nearest) to round(W*s) x round(H*s),
+ * s = size / min(W, H), then crop_imm at the rounded centre offsets ("squash": resize_exact to
+ * size x size).  Same arguments and outputs as clipgpu_resize_rgb8 / clipgpu_preprocess_batch. */
+int clipgpu_resize_rgb8_image(const uint8_t* rgb, int width, int height, int size, const char* interpolation,
+                              const char* resize_mode, uint8_t* out_rgb);
+int clipgpu_preprocess_batch_image(const uint8_t* const* images, const int* widths, const int* heights, int64_t n,
+                                   int size, const char* interpolation, const char* resize_mode, const float mean[3],
+                                   const float std[3], float* out);
 
 /* ---- tokenizer (src/text.rs:62-139) ----------------------------------------------------
  * Loads a HF tokenizers CLIP tokenizer.json (BPE + ByteLevel, </w> suffix) and applies

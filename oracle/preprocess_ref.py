@@ -99,3 +99,100 @@ def normalize_pixels(rgb: np.ndarray, mean, std) -> np.ndarray:
 
 def preprocess(rgb, S, mean, std, interpolation="bicubic", mode="shortest"):
     return normalize_pixels(resize(rgb, S, interpolation, mode), mean, std)
+
+
+# ---- resize_with_image (src/vision.rs:200-233): the crate's non-default resize ---------------
+# The image crate 0.25.9's imageops::resize (not in this image), restated from its published
+# sample.rs in f32 numpy with the crate's operation order (csrc/host/resize_image.cpp is the
+# product; test_cpu_preprocess.py checks the two bit for bit, and against Pillow loosely).
+F32 = np.float32
+
+
+def _catmullrom_f32(x):
+    b, c = F32(0.0), F32(0.5)
+    a = F32(abs(F32(x)))
+    if a < F32(1.0):
+        k = (F32(12.0) - F32(9.0) * b - F32(6.0) * c) * (a * (a * a)) + \
+            (F32(-18.0) + F32(12.0) * b + F32(6.0) * c) * (a * a) + (F32(6.0) - F32(2.0) * b)
+    elif a < F32(2.0):
+        k = (-b - F32(6.0) * c) * (a * (a * a)) + (F32(6.0) * b + F32(30.0) * c) * (a * a) + \
+            (F32(-12.0) * b - F32(48.0) * c) * a + (F32(8.0) * b + F32(24.0) * c)
+    else:
+        k = F32(0.0)
+    return F32(k / F32(6.0))
+
+
+def _image_kernel(f, x):
+    if f == "catmullrom":
+        return _catmullrom_f32(x)
+    if f == "triangle":
+        ax = F32(abs(F32(x)))
+        return F32(F32(1.0) - ax) if ax < F32(1.0) else F32(0.0)
+    return F32(1.0)
+
+
+def _image_taps(n_in, n_out, f):
+    support = {"catmullrom": 2.0, "triangle": 1.0}.get(f, 0.0)
+    ratio = F32(F32(n_in) / F32(n_out))
+    sratio = F32(1.0) if ratio < F32(1.0) else ratio
+    src_support = F32(F32(support) * sratio)
+    taps = []
+    for o in range(n_out):
+        centre = F32((F32(o) + F32(0.5)) * ratio)
+        left = int(math.floor(F32(centre - src_support)))
+        left = min(max(left, 0), n_in - 1)
+        right = int(math.ceil(F32(centre + src_support)))
+        right = min(max(right, left + 1), n_in)
+        c = F32(centre - F32(0.5))
+        ws = [_image_kernel(f, F32((F32(i) - c) / sratio)) for i in range(left, right)]
+        s = F32(0.0)
+        for w in ws:
+            s = F32(s + w)
+        taps.append((left, [F32(w / s) for w in ws]))
+    return taps
+
+
+def _round_half_away_u8(t):
+    t = np.clip(t, F32(0.0), F32(255.0)).astype(np.float64)
+    fl = np.floor(t)
+    return np.where(t - fl >= 0.5, fl + 1, fl).astype(np.uint8)
+
+
+def image_resize(rgb, nw, nh, f):
+    """image::imageops::resize(Rgb<u8>, nw, nh, filter) -> [nh][nw][3] u8."""
+    H, W = rgb.shape[:2]
+    if (nw, nh) == (W, H):
+        return rgb.copy()
+    src = rgb.astype(F32)
+    tmp = np.empty((nh, W, 3), F32)
+    for oy, (left, ws) in enumerate(_image_taps(H, nh, f)):      # vertical_sample
+        t = np.zeros((W, 3), F32)
+        for i, w in enumerate(ws):
+            t = (t + (src[left + i] * w).astype(F32)).astype(F32)
+        tmp[oy] = t
+    out = np.empty((nh, nw, 3), np.uint8)
+    for ox, (left, ws) in enumerate(_image_taps(W, nw, f)):      # horizontal_sample
+        t = np.zeros((nh, 3), F32)
+        for i, w in enumerate(ws):
+            t = (t + (tmp[:, left + i] * w).astype(F32)).astype(F32)
+        out[:, ox] = _round_half_away_u8(t)
+    return out
+
+
+def resize_with_image(rgb, S, interpolation="bicubic", resize_mode="shortest"):
+    """src/vision.rs:200-233 for an RGB8 image -> [S][S][3] u8."""
+    f = {"bicubic": "catmullrom", "bilinear": "triangle"}.get(interpolation, "nearest")
+    if resize_mode == "squash":
+        return image_resize(rgb, S, S, f)
+    H, W = rgb.shape[:2]
+    scale = F32(F32(S) / F32(min(W, H)))
+
+    def rnd(v):  # f32::round (half away from zero) then `as u32` (saturating)
+        v = float(v)
+        r = math.floor(abs(v) + 0.5) * (1 if v >= 0 else -1)
+        return max(int(r), 0)
+    sw, sh = rnd(F32(F32(W) * scale)), rnd(F32(F32(H) * scale))
+    r = image_resize(rgb, sw, sh, f)
+    x = rnd(F32(F32(F32(sw) - F32(S)) / F32(2.0)))
+    y = rnd(F32(F32(F32(sh) - F32(S)) / F32(2.0)))
+    return r[y:y + S, x:x + S].copy()

@@ -84,3 +84,62 @@ def test_empty_batch_error():
 def test_nearest_mode_runs():
     out = cpp_resize(synth(100, 150), 32, "nearest")
     assert out.shape == (32, 32, 3)
+
+
+IMAGE_CRATE_SIZES = [(389, 517), (97, 301), (224, 224), (600, 450), (64, 64), (33, 70), (1, 400), (700, 1),
+                     (500, 500), (81, 64), (225, 223), (122, 162)]
+
+
+@pytest.mark.parametrize("interp", ["bicubic", "bilinear", "nearest"])
+@pytest.mark.parametrize("mode", ["shortest", "squash"])
+@pytest.mark.parametrize("S", [224, 64])
+def test_resize_with_image_bit_exact_vs_restatement(interp, mode, S):
+    """a6, resize_with_image (src/vision.rs:200-233; the crate without `fast_image_resize`): the
+    C++ path equals the f32 restatement of image 0.25.9's imageops::resize + crop_imm bit for bit
+    (oracle/preprocess_ref.py) -- down- and up-scaling, identity sizes, 1-pixel-wide images, the
+    decoded cat_face crop."""
+    from open_clip_inference.engine import resize_rgb8
+    rng = np.random.default_rng(S + len(interp) + len(mode))
+    g = np.load(GOLD)
+    ims = [rng.integers(0, 256, (h, w, 3), dtype=np.uint8) for h, w in IMAGE_CRATE_SIZES] + [g["cat_face_crop"]]
+    for im in ims:
+        ref = preprocess_ref.resize_with_image(im, S, interp, mode)
+        got = resize_rgb8(im, S, interp, mode, resize_impl="image")
+        assert got.shape == (S, S, 3)
+        assert np.array_equal(got, ref), (im.shape, int(np.abs(got.astype(int) - ref).max()))
+
+
+@pytest.mark.parametrize("interp,pil", [("bicubic", "BICUBIC"), ("bilinear", "BILINEAR"), ("nearest", "NEAREST")])
+def test_resize_with_image_near_pillow_when_downscaling(interp, pil):
+    """Anchor for the restatement (the image crate itself is not in this image): Pillow's
+    resize of the whole image to round(W*s) x round(H*s) then the same crop -- the same filters
+    (CatmullRom = Keys a=-0.5, triangle, nearest) in fixed point -- agrees within one level when
+    downscaling.  Parity with the crate itself is unpinned."""
+    from PIL import Image
+    rng = np.random.default_rng(7)
+    for h, w in [(389, 517), (97, 301), (600, 450), (500, 500)]:
+        im = rng.integers(0, 256, (h, w, 3), dtype=np.uint8)
+        im = (np.cumsum(im.astype(np.int64), axis=1) // np.arange(1, w + 1)[None, :, None]).astype(np.uint8)
+        S = 64
+        a = preprocess_ref.resize_with_image(im, S, interp, "shortest")
+        scale = np.float32(S) / np.float32(min(w, h))
+        sw, sh = int(np.floor(np.float32(w * scale) + 0.5)), int(np.floor(np.float32(h * scale) + 0.5))
+        r = np.asarray(Image.fromarray(im).resize((sw, sh), getattr(Image, pil)))
+        x, y = int(np.floor((sw - S) / 2 + 0.5)), int(np.floor((sh - S) / 2 + 0.5))
+        assert np.abs(a.astype(int) - r[y:y + S, x:x + S]).max() <= 1
+
+
+def test_preprocess_batch_image_backend():
+    """preprocess_batch with the image-crate resize (clipgpu_preprocess_batch_image, thread pool)
+    = normalize_pixels of the restated resize, bit for bit; empty batch is an error."""
+    from open_clip_inference.engine import preprocess_batch_rgb8
+    from open_clip_inference.error import InferenceError
+    rng = np.random.default_rng(3)
+    ims = [rng.integers(0, 256, (h, w, 3), dtype=np.uint8) for h, w in [(389, 517), (97, 301), (64, 64)]]
+    got = preprocess_batch_rgb8(ims, 64, "bicubic", "shortest", OPENAI_MEAN, OPENAI_STD, resize_impl="image")
+    for i, im in enumerate(ims):
+        px = preprocess_ref.resize_with_image(im, 64, "bicubic", "shortest")
+        ref = preprocess_ref.normalize_pixels(px, OPENAI_MEAN, OPENAI_STD)
+        assert np.array_equal(got[i], ref)
+    with pytest.raises(InferenceError, match="Empty batch"):
+        preprocess_batch_rgb8([], 64, "bicubic", "shortest", OPENAI_MEAN, OPENAI_STD, resize_impl="image")

@@ -167,18 +167,24 @@ def test_gemm_mx_rejects_bad_shapes():
 
 
 # ---- fp8 engines end to end ------------------------------------------------------------------
-# The fp8 path is lossy by construction (e4m3 keeps 3 mantissa bits): it cannot meet the bf16
-# path's cos >= 0.9999 bar, and the reference has no fp8 arithmetic to match bit-wise.  The bar
-# here is FP8_COS (stated in DESIGN.md) against the fp64 oracle on the seeded weights; the
-# measured values are printed (pytest -s) and recorded in DESIGN.md.
-FP8_COS = 0.99
+# The fp8 path is lossy by construction (e4m3 keeps 3 mantissa bits), and the reference has no
+# fp8 arithmetic to match bit-wise.  The per-site ablation (tools/mx_ablation.py, DESIGN.md §1,
+# profiles/r02_mx_ablation.jsonl) shows every MX site costs cosine roughly additively and that no
+# split with a useful speed-up keeps the bf16 path's 0.9999: the default split (QKV, c_fc, c_proj)
+# measured min 0.99920-0.99944 on the vision towers and 0.99442-0.99491 on the text towers against
+# the fp32 reference.  These are the bars the shipped split meets (against the fp64 oracle on the
+# seeded weights); the QKV-only split meets the north-star bar on the CLIP vision towers.
+FP8_COS_VISION = 0.999
+FP8_COS_TEXT = 0.993
+FP8_COS = FP8_COS_VISION
 
 
-def _fp8_check(got, ref, label):
+def _fp8_check(got, ref, label, bar=None):
+    bar = (FP8_COS_TEXT if "text" in label else FP8_COS_VISION) if bar is None else bar
     cos = clip_ref.cosine_rows(got, ref)
     print(f"\n[fp8] {label}: cos min {cos.min():.6f} mean {cos.mean():.6f}")
     assert np.all(np.abs(np.linalg.norm(got, axis=1) - 1) < 1e-5)
-    assert cos.min() >= FP8_COS, cos.min()
+    assert cos.min() >= bar, cos.min()
     return cos
 
 
@@ -282,3 +288,27 @@ def test_fp8_input_paths_agree():
     assert np.array_equal(e.embed_images_rgb8(ims), host)
     multi = Engine(make_model_dir(VIT_B_32_CFG, 1234), 0, [0, 0], "fp8", 2)
     assert np.array_equal(multi.embed_images_rgb8(ims), host)
+
+
+@pytest.mark.parametrize("cfg_name", ["VIT_B_32_CFG", "VIT_H_14_378_CFG"])
+def test_fp8_qkv_only_split_meets_the_north_star_bar_on_clip_vision(cfg_name, monkeypatch):
+    """CLIPGPU_MX_SITES=qkv (only the QKV projection in MX-fp8): the CLIP vision towers keep
+    cos >= 0.9999 against the fp64 oracle (the ablation's one split that does)."""
+    from oracle import model_spec, weights
+    from oracle.model_spec import OPENAI_MEAN, OPENAI_STD
+    from tests.helpers import COS_TOL, normalized_pixels, specs
+    cfg = getattr(model_spec, cfg_name)
+    v, _ = specs(cfg)
+    px = normalized_pixels(weights.synth_images_u8(13, 2, v.image_size), OPENAI_MEAN, OPENAI_STD)
+    monkeypatch.setenv("CLIPGPU_MX_SITES", "qkv")
+    e = _engine(cfg, 0, "fp8", 2)
+    _fp8_check(e.embed_pixels(px), clip_ref.encode_image(weights.vision_weights(v, 1234), v, px),
+               f"{cfg_name} vision, MX at QKV only", bar=COS_TOL)
+
+
+def test_fp8_site_selection_is_validated(monkeypatch):
+    from open_clip_inference import _lib as L
+    from oracle.model_spec import VIT_B_32_CFG
+    monkeypatch.setenv("CLIPGPU_MX_SITES", "proj")
+    with pytest.raises(L.ClipError, match="proj in MX needs fc"):
+        _engine(VIT_B_32_CFG, 0, "fp8", 2)
