@@ -67,6 +67,10 @@ using namespace gemm_detail;
 
 constexpr int BK = 64;
 
+#ifndef CLIPGPU_GEMM_SPREAD_ALL
+#define CLIPGPU_GEMM_SPREAD_ALL 0
+#endif
+
 template <typename T>
 __device__ __forceinline__ T to16(float v) { return (T)v; }
 
@@ -405,18 +409,33 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
 // launch_pipe): phase1 of step g issues the DMA of step g+3 into g's buffer, and the wait
 // before the barrier lets the DMA of step g+2 stay in flight, so each DMA has two K-steps to
 // land instead of one (c_proj at K = 3072 with one block per CU was bound by that latency).
-template <typename T, int BM, int BN, int WGM, int WGN, int EPI, int ACT, int NS = 2>
-__global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_pipe_kernel(GemmParams p) {
+// LDS-DMA pieces: a K-step stages BN / 8 W pieces then BM / 8 A pieces of 1 KiB (8 rows x 64 k);
+// piece q goes to wave q % NW, so a wave issues NP = ceil(pieces / NW) of them (one fewer on some
+// waves when NW does not divide the count: uneven tiles, 2-stage schedule only).
+// OCC: blocks per CU the tile is built for; 8-wave tiles at OCC 2 run 4 waves per SIMD (<= 128 VGPRs).
+template <int NW, int OCC>
+struct PipeBounds {
+  static constexpr int waves_per_eu = NW == 8 && OCC >= 2 ? 4 : 2;
+};
+
+template <typename T, int BM, int BN, int WGM, int WGN, int EPI, int ACT, int NS = 2, int OCC = 2>
+__global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_per_eu)) void gemm_pipe_kernel(
+    GemmParams p) {
   typedef typename Vec8<T>::type V8;
   constexpr int NW = WGM * WGN;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
-  constexpr int A_INSTR = BM / 8 / NW, B_INSTR = BN / 8 / NW, NP = A_INSTR + B_INSTR;
+  constexpr int PW = BN / 8, PA = BM / 8, PT = PW + PA;
+  constexpr int NP = (PT + NW - 1) / NW;    // DMA pieces per wave and K-step
+  constexpr bool EVEN = PT % NW == 0;       // every wave issues NP pieces
+  constexpr bool WSPLIT = PW % NW == 0;     // piece i of every wave is a W piece iff i < PW / NW
   constexpr int TM = BM / WGM, TN = BN / WGN, MI = TM / 16, NI = TN / 16;
   constexpr int LG = NI == 2 ? 1 : NI == 4 ? 2 : 3;
-  constexpr bool SPREAD = MI * NI >= 32;
-  static_assert(A_INSTR >= 1 && B_INSTR >= 1 && MI >= 1 && BN <= 256, "bad tile");
+  // DMA pieces spread between MFMA groups of phase 1 (>= 32 MFMAs per phase), else issued up front
+  // (CLIPGPU_GEMM_SPREAD_ALL=1 at build time spreads them on every tile: an experiment switch)
+  constexpr bool SPREAD = MI * NI >= 32 || CLIPGPU_GEMM_SPREAD_ALL;
+  static_assert(BM % 8 == 0 && BN % 8 == 0 && MI >= 1 && BN <= 256 && PT >= NW, "bad tile");
   static_assert(NI == 2 || NI == 4 || NI == 8, "column permutation needs NI in {2,4,8}");
-  static_assert(NS == 2 || NS == 3, "2 or 3 LDS stages");
+  static_assert(NS == 2 || (NS == 3 && EVEN), "2 LDS stages, or 3 with an even piece split");
   __shared__ __attribute__((aligned(16))) char smem[NS * STAGE + 2048];
 
   const int tid = threadIdx.x;
@@ -455,23 +474,28 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_pipe_kernel(GemmParams 
   auto swW = [](int r) { return (r & 2) | (((r >> (2 + LG)) & 1) << 2); };
 
   // ---- LDS-DMA cursor (global step d_g = tile d_ti, K-step d_kt) -----------
-  uint32_t woff[B_INSTR];
-  uint32_t aoff[A_INSTR];
+  // poff[i]: per-lane source byte offset of this wave's piece i (q = wave + NW * i) from the
+  // kernel-argument base pointer (A or W), for the current unit's first K-step.
+  uint32_t poff[NP];
   const char* const Wb = (const char*)p.W;
   const char* const Ab = (const char*)p.A;
+  auto piece_is_w = [&](int i, int q) { return WSPLIT ? (i < PW / NW) : (q < PW); };
   auto set_tile = [&](int m0, int n0, int slice) {
     const int k0 = slice * nk * BK;  // first k of the unit's K-slice
 #pragma unroll
-    for (int i = 0; i < B_INSTR; ++i) {
-      const int r = (wave * B_INSTR + i) * 8 + (lane >> 3);
-      const int c = (lane & 7) ^ swW(r);
-      woff[i] = (uint32_t)(min(n0 + r, p.N - 1) * (int)p.ldw + k0 + c * 8) * 2u;
-    }
-#pragma unroll
-    for (int i = 0; i < A_INSTR; ++i) {
-      const int r = (wave * A_INSTR + i) * 8 + (lane >> 3);
-      const int c = (lane & 7) ^ ((r >> 1) & 7);
-      aoff[i] = (uint32_t)(min(m0 + r, p.M - 1) * (int)p.lda + k0 + c * 8) * 2u;
+    for (int i = 0; i < NP; ++i) {
+      const int q = wave + NW * i;
+      if (!EVEN && q >= PT) {
+        poff[i] = 0;
+      } else if (piece_is_w(i, q)) {
+        const int r = q * 8 + (lane >> 3);
+        const int c = (lane & 7) ^ swW(r);
+        poff[i] = (uint32_t)(min(n0 + r, p.N - 1) * (int)p.ldw + k0 + c * 8) * 2u;
+      } else {
+        const int r = (q - PW) * 8 + (lane >> 3);
+        const int c = (lane & 7) ^ ((r >> 1) & 7);
+        poff[i] = (uint32_t)(min(m0 + r, p.M - 1) * (int)p.lda + k0 + c * 8) * 2u;
+      }
     }
   };
   int d_g = 0, d_kt = 0, d_t = t_first, d_n0 = 0, d_ti = 0;
@@ -481,15 +505,13 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_pipe_kernel(GemmParams 
     set_tile(m0, n0, sl);
     d_n0 = n0;
   }
-  auto dma_piece = [&](auto jc) {  // W pieces first, then A pieces
-    constexpr int j = decltype(jc)::value;
+  auto dma_piece = [&](auto ic) {
+    constexpr int i = decltype(ic)::value;
+    const int q = wave + NW * i;
+    if (!EVEN && q >= PT) return;
     char* const st = smem + (d_g % NS) * STAGE;
-    if constexpr (j < B_INSTR) {
-      glds16(Wb + (size_t)d_kt * (BK * 2) + woff[j], st + A_BYTES + (wave * B_INSTR + j) * 1024);
-    } else {
-      constexpr int i = j - B_INSTR;
-      glds16(Ab + (size_t)d_kt * (BK * 2) + aoff[i], st + (wave * A_INSTR + i) * 1024);
-    }
+    if (piece_is_w(i, q)) glds16(Wb + (size_t)d_kt * (BK * 2) + poff[i], st + A_BYTES + q * 1024);
+    else glds16(Ab + (size_t)d_kt * (BK * 2) + poff[i], st + (q - PW) * 1024);
   };
   auto dma_bias = [&]() {  // the tile's bias slice, with its first K-step (tile-parity buffer)
     if (p.bias != nullptr && wave == 0 && d_kt == 0) {
@@ -784,29 +806,33 @@ hipError_t launch_cfg(const GemmParams& p, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <typename T, int BM, int BN, int WGM, int WGN, int EPI, int ACT>
+// OCC: resident blocks per CU the tile's registers allow (4-wave tiles: up to 3 by LDS; 8-wave
+// tiles: 1, or 2 when built for 4 waves per SIMD).
+template <typename T, int BM, int BN, int WGM, int WGN, int EPI, int ACT, int OCC = 3>
 hipError_t launch_pipe(const GemmParams& p, hipStream_t s) {
+  constexpr int NW = WGM * WGN;
+  constexpr int KOCC = NW == 8 ? (OCC >= 2 ? 2 : 1) : 2;  // kernel template's OCC (launch bounds)
   const int nTn = (p.N + BN - 1) / BN, nTm = (p.M + BM - 1) / BM;
   const int ntiles = nTn * nTm * (p.ksplit > 1 ? p.ksplit : 1);
-  // resident blocks per CU: by LDS (stages + 2 KiB bias) and the 8-wave tiles' registers
+  // resident blocks per CU: by LDS (stages + 2 KiB bias) and by registers (OCC)
   auto per_cu = [&](int ns) {
     const int lds = ns * (BM + BN) * BK * 2 + 2048;
-    return WGM * WGN == 8 ? 1 : std::min(3, (160 * 1024) / lds);
+    return std::max(1, std::min(NW == 8 ? KOCC : OCC, (160 * 1024) / lds));
   };
   // 3 stages for K-long GEMMs whose tiles fit in one round of 3-stage blocks: there the
   // K-step is DMA-latency-bound and the extra stage costs no occupancy (>= 3 K-steps per
-  // unit keep the bias double buffer safe)
-  constexpr bool FITS3 = 3 * (BM + BN) * BK * 2 + 2048 <= 160 * 1024;
+  // unit keep the bias double buffer safe); even DMA piece splits only
+  constexpr bool FITS3 = 3 * (BM + BN) * BK * 2 + 2048 <= 160 * 1024 && (BM / 8 + BN / 8) % NW == 0;
   if constexpr (FITS3) {
     const int nk = p.K / BK / (p.ksplit > 1 ? p.ksplit : 1);
     if (p.pipe3 == 1 && p.K >= 1024 && nk >= 3 && ntiles <= device_cus() * per_cu(3)) {
-      gemm_launch(gemm_pipe_kernel<T, BM, BN, WGM, WGN, EPI, ACT, 3>, ntiles, WGM * WGN * 64, s, p);
+      gemm_launch(gemm_pipe_kernel<T, BM, BN, WGM, WGN, EPI, ACT, 3, KOCC>, ntiles, NW * 64, s, p);
       return hipGetLastError();
     }
   }
   const int resident = device_cus() * per_cu(2);
   const int grid = ntiles <= resident ? ntiles : resident;
-  gemm_launch(gemm_pipe_kernel<T, BM, BN, WGM, WGN, EPI, ACT>, grid, WGM * WGN * 64, s, p);
+  gemm_launch(gemm_pipe_kernel<T, BM, BN, WGM, WGN, EPI, ACT, 2, KOCC>, grid, NW * 64, s, p);
   return hipGetLastError();
 }
 
@@ -917,6 +943,10 @@ hipError_t launch_tile(const GemmParams& p, hipStream_t s) {
       case TILE_64x128_PIPE: return launch_pipe<T, 64, 128, 2, 2, EPI, ACT>(p, s);
       case TILE_160x128_PIPE: return launch_pipe<T, 160, 128, 2, 2, EPI, ACT>(p, s);
       case TILE_160x64_PIPE: return launch_pipe<T, 160, 64, 2, 2, EPI, ACT>(p, s);
+      case TILE_160x128_W8: return launch_pipe<T, 160, 128, 2, 4, EPI, ACT, 2>(p, s);
+      case TILE_128x128_W8: return launch_pipe<T, 128, 128, 2, 4, EPI, ACT, 2>(p, s);
+      case TILE_192x128_W8: return launch_pipe<T, 192, 128, 2, 4, EPI, ACT, 1>(p, s);
+      case TILE_160x256_W8: return launch_pipe<T, 160, 256, 2, 4, EPI, ACT, 1>(p, s);
       default: return launch_pipe<T, 128, 128, 2, 2, EPI, ACT>(p, s);
     }
   }
@@ -929,6 +959,10 @@ hipError_t launch_tile(const GemmParams& p, hipStream_t s) {
       case TILE_64x128_PIPE: return launch_pipe<T, 64, 128, 2, 2, EPI, ACT>(p, s);
       case TILE_160x128_PIPE: return launch_pipe<T, 160, 128, 2, 2, EPI, ACT>(p, s);
       case TILE_160x64_PIPE: return launch_pipe<T, 160, 64, 2, 2, EPI, ACT>(p, s);
+      case TILE_160x128_W8: return launch_pipe<T, 160, 128, 2, 4, EPI, ACT, 2>(p, s);
+      case TILE_128x128_W8: return launch_pipe<T, 128, 128, 2, 4, EPI, ACT, 2>(p, s);
+      case TILE_192x128_W8: return launch_pipe<T, 192, 128, 2, 4, EPI, ACT, 1>(p, s);
+      case TILE_160x256_W8: return launch_pipe<T, 160, 256, 2, 4, EPI, ACT, 1>(p, s);
       default: break;
     }
   }

@@ -55,7 +55,13 @@ enum GemmTile {
                           // (a 128-image lane of ViT-B/32) is 40 row tiles, 960 tiles = 1.9 rounds of 512
   TILE_160x64_PIPE = 8,   // gemm_pipe_kernel: 4 waves (80x32 each), 58 KiB LDS, 2 blocks / CU: the N = 768
                           // GEMMs at M = 6400 are 480 tiles, one round with two blocks on most CUs
-  TILE_LAST = TILE_160x64_PIPE,  // (last of the tiled kernels: the range the tuners and pins take)
+  // 8-wave tiles (two or four waves per SIMD: one wave's fragment reads, DMA issue and barrier
+  // waits overlap another's MFMAs on the same SIMD), 2 x 4 waves:
+  TILE_160x128_W8 = 9,    // 80x32 per wave, 74 KiB LDS, 2 blocks / CU (<= 128 VGPRs); uneven DMA split
+  TILE_128x128_W8 = 10,   // 64x32 per wave, 66 KiB LDS, 2 blocks / CU
+  TILE_192x128_W8 = 11,   // 96x32 per wave, 82 KiB LDS, 1 block / CU
+  TILE_160x256_W8 = 12,   // 80x64 per wave, 106 KiB LDS, 1 block / CU; uneven DMA split
+  TILE_LAST = TILE_160x256_W8,  // (last of the tiled kernels: the range the tuners and pins take)
   TILE_SKINNY = 100,      // gemm_skinny_kernel: one wave per 16x16 block, M <= 256 (TILE_AUTO's pick there);
                           // a fixed id outside the tunable range, so new tiles append without renumbering
 };
