@@ -71,6 +71,10 @@ def text_flops(B, T=77, executed=False):
     return L * (2 * B * T * (3 * D * D + D * D + 2 * D * M) + 2 * 2 * B * T * T * D) + 2 * B * D * E - pruned
 
 
+# GemmTile ids (csrc/kernels/kernels.hpp)
+TILE_NAMES = {0: "heuristic", 1: "128x128", 2: "256x128", 3: "256x256", 4: "128x128pipe", 5: "128x64pipe",
+              6: "64x128pipe", 7: "160x128pipe", 8: "160x64pipe", 9: "160x128w8", 10: "128x128w8",
+              11: "192x128w8", 12: "160x256w8"}
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md chip table)
 B_VISION = 256
 B_TEXT = 1024
@@ -265,12 +269,11 @@ def main():
 
     tiles = (ctypes.c_int * 4)()
     _lib.check(_lib.lib().clipgpu_test_engine_tiles(ve._h, tiles))
-    tile_names = {0: "heuristic", 1: "128x128", 2: "256x128", 3: "256x256", 4: "128x128pipe", 5: "128x64pipe",
-                  6: "64x128pipe", 7: "160x128pipe",
-                  8: "160x64pipe"}
+    dev_lanes = ctypes.c_int()
+    _lib.check(_lib.lib().clipgpu_test_engine_lanes(ve._h, ctypes.byref(dev_lanes)))
     mx_names = {0: "heuristic", 2: "mx256x128", 3: "mx128x128"}  # fp8 engines: QKV / c_fc / c_proj sites
     fp8 = args.dtype == "fp8"
-    gemm_tiles = {site: (mx_names if fp8 and site != "out_proj" else tile_names)[t]
+    gemm_tiles = {site: (mx_names if fp8 and site != "out_proj" else TILE_NAMES).get(t, f"tile{t}")
                   for site, t in zip(["qkv", "out_proj", "c_fc", "c_proj"], tiles)}
     # the dominant kernel's peak: the dense bf16 MFMA rate, or the block-scaled MX-fp8 rate (2x)
     peak = PEAK_BF16_TFLOPS * (2 if fp8 else 1)
@@ -404,7 +407,7 @@ def main():
             "config": {"workload": "BASELINE.json configs[1]: ViT-B/32-224 VisionEmbedder, batch 256 "
                                    "synthetic 224x224 per GPU, device-resident input",
                        "global_batch": world * B_VISION, "seq_len": 50,
-                       "parallelism": f"dp{world}, {os.environ.get('CLIPGPU_LANES', '2')} concurrent sub-batch lanes/GPU" + (" + the engine's RCCL all-gather (ncclAllGather in the C ABI) of the [B,512] embeddings on every rank" if dp else "")},
+                       "parallelism": f"dp{world}, {dev_lanes.value} concurrent sub-batch lane(s)/GPU (creation-time tuned)" + (" + the engine's RCCL all-gather (ncclAllGather in the C ABI) of the [B,512] embeddings on every rank" if dp else "")},
             "roofline": {"bound": "mfma", "kernel": f"c_fc GEMM ({int(fc_rows_per_launch)}x3072x768, +QuickGELU, tile {gemm_tiles['c_fc']})",
                          "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
                          "frac": round(achieved / peak, 4), "traffic": traffic,

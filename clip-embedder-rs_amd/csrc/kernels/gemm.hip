@@ -509,6 +509,9 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
     constexpr int i = decltype(ic)::value;
     const int q = wave + NW * i;
     if (!EVEN && q >= PT) return;
+#ifdef CLIPGPU_GEMM_STAMPS
+    if (p.diag & 4) return;  // timing experiment: no operand DMA in the loop (stale LDS tiles)
+#endif
     char* const st = smem + (d_g % NS) * STAGE;
     if (piece_is_w(i, q)) glds16(Wb + (size_t)d_kt * (BK * 2) + poff[i], st + A_BYTES + q * 1024);
     else glds16(Ab + (size_t)d_kt * (BK * 2) + poff[i], st + (q - PW) * 1024);
@@ -653,7 +656,13 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
       if constexpr (EPI == EPI_PATCH) return p.pos + (long)(p.cls + m % G2) * p.N + nc;
       else return (const float*)p.out + (long)m * p.ldo + nc;
     };
-    float4 xr[2][NI];
+    // The rows added in (residual x / positional embedding) are loaded before the epilogue math:
+    // all MI row blocks at once when they fit in the fragment registers the main loop no longer
+    // needs (MI * NI <= 20: one memory round trip instead of MI dependent ones), else one row
+    // block ahead.
+    constexpr bool XALL = MI * NI <= 20;
+    constexpr int XR = XALL ? MI : 2;
+    float4 xr[XR][NI];
     auto load_x = [&](int mi, float4(&dst)[NI]) {
       const int m = m0 + wm + mi * 16 + fr;
       if (m < p.M && nfull) {
@@ -662,10 +671,17 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
         for (int ni = 0; ni < NI; ++ni) dst[ni] = *(const float4*)(src + ni * 4);
       }
     };
-    if constexpr (ADDX) load_x(0, xr[0]);
+    if constexpr (ADDX) {
+      if constexpr (XALL) {
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi) load_x(mi, xr[mi]);
+      } else {
+        load_x(0, xr[0]);
+      }
+    }
 #pragma unroll
     for (int mi = 0; mi < MI; ++mi) {
-      if constexpr (ADDX) {
+      if constexpr (ADDX && !XALL) {
         if (mi + 1 < MI) load_x(mi + 1, xr[(mi + 1) & 1]);
       }
       const int m = m0 + wm + mi * 16 + fr;
@@ -710,7 +726,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
           for (int ni = 0; ni < NI; ++ni) {
             float4 w = make_float4(v[ni][0], v[ni][1], v[ni][2], v[ni][3]);
             if constexpr (ADDX) {
-              const float4 x = xr[mi & 1][ni];
+              const float4 x = xr[XALL ? mi : (mi & 1)][ni];
               w.x += x.x; w.y += x.y; w.z += x.z; w.w += x.w;
             }
             *(float4*)(o + ni * 4) = w;
@@ -770,7 +786,11 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
         else vm_wait<0>();
       }
       after_full_epi = false;
+#ifdef CLIPGPU_GEMM_STAMPS
+      if (!(p.diag & 8)) __builtin_amdgcn_s_barrier();  // bit 3: no step barrier (timing only)
+#else
       __builtin_amdgcn_s_barrier();
+#endif
       phase1(kt + 1 < nk, lds0 + ((g + 1) % NS) * STAGE);
       if (ti == 0 && kt + 1 < nk) GEMM_STAMP(34 + kt);
     }

@@ -66,6 +66,7 @@ _PROTOS = [
     ("clipgpu_test_layernorm", c_int, [c_int, c_int64, c_int64, c_float, c_void_p, c_void_p, c_void_p, c_void_p]),
     ("clipgpu_test_gemm_bench", c_int, [c_int, c_int, c_int, c_int64, c_int64, c_int64, c_int, c_int, POINTER(c_double)]),
     ("clipgpu_test_engine_tiles", c_int, [c_void_p, POINTER(c_int)]),
+    ("clipgpu_test_engine_lanes", c_int, [c_void_p, POINTER(c_int)]),
     ("clipgpu_test_read_weights", c_int, [c_char_p, c_int, c_char_p, c_void_p, c_int64]),
     ("clipgpu_test_patch_embed", c_int, [c_int, c_int, c_int64, c_int64, c_int64, c_int64, c_void_p, POINTER(c_float), POINTER(c_float), c_void_p, c_void_p, c_void_p]),
     ("clipgpu_test_resize_rgb8_gpu", c_int, [POINTER(c_void_p), POINTER(c_int), POINTER(c_int), c_int64, c_int, c_char_p, c_char_p, c_void_p]),

@@ -95,6 +95,9 @@ int clipgpu_test_read_weights(const char* model_dir, int tower, const char* name
  * to pin the four sites. */
 struct clipgpu_engine;
 int clipgpu_test_engine_tiles(const struct clipgpu_engine* e, int tiles[4]);
+/* Concurrent sub-batches the engine's device-side forwards run (the creation-time tuning's pick,
+ * or CLIPGPU_LANES). */
+int clipgpu_test_engine_lanes(const struct clipgpu_engine* e, int* dev_lanes);
 
 #ifdef __cplusplus
 }

@@ -23,6 +23,10 @@ lib.clipgpu_last_error.restype = ctypes.c_char_p
 NB = 2048
 
 CASES = [
+    ("vis_c_fc 160x128p", 0, 1, 6400, 3072, 768, 7),
+    ("vis_c_fc 160x128w8", 0, 1, 6400, 3072, 768, 9),
+    ("vis_c_proj 160x128p", 1, 0, 6400, 768, 3072, 7),
+    ("vis_c_proj 160x64p", 1, 0, 6400, 768, 3072, 8),
     ("vis_c_fc 128", 0, 1, 6400, 3072, 768, 1),
     ("vis_c_fc 256x256", 0, 1, 6400, 3072, 768, 3),
     ("vis_qkv 256x256", 0, 0, 6400, 2304, 768, 3),
