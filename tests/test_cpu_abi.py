@@ -173,3 +173,16 @@ def test_library_provenance_is_checked(monkeypatch):
     monkeypatch.setattr(_source_hash, "source_hash", lambda d: "0" * 64)
     with pytest.raises(ClipError, match="stale native library"):
         _lib._check_provenance(L)
+
+
+def test_bench_names_every_gemm_tile():
+    """bench.py reports the autotuned tiles by name: its table covers every GemmTile id the tuners
+    can pick (kernels.hpp TILE_LAST), so a new tile cannot crash the bench line."""
+    import importlib.util
+    hdr = open(os.path.join(ROOT, "clip-embedder-rs_amd", "csrc", "kernels", "kernels.hpp")).read()
+    ids = {m.group(1): int(m.group(2)) for m in re.finditer(r"\b(TILE_\w+)\s*=\s*(\d+)", hdr)}
+    last = ids[re.search(r"TILE_LAST\s*=\s*(TILE_\w+)", hdr).group(1)]
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    assert set(range(0, last + 1)) <= set(bench.TILE_NAMES)
