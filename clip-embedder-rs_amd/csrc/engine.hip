@@ -197,6 +197,18 @@ struct clipgpu_engine {
   // the extra f32 slab round trip costs more than the better CU fill returns).
   int ksplit = 1;
   int pipe3 = 0;  // CLIPGPU_GEMM_PIPE3=1: 3-stage LDS schedule for K-long one-round GEMMs (GemmParams::pipe3)
+  // Row-complete residual GEMM + LayerNorm (gemm_rowln.hip) for out_proj -> ln_2 / c_proj ->
+  // next ln_1, decided per engine at creation (bit-identical across batch and lane splits).
+  // Eligible: 16-bit sites without split-K whose following LN feeds a 16-bit GEMM, width
+  // 512/768/1024.  CLIPGPU_FUSE_LN=1 fuses every eligible site; =auto lets the creation-time
+  // forward tuning keep a site fused only when the whole forward measures faster; unset / 0:
+  // off.  Off by default: at the ViT-B/32 shapes the fused kernel's 64-row x full-width tiles
+  // (one 156 KiB block per CU, K-steps of 32) measure slower than the tiled GEMM + LayerNorm
+  // pair (profiles/r02_rowln.txt).
+  bool fuse_ok_out = false, fuse_ok_proj = false;
+  bool fuse_out = false, fuse_proj = false;
+  int fuse_mode = 0;  // CLIPGPU_FUSE_LN: 0 off, 1 on, -1 auto
+  int rowln_pf = 8;  // its L2 prefetch distance in K-steps (CLIPGPU_ROWLN_PF; 0 off)
   clipgpu::TowerSpec spec;
   clipgpu::PreprocessCfg pre;
   clipgpu::DType dt = clipgpu::DT_BF16;
@@ -685,11 +697,30 @@ PoolSrc trunk(const clipgpu_engine& e, const Replica& r, int B, int causal, cons
       ProfScope ps(e, PC_TAIL, st);
       check(launch_gather_pooled(r.x, r.h, ids, T, c.x, c.h, B, D, st), "gather pooled rows");
     }
-    gemm(GS_OUT, PC_OUT_PROJ, "out_proj gemm");
-    { ProfScope ps(e, compact ? PC_TAIL : PC_LN, st);
+    // out_proj + residual + ln_2 (c_proj + residual + the next ln_1) in one kernel when fused
+    auto rowln = [&](const void* A, int K, const void* W, const float* bias, float* x, const float* lw,
+                     const float* lb, void* h, int cat, const char* what) {
+      ProfScope ps(e, rows == B * T ? cat : PC_TAIL, st, /*gemm=*/true);
+      RowLnParams p;
+      p.A = A; p.lda = K; p.W = W; p.ldw = K; p.bias = bias; p.x = x;
+      p.ln_w = lw; p.ln_b = lb; p.eps = s.ln_eps; p.h = h;
+      p.M = rows; p.D = D; p.K = K; p.pf = e.rowln_pf;
+      check(launch_gemm_rowln(e.dt, p, st), what);
+    };
+    if (e.fuse_out) {
+      rowln(c.h, D, L.wo, L.bo, c.x, L.ln2_w, L.ln2_b, c.h, PC_OUT_PROJ, "out_proj + ln_2");
+    } else {
+      gemm(GS_OUT, PC_OUT_PROJ, "out_proj gemm");
+      ProfScope ps(e, compact ? PC_TAIL : PC_LN, st);
       check(launch_ln_rows_add(e.dt, c.x, site_split(e, GS_OUT) ? c.slab : nullptr, L.ln2_w, L.ln2_b, s.ln_eps, c.h,
-                               rows, D, st, ln_q(e, GS_FC, c.hs)), "ln_2"); }
+                               rows, D, st, ln_q(e, GS_FC, c.hs)), "ln_2");
+    }
     gemm(GS_FC, PC_C_FC, "c_fc gemm");
+    if (e.fuse_proj && l + 1 < s.layers) {
+      const LayerW& N1 = r.w.layers[l + 1];
+      rowln(r.big, mlp_pad(s), L.w2, L.b2, r.x, N1.ln1_w, N1.ln1_b, r.h, PC_C_PROJ, "c_proj + ln_1");
+      continue;
+    }
     gemm(GS_PROJ, PC_C_PROJ, "c_proj gemm");
     if (l + 1 < s.layers) {  // (the last c_proj's slab is added by the head's first LayerNorm)
       ProfScope ps(e, PC_LN, st);
@@ -771,6 +802,12 @@ void autotune_tiles(clipgpu_engine& e, Replica& r) {
           e.tile[site] = t;
         }
       }
+      continue;
+    }
+    // fused sites run gemm_rowln; c_proj's plain GEMM then only runs in the last layer, at full
+    // rows only when that layer is not pruned
+    if ((site == GS_OUT && e.fuse_out) || (site == GS_PROJ && e.fuse_proj && e.prune)) {
+      e.tile[site] = TILE_AUTO;
       continue;
     }
     e.tile[site] = tune(site_gemm(e, r, L, site, rows), site_epi(site), site == GS_FC ? e.spec.act : ACT_NONE);
@@ -1056,7 +1093,18 @@ void tune_forward(clipgpu_engine& e, Replica& r) {
       e.tuned_rows = keep_rows;
     }
   }
+  // fused residual GEMM + LN per eligible site (auto mode): kept when the forward is faster
+  if (e.fuse_mode < 0) {
+    for (bool* f : {&e.fuse_out, &e.fuse_proj}) {
+      if (!(f == &e.fuse_out ? e.fuse_ok_out : e.fuse_ok_proj)) continue;
+      *f = true;
+      const float ms = time_fwd();
+      if (ms < 0.99f * best) best = ms;
+      else *f = false;
+    }
+  }
   for (int site = 0; site < GS_N; ++site) {
+    if ((site == GS_OUT && e.fuse_out) || (site == GS_PROJ && e.fuse_proj && e.prune)) continue;
     const int keep = e.tile[site];
     for (int t = TILE_128x128; t <= TILE_LAST; ++t) {
       if (t == keep || (site_split(e, site) && t == TILE_128x128)) continue;
@@ -1483,6 +1531,16 @@ int clipgpu_create(const char* model_dir, int tower, const int* device_ids, int 
     if (!s.unsupported.empty()) throw ClipErr(CLIPGPU_ERR_CONFIG, s.unsupported);
     if (const char* sp = getenv("CLIPGPU_GEMM_SPLIT")) e->ksplit = sp[0] == '1' ? 2 : 1;
     if (const char* p3 = getenv("CLIPGPU_GEMM_PIPE3")) e->pipe3 = p3[0] == '1' ? 1 : 0;
+    {
+      if (const char* fl = getenv("CLIPGPU_FUSE_LN")) e->fuse_mode = fl[0] == '1' ? 1 : (fl[0] == 'a' ? -1 : 0);
+      if (const char* pf = getenv("CLIPGPU_ROWLN_PF")) e->rowln_pf = std::max(0, atoi(pf));
+      e->fuse_ok_out = e->fuse_mode != 0 && gemm_rowln_supported(s.width, s.width) && !site_split(*e, GS_OUT) &&
+                       !e->mx_site[GS_FC];
+      e->fuse_ok_proj = e->fuse_mode != 0 && gemm_rowln_supported(s.width, mlp_pad(s)) &&
+                        !site_split(*e, GS_PROJ) && !e->mx_site[GS_PROJ] && !e->mx_site[GS_QKV];
+      e->fuse_out = e->fuse_mode == 1 && e->fuse_ok_out;
+      e->fuse_proj = e->fuse_mode == 1 && e->fuse_ok_proj;
+    }
     if (s.heads <= 0 || s.width % s.heads || s.width % 64)
       throw ClipErr(CLIPGPU_ERR_CONFIG, "Configuration error: width must be a multiple of 64 and of heads");
     const int hd = s.width / s.heads;

@@ -71,6 +71,28 @@ int device_cus();  // CUs of the current device (cached)
 // act: Act enum from common.hpp (only used with EPI_STORE16)
 hipError_t launch_gemm(DType dt, int asrc, int epi, int act, const GemmParams& p, hipStream_t s);
 
+// Row-complete residual GEMM + LayerNorm (gemm_rowln.hip): x[m] += A[m] . W^T + bias (f32,
+// in place) and h[m] = LN(x[m]) * ln_w + ln_b (16-bit; skipped when h is null) for the
+// N = width GEMMs followed by a LayerNorm (out_proj -> ln_2, c_proj -> the next ln_1).
+// A [M][lda], W [D][ldw] 16-bit; x, h [M][D].  h may alias A (each block reads its own rows
+// before it writes them).
+struct RowLnParams {
+  const void* A = nullptr;
+  long lda = 0;
+  const void* W = nullptr;
+  long ldw = 0;
+  const float* bias = nullptr;
+  float* x = nullptr;
+  const float* ln_w = nullptr;
+  const float* ln_b = nullptr;
+  float eps = 1e-5f;
+  void* h = nullptr;
+  int M = 0, D = 0, K = 0;
+  int pf = 8;  // L2 prefetch distance in K-steps (0: off); speed only
+};
+bool gemm_rowln_supported(int D, int K);
+hipError_t launch_gemm_rowln(DType dt, const RowLnParams& p, hipStream_t s);
+
 // Kernel-boundary timing of the next GEMM launch on this thread (clipgpu_profile_*): when
 // both events are set, launch_gemm launches through hipExtLaunchKernelGGL with them, so the
 // events stamp the kernel's own start and end (an event pair recorded around a launch also
@@ -153,6 +175,7 @@ hipError_t launch_cast_f32(DType dt, const float* in, void* out, long n, hipStre
 #ifdef CLIPGPU_GEMM_STAMPS
 // Diagnostic build: copy (or clear) the per-block s_memtime stamps of the last GEMM launch.
 hipError_t read_gemm_stamps(unsigned long long* host, int nblocks, bool clear);
+hipError_t read_rowln_stamps(unsigned long long* host, int nblocks, bool clear);
 #endif
 
 // ---- MX-fp8 path (gemm_mx.hip) ---------------------------------------------------------

@@ -274,6 +274,81 @@ int clipgpu_test_gemm_bench(int dtype, int epi, int act, int64_t M, int64_t N, i
   });
 }
 
+int clipgpu_test_gemm_rowln(int dtype, int64_t M, int64_t D, int64_t K, const float* A, const float* W,
+                            const float* bias, float* x, const float* ln_w, const float* ln_b, float eps, float* h) {
+  return guarded([&]() {
+    const DType dt = dt_of(dtype);
+    if (M <= 0 || !gemm_rowln_supported((int)D, (int)K)) throw ClipErr(CLIPGPU_ERR_INVALID, "bad rowln shape");
+    DevBuf dA(M * K * 2), dW(D * K * 2), dB(D * 4), dx(M * D * 4), dlw(D * 4), dlb(D * 4), dh(M * D * 2);
+    up16(dt, dA.p, A, M * K);
+    up16(dt, dW.p, W, D * K);
+    if (bias) up(dB.p, bias, D * 4);
+    up(dx.p, x, M * D * 4);
+    if (h) {
+      up(dlw.p, ln_w, D * 4);
+      up(dlb.p, ln_b, D * 4);
+    }
+    RowLnParams p;
+    p.A = dA.p; p.lda = K; p.W = dW.p; p.ldw = K; p.bias = bias ? dB.as<float>() : nullptr;
+    p.x = dx.as<float>(); p.ln_w = dlw.as<float>(); p.ln_b = dlb.as<float>(); p.eps = eps;
+    p.h = h ? dh.p : nullptr; p.M = (int)M; p.D = (int)D; p.K = (int)K;
+    if (const char* pf = getenv("CLIPGPU_ROWLN_PF")) p.pf = atoi(pf);
+    TCHECK(launch_gemm_rowln(dt, p, nullptr));
+    TCHECK(hipDeviceSynchronize());
+    down(x, dx.p, M * D * 4);
+    if (h) down16(dt, h, dh.p, M * D);
+  });
+}
+
+int clipgpu_test_gemm_rowln_bench(int dtype, int mode, int64_t M, int64_t D, int64_t K, int iters,
+                                  double* us_per_launch) {
+  return guarded([&]() {
+    const DType dt = dt_of(dtype);
+    if (M <= 0 || !gemm_rowln_supported((int)D, (int)K) || iters <= 0 || !us_per_launch)
+      throw ClipErr(CLIPGPU_ERR_INVALID, "bad rowln bench arguments");
+    DevBuf fA(M * K * 4), fW(D * K * 4), dA(M * K * 2), dW(D * K * 2), dB(D * 4), dx(M * D * 4), dlw(D * 4),
+        dlb(D * 4), dh(M * D * 2);
+    hipLaunchKernelGGL(fill_random, dim3(2048), dim3(256), 0, nullptr, fA.as<float>(), (long)(M * K), 1u);
+    hipLaunchKernelGGL(fill_random, dim3(2048), dim3(256), 0, nullptr, fW.as<float>(), (long)(D * K), 2u);
+    hipLaunchKernelGGL(fill_random, dim3(64), dim3(256), 0, nullptr, dB.as<float>(), (long)D, 3u);
+    hipLaunchKernelGGL(fill_random, dim3(64), dim3(256), 0, nullptr, dlw.as<float>(), (long)D, 4u);
+    hipLaunchKernelGGL(fill_random, dim3(64), dim3(256), 0, nullptr, dlb.as<float>(), (long)D, 5u);
+    TCHECK(launch_cast_f32(dt, fA.as<float>(), dA.p, (long)(M * K), nullptr));
+    TCHECK(launch_cast_f32(dt, fW.as<float>(), dW.p, (long)(D * K), nullptr));
+    TCHECK(hipDeviceSynchronize());
+    RowLnParams p;
+    p.A = dA.p; p.lda = K; p.W = dW.p; p.ldw = K; p.bias = dB.as<float>(); p.x = dx.as<float>();
+    p.ln_w = dlw.as<float>(); p.ln_b = dlb.as<float>(); p.h = mode == 2 ? nullptr : dh.p;
+    p.M = (int)M; p.D = (int)D; p.K = (int)K;
+    if (const char* pf = getenv("CLIPGPU_ROWLN_PF")) p.pf = atoi(pf);
+    GemmParams g{};  // mode 1: the unfused pair (tiled residual GEMM + ln_rows_add)
+    g.A = dA.p; g.lda = K; g.W = dW.p; g.ldw = K; g.bias = dB.as<float>();
+    g.out = dx.p; g.ldo = D; g.M = (int)M; g.N = (int)D; g.K = (int)K; g.tile = tile_override();
+    auto run = [&]() {
+      if (mode != 1) {
+        TCHECK(launch_gemm_rowln(dt, p, nullptr));
+      } else {
+        TCHECK(launch_gemm(dt, A_ROWS, EPI_RESID, 0, g, nullptr));
+        TCHECK(launch_ln_rows_add(dt, dx.as<float>(), nullptr, dlw.as<float>(), dlb.as<float>(), 1e-5f, dh.p, (int)M,
+                                  (int)D, nullptr));
+      }
+    };
+    for (int i = 0; i < 3; ++i) run();
+    hipEvent_t a, b;
+    TCHECK(hipEventCreate(&a));
+    TCHECK(hipEventCreate(&b));
+    TCHECK(hipEventRecord(a, nullptr));
+    for (int i = 0; i < iters; ++i) run();
+    TCHECK(hipEventRecord(b, nullptr));
+    TCHECK(hipEventSynchronize(b));
+    float ms = 0.f;
+    TCHECK(hipEventElapsedTime(&ms, a, b));
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    *us_per_launch = (double)ms * 1000.0 / iters;
+  });
+}
+
 int clipgpu_test_attention_bench(int dtype, int64_t B, int64_t N, int64_t H, int64_t HD, int causal, int iters,
                                  double* us_per_launch) {
   return guarded([&]() {
@@ -430,6 +505,32 @@ int clipgpu_diag_gemm_stamps(int dtype, int epi, int act, int64_t M, int64_t N, 
     TCHECK(launch_gemm(dt, A_ROWS, e, epi == 0 ? act : 0, g, nullptr));
     TCHECK(hipDeviceSynchronize());
     TCHECK(read_gemm_stamps(out, nblocks, false));
+  });
+}
+
+// The fused residual GEMM + LayerNorm with stamps (gemm_rowln.hip slots); with_ln 0: no LN output.
+int clipgpu_diag_rowln_stamps(int dtype, int64_t M, int64_t D, int64_t K, int pf, int with_ln,
+                              unsigned long long* out, int nblocks) {
+  return guarded([&]() {
+    const DType dt = dt_of(dtype);
+    DevBuf fA(M * K * 4), fW(D * K * 4), dA(M * K * 2), dW(D * K * 2), dB(D * 4), dx(M * D * 4), dl(D * 4),
+        dh(M * D * 2);
+    hipLaunchKernelGGL(fill_random, dim3(2048), dim3(256), 0, nullptr, fA.as<float>(), (long)(M * K), 1u);
+    hipLaunchKernelGGL(fill_random, dim3(2048), dim3(256), 0, nullptr, fW.as<float>(), (long)(D * K), 2u);
+    hipLaunchKernelGGL(fill_random, dim3(64), dim3(256), 0, nullptr, dB.as<float>(), (long)D, 3u);
+    hipLaunchKernelGGL(fill_random, dim3(64), dim3(256), 0, nullptr, dl.as<float>(), (long)D, 4u);
+    TCHECK(launch_cast_f32(dt, fA.as<float>(), dA.p, (long)(M * K), nullptr));
+    TCHECK(launch_cast_f32(dt, fW.as<float>(), dW.p, (long)(D * K), nullptr));
+    RowLnParams p;
+    p.A = dA.p; p.lda = K; p.W = dW.p; p.ldw = K; p.bias = dB.as<float>(); p.x = dx.as<float>();
+    p.ln_w = dl.as<float>(); p.ln_b = dl.as<float>(); p.h = with_ln ? dh.p : nullptr;
+    p.M = (int)M; p.D = (int)D; p.K = (int)K; p.pf = pf;
+    for (int i = 0; i < 20; ++i) TCHECK(launch_gemm_rowln(dt, p, nullptr));
+    TCHECK(hipDeviceSynchronize());
+    TCHECK(read_rowln_stamps(nullptr, nblocks, true));
+    TCHECK(launch_gemm_rowln(dt, p, nullptr));
+    TCHECK(hipDeviceSynchronize());
+    TCHECK(read_rowln_stamps(out, nblocks, false));
   });
 }
 #endif

@@ -57,6 +57,17 @@ int clipgpu_test_patch_rows(int dtype, int mode, int64_t B, int64_t S, int64_t P
 int clipgpu_test_gemm_bench(int dtype, int epi, int act, int64_t M, int64_t N, int64_t K, int tile, int iters,
                             double* us_per_launch);
 
+/* Row-complete residual GEMM + LayerNorm (gemm_rowln.hip): x[M][D] += A[M][K] . W[D][K]^T + bias
+ * (in place, f32), then h[M][D] = LN(x) * ln_w + ln_b (16-bit, returned as f32; skipped when h is
+ * NULL).  D in {512, 768, 1024}, K % 32 == 0. */
+int clipgpu_test_gemm_rowln(int dtype, int64_t M, int64_t D, int64_t K, const float* A, const float* W,
+                            const float* bias, float* x, const float* ln_w, const float* ln_b, float eps, float* h);
+/* Its timing (random operands): mode 0 the fused kernel, 2 the fused kernel without the LN output,
+ * 1 the unfused pair (residual GEMM with
+ * CLIPGPU_TEST_TILE's tile + ln_rows_add).  Mean µs per launch (pair) over `iters`. */
+int clipgpu_test_gemm_rowln_bench(int dtype, int mode, int64_t M, int64_t D, int64_t K, int iters,
+                                  double* us_per_launch);
+
 /* Device-resident attention timing (random 16-bit qkv): mean µs per launch_attention over `iters`. */
 int clipgpu_test_attention_bench(int dtype, int64_t B, int64_t N, int64_t H, int64_t HD, int causal, int iters,
                                  double* us_per_launch);

@@ -248,6 +248,45 @@ def test_layernorm(dtype, D):
     assert np.all(np.abs(out - ref) <= 1.01 * rel * np.abs(ref) + 1e-5)
 
 
+@pytest.mark.parametrize("dtype", [BF16, F16])
+@pytest.mark.parametrize("M,D,K", [(64, 512, 512), (100, 768, 768), (333, 768, 3072), (1000, 512, 2048),
+                                   (130, 1024, 1024), (1, 768, 768), (12800, 768, 768)])
+def test_gemm_rowln(dtype, M, D, K):
+    """Fused residual GEMM + LayerNorm (gemm_rowln.hip): the residual stream is bit-identical to the
+    tiled residual GEMM (same K-ordered MFMA sums, same epilogue adds); h is LN of that stream within
+    the 16-bit output rounding."""
+    L = _lib()
+    rng = np.random.default_rng(M + D + K)
+    A = round16(rng.standard_normal((M, K)), dtype)
+    W = round16(rng.standard_normal((D, K)) / np.sqrt(K), dtype)
+    bias = rng.standard_normal(D).astype(np.float32)
+    x0 = (rng.standard_normal((M, D)) * 2).astype(np.float32)
+    w = (1 + 0.1 * rng.standard_normal(D)).astype(np.float32)
+    b = (0.1 * rng.standard_normal(D)).astype(np.float32)
+    x = x0.copy()
+    h = np.empty((M, D), np.float32)
+    L.check(L.lib().clipgpu_test_gemm_rowln(dtype, M, D, K, A.ctypes.data, W.ctypes.data, bias.ctypes.data,
+                                            x.ctypes.data, w.ctypes.data, b.ctypes.data, 1e-5, h.ctypes.data))
+    want = run_gemm(dtype, 1, 0, A, W, bias, x0)
+    assert np.array_equal(x, want)
+    ref = clip_ref.layer_norm(x.astype(np.float64), w, b, 1e-5)
+    rel = 2 ** -8 if dtype == BF16 else 2 ** -11
+    assert np.all(np.abs(h - ref) <= 1.01 * rel * np.abs(ref) + 2e-5)
+    # residual only (no LayerNorm output)
+    x2 = x0.copy()
+    L.check(L.lib().clipgpu_test_gemm_rowln(dtype, M, D, K, A.ctypes.data, W.ctypes.data, bias.ctypes.data,
+                                            x2.ctypes.data, None, None, 1e-5, None))
+    assert np.array_equal(x2, want)
+
+
+def test_gemm_rowln_rejects_unsupported_shapes():
+    L = _lib()
+    z = np.zeros(4, np.float32)
+    for D, K in ((640, 640), (768, 48), (1280, 1280)):
+        assert L.lib().clipgpu_test_gemm_rowln(BF16, 4, D, K, z.ctypes.data, z.ctypes.data, None, z.ctypes.data,
+                                               None, None, 1e-5, None) != 0
+
+
 @pytest.mark.parametrize("mode", [0, 1])
 @pytest.mark.parametrize("S,P", [(224, 32), (64, 16), (70, 14), (384, 16)])
 def test_patch_rows_bit_exact(mode, S, P):

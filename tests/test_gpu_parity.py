@@ -261,6 +261,38 @@ def test_split_k_on_and_off_match_oracle(tower, monkeypatch):
 
 
 @pytest.mark.parametrize("tower", [0, 1])
+def test_fused_residual_gemm_layernorm_matches_oracle(tower, monkeypatch):
+    """CLIPGPU_FUSE_LN=1 (out_proj + ln_2 and c_proj + the next ln_1 in gemm_rowln.hip) meets the
+    north-star tolerance, stays bit-identical across batch splits, lanes and last-layer pruning,
+    and agrees with the unfused engine to within the LayerNorm's reduction-order rounding."""
+    v, t = specs(VIT_B_32_CFG)
+    B = 37
+    if tower == 0:
+        data = normalized_pixels(weights.synth_images_u8(47, B, v.image_size), OPENAI_MEAN, OPENAI_STD)
+        ref = oracle_vision(VIT_B_32_CFG, 1234, data[:6])
+    else:
+        data = weights.synth_token_ids(47, B, t.context_length, t.vocab_size, t.vocab_size - 2,
+                                       t.vocab_size - 1, random_eot=True)
+        ref = oracle_text(VIT_B_32_CFG, 1234, data[:6])
+    emb = (lambda e, d: e.embed_pixels(d)) if tower == 0 else (lambda e, d: e.embed_tokens(d))
+    outs = {}
+    for fuse, lanes, prune in (("1", "1", "1"), ("1", "2", "1"), ("1", "2", "0"), ("0", "2", "1")):
+        monkeypatch.setenv("CLIPGPU_FUSE_LN", fuse)
+        monkeypatch.setenv("CLIPGPU_LANES", lanes)
+        monkeypatch.setenv("CLIPGPU_PRUNE_LAST", prune)
+        e = engine(VIT_B_32_CFG, tower, max_batch=B)
+        outs[(fuse, lanes, prune)] = emb(e, data)
+        if fuse == "1" and lanes == "1":
+            part = emb(e, data[5:9])
+            assert np.array_equal(part, outs[(fuse, lanes, prune)][5:9])
+    fused = outs[("1", "1", "1")]
+    assert np.array_equal(fused, outs[("1", "2", "1")])
+    assert np.array_equal(fused, outs[("1", "2", "0")])
+    check_rows(fused[:6], ref)
+    assert clip_ref.cosine_rows(fused, outs[("0", "2", "1")]).min() >= 0.99999
+
+
+@pytest.mark.parametrize("tower", [0, 1])
 def test_concurrent_lanes_are_bit_exact(tower, monkeypatch):
     """Splitting a batch over concurrent lanes (sub-batches on their own streams)
     is invisible in the output: rows never interact outside attention."""
