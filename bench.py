@@ -162,15 +162,20 @@ def cpu_baseline(px_host, ids_host, gpu_vision, gpu_text, fp8_vision=None, targe
     return res
 
 
-def load_traffic():
+def load_traffic(rows_per_launch):
     """HBM bytes per c_fc launch: NOT measured in this run -- read from the committed PMC summary
     (separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench, gfx950 FETCH_SIZE x2
-    correction, tools/pmc_traffic.py); its `source` names the run it came from."""
+    correction, tools/pmc_traffic.py); its `source` names the run it came from.  Only used when
+    it was measured at this run's rows per launch (the lane split sets them)."""
     p = os.path.join(ROOT, "profiles", "pmc_c_fc.json")
     if os.path.exists(p):
         with open(p) as f:
             d = json.load(f)
-        return d.get("hbm_bytes_per_launch"), "profiles/pmc_c_fc.json: " + d.get("source", "rocprofv3 PMC passes")
+        rec = d.get("by_rows", {}).get(str(int(rows_per_launch)))
+        if rec is None:
+            return None, (f"profiles/pmc_c_fc.json has no measurement at {int(rows_per_launch)} rows per launch "
+                          f"(has {sorted(d.get('by_rows', {}))})")
+        return rec.get("hbm_bytes_per_launch"), "profiles/pmc_c_fc.json: " + rec.get("source", "rocprofv3 PMC passes")
     return None, None
 
 
@@ -389,7 +394,7 @@ def main():
         torch.cuda.synchronize()
         cpu = cpu_baseline(px.cpu().numpy(), ids.cpu().numpy(), out.cpu().numpy(), tout_host, fout_host)
 
-    traffic, traffic_src = load_traffic() if not fp8 else (None, None)
+    traffic, traffic_src = load_traffic(fc_rows_per_launch) if not fp8 else (None, None)
     if rank == 0:
         line = {
             "metric": "images/sec embedding, ViT-B/32-224 vision tower, batch 256 per GPU",
@@ -409,12 +414,14 @@ def main():
                        "global_batch": world * B_VISION, "seq_len": 50,
                        "parallelism": f"dp{world}, {dev_lanes.value} concurrent sub-batch lane(s)/GPU (creation-time tuned)" + (" + the engine's RCCL all-gather (ncclAllGather in the C ABI) of the [B,512] embeddings on every rank" if dp else "")},
             "roofline": {"bound": "mfma", "kernel": f"c_fc GEMM ({int(fc_rows_per_launch)}x3072x768, +QuickGELU, tile {gemm_tiles['c_fc']})",
+                         "rows_per_launch": int(fc_rows_per_launch),
                          "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
                          "frac": round(achieved / peak, 4), "traffic": traffic,
                          "traffic_source": traffic_src,
                          "launches_timed": fc_n, "avg_launch_us": round(fc_avg_s * 1e6, 2)},
             "gemm_tiles": gemm_tiles,
             "gemm_tiles_env": ",".join(str(t) for t in tiles),
+            "lanes_env": dev_lanes.value,
             "whole_forward_mfma_tflops_per_gpu": round(whole_tflops, 1),
             "whole_forward_frac_of_peak": round(whole_tflops / PEAK_BF16_TFLOPS, 4),
             "last_layer_pruned": PRUNE_LAST,

@@ -29,9 +29,10 @@ for s in $STEPS; do
       run bench 600 python bench.py --steps 20 --warmup 5 || exit $? ;;
     breakdown)
       run breakdown 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-fp8 --no-text --no-e2e --breakdown || exit $? ;;
-    vtrace)  # kernel trace of the vision leg alone (per-kernel durations of the timed steps)
+    vtrace)  # kernel trace of the vision leg alone; per-kernel stats of the timed steps only (tools/trace_timed.py)
       run vtrace 300 rocprofv3 --kernel-trace --stats -d gpurun_out/vtrace -o run --output-format csv -- \
-          python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-fp8 --no-text --no-e2e || exit $? ;;
+          python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-fp8 --no-text --no-e2e || exit $?
+      python3 tools/trace_timed.py gpurun_out/vtrace/run_kernel_trace.csv 10 gpurun_out/vtrace_timed_kernels.txt || exit $? ;;
     prof)
       run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
           python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline || exit $?
@@ -39,13 +40,15 @@ for s in $STEPS; do
     pmc)  # HBM bytes of the roofline kernel: FETCH_SIZE and WRITE_SIZE in separate passes,
           # GEMM tiles pinned to the ones the un-profiled bench autotuned (profiling skews tuning)
       export CLIPGPU_GEMM_TILES=$(python3 -c "import json;print([json.loads(l) for l in open('gpurun_out/bench.log') if l.startswith('{')][-1]['gemm_tiles_env'])") || exit 1
+      export CLIPGPU_LANES=$(python3 -c "import json;print([json.loads(l) for l in open('gpurun_out/bench.log') if l.startswith('{')][-1]['lanes_env'])") || exit 1
       for C in FETCH_SIZE WRITE_SIZE; do
         run pmc_$C 600 rocprofv3 --pmc $C --output-format csv -d gpurun_out/pmc_bench/$C -o run -- \
             python3 bench.py --steps 3 --warmup 1 --no-text --no-cpu-baseline --no-fp8 --no-e2e || exit $?
       done
+      ROWS=$(python3 -c "import json;print([json.loads(l) for l in open('gpurun_out/bench.log') if l.startswith('{')][-1]['roofline']['rows_per_launch'])") || exit 1
       python3 tools/pmc_traffic.py gpurun_out/pmc_bench/FETCH_SIZE gpurun_out/pmc_bench/WRITE_SIZE \
-          gpurun_out/pmc_c_fc.json 6400 "${PMC_LABEL:-this run}: --pmc FETCH_SIZE and --pmc WRITE_SIZE passes of bench.py --no-text, tiles $CLIPGPU_GEMM_TILES" || exit $?
-      unset CLIPGPU_GEMM_TILES ;;
+          gpurun_out/pmc_c_fc.json $ROWS "${PMC_LABEL:-this run}: --pmc FETCH_SIZE and --pmc WRITE_SIZE passes of bench.py --no-text, tiles $CLIPGPU_GEMM_TILES" || exit $?
+      unset CLIPGPU_GEMM_TILES CLIPGPU_LANES ;;
   esac
 done
 echo "=== done"

@@ -19,7 +19,7 @@ import re
 import statistics
 import sys
 
-C_FC = re.compile(r"gemm_(bt|pipe)_kernelIDF16bLi\d+ELi\d+ELi\d+ELi\d+ELi0ELi1E(?:Li\dE)?EEv")
+C_FC = re.compile(r"gemm_(bt|pipe)_kernelIDF16bLi\d+ELi\d+ELi\d+ELi\d+ELi0ELi1E(?:Li\d+E)*EEv")
 
 
 def per_launch_kb(d, counter):
@@ -43,7 +43,7 @@ def main():
     M, N, K = (int(sys.argv[4]) if len(sys.argv) > 4 else 128 * 50), 3072, 768
     compulsory = 2 * (M * K + N * K + M * N) + 4 * N
     res = {
-        "kernel": f"c_fc GEMM ({M}x3072x768, bf16, +QuickGELU)",
+        "kernel": f"c_fc GEMM ({M}x3072x768, bf16, +QuickGELU)", "rows_per_launch": M,
         "fetch_size_kb_median": f_kb, "write_size_kb_median": w_kb,
         "fetch_dispatches": nf, "write_dispatches": nw,
         "hbm_read_bytes_per_launch": read_b, "hbm_write_bytes_per_launch": write_b,
@@ -52,6 +52,15 @@ def main():
         "compulsory_bytes_per_launch": compulsory,
         "correction": "FETCH_SIZE x2 (gfx950 wide streaming reads), KB x 1024; WRITE_SIZE as reported",
     }
+    # one record per rows-per-launch (the lane split the creation-time tuning picks sets it):
+    # merged into OUT_JSON's "by_rows", the latest also at the top level
+    prev = {}
+    if os.path.exists(out):
+        with open(out) as fh:
+            prev = json.load(fh)
+    by_rows = prev.get("by_rows", {})
+    by_rows[str(M)] = res
+    res = dict(res, by_rows=by_rows)
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
     print(json.dumps(res))
