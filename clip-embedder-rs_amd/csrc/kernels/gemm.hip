@@ -658,10 +658,13 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
     };
     // The rows added in (residual x / positional embedding) are loaded before the epilogue math:
     // all MI row blocks at once when they fit in the fragment registers the main loop no longer
-    // needs (MI * NI <= 20: one memory round trip instead of MI dependent ones), else one row
-    // block ahead.
-    constexpr bool XALL = MI * NI <= 20;
-    constexpr int XR = XALL ? MI : 2;
+    // needs (MI * NI <= 20: one memory round trip instead of MI dependent ones), else a ring of
+    // XR row blocks loaded XR - 1 ahead.  8-wave tiles have less register room (160x256 at 2 waves
+    // per SIMD spilled with all 20 blocks up front; the 4-waves-per-SIMD builds have 128
+    // registers): a ring of 3 at 2 waves per SIMD, of 2 at 4.
+    constexpr bool XALL = MI * NI <= (NW == 8 ? (OCC >= 2 ? 4 : 12) : 20);
+    constexpr int XRING = (NW == 8 && OCC < 2 && MI * NI <= 24) ? 3 : 2;
+    constexpr int XR = XALL ? MI : (XRING < MI ? XRING : MI);
     float4 xr[XR][NI];
     auto load_x = [&](int mi, float4(&dst)[NI]) {
       const int m = m0 + wm + mi * 16 + fr;
@@ -676,13 +679,14 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
 #pragma unroll
         for (int mi = 0; mi < MI; ++mi) load_x(mi, xr[mi]);
       } else {
-        load_x(0, xr[0]);
+#pragma unroll
+        for (int mi = 0; mi + 1 < XR; ++mi) load_x(mi, xr[mi]);
       }
     }
 #pragma unroll
     for (int mi = 0; mi < MI; ++mi) {
       if constexpr (ADDX && !XALL) {
-        if (mi + 1 < MI) load_x(mi + 1, xr[(mi + 1) & 1]);
+        if (mi + XR - 1 < MI) load_x(mi + XR - 1, xr[(mi + XR - 1) % XR]);
       }
       const int m = m0 + wm + mi * 16 + fr;
       if (m >= p.M) continue;
@@ -726,7 +730,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
           for (int ni = 0; ni < NI; ++ni) {
             float4 w = make_float4(v[ni][0], v[ni][1], v[ni][2], v[ni][3]);
             if constexpr (ADDX) {
-              const float4 x = xr[XALL ? mi : (mi & 1)][ni];
+              const float4 x = xr[XALL ? mi : mi % XR][ni];
               w.x += x.x; w.y += x.y; w.z += x.z; w.w += x.w;
             }
             *(float4*)(o + ni * 4) = w;
@@ -967,6 +971,7 @@ hipError_t launch_tile(const GemmParams& p, hipStream_t s) {
       case TILE_128x128_W8: return launch_pipe<T, 128, 128, 2, 4, EPI, ACT, 2>(p, s);
       case TILE_192x128_W8: return launch_pipe<T, 192, 128, 2, 4, EPI, ACT, 1>(p, s);
       case TILE_160x256_W8: return launch_pipe<T, 160, 256, 2, 4, EPI, ACT, 1>(p, s);
+      case TILE_192x256_W8: return launch_pipe<T, 192, 256, 2, 4, EPI, ACT, 1>(p, s);
       default: return launch_pipe<T, 128, 128, 2, 2, EPI, ACT>(p, s);
     }
   }
@@ -983,6 +988,7 @@ hipError_t launch_tile(const GemmParams& p, hipStream_t s) {
       case TILE_128x128_W8: return launch_pipe<T, 128, 128, 2, 4, EPI, ACT, 2>(p, s);
       case TILE_192x128_W8: return launch_pipe<T, 192, 128, 2, 4, EPI, ACT, 1>(p, s);
       case TILE_160x256_W8: return launch_pipe<T, 160, 256, 2, 4, EPI, ACT, 1>(p, s);
+      case TILE_192x256_W8: return launch_pipe<T, 192, 256, 2, 4, EPI, ACT, 1>(p, s);
       default: break;
     }
   }

@@ -61,7 +61,9 @@ enum GemmTile {
   TILE_128x128_W8 = 10,   // 64x32 per wave, 66 KiB LDS, 2 blocks / CU
   TILE_192x128_W8 = 11,   // 96x32 per wave, 82 KiB LDS, 1 block / CU
   TILE_160x256_W8 = 12,   // 80x64 per wave, 106 KiB LDS, 1 block / CU; uneven DMA split
-  TILE_LAST = TILE_160x256_W8,  // (last of the tiled kernels: the range the tuners and pins take)
+  TILE_192x256_W8 = 13,   // 96x64 per wave, 114 KiB LDS, 1 block / CU: the N = 768 GEMMs at M = 12800
+                          // are 67 x 3 = 201 tiles (one round) at fewer LDS bytes per MFMA than 160x128
+  TILE_LAST = TILE_192x256_W8,  // (last of the tiled kernels: the range the tuners and pins take)
   TILE_SKINNY = 100,      // gemm_skinny_kernel: one wave per 16x16 block, M <= 256 (TILE_AUTO's pick there);
                           // a fixed id outside the tunable range, so new tiles append without renumbering
 };

@@ -48,8 +48,10 @@ def run_gemm(dtype, mode, act, A, W, bias=None, resid=None):
     return out
 
 
-@pytest.fixture(params=[1, 2, 3, 4, 5, 6, 7, 8], ids=["t128x128", "pipe256x128", "pipe256x256", "pipe128x128",
-                                                      "pipe128x64", "pipe64x128", "pipe160x128", "pipe160x64"])
+@pytest.fixture(params=[1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13],
+                ids=["t128x128", "pipe256x128", "pipe256x256", "pipe128x128", "pipe128x64", "pipe64x128",
+                     "pipe160x128", "pipe160x64", "w8_160x128", "w8_128x128", "w8_192x128", "w8_160x256",
+                     "w8_192x256"])
 def tile(request, monkeypatch):
     """Every GEMM tile configuration (GemmTile) through the same numerics checks."""
     monkeypatch.setenv("CLIPGPU_TEST_TILE", str(request.param))

@@ -35,6 +35,14 @@ CASES = [
     ("vis_out 128", 1, 0, 6400, 768, 768, 1),
     ("square8k 256x256", 0, 0, 8192, 8192, 8192, 3),
     ("square8k 128", 0, 0, 8192, 8192, 8192, 1),
+    ("b256_c_proj 160x128p", 1, 0, 12800, 768, 3072, 7),
+    ("b256_c_proj 160x256w8", 1, 0, 12800, 768, 3072, 12),
+    ("b256_c_proj 256x256", 1, 0, 12800, 768, 3072, 3),
+    ("b256_c_fc 256x256", 0, 1, 12800, 3072, 768, 3),
+    ("b256_c_fc 160x256w8", 0, 1, 12800, 3072, 768, 12),
+    ("b256_c_proj 192x256w8", 1, 0, 12800, 768, 3072, 13),
+    ("b256_out 192x256w8", 1, 0, 12800, 768, 768, 13),
+    ("b256_out 128x64p", 1, 0, 12800, 768, 768, 5),
 ]
 if len(sys.argv) > 1:
     CASES = [c for c in CASES if any(a in c[0] for a in sys.argv[1:])]
