@@ -12,12 +12,14 @@ import torch  # noqa: F401,E402
 from open_clip_inference import _lib  # noqa: E402
 
 CASES = [("h14_vision", 32, 730, 16, 80, 0), ("so400m_vision", 64, 576, 16, 72, 0), ("h14_text", 32, 77, 16, 64, 1),
-         ("b32_vision", 128, 50, 12, 64, 0), ("b32_text", 512, 77, 8, 64, 1)]
+         ("b32_vision", 128, 50, 12, 64, 0), ("b32_text", 512, 77, 8, 64, 1),
+         ("b32_vision_1lane", 256, 50, 12, 64, 0), ("b32_text_1lane", 1024, 77, 8, 64, 1)]
 
 L = _lib.lib()
 us = ctypes.c_double()
 for name, B, N, H, HD, causal in CASES:
     _lib.check(L.clipgpu_test_attention_bench(0, B, N, H, HD, causal, 20, ctypes.byref(us)))
     fl = 4.0 * B * H * N * N * HD
+    hbm = 2.0 * B * N * H * HD * 4  # qkv read (3 x) + out write (1 x), 16-bit
     print(json.dumps({"case": name, "B": B, "N": N, "H": H, "hd": HD, "us": round(us.value, 1),
-                      "tflops": round(fl / us.value / 1e6, 1)}), flush=True)
+                      "tflops": round(fl / us.value / 1e6, 1), "hbm_gbs": round(hbm / us.value / 1e3, 1)}), flush=True)
