@@ -63,10 +63,30 @@ __device__ unsigned long long g_gemm_stamps[kStampBlocks * kStampSlots];
 
 namespace {
 
+#if CLIPGPU_GEMM_POISON
+// (race-check build) NaN bytes over the 1 KiB an LDS-DMA of this wave is about to fill; the
+// store is complete before the DMA is issued
+__device__ __forceinline__ void poison_lds(char* dst) {
+  const int lane = threadIdx.x & 63;
+  *(uint4*)(dst + lane * 16) = make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+#define GEMM_POISON(dst) poison_lds(dst)
+#else
+#define GEMM_POISON(dst) do {} while (0)
+#endif
+
 using namespace gemm_detail;
 
 constexpr int BK = 64;
 
+// Race-check build (make poison -> lib/libclipgpu_poison.so, tests/test_gpu_kernels.py): before
+// each LDS-DMA of the pipelined kernel, the issuing wave fills the destination with NaN bytes, so
+// a fragment read that runs ahead of its DMA (a missing vmcnt wait or barrier) reads NaN instead
+// of a stale but finite tile, and the result is no longer bit-identical to the product build's.
+#ifndef CLIPGPU_GEMM_POISON
+#define CLIPGPU_GEMM_POISON 0
+#endif
 #ifndef CLIPGPU_GEMM_SPREAD_ALL
 #define CLIPGPU_GEMM_SPREAD_ALL 0
 #endif
@@ -513,12 +533,15 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
     if (p.diag & 4) return;  // timing experiment: no operand DMA in the loop (stale LDS tiles)
 #endif
     char* const st = smem + (d_g % NS) * STAGE;
-    if (piece_is_w(i, q)) glds16(Wb + (size_t)d_kt * (BK * 2) + poff[i], st + A_BYTES + q * 1024);
-    else glds16(Ab + (size_t)d_kt * (BK * 2) + poff[i], st + (q - PW) * 1024);
+    char* const dst = piece_is_w(i, q) ? st + A_BYTES + q * 1024 : st + (q - PW) * 1024;
+    GEMM_POISON(dst);
+    if (piece_is_w(i, q)) glds16(Wb + (size_t)d_kt * (BK * 2) + poff[i], dst);
+    else glds16(Ab + (size_t)d_kt * (BK * 2) + poff[i], dst);
   };
   auto dma_bias = [&]() {  // the tile's bias slice, with its first K-step (tile-parity buffer)
     if (p.bias != nullptr && wave == 0 && d_kt == 0) {
       const int n = min(d_n0 + lane * 4, ((p.N - 1) / 4) * 4);
+      GEMM_POISON(smem + NS * STAGE + (d_ti & 1) * 1024);
       glds16(p.bias + n, smem + NS * STAGE + (d_ti & 1) * 1024);
     }
   };
@@ -786,8 +809,12 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
         if (after_full_epi) vm_wait<(EPI_VM + NP < 63 ? EPI_VM + NP : 63)>();
         else vm_wait<NP>();
       } else {
+#if CLIPGPU_GEMM_POISON_SELFTEST  // (the race check's own test: drop the wait on the 2-stage path)
+        (void)EW;
+#else
         if (after_full_epi) vm_wait<EW>();
         else vm_wait<0>();
+#endif
       }
       after_full_epi = false;
 #ifdef CLIPGPU_GEMM_STAMPS

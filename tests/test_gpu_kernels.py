@@ -124,6 +124,47 @@ def test_gemm_three_stage_pipeline_is_bit_exact(mode, act, M, N, K, tiles, monke
         assert np.all(np.abs(outs[0] - ref) <= 3e-5 * (np.abs(A) @ np.abs(W).T) + 1e-6)
 
 
+def _poison_lib():
+    """lib/libclipgpu_poison.so (Makefile `poison`, built by `all`): the product library with the
+    pipelined GEMM's LDS-DMA destinations NaN-filled before every DMA."""
+    import ctypes
+    import os
+    path = os.environ.get("CLIPGPU_POISON_LIB") or os.path.join(
+        os.path.dirname(os.path.abspath(__file__)), "..", "clip-embedder-rs_amd", "lib", "libclipgpu_poison.so")
+    if not os.path.exists(path):
+        pytest.skip("race-check library not built (make -C clip-embedder-rs_amd poison)")
+    L = ctypes.CDLL(path)
+    L.clipgpu_test_gemm.argtypes = [ctypes.c_int] * 3 + [ctypes.c_int64] * 3 + [ctypes.c_void_p] * 5
+    L.clipgpu_test_gemm.restype = ctypes.c_int
+    L.clipgpu_last_error.restype = ctypes.c_char_p
+    return L
+
+
+@pytest.mark.parametrize("M,N,K,mode,act", [(1000, 768, 3072, 1, 0), (2600, 3072, 768, 0, 1), (333, 520, 1280, 2, 0),
+                                            (6400, 768, 3072, 1, 0)])
+def test_gemm_pipelines_never_read_a_stage_before_its_dma_lands(M, N, K, mode, act, monkeypatch):
+    """Race check of the LDS-DMA schedules (2- and 3-stage, every pipelined tile, persistent
+    multi-tile walks, M / N tails): in the poison build every DMA destination holds NaN until the
+    DMA lands, so a fragment or bias read that runs ahead of its vmcnt wait / barrier turns the
+    output NaN.  The outputs must equal the product build's bit for bit."""
+    P = _poison_lib()
+    rng = np.random.default_rng(M + N + K)
+    A = np.ascontiguousarray(round16(rng.standard_normal((M, K)), BF16))
+    W = np.ascontiguousarray(round16(rng.standard_normal((N, K)) / np.sqrt(K), BF16))
+    bias = rng.standard_normal(N).astype(np.float32)
+    resid = rng.standard_normal((M, N)).astype(np.float32) if mode == 1 else None
+    for t in range(2, 14):
+        for p3 in ("0", "1"):
+            monkeypatch.setenv("CLIPGPU_TEST_TILE", str(t))
+            monkeypatch.setenv("CLIPGPU_GEMM_PIPE3", p3)
+            want = run_gemm(BF16, mode, act, A, W, bias, resid)
+            got = np.empty((M, N), np.float32)
+            rc = P.clipgpu_test_gemm(BF16, mode, act, M, N, K, A.ctypes.data, W.ctypes.data, bias.ctypes.data,
+                                     None if resid is None else resid.ctypes.data, got.ctypes.data)
+            assert rc == 0, P.clipgpu_last_error()
+            assert np.array_equal(got, want), (t, p3, int(np.isnan(got).sum()))
+
+
 @pytest.mark.parametrize("mode,act", [(0, 1), (0, 2), (1, 0), (2, 0)])
 @pytest.mark.parametrize("M,N,K", [(1, 512, 768), (5, 64, 256), (77, 768, 768), (128, 3072, 768),
                                    (128, 768, 3072), (200, 2304, 1024), (256, 512, 768)])
