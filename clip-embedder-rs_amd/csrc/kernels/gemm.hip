@@ -438,7 +438,7 @@ struct PipeBounds {
   static constexpr int waves_per_eu = NW == 8 && OCC >= 2 ? 4 : 2;
 };
 
-template <typename T, int BM, int BN, int WGM, int WGN, int EPI, int ACT, int NS = 2, int OCC = 2>
+template <typename T, int BM, int BN, int WGM, int WGN, int EPI, int ACT, int NS = 2, int OCC = 2, int RS = 0>
 __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_per_eu)) void gemm_pipe_kernel(
     GemmParams p) {
   typedef typename Vec8<T>::type V8;
@@ -587,14 +587,34 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
   auto read_a = [&](V8(&a)[MI], uint32_t base) {
     static_for<MI>([&](auto mi) { ds_read_b128<(int)mi * 2048>(a[mi], base); });
   };
+  // RS = 1 (read schedule): a phase's NI + MI fragment reads for the next phase go out after the
+  // first RG = MI - 2 MFMA groups, RPG per group, instead of NI up front and one A read after every
+  // group, so the last read has two MFMA groups to land before the phase-end lgkmcnt wait.
+  constexpr int NR = NI + MI, RG = RS ? (MI > 2 ? MI - 2 : 1) : MI, RPG = (NR + RG - 1) / RG;
+  auto read_k = [&](auto kc, V8(&a)[MI], V8(&b)[NI], uint32_t base_b, uint32_t base_a) {
+    constexpr int k = decltype(kc)::value;
+    if constexpr (k < NI) ds_read_b128<k * 512>(b[k], base_b);
+    else ds_read_b128<(k - NI) * 2048>(a[k - NI], base_a);
+  };
+  auto reads_after_group = [&](auto mi, V8(&a)[MI], V8(&b)[NI], uint32_t base_b, uint32_t base_a) {
+    static_for<RPG>([&](auto j) {
+      constexpr int k = (int)decltype(mi)::value * RPG + (int)decltype(j)::value;
+      if constexpr ((int)decltype(mi)::value < RG && k < NR) read_k(std::integral_constant<int, k>{}, a, b, base_b, base_a);
+    });
+  };
   auto phase0 = [&](auto zero, uint32_t buf) {
-    read_b(b1, buf + offB[1]);
+    if constexpr (!RS) read_b(b1, buf + offB[1]);
     static_for<MI>([&](auto mi) {
 #pragma unroll
       for (int ni = 0; ni < NI; ++ni)
         acc[ni][mi] = mfma_16x16x32(b0[ni], a0[mi], decltype(zero)::value ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[ni][mi]);
       __builtin_amdgcn_sched_barrier(0);
-      ds_read_b128<(int)mi * 2048>(a1[mi], buf + offA[1]);
+      if constexpr (RS) {
+        reads_after_group(mi, a1, b1, buf + offB[1], buf + offA[1]);
+        __builtin_amdgcn_sched_barrier(0);
+      } else {
+        ds_read_b128<(int)mi * 2048>(a1[mi], buf + offA[1]);
+      }
     });
     lgkm_wait_all(a1, b1);
   };
@@ -604,7 +624,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
     // the other buffer, unused): a conditional read made the compiler keep a second copy
     // of the fragment registers across the branch
     (void)next;
-    read_b(b0, nbuf + offB[0]);
+    if constexpr (!RS) read_b(b0, nbuf + offB[0]);
     if (dma) {
       dma_bias();
       if constexpr (!SPREAD) static_for<NP>([&](auto j) { dma_piece(j); });
@@ -613,7 +633,8 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
 #pragma unroll
       for (int ni = 0; ni < NI; ++ni) acc[ni][mi] = mfma_16x16x32(b1[ni], a1[mi], acc[ni][mi]);
       __builtin_amdgcn_sched_barrier(0);
-      ds_read_b128<(int)mi * 2048>(a0[mi], nbuf + offA[0]);
+      if constexpr (RS) reads_after_group(mi, a0, b0, nbuf + offB[0], nbuf + offA[0]);
+      else ds_read_b128<(int)mi * 2048>(a0[mi], nbuf + offA[0]);
       if constexpr (SPREAD) {
         static_for<NP>([&](auto j) {
           if constexpr (((int)j * MI) / NP == (int)mi) {
@@ -859,7 +880,7 @@ hipError_t launch_cfg(const GemmParams& p, hipStream_t s) {
 
 // OCC: resident blocks per CU the tile's registers allow (4-wave tiles: up to 3 by LDS; 8-wave
 // tiles: 1, or 2 when built for 4 waves per SIMD).
-template <typename T, int BM, int BN, int WGM, int WGN, int EPI, int ACT, int OCC = 3>
+template <typename T, int BM, int BN, int WGM, int WGN, int EPI, int ACT, int OCC = 3, int RS = 0>
 hipError_t launch_pipe(const GemmParams& p, hipStream_t s) {
   constexpr int NW = WGM * WGN;
   constexpr int KOCC = NW == 8 ? (OCC >= 2 ? 2 : 1) : 2;  // kernel template's OCC (launch bounds)
@@ -877,13 +898,13 @@ hipError_t launch_pipe(const GemmParams& p, hipStream_t s) {
   if constexpr (FITS3) {
     const int nk = p.K / BK / (p.ksplit > 1 ? p.ksplit : 1);
     if (p.pipe3 == 1 && p.K >= 1024 && nk >= 3 && ntiles <= device_cus() * per_cu(3)) {
-      gemm_launch(gemm_pipe_kernel<T, BM, BN, WGM, WGN, EPI, ACT, 3, KOCC>, ntiles, NW * 64, s, p);
+      gemm_launch(gemm_pipe_kernel<T, BM, BN, WGM, WGN, EPI, ACT, 3, KOCC, RS>, ntiles, NW * 64, s, p);
       return hipGetLastError();
     }
   }
   const int resident = device_cus() * per_cu(2);
   const int grid = ntiles <= resident ? ntiles : resident;
-  gemm_launch(gemm_pipe_kernel<T, BM, BN, WGM, WGN, EPI, ACT, 2, KOCC>, grid, NW * 64, s, p);
+  gemm_launch(gemm_pipe_kernel<T, BM, BN, WGM, WGN, EPI, ACT, 2, KOCC, RS>, grid, NW * 64, s, p);
   return hipGetLastError();
 }
 
@@ -999,6 +1020,10 @@ hipError_t launch_tile(const GemmParams& p, hipStream_t s) {
       case TILE_192x128_W8: return launch_pipe<T, 192, 128, 2, 4, EPI, ACT, 1>(p, s);
       case TILE_160x256_W8: return launch_pipe<T, 160, 256, 2, 4, EPI, ACT, 1>(p, s);
       case TILE_192x256_W8: return launch_pipe<T, 192, 256, 2, 4, EPI, ACT, 1>(p, s);
+      case TILE_256x256_RS: return launch_pipe<T, 256, 256, 2, 4, EPI, ACT, 3, 1>(p, s);
+      case TILE_160x128_RS: return launch_pipe<T, 160, 128, 2, 2, EPI, ACT, 3, 1>(p, s);
+      case TILE_128x64_RS: return launch_pipe<T, 128, 64, 2, 2, EPI, ACT, 3, 1>(p, s);
+      case TILE_160x128_W8_RS: return launch_pipe<T, 160, 128, 2, 4, EPI, ACT, 2, 1>(p, s);
       default: return launch_pipe<T, 128, 128, 2, 2, EPI, ACT>(p, s);
     }
   }
@@ -1016,6 +1041,10 @@ hipError_t launch_tile(const GemmParams& p, hipStream_t s) {
       case TILE_192x128_W8: return launch_pipe<T, 192, 128, 2, 4, EPI, ACT, 1>(p, s);
       case TILE_160x256_W8: return launch_pipe<T, 160, 256, 2, 4, EPI, ACT, 1>(p, s);
       case TILE_192x256_W8: return launch_pipe<T, 192, 256, 2, 4, EPI, ACT, 1>(p, s);
+      case TILE_256x256_RS: return launch_pipe<T, 256, 256, 2, 4, EPI, ACT, 3, 1>(p, s);
+      case TILE_160x128_RS: return launch_pipe<T, 160, 128, 2, 2, EPI, ACT, 3, 1>(p, s);
+      case TILE_128x64_RS: return launch_pipe<T, 128, 64, 2, 2, EPI, ACT, 3, 1>(p, s);
+      case TILE_160x128_W8_RS: return launch_pipe<T, 160, 128, 2, 4, EPI, ACT, 2, 1>(p, s);
       default: break;
     }
   }

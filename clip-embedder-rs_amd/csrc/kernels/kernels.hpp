@@ -63,7 +63,13 @@ enum GemmTile {
   TILE_160x256_W8 = 12,   // 80x64 per wave, 106 KiB LDS, 1 block / CU; uneven DMA split
   TILE_192x256_W8 = 13,   // 96x64 per wave, 114 KiB LDS, 1 block / CU: the N = 768 GEMMs at M = 12800
                           // are 67 x 3 = 201 tiles (one round) at fewer LDS bytes per MFMA than 160x128
-  TILE_LAST = TILE_192x256_W8,  // (last of the tiled kernels: the range the tuners and pins take)
+  // the same tiles with the spread fragment-read schedule (gemm_pipe_kernel RS = 1: a phase's reads
+  // for the next phase go out over its first MI - 2 MFMA groups); bit-identical, speed only
+  TILE_256x256_RS = 14,
+  TILE_160x128_RS = 15,
+  TILE_128x64_RS = 16,
+  TILE_160x128_W8_RS = 17,
+  TILE_LAST = TILE_160x128_W8_RS,  // (last of the tiled kernels: the range the tuners and pins take)
   TILE_SKINNY = 100,      // gemm_skinny_kernel: one wave per 16x16 block, M <= 256 (TILE_AUTO's pick there);
                           // a fixed id outside the tunable range, so new tiles append without renumbering
 };
