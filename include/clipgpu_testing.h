@@ -17,8 +17,8 @@ extern "C" {
 
 /* out[M][N] = act(A[M][K] . W[N][K]^T + bias[N]) (act: 0 none, 1 quick_gelu, 2 gelu, 3 gelu_tanh).
  * mode 0: 16-bit output (returned as f32); mode 1: residual (out = resid + ...); mode 2: f32 output.
- * bias and resid may be NULL.  CLIPGPU_TEST_TILE = a GemmTile id (kernels.hpp: 0 auto, 1..8 the tiled
- * kernels, 100 skinny) forces the tile; CLIPGPU_GEMM_PIPE3=1 the 3-stage schedule. */
+ * bias and resid may be NULL.  CLIPGPU_TEST_TILE = a GemmTile id (kernels.hpp: 0 auto, 1..TILE_LAST (17)
+ * the tiled kernels, 100 skinny) forces the tile; CLIPGPU_GEMM_PIPE3=1 the 3-stage schedule. */
 int clipgpu_test_gemm(int dtype, int mode, int act, int64_t M, int64_t N, int64_t K, const float* A,
                       const float* W, const float* bias, const float* resid, float* out);
 
@@ -52,8 +52,8 @@ int clipgpu_test_patch_rows(int dtype, int mode, int64_t B, int64_t S, int64_t P
                             const float mean[3], const float std[3], float* rows_out);
 
 /* Device-resident GEMM timing (random operands): `iters` back-to-back launches of the same
- * GEMM as the engine issues it (epi: 0 store16 (+act), 1 residual f32, 2 store32), tile:
- * 0 auto, 1 128x128, 2 256x128, 3 256x256, 4 128x128 pipelined.  Returns the mean µs per launch (HIP events). */
+ * GEMM as the engine issues it (epi: 0 store16 (+act), 1 residual f32, 2 store32), tile: a GemmTile
+ * id (kernels.hpp; 0 auto).  Returns the mean µs per launch (HIP events). */
 int clipgpu_test_gemm_bench(int dtype, int epi, int act, int64_t M, int64_t N, int64_t K, int tile, int iters,
                             double* us_per_launch);
 
