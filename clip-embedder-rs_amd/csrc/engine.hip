@@ -759,7 +759,7 @@ void autotune_tiles(clipgpu_engine& e, Replica& r) {
                        TILE_128x64_PIPE,  TILE_64x128_PIPE,  TILE_160x128_PIPE, TILE_160x64_PIPE,
                        TILE_160x128_W8,   TILE_128x128_W8,   TILE_192x128_W8,  TILE_160x256_W8,
                        TILE_192x256_W8,   TILE_256x256_RS,   TILE_160x128_RS,  TILE_128x64_RS,
-                       TILE_160x128_W8_RS};
+                       TILE_160x128_W8_RS, TILE_256x256_HALF};
   hipEvent_t a, b;
   HIP_CHECK(hipEventCreate(&a));
   HIP_CHECK(hipEventCreate(&b));

@@ -438,7 +438,15 @@ struct PipeBounds {
   static constexpr int waves_per_eu = NW == 8 && OCC >= 2 ? 4 : 2;
 };
 
-template <typename T, int BM, int BN, int WGM, int WGN, int EPI, int ACT, int NS = 2, int OCC = 2, int RS = 0>
+// HM = 1 (half-tile last round; 2 x 4 waves, 2-stage, no split-K): each XCD's tiles run in the plain
+// strided order for F = cnt / nbx whole rounds, and the R = cnt % nbx tiles of the partial last
+// round as 2R half tiles (rows m0 .. m0 + BM/2 - 1 and m0 + BM/2 .. m0 + BM - 1, full K) on 2R of the
+// XCD's blocks, computed by the waves of the first row half (one per SIMD) while the other four only
+// stage operands and meet the barriers.  The last round then takes a half tile's time instead of a
+// tile's (c_fc at 12800 rows on 256x256: 75 tiles per XCD over 32 blocks, 2 + 11 / 32 rounds of
+// work paid as 3 before).  No K split: every output is the same MFMA chain as in the whole tile.
+template <typename T, int BM, int BN, int WGM, int WGN, int EPI, int ACT, int NS = 2, int OCC = 2, int RS = 0,
+          int HM = 0>
 __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_per_eu)) void gemm_pipe_kernel(
     GemmParams p) {
   typedef typename Vec8<T>::type V8;
@@ -471,8 +479,22 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
   const int nk = p.K / BK / ks;  // K-steps per unit
 
   const int nb = gridDim.x;
+  static_assert(!HM || (NS == 2 && WGM == 2), "half tiles: 2 x N waves, 2-stage schedule");
   int t_first, t_stride, t_end;
-  if (nb % 8 == 0 && nb < ntiles) {
+  int hm_F = 0, hm_start = 0, hm_nbx = 1, hm_j = 0;  // HM: whole rounds, XCD range start, blocks, index
+  if constexpr (HM) {
+    const int x = blockIdx.x & 7, nbx = nb >> 3, j = blockIdx.x >> 3;
+    const int q = ntiles >> 3, r = ntiles & 7;
+    hm_start = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
+    const int cnt = q + (x < r ? 1 : 0);
+    hm_F = cnt / nbx;
+    hm_nbx = nbx;
+    hm_j = j;
+    // units: the F whole tiles, then (blocks j < 2R) one half tile
+    t_first = 0;
+    t_stride = 1;
+    t_end = hm_F + (j < 2 * (cnt % nbx) ? 1 : 0);
+  } else if (nb % 8 == 0 && nb < ntiles) {
     const int x = blockIdx.x & 7, nbx = nb >> 3;
     const int q = ntiles >> 3, r = ntiles & 7;
     const int start = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
@@ -487,9 +509,22 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
   if (t_first >= t_end) return;
   const int total = ((t_end - t_first + t_stride - 1) / t_stride) * nk;  // this block's K-steps
   auto unit_coords = [&](int u, int& m0, int& n0, int& slice) {
+    if constexpr (HM) {  // u < F: whole tile j + u nbx; u == F: half (j & 1) of tile F nbx + j / 2
+      slice = 0;
+      if (u < hm_F) {
+        tile_coords(hm_start + hm_j + u * hm_nbx, nTm, nTn, BM, BN, m0, n0);
+      } else {
+        tile_coords(hm_start + hm_F * hm_nbx + (hm_j >> 1), nTm, nTn, BM, BN, m0, n0);
+        m0 += (hm_j & 1) * (BM / 2);
+      }
+      return;
+    }
     slice = u % ks;
     tile_coords(u / ks, nTm, nTn, BM, BN, m0, n0);
   };
+  // HM: whether this wave computes the current unit (all waves, except the second row half's on a
+  // half tile); wave-uniform
+  bool cur_act = true;
 
   auto swW = [](int r) { return (r & 2) | (((r >> (2 + LG)) & 1) << 2); };
 
@@ -605,9 +640,11 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
   auto phase0 = [&](auto zero, uint32_t buf) {
     if constexpr (!RS) read_b(b1, buf + offB[1]);
     static_for<MI>([&](auto mi) {
+      if (!HM || cur_act) {
 #pragma unroll
-      for (int ni = 0; ni < NI; ++ni)
-        acc[ni][mi] = mfma_16x16x32(b0[ni], a0[mi], decltype(zero)::value ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[ni][mi]);
+        for (int ni = 0; ni < NI; ++ni)
+          acc[ni][mi] = mfma_16x16x32(b0[ni], a0[mi], decltype(zero)::value ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[ni][mi]);
+      }
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (RS) {
         reads_after_group(mi, a1, b1, buf + offB[1], buf + offA[1]);
@@ -630,8 +667,10 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
       if constexpr (!SPREAD) static_for<NP>([&](auto j) { dma_piece(j); });
     }
     static_for<MI>([&](auto mi) {
+      if (!HM || cur_act) {
 #pragma unroll
-      for (int ni = 0; ni < NI; ++ni) acc[ni][mi] = mfma_16x16x32(b1[ni], a1[mi], acc[ni][mi]);
+        for (int ni = 0; ni < NI; ++ni) acc[ni][mi] = mfma_16x16x32(b1[ni], a1[mi], acc[ni][mi]);
+      }
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (RS) reads_after_group(mi, a0, b0, nbuf + offB[0], nbuf + offA[0]);
       else ds_read_b128<(int)mi * 2048>(a0[mi], nbuf + offA[0]);
@@ -816,6 +855,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
   for (int t = t_first; t < t_end; t += t_stride, ++ti) {
     int m0, n0, slice;
     unit_coords(t, m0, n0, slice);
+    if constexpr (HM) cur_act = t < hm_F || wave < WGN;  // a half tile: the first row half's waves
     GEMM_STAMP(2 + ti * 4);
     for (int kt = 0; kt < nk; ++kt, ++g) {
       if (kt + 1 == nk) GEMM_STAMP(3 + ti * 4);
@@ -847,9 +887,9 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
       if (ti == 0 && kt + 1 < nk) GEMM_STAMP(34 + kt);
     }
     GEMM_STAMP(4 + ti * 4);
-    epilogue(m0, n0, ti & 1, slice);
-    // partial tiles and slab units issue fewer vm ops than EPI_VM: drain them
-    after_full_epi = slice == 0 && m0 + BM <= p.M && n0 + BN <= p.N;
+    if (!HM || cur_act) epilogue(m0, n0, ti & 1, slice);
+    // partial tiles, half tiles and slab units issue fewer vm ops than EPI_VM: drain them
+    after_full_epi = slice == 0 && m0 + BM <= p.M && n0 + BN <= p.N && (!HM || t < hm_F);
     if (!after_full_epi) vm_wait<0>();
     if (t + t_stride < t_end) {  // the next tile's step 0 landed at the last barrier
       const uint32_t buf = lds0 + (g % NS) * STAGE;
@@ -905,6 +945,24 @@ hipError_t launch_pipe(const GemmParams& p, hipStream_t s) {
   const int resident = device_cus() * per_cu(2);
   const int grid = ntiles <= resident ? ntiles : resident;
   gemm_launch(gemm_pipe_kernel<T, BM, BN, WGM, WGN, EPI, ACT, 2, KOCC, RS>, grid, NW * 64, s, p);
+  return hipGetLastError();
+}
+
+// Half-tile last round for the 256x256 RS tile (gemm_pipe_kernel HM = 1, one block per CU): when the
+// tiles leave a partial last round of at most nbx / 2 tiles per XCD after >= 1 whole round; else the
+// plain RS launch (the same sums, bit for bit).
+template <typename T, int EPI, int ACT>
+hipError_t launch_pipe_half(const GemmParams& p, hipStream_t s) {
+  const int nb = device_cus();
+  const int ntiles = ((p.N + 255) / 256) * ((p.M + 255) / 256);
+  bool ok = p.ksplit <= 1 && nb % 8 == 0 && ntiles % nb != 0;
+  const int nbx = nb >> 3, q = ntiles >> 3, r = ntiles & 7;
+  for (int x = 0; ok && x < 8; ++x) {
+    const int cnt = q + (x < r ? 1 : 0);
+    ok = cnt >= nbx && 2 * (cnt % nbx) <= nbx;
+  }
+  if (!ok) return launch_pipe<T, 256, 256, 2, 4, EPI, ACT, 3, 1>(p, s);
+  gemm_launch(gemm_pipe_kernel<T, 256, 256, 2, 4, EPI, ACT, 2, 2, 1, 1>, nb, 512, s, p);
   return hipGetLastError();
 }
 
@@ -1045,6 +1103,7 @@ hipError_t launch_tile(const GemmParams& p, hipStream_t s) {
       case TILE_160x128_RS: return launch_pipe<T, 160, 128, 2, 2, EPI, ACT, 3, 1>(p, s);
       case TILE_128x64_RS: return launch_pipe<T, 128, 64, 2, 2, EPI, ACT, 3, 1>(p, s);
       case TILE_160x128_W8_RS: return launch_pipe<T, 160, 128, 2, 4, EPI, ACT, 2, 1>(p, s);
+      case TILE_256x256_HALF: return launch_pipe_half<T, EPI, ACT>(p, s);
       default: break;
     }
   }

@@ -69,7 +69,8 @@ enum GemmTile {
   TILE_160x128_RS = 15,
   TILE_128x64_RS = 16,
   TILE_160x128_W8_RS = 17,
-  TILE_LAST = TILE_160x128_W8_RS,  // (last of the tiled kernels: the range the tuners and pins take)
+  TILE_256x256_HALF = 18,  // 256x256 RS with the partial last round as half tiles (gemm_pipe_kernel HM = 1)
+  TILE_LAST = TILE_256x256_HALF,  // (last of the tiled kernels: the range the tuners and pins take)
   TILE_SKINNY = 100,      // gemm_skinny_kernel: one wave per 16x16 block, M <= 256 (TILE_AUTO's pick there);
                           // a fixed id outside the tunable range, so new tiles append without renumbering
 };

@@ -48,11 +48,11 @@ def run_gemm(dtype, mode, act, A, W, bias=None, resid=None):
     return out
 
 
-@pytest.fixture(params=[1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17],
+@pytest.fixture(params=[1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18],
                 ids=["t128x128", "pipe256x128", "pipe256x256", "pipe128x128", "pipe128x64", "pipe64x128",
                      "pipe160x128", "pipe160x64", "w8_160x128", "w8_128x128", "w8_192x128", "w8_160x256",
                      "w8_192x256", "rs_256x256", "rs_160x128", "rs_128x64",
-                     "rs_w8_160x128"])
+                     "rs_w8_160x128", "half_256x256"])
 def tile(request, monkeypatch):
     """Every GEMM tile configuration (GemmTile) through the same numerics checks."""
     monkeypatch.setenv("CLIPGPU_TEST_TILE", str(request.param))
@@ -141,6 +141,28 @@ def _poison_lib():
     return L
 
 
+@pytest.mark.parametrize("M,N,K,mode,act", [(12800, 3072, 768, 0, 1), (6400, 3072, 768, 0, 1), (6400, 3072, 768, 2, 0),
+                                            (12801, 3072, 768, 0, 1)])
+def test_half_tile_last_round_is_bit_exact(M, N, K, mode, act, monkeypatch):
+    """TILE_256x256_HALF (18) at shapes where its half-tile last round applies (256 CUs: 600 / 300 /
+    650 tiles of 256x256 leave a partial round of <= 16 tiles per XCD): bit-equal to the plain
+    256x256 RS tile, and the race-check build (NaN-poisoned LDS-DMA destinations) too."""
+    rng = np.random.default_rng(M + N)
+    A = np.ascontiguousarray(round16(rng.standard_normal((M, K)), BF16))
+    W = np.ascontiguousarray(round16(rng.standard_normal((N, K)) / np.sqrt(K), BF16))
+    bias = rng.standard_normal(N).astype(np.float32)
+    monkeypatch.setenv("CLIPGPU_TEST_TILE", "14")
+    want = run_gemm(BF16, mode, act, A, W, bias)
+    monkeypatch.setenv("CLIPGPU_TEST_TILE", "18")
+    assert np.array_equal(run_gemm(BF16, mode, act, A, W, bias), want)
+    P = _poison_lib()
+    got = np.empty((M, N), np.float32)
+    rc = P.clipgpu_test_gemm(BF16, mode, act, M, N, K, A.ctypes.data, W.ctypes.data, bias.ctypes.data, None,
+                             got.ctypes.data)
+    assert rc == 0, P.clipgpu_last_error()
+    assert np.array_equal(got, want), int(np.isnan(got).sum())
+
+
 @pytest.mark.parametrize("M,N,K,mode,act", [(1000, 768, 3072, 1, 0), (2600, 3072, 768, 0, 1), (333, 520, 1280, 2, 0),
                                             (6400, 768, 3072, 1, 0)])
 def test_gemm_pipelines_never_read_a_stage_before_its_dma_lands(M, N, K, mode, act, monkeypatch):
@@ -154,7 +176,7 @@ def test_gemm_pipelines_never_read_a_stage_before_its_dma_lands(M, N, K, mode, a
     W = np.ascontiguousarray(round16(rng.standard_normal((N, K)) / np.sqrt(K), BF16))
     bias = rng.standard_normal(N).astype(np.float32)
     resid = rng.standard_normal((M, N)).astype(np.float32) if mode == 1 else None
-    for t in range(2, 18):
+    for t in range(2, 19):
         for p3 in ("0", "1"):
             monkeypatch.setenv("CLIPGPU_TEST_TILE", str(t))
             monkeypatch.setenv("CLIPGPU_GEMM_PIPE3", p3)
