@@ -1113,8 +1113,20 @@ void tune_forward(clipgpu_engine& e, Replica& r) {
       const int prev = e.tile[site];
       e.tile[site] = t;
       const float ms = time_fwd();
-      if (ms < 0.99f * best) best = ms;
-      else e.tile[site] = prev;
+      if (ms < 0.99f * best) {  // confirm against the kept tile re-timed now: a lucky timing of the
+        e.tile[site] = prev;    // candidate or a slow one of `best` must not decide the choice
+        const float kept = time_fwd();
+        e.tile[site] = t;
+        const float again = time_fwd();
+        if (again < 0.99f * kept) {
+          best = std::min(ms, again);
+        } else {
+          e.tile[site] = prev;
+          best = std::min(best, kept);
+        }
+      } else {
+        e.tile[site] = prev;
+      }
     }
   }
   (void)hipEventDestroy(a);

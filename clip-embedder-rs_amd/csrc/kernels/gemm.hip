@@ -441,10 +441,11 @@ struct PipeBounds {
 // HM = 1 (half-tile last round; 2 x 4 waves, 2-stage, no split-K): each XCD's tiles run in the plain
 // strided order for F = cnt / nbx whole rounds, and the R = cnt % nbx tiles of the partial last
 // round as 2R half tiles (rows m0 .. m0 + BM/2 - 1 and m0 + BM/2 .. m0 + BM - 1, full K) on 2R of the
-// XCD's blocks, computed by the waves of the first row half (one per SIMD) while the other four only
-// stage operands and meet the barriers.  The last round then takes a half tile's time instead of a
-// tile's (c_fc at 12800 rows on 256x256: 75 tiles per XCD over 32 blocks, 2 + 11 / 32 rounds of
-// work paid as 3 before).  No K split: every output is the same MFMA chain as in the whole tile.
+// XCD's blocks.  On a half tile every wave takes half its rows (wave tile TM/2 x TN, MI/2 MFMA row
+// groups), so both waves of each SIMD keep computing.  The last round then takes about half a
+// tile's time instead of a tile's (c_fc at 12800 rows on 256x256: 75 tiles per XCD over 32 blocks,
+// 2 + 11 / 32 rounds of work paid as 3 before).  No K split: every output is the same MFMA chain
+// as in the whole tile.
 template <typename T, int BM, int BN, int WGM, int WGN, int EPI, int ACT, int NS = 2, int OCC = 2, int RS = 0,
           int HM = 0>
 __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_per_eu)) void gemm_pipe_kernel(
@@ -522,9 +523,6 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
     slice = u % ks;
     tile_coords(u / ks, nTm, nTn, BM, BN, m0, n0);
   };
-  // HM: whether this wave computes the current unit (all waves, except the second row half's on a
-  // half tile); wave-uniform
-  bool cur_act = true;
 
   auto swW = [](int r) { return (r & 2) | (((r >> (2 + LG)) & 1) << 2); };
 
@@ -612,6 +610,19 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
     offA[kk] = (uint32_t)((wm + fr) * 128 + (((kk * 4 + fq) ^ (fr >> 1)) << 4));
     offB[kk] = (uint32_t)(A_BYTES + rowB * 128 + (((kk * 4 + fq) ^ swW(rowB)) << 4));
   }
+  // the current unit's row layout (HM half tiles: row offset (wave / WGN) * TM / 2, MI / 2 groups)
+  int wm_cur = wm, mi_lim = MI;
+  uint32_t offA_cur[2] = {offA[0], offA[1]};
+  auto set_layout = [&](int u) {
+    if constexpr (HM) {
+      const bool half = u >= hm_F;
+      wm_cur = half ? (wave / WGN) * (TM / 2) : wm;
+      mi_lim = half ? MI / 2 : MI;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) offA_cur[kk] = offA[kk] - (uint32_t)((wm - wm_cur) * 128);
+    }
+    (void)u;
+  };
   const uint32_t lds0 = lds_addr(smem);
   f32x4 acc[NI][MI];
   V8 a0[MI], b0[NI], a1[MI], b1[NI];
@@ -640,17 +651,17 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
   auto phase0 = [&](auto zero, uint32_t buf) {
     if constexpr (!RS) read_b(b1, buf + offB[1]);
     static_for<MI>([&](auto mi) {
-      if (!HM || cur_act) {
+      if (!HM || (int)mi < mi_lim) {
 #pragma unroll
         for (int ni = 0; ni < NI; ++ni)
           acc[ni][mi] = mfma_16x16x32(b0[ni], a0[mi], decltype(zero)::value ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[ni][mi]);
       }
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (RS) {
-        reads_after_group(mi, a1, b1, buf + offB[1], buf + offA[1]);
+        reads_after_group(mi, a1, b1, buf + offB[1], buf + offA_cur[1]);
         __builtin_amdgcn_sched_barrier(0);
       } else {
-        ds_read_b128<(int)mi * 2048>(a1[mi], buf + offA[1]);
+        ds_read_b128<(int)mi * 2048>(a1[mi], buf + offA_cur[1]);
       }
     });
     lgkm_wait_all(a1, b1);
@@ -667,13 +678,13 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
       if constexpr (!SPREAD) static_for<NP>([&](auto j) { dma_piece(j); });
     }
     static_for<MI>([&](auto mi) {
-      if (!HM || cur_act) {
+      if (!HM || (int)mi < mi_lim) {
 #pragma unroll
         for (int ni = 0; ni < NI; ++ni) acc[ni][mi] = mfma_16x16x32(b1[ni], a1[mi], acc[ni][mi]);
       }
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr (RS) reads_after_group(mi, a0, b0, nbuf + offB[0], nbuf + offA[0]);
-      else ds_read_b128<(int)mi * 2048>(a0[mi], nbuf + offA[0]);
+      if constexpr (RS) reads_after_group(mi, a0, b0, nbuf + offB[0], nbuf + offA_cur[0]);
+      else ds_read_b128<(int)mi * 2048>(a0[mi], nbuf + offA_cur[0]);
       if constexpr (SPREAD) {
         static_for<NP>([&](auto j) {
           if constexpr (((int)j * MI) / NP == (int)mi) {
@@ -750,8 +761,8 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
     constexpr int XR = XALL ? MI : (XRING < MI ? XRING : MI);
     float4 xr[XR][NI];
     auto load_x = [&](int mi, float4(&dst)[NI]) {
-      const int m = m0 + wm + mi * 16 + fr;
-      if (m < p.M && nfull) {
+      const int m = m0 + wm_cur + mi * 16 + fr;
+      if (m < p.M && nfull && (!HM || mi < mi_lim)) {
         const float* src = add_src(m);
 #pragma unroll
         for (int ni = 0; ni < NI; ++ni) dst[ni] = *(const float4*)(src + ni * 4);
@@ -771,8 +782,8 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
       if constexpr (ADDX && !XALL) {
         if (mi + XR - 1 < MI) load_x(mi + XR - 1, xr[(mi + XR - 1) % XR]);
       }
-      const int m = m0 + wm + mi * 16 + fr;
-      if (m >= p.M) continue;
+      const int m = m0 + wm_cur + mi * 16 + fr;
+      if (m >= p.M || (HM && mi >= mi_lim)) continue;
       float v[NI][4];
 #pragma unroll
       for (int ni = 0; ni < NI; ++ni)
@@ -855,7 +866,6 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
   for (int t = t_first; t < t_end; t += t_stride, ++ti) {
     int m0, n0, slice;
     unit_coords(t, m0, n0, slice);
-    if constexpr (HM) cur_act = t < hm_F || wave < WGN;  // a half tile: the first row half's waves
     GEMM_STAMP(2 + ti * 4);
     for (int kt = 0; kt < nk; ++kt, ++g) {
       if (kt + 1 == nk) GEMM_STAMP(3 + ti * 4);
@@ -887,14 +897,15 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
       if (ti == 0 && kt + 1 < nk) GEMM_STAMP(34 + kt);
     }
     GEMM_STAMP(4 + ti * 4);
-    if (!HM || cur_act) epilogue(m0, n0, ti & 1, slice);
+    epilogue(m0, n0, ti & 1, slice);
     // partial tiles, half tiles and slab units issue fewer vm ops than EPI_VM: drain them
     after_full_epi = slice == 0 && m0 + BM <= p.M && n0 + BN <= p.N && (!HM || t < hm_F);
     if (!after_full_epi) vm_wait<0>();
     if (t + t_stride < t_end) {  // the next tile's step 0 landed at the last barrier
       const uint32_t buf = lds0 + (g % NS) * STAGE;
+      set_layout(t + t_stride);
       read_b(b0, buf + offB[0]);
-      read_a(a0, buf + offA[0]);
+      read_a(a0, buf + offA_cur[0]);
       lgkm_wait_all(a0, b0);
     }
     GEMM_STAMP(5 + ti * 4);
