@@ -17,7 +17,7 @@ extern "C" {
 
 /* out[M][N] = act(A[M][K] . W[N][K]^T + bias[N]) (act: 0 none, 1 quick_gelu, 2 gelu, 3 gelu_tanh).
  * mode 0: 16-bit output (returned as f32); mode 1: residual (out = resid + ...); mode 2: f32 output.
- * bias and resid may be NULL.  CLIPGPU_TEST_TILE = a GemmTile id (kernels.hpp: 0 auto, 1..TILE_LAST (17)
+ * bias and resid may be NULL.  CLIPGPU_TEST_TILE = a GemmTile id (kernels.hpp: 0 auto, 1..TILE_LAST
  * the tiled kernels, 100 skinny) forces the tile; CLIPGPU_GEMM_PIPE3=1 the 3-stage schedule. */
 int clipgpu_test_gemm(int dtype, int mode, int act, int64_t M, int64_t N, int64_t K, const float* A,
                       const float* W, const float* bias, const float* resid, float* out);
