@@ -1113,16 +1113,18 @@ void tune_forward(clipgpu_engine& e, Replica& r) {
       const int prev = e.tile[site];
       e.tile[site] = t;
       const float ms = time_fwd();
-      if (ms < 0.99f * best) {  // confirm against the kept tile re-timed now: a lucky timing of the
-        e.tile[site] = prev;    // candidate or a slow one of `best` must not decide the choice
-        const float kept = time_fwd();
+      if (ms < 0.99f * best) {  // confirm against the kept tile re-timed before and after the
+        e.tile[site] = prev;    // candidate's second timing: neither a lucky timing nor a clock
+        const float kept = time_fwd();  // drift between timings decides the choice
         e.tile[site] = t;
         const float again = time_fwd();
-        if (again < 0.99f * kept) {
+        e.tile[site] = prev;
+        const float kept2 = time_fwd();
+        if (again < 0.99f * std::min(kept, kept2)) {
+          e.tile[site] = t;
           best = std::min(ms, again);
         } else {
-          e.tile[site] = prev;
-          best = std::min(best, kept);
+          best = std::min(best, std::min(kept, kept2));
         }
       } else {
         e.tile[site] = prev;
