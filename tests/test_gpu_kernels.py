@@ -142,7 +142,7 @@ def _poison_lib():
 
 
 @pytest.mark.parametrize("M,N,K,mode,act", [(12800, 3072, 768, 0, 1), (6400, 3072, 768, 0, 1), (6400, 3072, 768, 2, 0),
-                                            (12801, 3072, 768, 0, 1)])
+                                            (12801, 3072, 768, 0, 1), (12800, 3072, 768, 1, 0)])
 def test_half_tile_last_round_is_bit_exact(M, N, K, mode, act, monkeypatch):
     """TILE_256x256_HALF (18) at shapes where its half-tile last round applies (256 CUs: 600 / 300 /
     650 tiles of 256x256 leave a partial round of <= 16 tiles per XCD): bit-equal to the plain
