@@ -102,6 +102,28 @@ def synth_inputs(rank, device):
     return px.to(device), ids.to(device)
 
 
+def num_cpus_rule():
+    """num_cpus::get(): the reference's ONNX Runtime intra-op thread count (src/onnx.rs:18-22,
+    `intra_threads = num_cpus::get()`).  num_cpus 1.x on Linux returns the CPUs in the process's
+    scheduler affinity, capped by a cgroup CPU quota when one is set (cgroup v2 cpu.max, v1
+    cpu.cfs_quota_us / cpu.cfs_period_us; quota / period rounded up)."""
+    n = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = -(-int(q) // int(per))
+    except (OSError, ValueError):
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0 and per > 0:
+                quota = -(-q // per)
+        except (OSError, ValueError):
+            pass
+    return max(1, min(n, quota) if quota else n), quota
+
+
 def host_info():
     """Host cores as the CPU leg sees them (the GPU box's CPU share, not the machine's count)."""
     model = ""
@@ -113,7 +135,9 @@ def host_info():
                     break
     except OSError:
         pass
+    rule, quota = num_cpus_rule()
     return {"nproc_affinity": len(os.sched_getaffinity(0)), "cpu_count": os.cpu_count(), "cpu_model": model,
+            "cgroup_cpu_quota": quota, "num_cpus_rule": rule,
             "torch_threads": torch.get_num_threads(), "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS")}
 
 
@@ -147,9 +171,17 @@ def cpu_baseline(px_host, ids_host, gpu_vision, gpu_text, fp8_vision=None, targe
         b = np.asarray(b, np.float64)
         return float(((a * b).sum(1) / (np.linalg.norm(a, axis=1) * np.linalg.norm(b, axis=1))).min())
 
+    # Threads: the reference's rule (num_cpus::get(), src/onnx.rs:18-22), held to the CPU share the
+    # GPU pool grants this box (OMP_NUM_THREADS, set by the pool: a box's worker pools must not
+    # exceed it) when that is smaller -- both numbers are reported in `host`.
+    rule, _ = num_cpus_rule()
+    share = int(os.environ.get("OMP_NUM_THREADS") or rule)
+    prev = torch.get_num_threads()
+    torch.set_num_threads(max(1, min(rule, share)))
     ve, vdt = run(vm, px_host, target_s, 32)
     te, tdt = run(tm, ids_host, target_s, 128)
     cores = torch.get_num_threads()
+    torch.set_num_threads(prev)
     res = {"value": round(len(ve) / vdt, 2), "unit": "images/s", "cores": cores, "kind": "port",
            "sample": f"{len(ve)} of the bench's 256 synthetic 224x224 images (batches of 32), ViT-B/32 vision tower, "
                      f"fp32 torch CPU port of the graph (oracle/torch_cpu.py), {cores} threads, {vdt:.1f} s",
@@ -163,11 +195,12 @@ def cpu_baseline(px_host, ids_host, gpu_vision, gpu_text, fp8_vision=None, targe
     return res
 
 
-def load_traffic(rows_per_launch):
+def load_traffic(rows_per_launch, tiles):
     """HBM bytes per c_fc launch: NOT measured in this run -- read from the committed PMC summary
     (separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench, gfx950 FETCH_SIZE x2
     correction, tools/pmc_traffic.py); its `source` names the run it came from.  Only used when
-    it was measured at this run's rows per launch (the lane split sets them)."""
+    it was measured at this run's rows per launch AND with this run's GEMM tiles (the record's
+    `tiles`); otherwise null, with the reason in traffic_source."""
     p = os.path.join(ROOT, "profiles", "pmc_c_fc.json")
     if os.path.exists(p):
         with open(p) as f:
@@ -176,6 +209,9 @@ def load_traffic(rows_per_launch):
         if rec is None:
             return None, (f"profiles/pmc_c_fc.json has no measurement at {int(rows_per_launch)} rows per launch "
                           f"(has {sorted(d.get('by_rows', {}))})")
+        if rec.get("tiles") != tiles:
+            return None, (f"profiles/pmc_c_fc.json's record at {int(rows_per_launch)} rows was taken with tiles "
+                          f"{rec.get('tiles')}, this run uses {tiles}: not applicable")
         return rec.get("hbm_bytes_per_launch"), "profiles/pmc_c_fc.json: " + rec.get("source", "rocprofv3 PMC passes")
     return None, None
 
@@ -395,7 +431,8 @@ def main():
         torch.cuda.synchronize()
         cpu = cpu_baseline(px.cpu().numpy(), ids.cpu().numpy(), out.cpu().numpy(), tout_host, fout_host)
 
-    traffic, traffic_src = load_traffic(fc_rows_per_launch) if not fp8 else (None, None)
+    traffic, traffic_src = (load_traffic(fc_rows_per_launch, ",".join(str(t) for t in tiles)) if not fp8
+                            else (None, None))
     if rank == 0:
         line = {
             "metric": "images/sec embedding, ViT-B/32-224 vision tower, batch 256 per GPU",
@@ -413,7 +450,7 @@ def main():
             "config": {"workload": "BASELINE.json configs[1]: ViT-B/32-224 VisionEmbedder, batch 256 "
                                    "synthetic 224x224 per GPU, device-resident input",
                        "global_batch": world * B_VISION, "seq_len": 50,
-                       "parallelism": f"dp{world}, {dev_lanes.value} concurrent sub-batch lane(s)/GPU (creation-time tuned)" + (" + the engine's RCCL all-gather (ncclAllGather in the C ABI) of the [B,512] embeddings on every rank" if dp else "")},
+                       "parallelism": f"dp{world}, {dev_lanes.value} concurrent sub-batch lane(s)/GPU (committed MI355X tile table)" + (" + the engine's RCCL all-gather (ncclAllGather in the C ABI) of the [B,512] embeddings on every rank" if dp else "")},
             "roofline": {"bound": "mfma", "kernel": f"c_fc GEMM ({int(fc_rows_per_launch)}x3072x768, +QuickGELU, tile {gemm_tiles['c_fc']})",
                          "rows_per_launch": int(fc_rows_per_launch),
                          "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",

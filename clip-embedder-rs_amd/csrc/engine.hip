@@ -200,14 +200,20 @@ struct clipgpu_engine {
   // Row-complete residual GEMM + LayerNorm (gemm_rowln.hip) for out_proj -> ln_2 / c_proj ->
   // next ln_1, decided per engine at creation (bit-identical across batch and lane splits).
   // Eligible: 16-bit sites without split-K whose following LN feeds a 16-bit GEMM, width
-  // 512/768/1024.  CLIPGPU_FUSE_LN=1 fuses every eligible site; =auto lets the creation-time
-  // forward tuning keep a site fused only when the whole forward measures faster; unset / 0:
-  // off.  Off by default: at the ViT-B/32 shapes the fused kernel's 64-row x full-width tiles
-  // (one 156 KiB block per CU, K-steps of 32) measure slower than the tiled GEMM + LayerNorm
-  // pair (profiles/r02_rowln.txt).
+  // 512/768/1024.  CLIPGPU_FUSE_LN=1 fuses every eligible site; unset / 0: off.  Its LayerNorm
+  // reduces in another order than ln_rows_kernel (last-bit differences in h), so the choice is
+  // explicit, never a timing outcome.  Off by default: at the ViT-B/32 shapes the fused kernel's
+  // 64-row x full-width tiles (one 156 KiB block per CU, K-steps of 32) measure slower than the
+  // tiled GEMM + LayerNorm pair (profiles/r02_rowln.txt).
   bool fuse_ok_out = false, fuse_ok_proj = false;
   bool fuse_out = false, fuse_proj = false;
-  int fuse_mode = 0;  // CLIPGPU_FUSE_LN: 0 off, 1 on, -1 auto
+  int fuse_mode = 0;  // CLIPGPU_FUSE_LN: 0 off, 1 on
+  bool tuning = false;  // clipgpu_options.tuning / CLIPGPU_GEMM_AUTOTUNE=1: timing tuner instead of the table
+  // Multi-device handles over distinct devices: the RCCL communicator is created on the first
+  // gathered call (comm_pending), or at creation when clipgpu_options.communicator = 1.
+  bool comm_pending = false;
+  std::vector<int> comm_devs;
+  bool force_bcast = false;  // test hook: gathered calls take the ragged (broadcast) branch
   int rowln_pf = 8;  // its L2 prefetch distance in K-steps (CLIPGPU_ROWLN_PF; 0 off)
   clipgpu::TowerSpec spec;
   clipgpu::PreprocessCfg pre;
@@ -732,17 +738,51 @@ PoolSrc trunk(const clipgpu_engine& e, const Replica& r, int B, int causal, cons
   return PoolSrc{r.x, T, ids};
 }
 
-// Times each candidate tile on every trunk GEMM site at max_batch rows (workspace
-// contents are scratch at this point) and keeps the fastest.  Tile choice changes
-// speed only: every tile computes the same sums in the same K order.
-void autotune_tiles(clipgpu_engine& e, Replica& r) {
-  // tuned for the rows one lane runs at max_batch
+// The committed MI355X tile table (default; clipgpu_options.tuning = 0).  A trunk site's tile is
+// a function of its GEMM shape at the rows one lane runs at max_batch, so an engine's kernels --
+// and the profiles and PMC records taken of them -- are the same on every box and every run.  The
+// entries are the timing tuner's (below) majority choice over repeated runs on MI355X
+// (tools/tile_table.py, profiles/r03_tile_table.jsonl); the tile choice never changes the output
+// bits (every tile computes the same K-ordered sums, test_gemm_tile_choice_is_bit_exact).
+//   qkv / c_fc (N = 3D / MLP wide, K = D): 256x256 with the half-tile last round (tile 18, which
+//     falls back to plain 256x256 RS where the half round does not apply);
+//   out_proj / c_proj (N = D, + residual): 160x128 8-wave RS (tile 17), two blocks per CU;
+//   rows < 2048 (small max_batch): the shape heuristic (TILE_AUTO; skinny kernel <= 256 rows).
+// One lane: the full-batch GEMMs quantize better over 256 CUs than two half-batch lanes (the
+// tuner's lane choice at the BASELINE batches).
+int table_tile(int site, int rows, int N, int K) {
+  (void)N;
+  (void)K;
+  if (rows < 2048) return TILE_AUTO;
+  switch (site) {
+    case GS_QKV: return TILE_256x256_HALF;
+    case GS_FC: return TILE_256x256_HALF;
+    default: return TILE_160x128_W8_RS;
+  }
+}
+
+void table_tiles(clipgpu_engine& e) {
+  if (!e.lanes_pinned) e.dev_lanes = 1;
   const int rows = (e.max_batch + e.dev_lanes - 1) / e.dev_lanes * e.spec.tokens();
   e.tuned_rows = rows;
+  const int D = e.spec.width, MLP = mlp_pad(e.spec);
+  const int shape[GS_N][2] = {{3 * D, D}, {D, D}, {MLP, D}, {D, MLP}};
+  for (int site = 0; site < GS_N; ++site)
+    e.tile[site] = e.mx_site[site] ? MX_TILE_AUTO : table_tile(site, rows, shape[site][0], shape[site][1]);
+  // the patch-embedding GEMM has the c_proj shape class (N = D, K = 3 P^2 padded)
+  const int G = e.spec.grid();
+  const int prow = e.spec.tower == TOWER_VISION ? rows / e.spec.tokens() * G * G : 0;
+  e.tile_patch = prow >= 2048 ? TILE_160x128_W8_RS : TILE_AUTO;
+}
+
+// Tool / test overrides of the tile choice: CLIPGPU_GEMM_TILES="q,o,f,p" pins every site,
+// CLIPGPU_GEMM_AUTOTUNE=0 leaves every site to the shape heuristic.  Returns true when one applied.
+bool tile_env_override(clipgpu_engine& e) {
   const char* env = getenv("CLIPGPU_GEMM_AUTOTUNE");
   if (env && env[0] == '0') {
     for (int& t : e.tile) t = TILE_AUTO;
-    return;
+    e.tile_patch = TILE_AUTO;
+    return true;
   }
   if (const char* fixed = getenv("CLIPGPU_GEMM_TILES")) {  // "q,o,f,p": pin every site (tests)
     int v[4];
@@ -753,8 +793,20 @@ void autotune_tiles(clipgpu_engine& e, Replica& r) {
       e.tile[i] = v[i];
       if (e.mx_site[i]) e.tile[i] = MX_TILE_AUTO;  // the pins name 16-bit tiles
     }
-    return;
+    return true;
   }
+  return false;
+}
+
+// Timing tuner (clipgpu_options.tuning = 1, or CLIPGPU_GEMM_AUTOTUNE=1; tools/tile_table.py uses
+// it to regenerate the table): times each candidate tile on every trunk GEMM site at max_batch
+// rows (workspace contents are scratch at this point) and keeps the fastest.  Tile choice changes
+// speed only: every tile computes the same sums in the same K order.
+void autotune_tiles(clipgpu_engine& e, Replica& r) {
+  // tuned for the rows one lane runs at max_batch
+  const int rows = (e.max_batch + e.dev_lanes - 1) / e.dev_lanes * e.spec.tokens();
+  e.tuned_rows = rows;
+  if (tile_env_override(e)) return;
   const int cands[] = {TILE_128x128,      TILE_128x128_PIPE, TILE_256x128,    TILE_256x256,
                        TILE_128x64_PIPE,  TILE_64x128_PIPE,  TILE_160x128_PIPE, TILE_160x64_PIPE,
                        TILE_160x128_W8,   TILE_128x128_W8,   TILE_192x128_W8,  TILE_160x256_W8,
@@ -1095,16 +1147,6 @@ void tune_forward(clipgpu_engine& e, Replica& r) {
       e.tuned_rows = keep_rows;
     }
   }
-  // fused residual GEMM + LN per eligible site (auto mode): kept when the forward is faster
-  if (e.fuse_mode < 0) {
-    for (bool* f : {&e.fuse_out, &e.fuse_proj}) {
-      if (!(f == &e.fuse_out ? e.fuse_ok_out : e.fuse_ok_proj)) continue;
-      *f = true;
-      const float ms = time_fwd();
-      if (ms < 0.99f * best) best = ms;
-      else *f = false;
-    }
-  }
   for (int site = 0; site < GS_N; ++site) {
     if ((site == GS_OUT && e.fuse_out) || (site == GS_PROJ && e.fuse_proj && e.prune)) continue;
     const int keep = e.tile[site];
@@ -1409,19 +1451,44 @@ void run_sharded(clipgpu_engine& e, int64_t B, F shard) {
 // output on its device, then one collective leaves the whole matrix, in rank order, on every
 // rank: an in-place ncclAllGather when all blocks are equal, else (ragged blocks) one in-place
 // ncclBroadcast per non-empty block inside a group.  `local` is replica i = rank rank0 + i.
+// The multi-device handle's communicator, created on its first gathered call (clipgpu_create_ex).
+void ensure_comm(clipgpu_engine& e) {
+  if (!e.comm_pending) return;
+  std::vector<ncclComm_t> comms(e.comm_devs.size());
+  NCCL_CHECK(ncclCommInitAll(comms.data(), (int)comms.size(), e.comm_devs.data()));
+  for (size_t i = 0; i < comms.size(); ++i) e.reps[i].comm = comms[i];
+  e.comm_pending = false;
+}
+
+// Host-side plan of a gathered call (no GPU; clipgpu_test_gather_plan checks it on the CPU):
+// off[r] = first output row of rank r's block (rank order), equal = every block the same size
+// (one ncclAllGather; else one ncclBroadcast per non-empty block), and per local replica the
+// forward chunks of at most max_batch rows, each written at its rows of the output.
+struct GatherPlan {
+  std::vector<int64_t> off;
+  bool equal = true;
+};
+GatherPlan plan_gather(int nr, const int64_t* rows) {
+  GatherPlan g;
+  g.off.assign((size_t)nr + 1, 0);
+  for (int r = 0; r < nr; ++r) {
+    if (rows[r] < 0) throw ClipErr(CLIPGPU_ERR_INVALID, "negative row count");
+    g.off[r + 1] = g.off[r] + rows[r];
+    g.equal = g.equal && rows[r] == rows[0];
+  }
+  if (g.off[nr] == 0) throw ClipErr(CLIPGPU_ERR_INVALID, "Empty batch");
+  return g;
+}
+
 template <typename Fwd>
 void sharded_gather(clipgpu_engine& e, const int64_t* rows, float* const* d_out, void* const* streams, Fwd fwd) {
   const int nr = e.comm_nranks, E = e.spec.embed_dim, G = (int)e.reps.size();
   if (nr <= 0) throw ClipErr(CLIPGPU_ERR_INVALID, "no communicator: create the handle over distinct devices "
                                                   "or call clipgpu_comm_init_rank first");
-  std::vector<int64_t> off((size_t)nr + 1, 0);
-  bool equal = true;
-  for (int r = 0; r < nr; ++r) {
-    if (rows[r] < 0) throw ClipErr(CLIPGPU_ERR_INVALID, "negative row count");
-    off[r + 1] = off[r] + rows[r];
-    equal = equal && rows[r] == rows[0];
-  }
-  if (off[nr] == 0) throw ClipErr(CLIPGPU_ERR_INVALID, "Empty batch");
+  const GatherPlan plan = plan_gather(nr, rows);
+  const std::vector<int64_t>& off = plan.off;
+  // (test hook clipgpu_test_force_broadcast: the ragged branch with equal blocks)
+  const bool equal = plan.equal && !e.force_bcast;
   std::vector<hipStream_t> sts((size_t)G);
   for (int i = 0; i < G; ++i) {
     Replica& r = e.reps[i];
@@ -1432,6 +1499,7 @@ void sharded_gather(clipgpu_engine& e, const int64_t* rows, float* const* d_out,
     for (int64_t c0 = 0; c0 < rows[rank]; c0 += e.max_batch)
       fwd(r, i, c0, (int)std::min<int64_t>(e.max_batch, rows[rank] - c0), d_out[i] + (off[rank] + c0) * E, sts[i]);
   }
+  ensure_comm(e);
   NCCL_CHECK(ncclGroupStart());
   for (int i = 0; i < G; ++i) {
     Replica& r = e.reps[i];
@@ -1448,10 +1516,33 @@ void sharded_gather(clipgpu_engine& e, const int64_t* rows, float* const* d_out,
   NCCL_CHECK(ncclGroupEnd());
 }
 
+// The handle's communicators: collectives may still be in flight on callers' streams, so every
+// device is drained first; then all of the clique's communicators are finalized inside one group
+// (a one-by-one finalize from one thread can block on peers) and destroyed.
+void destroy_comms(clipgpu_engine& e) {
+  bool any = false;
+  for (auto& r : e.reps)
+    if (r.comm) {
+      (void)hipSetDevice(r.device);
+      (void)hipDeviceSynchronize();
+      any = true;
+    }
+  if (!any) return;
+  if (ncclGroupStart() == ncclSuccess) {
+    for (auto& r : e.reps)
+      if (r.comm) (void)ncclCommFinalize(r.comm);
+    (void)ncclGroupEnd();
+  }
+  for (auto& r : e.reps)
+    if (r.comm) {
+      (void)ncclCommDestroy(r.comm);
+      r.comm = nullptr;
+    }
+}
+
 void destroy_replica(Replica& r) {
   (void)hipSetDevice(r.device);
   if (r.stream) (void)hipStreamSynchronize(r.stream);
-  if (r.comm) (void)ncclCommDestroy(r.comm);
   if (r.arena) (void)hipFree(r.arena);
   if (r.work) (void)hipFree(r.work);
   if (r.pin_in) (void)hipHostFree(r.pin_in);
@@ -1486,11 +1577,38 @@ extern "C" {
 
 int clipgpu_abi_version(void) { return CLIPGPU_ABI_VERSION; }
 
+int clipgpu_options_init(clipgpu_options* o) {
+  return guarded([&]() {
+    if (!o) throw ClipErr(CLIPGPU_ERR_INVALID, "opts is NULL");
+    std::memset(o, 0, sizeof(*o));
+    o->struct_size = sizeof(*o);
+  });
+}
+
 int clipgpu_create(const char* model_dir, int tower, const int* device_ids, int n_devices, int dtype, int max_batch,
                    clipgpu_engine** out) {
+  return clipgpu_create_ex(model_dir, tower, device_ids, n_devices, dtype, max_batch, nullptr, out);
+}
+
+int clipgpu_create_ex(const char* model_dir, int tower, const int* device_ids, int n_devices, int dtype,
+                      int max_batch, const clipgpu_options* opts_in, clipgpu_engine** out) {
   return guarded([&]() {
     if (!out) throw ClipErr(CLIPGPU_ERR_INVALID, "out is NULL");
     *out = nullptr;
+    clipgpu_options opts;
+    std::memset(&opts, 0, sizeof(opts));
+    opts.struct_size = sizeof(opts);
+    if (opts_in) {  // an older caller's smaller struct: its prefix, defaults for the rest
+      if (opts_in->struct_size < 2 * sizeof(uint32_t) || opts_in->struct_size > sizeof(opts))
+        throw ClipErr(CLIPGPU_ERR_INVALID, "clipgpu_options.struct_size: call clipgpu_options_init first");
+      std::memcpy(&opts, opts_in, opts_in->struct_size);
+    }
+    if (opts.mx_sites & ~(CLIPGPU_MX_QKV | CLIPGPU_MX_FC | CLIPGPU_MX_PROJ))
+      throw ClipErr(CLIPGPU_ERR_INVALID, "clipgpu_options.mx_sites: unknown bits");
+    if (opts.lanes < 0 || opts.lanes > 4) throw ClipErr(CLIPGPU_ERR_INVALID, "clipgpu_options.lanes must be 0..4");
+    if (opts.tuning < 0 || opts.tuning > 1) throw ClipErr(CLIPGPU_ERR_INVALID, "clipgpu_options.tuning must be 0 or 1");
+    if (opts.communicator < 0 || opts.communicator > 1)
+      throw ClipErr(CLIPGPU_ERR_INVALID, "clipgpu_options.communicator must be 0 or 1");
     if (!model_dir) throw ClipErr(CLIPGPU_ERR_INVALID, "model_dir is NULL");
     if (tower != CLIPGPU_TOWER_VISION && tower != CLIPGPU_TOWER_TEXT) throw ClipErr(CLIPGPU_ERR_INVALID, "bad tower");
     if (dtype != CLIPGPU_DTYPE_BF16 && dtype != CLIPGPU_DTYPE_F16 && dtype != CLIPGPU_DTYPE_FP8)
@@ -1514,30 +1632,44 @@ int clipgpu_create(const char* model_dir, int tower, const int* device_ids, int 
     e->pre = oc.pre;
     e->dt = dtype == CLIPGPU_DTYPE_F16 ? DT_F16 : DT_BF16;  // fp8 engines keep bf16 outside the MX GEMMs
     e->mx = dtype == CLIPGPU_DTYPE_FP8;
-    if (e->mx) {
-      const char* ms = getenv("CLIPGPU_MX_SITES");
-      const std::string sites = ms ? ms : "qkv,fc,proj";
-      auto has = [&](const char* k) {
-        size_t p = 0;
-        while ((p = sites.find(k, p)) != std::string::npos) {
-          const size_t q = p + strlen(k);
-          if ((p == 0 || sites[p - 1] == ',') && (q == sites.size() || sites[q] == ',')) return true;
-          p = q;
-        }
-        return false;
-      };
-      e->mx_site[GS_QKV] = has("qkv");
-      e->mx_site[GS_FC] = has("fc");
-      e->mx_site[GS_PROJ] = has("proj");
+    if (e->mx) {  // the MX split: the options' bits, else CLIPGPU_MX_SITES, else all three sites
+      uint32_t bits = opts.mx_sites;
+      if (bits == 0) {
+        const char* ms = getenv("CLIPGPU_MX_SITES");
+        const std::string sites = ms ? ms : "qkv,fc,proj";
+        auto has = [&](const char* k) {
+          size_t p = 0;
+          while ((p = sites.find(k, p)) != std::string::npos) {
+            const size_t q = p + strlen(k);
+            if ((p == 0 || sites[p - 1] == ',') && (q == sites.size() || sites[q] == ',')) return true;
+            p = q;
+          }
+          return false;
+        };
+        bits = (has("qkv") ? CLIPGPU_MX_QKV : 0u) | (has("fc") ? CLIPGPU_MX_FC : 0u) |
+               (has("proj") ? CLIPGPU_MX_PROJ : 0u);
+      }
+      e->mx_site[GS_QKV] = (bits & CLIPGPU_MX_QKV) != 0;
+      e->mx_site[GS_FC] = (bits & CLIPGPU_MX_FC) != 0;
+      e->mx_site[GS_PROJ] = (bits & CLIPGPU_MX_PROJ) != 0;
       if (e->mx_site[GS_PROJ] && !e->mx_site[GS_FC])
-        throw ClipErr(CLIPGPU_ERR_INVALID, "CLIPGPU_MX_SITES: proj in MX needs fc in MX");
+        throw ClipErr(CLIPGPU_ERR_INVALID, "MX sites: proj in MX needs fc in MX");
+    } else if (opts.mx_sites) {
+      throw ClipErr(CLIPGPU_ERR_INVALID, "clipgpu_options.mx_sites needs dtype CLIPGPU_DTYPE_FP8");
     }
     e->max_batch = max_batch;
-    if (const char* ln = getenv("CLIPGPU_LANES")) {
+    if (opts.lanes > 0) {
+      e->lanes = opts.lanes;
+      e->lanes_pinned = true;
+    } else if (const char* ln = getenv("CLIPGPU_LANES")) {
       e->lanes = std::max(1, std::min(4, atoi(ln)));
       e->lanes_pinned = true;
     } else {
-      e->lanes = 2;
+      e->lanes = 2;  // host-path staging slots (run_host_shard); the device-side lane count is the table's
+    }
+    {
+      const char* at = getenv("CLIPGPU_GEMM_AUTOTUNE");
+      e->tuning = opts.tuning == 1 || (at && at[0] == '1');
     }
     e->dev_lanes = e->lanes;
     if (const char* gr = getenv("CLIPGPU_GRAPHS")) e->graphs = gr[0] != '0';
@@ -1548,7 +1680,7 @@ int clipgpu_create(const char* model_dir, int tower, const int* device_ids, int 
     if (const char* sp = getenv("CLIPGPU_GEMM_SPLIT")) e->ksplit = sp[0] == '1' ? 2 : 1;
     if (const char* p3 = getenv("CLIPGPU_GEMM_PIPE3")) e->pipe3 = p3[0] == '1' ? 1 : 0;
     {
-      if (const char* fl = getenv("CLIPGPU_FUSE_LN")) e->fuse_mode = fl[0] == '1' ? 1 : (fl[0] == 'a' ? -1 : 0);
+      if (const char* fl = getenv("CLIPGPU_FUSE_LN")) e->fuse_mode = fl[0] == '1' ? 1 : 0;
       if (const char* pf = getenv("CLIPGPU_ROWLN_PF")) e->rowln_pf = std::max(0, atoi(pf));
       e->fuse_ok_out = e->fuse_mode != 0 && gemm_rowln_supported(s.width, s.width) && !site_split(*e, GS_OUT) &&
                        !e->mx_site[GS_FC];
@@ -1595,23 +1727,30 @@ int clipgpu_create(const char* model_dir, int tower, const int* device_ids, int 
       HIP_CHECK(hipStreamCreateWithFlags(&r.stream, hipStreamNonBlocking));
       upload_weights(*e, r, m);
       alloc_workspace(*e, r);
-      if (i == 0) {  // one tuning, shared by identical devices
-        autotune_tiles(*e, r);
-        tune_forward(*e, r);
+      if (i == 0) {  // one tile choice, shared by identical devices
+        if (e->tuning) {
+          autotune_tiles(*e, r);
+          tune_forward(*e, r);
+        } else {
+          table_tiles(*e);
+          tile_env_override(*e);
+        }
       }
     }
-    // A multi-device handle gets one communicator over its devices (ncclCommInitAll; rank i =
-    // device_ids[i]) when they are distinct (RCCL refuses two ranks on one GPU; a handle that
-    // lists a device twice keeps the host-buffer sharding and has no collective entry points).
+    // A multi-device handle over distinct devices gets one communicator (ncclCommInitAll; rank i
+    // = device_ids[i]; RCCL refuses two ranks on one GPU, so a handle that lists a device twice
+    // keeps the host-buffer sharding and has no collective entry points).  It is created on the
+    // first gathered call (ensure_comm) unless the options ask for it now: creation and the
+    // host-buffer entry points never depend on RCCL.
     bool distinct = devs.size() > 1;
     for (size_t i = 0; i < devs.size() && distinct; ++i)
       for (size_t j = i + 1; j < devs.size(); ++j) distinct = distinct && devs[i] != devs[j];
     if (distinct) {
-      std::vector<ncclComm_t> comms(devs.size());
-      NCCL_CHECK(ncclCommInitAll(comms.data(), (int)devs.size(), devs.data()));
-      for (size_t i = 0; i < devs.size(); ++i) e->reps[i].comm = comms[i];
+      e->comm_devs = devs;
+      e->comm_pending = true;
       e->comm_nranks = (int)devs.size();
       e->comm_rank0 = 0;
+      if (opts.communicator == 1) ensure_comm(*e);
     }
     *out = e.release();
   });
@@ -1620,6 +1759,7 @@ int clipgpu_create(const char* model_dir, int tower, const int* device_ids, int 
 void clipgpu_destroy(clipgpu_engine* e) {
   if (!e) return;
   for (hipEvent_t ev : e->prof.pool) (void)hipEventDestroy(ev);
+  destroy_comms(*e);
   for (auto& r : e->reps) destroy_replica(r);
   delete e;
 }
@@ -1930,6 +2070,35 @@ int clipgpu_test_engine_tiles(const clipgpu_engine* e, int tiles[4]) {
   return guarded([&]() {
     if (!e || !tiles) throw ClipErr(CLIPGPU_ERR_INVALID, "NULL argument");
     for (int i = 0; i < 4; ++i) tiles[i] = e->tile[i];
+  });
+}
+
+int clipgpu_engine_info(const clipgpu_engine* e, int tiles[4], int* lanes, uint32_t* mx_sites) {
+  return guarded([&]() {
+    if (!e) throw ClipErr(CLIPGPU_ERR_INVALID, "engine is NULL");
+    if (tiles)
+      for (int i = 0; i < 4; ++i) tiles[i] = e->tile[i];
+    if (lanes) *lanes = e->dev_lanes;
+    if (mx_sites)
+      *mx_sites = (e->mx_site[GS_QKV] ? CLIPGPU_MX_QKV : 0u) | (e->mx_site[GS_FC] ? CLIPGPU_MX_FC : 0u) |
+                  (e->mx_site[GS_PROJ] ? CLIPGPU_MX_PROJ : 0u);
+  });
+}
+
+int clipgpu_test_force_broadcast(clipgpu_engine* e, int on) {
+  return guarded([&]() {
+    if (!e) throw ClipErr(CLIPGPU_ERR_INVALID, "engine is NULL");
+    std::lock_guard<std::mutex> lk(e->mu);
+    e->force_bcast = on != 0;
+  });
+}
+
+int clipgpu_test_gather_plan(int nranks, const int64_t* rows, int64_t* off, int* equal) {
+  return guarded([&]() {
+    if (nranks < 1 || !rows || !off || !equal) throw ClipErr(CLIPGPU_ERR_INVALID, "bad arguments");
+    const GatherPlan g = plan_gather(nranks, rows);
+    for (int r = 0; r <= nranks; ++r) off[r] = g.off[r];
+    *equal = g.equal ? 1 : 0;
   });
 }
 

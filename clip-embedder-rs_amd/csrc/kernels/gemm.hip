@@ -1115,6 +1115,12 @@ hipError_t launch_tile(const GemmParams& p, hipStream_t s) {
       case TILE_128x64_RS: return launch_pipe<T, 128, 64, 2, 2, EPI, ACT, 3, 1>(p, s);
       case TILE_160x128_W8_RS: return launch_pipe<T, 160, 128, 2, 4, EPI, ACT, 2, 1>(p, s);
       case TILE_256x256_HALF: return launch_pipe_half<T, EPI, ACT>(p, s);
+#if CLIPGPU_GEMM_DIAG_224
+      // (diagnostic build only, tools/check_lds_waits.py: the dropped 224x256 8-wave tile)
+      case 19:
+        if constexpr (EPI == EPI_STORE32 || EPI == EPI_RESID) return launch_pipe<T, 224, 256, 2, 4, EPI, ACT, 1>(p, s);
+        break;
+#endif
       default: break;
     }
   }
@@ -1171,16 +1177,47 @@ int pick_gemm_tile(int M, int N, int K) {
   return eff(256, 256) >= 0.85 * eff(256, 128) ? TILE_256x256 : TILE_256x128;
 }
 
+// Rows one launch may cover: the kernels address their operands with 32-bit per-lane byte offsets
+// from the kernel-argument base pointers (SGPR base + VGPR offset DMA), so a launch keeps
+// rows * lda * 2 bytes under 2^31.  Larger M runs as consecutive row chunks (launch_gemm below);
+// every output row is the same MFMA chain whichever launch computes it, so the chunking is
+// bit-invisible (test_gemm_row_chunks_are_bit_exact, the SO400M max_batch 1024 test).
+long gemm_chunk_rows(long lda, int G) {
+  long rows = ((1L << 31) - 1) / (2 * lda);
+  rows -= rows % 256;                           // whole 256-row tiles
+  if (G > 0) rows -= rows % ((long)G * G);      // EPI_PATCH: whole images
+  return rows;
+}
+
 hipError_t launch_gemm(DType dt, int asrc, int epi, int act, const GemmParams& p, hipStream_t s) {
   if (p.K % BK != 0 || p.M <= 0 || p.N <= 0) return hipErrorInvalidValue;
   if (p.bias != nullptr && p.N % 4 != 0) return hipErrorInvalidValue;  // 16-byte bias DMA
-  // 32-bit staging offsets
-  if ((long)p.M * p.lda * 2 >= (1L << 31) || (long)p.N * p.ldw * 2 >= (1L << 31)) return hipErrorInvalidValue;
+  // 32-bit staging offsets: W must fit whole; A is chunked by rows
+  if ((long)p.N * p.ldw * 2 >= (1L << 31) || p.lda <= 0) return hipErrorInvalidValue;
   if (asrc != A_ROWS) return hipErrorInvalidValue;  // pixels go through launch_patch_rows first
   if (p.ksplit > 1) {  // each K-slice >= 2 K-steps (pipelined kernel); f32 epilogues only; a slab
     if (p.K % (BK * p.ksplit) != 0 || p.K / p.ksplit < 2 * BK || p.slab == nullptr ||
         (epi != EPI_RESID && epi != EPI_STORE32) || p.ldo % 4 != 0)
       return hipErrorInvalidValue;
+  }
+  if ((long)p.M * p.lda * 2 >= (1L << 31)) {
+    // slab slices are [ksplit - 1][M][ldo]: chunk offsets hold for one extra slice only
+    if (p.ksplit > 2) return hipErrorInvalidValue;
+    const int G = epi == EPI_PATCH ? p.G : 0;
+    const long chunk = gemm_chunk_rows(p.lda, G);
+    if (chunk <= 0) return hipErrorInvalidValue;
+    const long osz = epi == EPI_STORE16 ? 2 : 4;
+    for (long m0 = 0; m0 < p.M; m0 += chunk) {
+      GemmParams q = p;
+      q.M = (int)std::min<long>(chunk, p.M - m0);
+      q.A = (const char*)p.A + m0 * p.lda * 2;
+      const long orow = G > 0 ? m0 / ((long)G * G) * ((long)G * G + p.cls) : m0;  // EPI_PATCH: token rows
+      q.out = (char*)p.out + orow * p.ldo * osz;
+      if (p.slab) q.slab = p.slab + m0 * p.ldo;
+      const hipError_t err = dt == DT_BF16 ? launch_typed<__bf16>(epi, act, q, s) : launch_typed<_Float16>(epi, act, q, s);
+      if (err != hipSuccess) return err;
+    }
+    return hipSuccess;
   }
   return dt == DT_BF16 ? launch_typed<__bf16>(epi, act, p, s) : launch_typed<_Float16>(epi, act, p, s);
 }

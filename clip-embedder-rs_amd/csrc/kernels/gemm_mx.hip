@@ -489,10 +489,29 @@ hipError_t launch_gemm_mx(DType dt, int epi, int act, const MxGemmParams& p, hip
   if (p.lda % 16 || p.ldw % 16 || p.ldas % 4 || p.ldws % 4 || p.lda < p.K || p.ldw < p.K || p.ldas < p.K / 32 ||
       p.ldws < p.K / 32)
     return hipErrorInvalidValue;
-  if ((long)p.M * p.lda >= (1L << 31) || (long)p.N * p.ldw >= (1L << 31)) return hipErrorInvalidValue;
+  if ((long)p.N * p.ldw >= (1L << 31)) return hipErrorInvalidValue;
   if (epi == EPI_STOREQ && (p.outs == nullptr || p.ldo % 16 || p.ldos < p.N / 32)) return hipErrorInvalidValue;
   if (epi == EPI_STORE16 && p.ldo % 8) return hipErrorInvalidValue;
   if ((epi == EPI_RESID || epi == EPI_STORE32) && p.ldo % 4) return hipErrorInvalidValue;
+  if ((long)p.M * p.lda >= (1L << 31)) {
+    // 32-bit per-lane staging offsets (as launch_gemm): consecutive row chunks of whole 256-row
+    // tiles, bit-invisible (per-row scales, per-row MFMA chains)
+    long chunk = ((1L << 31) - 1) / p.lda;
+    chunk -= chunk % 256;
+    const long osz = epi == EPI_STORE16 ? 2 : (epi == EPI_STOREQ ? 1 : 4);
+    for (long m0 = 0; m0 < p.M; m0 += chunk) {
+      MxGemmParams q = p;
+      q.M = (int)std::min<long>(chunk, p.M - m0);
+      q.A = p.A + m0 * p.lda;
+      q.As = p.As + m0 * p.ldas;
+      q.out = (char*)p.out + m0 * p.ldo * osz;
+      if (p.outs) q.outs = p.outs + m0 * p.ldos;
+      const hipError_t err =
+          dt == DT_BF16 ? launch_mx_typed<__bf16>(epi, act, q, s) : launch_mx_typed<_Float16>(epi, act, q, s);
+      if (err != hipSuccess) return err;
+    }
+    return hipSuccess;
+  }
   return dt == DT_BF16 ? launch_mx_typed<__bf16>(epi, act, p, s) : launch_mx_typed<_Float16>(epi, act, p, s);
 }
 

@@ -13,6 +13,8 @@
 // epilogue float ops: y = (acc + bias) + x), so the residual stream equals the unfused path's;
 // the LayerNorm reduces in a different order than ln_rows_kernel (two-pass f32 mean / biased
 // variance, torch semantics), so h differs from the unfused path in the last bits.
+#include <algorithm>
+
 #include <hip/hip_ext.h>
 
 #include "common.hpp"
@@ -356,8 +358,22 @@ bool gemm_rowln_supported(int D, int K) {
 
 hipError_t launch_gemm_rowln(DType dt, const RowLnParams& p, hipStream_t s) {
   if (!gemm_rowln_supported(p.D, p.K) || p.M <= 0 || p.lda % 8 || p.ldw % 8) return hipErrorInvalidValue;
-  if ((long)p.M * p.lda * 2 >= (1L << 31) || (long)p.D * p.ldw * 2 >= (1L << 31)) return hipErrorInvalidValue;
+  if ((long)p.D * p.ldw * 2 >= (1L << 31)) return hipErrorInvalidValue;
   if (p.h != nullptr && (p.ln_w == nullptr || p.ln_b == nullptr)) return hipErrorInvalidValue;
+  if ((long)p.M * p.lda * 2 >= (1L << 31)) {  // 32-bit per-lane staging offsets: row chunks (bit-invisible)
+    long chunk = ((1L << 31) - 1) / (2 * p.lda);
+    chunk -= chunk % 256;
+    for (long m0 = 0; m0 < p.M; m0 += chunk) {
+      RowLnParams q = p;
+      q.M = (int)std::min<long>(chunk, p.M - m0);
+      q.A = (const char*)p.A + m0 * p.lda * 2;
+      q.x = p.x + m0 * p.D;
+      if (p.h) q.h = (char*)p.h + m0 * p.D * 2;
+      const hipError_t err = launch_gemm_rowln(dt, q, s);
+      if (err != hipSuccess) return err;
+    }
+    return hipSuccess;
+  }
   switch (p.D) {
     case 512: return dt == DT_BF16 ? launch_rowln_t<__bf16, 512>(p, s) : launch_rowln_t<_Float16, 512>(p, s);
     case 768: return dt == DT_BF16 ? launch_rowln_t<__bf16, 768>(p, s) : launch_rowln_t<_Float16, 768>(p, s);

@@ -27,6 +27,9 @@ _PROTOS = [
     ("clipgpu_abi_version", c_int, []),
     ("clipgpu_build_source_hash", c_char_p, []),
     ("clipgpu_create", c_int, [c_char_p, c_int, POINTER(c_int), c_int, c_int, c_int, POINTER(c_void_p)]),
+    ("clipgpu_options_init", c_int, [c_void_p]),
+    ("clipgpu_create_ex", c_int, [c_char_p, c_int, POINTER(c_int), c_int, c_int, c_int, c_void_p, POINTER(c_void_p)]),
+    ("clipgpu_engine_info", c_int, [c_void_p, POINTER(c_int), POINTER(c_int), POINTER(ctypes.c_uint32)]),
     ("clipgpu_destroy", None, [c_void_p]),
     ("clipgpu_embed_dim", c_int, [c_void_p]),
     ("clipgpu_input_size", c_int, [c_void_p]),
@@ -67,6 +70,8 @@ _PROTOS = [
     ("clipgpu_test_gemm_bench", c_int, [c_int, c_int, c_int, c_int64, c_int64, c_int64, c_int, c_int, POINTER(c_double)]),
     ("clipgpu_test_engine_tiles", c_int, [c_void_p, POINTER(c_int)]),
     ("clipgpu_test_engine_lanes", c_int, [c_void_p, POINTER(c_int)]),
+    ("clipgpu_test_force_broadcast", c_int, [c_void_p, c_int]),
+    ("clipgpu_test_gather_plan", c_int, [c_int, POINTER(c_int64), POINTER(c_int64), POINTER(c_int)]),
     ("clipgpu_test_read_weights", c_int, [c_char_p, c_int, c_char_p, c_void_p, c_int64]),
     ("clipgpu_test_patch_embed", c_int, [c_int, c_int, c_int64, c_int64, c_int64, c_int64, c_void_p, POINTER(c_float), POINTER(c_float), c_void_p, c_void_p, c_void_p]),
     ("clipgpu_test_resize_rgb8_gpu", c_int, [POINTER(c_void_p), POINTER(c_int), POINTER(c_int), c_int64, c_int, c_char_p, c_char_p, c_void_p]),
@@ -103,7 +108,36 @@ def lib():
     return _lib
 
 
-def _check_provenance(L) -> None:
+HOST_LIB_PATH = os.path.join(os.path.dirname(LIB_PATH), "libclipgpu_host.so")
+_host = None
+
+
+def host_lib():
+    """The host-only library (lib/libclipgpu_host.so: no HIP, no RCCL) with the Clip facade's
+    bit-exact score arithmetic (clipgpu_facade_scores, csrc/host/facade.cpp) -- loadable on a
+    host without ROCm.  Same provenance check as lib()."""
+    global _host
+    if _host is None:
+        if not os.path.exists(HOST_LIB_PATH):
+            raise ClipError(f"clipgpu host library not found at {HOST_LIB_PATH}; run `make -C clip-embedder-rs_amd`")
+        L = ctypes.CDLL(HOST_LIB_PATH)
+        for name, res, args in _PROTOS:
+            if name in ("clipgpu_last_error", "clipgpu_facade_scores", "clipgpu_build_source_hash"):
+                fn = getattr(L, name)
+                fn.restype = res
+                fn.argtypes = args
+        _check_provenance(L, HOST_LIB_PATH)
+        _host = L
+    return _host
+
+
+def check_host(rc: int) -> None:
+    if rc != 0:
+        msg = host_lib().clipgpu_last_error().decode("utf-8", "replace")
+        raise error_for_status(rc, msg)
+
+
+def _check_provenance(L, path=LIB_PATH) -> None:
     """The library must have been built from the sources next to it (binary provenance)."""
     from ._source_hash import source_hash
     fn = L.clipgpu_build_source_hash
@@ -112,7 +146,7 @@ def _check_provenance(L) -> None:
     built = fn().decode()
     here = source_hash(os.path.dirname(_HERE))
     if built != here:
-        raise ClipError(f"stale native library {LIB_PATH}: built from sources {built[:12]}, the tree has "
+        raise ClipError(f"stale native library {path}: built from sources {built[:12]}, the tree has "
                         f"{here[:12]}; rebuild with `make -C clip-embedder-rs_amd` (__graft_entry__.build())")
 
 

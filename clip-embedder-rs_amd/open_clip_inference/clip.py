@@ -56,7 +56,7 @@ class Clip:
     def _scores(self, embs: np.ndarray, query: np.ndarray, activation: str) -> np.ndarray:
         """logits = embs . query, mul_add(scale, bias), then the activation -- the reference's
         f32 arithmetic bit for bit (clipgpu_facade_scores, csrc/host/facade.cpp)."""
-        from ._lib import check, lib
+        from ._lib import check_host, host_lib
         from .engine import SIM_ACTIVATIONS
         e = np.ascontiguousarray(embs, dtype=np.float32)
         q = np.ascontiguousarray(query, dtype=np.float32).reshape(-1)
@@ -65,8 +65,9 @@ class Clip:
             raise ShapeError(f"Shape error: {e.shape} . {q.shape}")
         scale, bias = self._scale_bias()
         out = np.empty(e.shape[0], np.float32)
-        check(lib().clipgpu_facade_scores(e.ctypes.data, e.shape[0], q.ctypes.data, e.shape[1], float(scale),
-                                          float(bias), SIM_ACTIVATIONS[activation], out.ctypes.data))
+        check_host(host_lib().clipgpu_facade_scores(e.ctypes.data, e.shape[0], q.ctypes.data, e.shape[1],
+                                                    float(scale), float(bias), SIM_ACTIVATIONS[activation],
+                                                    out.ctypes.data))
         return out
 
     def compare(self, image, text: str) -> float:  # src/clip.rs:79-90
@@ -122,20 +123,23 @@ class Clip:
 
     @staticmethod
     def softmax(logits) -> np.ndarray:  # src/clip.rs:172-179 (f32, sequential sum; facade.cpp)
-        from ._lib import check, lib
+        # host-only library (no HIP / RCCL): usable on a host without ROCm
+        from ._lib import check_host, host_lib
         x = np.ascontiguousarray(logits, dtype=np.float32).reshape(-1)
         if x.size == 0:
             return x.copy()
         one = np.ones(1, np.float32)  # logits = x[i] * 1 (exact) .mul_add(1, 0) (exact)
         out = np.empty(x.size, np.float32)
-        check(lib().clipgpu_facade_scores(x.ctypes.data, x.size, one.ctypes.data, 1, 1.0, 0.0, 0, out.ctypes.data))
+        check_host(host_lib().clipgpu_facade_scores(x.ctypes.data, x.size, one.ctypes.data, 1, 1.0, 0.0, 0,
+                                                    out.ctypes.data))
         return out
 
     @staticmethod
     def sigmoid(logit: float) -> float:  # src/clip.rs:181-185
-        from ._lib import check, lib
+        from ._lib import check_host, host_lib
         x = np.array([logit], np.float32)
         one = np.ones(1, np.float32)
         out = np.empty(1, np.float32)
-        check(lib().clipgpu_facade_scores(x.ctypes.data, 1, one.ctypes.data, 1, 1.0, 0.0, 1, out.ctypes.data))
+        check_host(host_lib().clipgpu_facade_scores(x.ctypes.data, 1, one.ctypes.data, 1, 1.0, 0.0, 1,
+                                                    out.ctypes.data))
         return float(out[0])

@@ -13,20 +13,64 @@ from . import _lib
 from ._lib import check, f3, lib
 
 
+class Options(ctypes.Structure):
+    """``clipgpu_options`` (include/clipgpu.h): per-engine settings of clipgpu_create_ex."""
+    _fields_ = [("struct_size", ctypes.c_uint32), ("mx_sites", ctypes.c_uint32), ("lanes", ctypes.c_int32),
+                ("tuning", ctypes.c_int32), ("communicator", ctypes.c_int32)]
+
+
+MX_SITE_BITS = {"qkv": 1, "fc": 2, "proj": 4}  # CLIPGPU_MX_QKV / _FC / _PROJ
+
+
+def mx_site_bits(sites) -> int:
+    """"qkv,fc" / ["qkv", "fc"] -> CLIPGPU_MX_* bits (0 = the default split)."""
+    if sites is None:
+        return 0
+    if isinstance(sites, str):
+        sites = [s for s in sites.split(",") if s]
+    bits = 0
+    for s in sites:
+        if s not in MX_SITE_BITS:
+            raise ValueError(f"unknown MX site {s!r}: one of {sorted(MX_SITE_BITS)}")
+        bits |= MX_SITE_BITS[s]
+    return bits
+
+
 class Engine:
     def __init__(self, model_dir: str, tower: int, devices: Optional[Sequence[int]] = None,
-                 dtype: str = "bf16", max_batch: int = 256):
+                 dtype: str = "bf16", max_batch: int = 256, mx_sites=None, lanes: int = 0, tuning: bool = False,
+                 communicator: bool = False):
+        """mx_sites: fp8 engines' MX split ("qkv,fc,proj" by default); lanes: concurrent sub-batch lanes
+        (0 = the tile table's); tuning: time the GEMM tiles at creation instead of the committed table;
+        communicator: create a multi-device handle's RCCL communicator now, not on the first gather."""
         self.model_dir = model_dir
         self.tower = tower
         self.devices = list(devices) if devices else [0]
         self.dtype = dtype
         self.max_batch = int(max_batch)
+        self.opts = {"mx_sites": mx_sites, "lanes": int(lanes), "tuning": bool(tuning),
+                     "communicator": bool(communicator)}  # duplicate() rebuilds with the same
         dt = {"bf16": _lib.DTYPE_BF16, "f16": _lib.DTYPE_F16, "fp16": _lib.DTYPE_F16, "fp8": _lib.DTYPE_FP8}[dtype]
         devs = (c_int * len(self.devices))(*self.devices)
+        opts = Options()
+        check(lib().clipgpu_options_init(ctypes.byref(opts)))
+        opts.mx_sites = mx_site_bits(mx_sites)
+        opts.lanes = int(lanes)
+        opts.tuning = 1 if tuning else 0
+        opts.communicator = 1 if communicator else 0
         h = c_void_p()
-        check(lib().clipgpu_create(model_dir.encode(), tower, devs, len(self.devices), dt, self.max_batch,
-                                   ctypes.byref(h)))
+        check(lib().clipgpu_create_ex(model_dir.encode(), tower, devs, len(self.devices), dt, self.max_batch,
+                                      ctypes.byref(opts), ctypes.byref(h)))
         self._h = h
+
+    def info(self):
+        """(tiles per trunk site [qkv, out_proj, c_fc, c_proj], device lanes, MX site names)."""
+        tiles = (c_int * 4)()
+        lanes = c_int()
+        bits = ctypes.c_uint32()
+        check(lib().clipgpu_engine_info(self.handle, tiles, ctypes.byref(lanes), ctypes.byref(bits)))
+        sites = [s for s, b in MX_SITE_BITS.items() if bits.value & b]
+        return list(tiles), lanes.value, sites
 
     @property
     def handle(self):

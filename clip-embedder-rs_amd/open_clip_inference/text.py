@@ -38,18 +38,18 @@ class TextEmbedder:
         return _Builder(cls, model_id=model_id)
 
     @classmethod
-    def _build(cls, model_dir, devices, dtype, max_batch, **_opts):  # src/text.rs:54-101
+    def _build(cls, model_dir, devices, dtype, max_batch, engine_opts=None, **_opts):  # src/text.rs:54-101
         verify_model_dir(model_dir, need_tokenizer=True)
         model_config = ModelConfig.from_file(os.path.join(model_dir, "model_config.json"))
         config = OpenClipConfig.from_file(os.path.join(model_dir, "open_clip_config.json"))
         ctx = config.model_cfg.text_cfg.context_length
         tok = Tokenizer(os.path.join(model_dir, "tokenizer.json"), ctx, model_config.pad_id)
-        engine = Engine(model_dir, _lib.TOWER_TEXT, devices, dtype, max_batch or 1024)
+        engine = Engine(model_dir, _lib.TOWER_TEXT, devices, dtype, max_batch or 1024, **(engine_opts or {}))
         return cls(engine, config, model_config, model_dir, tok)
 
     def duplicate(self) -> "TextEmbedder":  # src/text.rs:103-108
         e = self.session
-        return self._build(self.model_dir, e.devices, e.dtype, e.max_batch)
+        return self._build(self.model_dir, e.devices, e.dtype, e.max_batch, e.opts)
 
     def tokenize(self, texts: Sequence[str]):  # src/text.rs:110-139
         return self._tokenizer.encode_batch(list(texts), lowercase=self.model_config.tokenizer_needs_lowercase)

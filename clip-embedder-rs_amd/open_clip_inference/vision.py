@@ -41,6 +41,7 @@ class _Builder:
         self._dtype = "bf16"
         self._max_batch = None
         self._opts = {}
+        self._engine = {}
 
     def base_folder(self, path: str):
         self._base = path
@@ -58,6 +59,17 @@ class _Builder:
         self._max_batch = int(n)
         return self
 
+    def with_mx_sites(self, sites):
+        """fp8 engines: the GEMM sites that run MX-fp8 ("qkv", "fc", "proj"; default all three),
+        per engine (clipgpu_options.mx_sites)."""
+        self._engine["mx_sites"] = sites
+        return self
+
+    def with_lanes(self, lanes: int):
+        """Concurrent sub-batch lanes per device (clipgpu_options.lanes; 0 = the tile table's)."""
+        self._engine["lanes"] = int(lanes)
+        return self
+
     def with_resize_impl(self, impl: str):
         """The resize the crate's `fast_image_resize` feature selects (src/vision.rs:149-157):
         "fast_image_resize" (default feature) or "image" (resize_with_image, :200-233)."""
@@ -71,7 +83,8 @@ class _Builder:
         d = self._model_dir
         if d is None:
             d = os.path.join(self._base or get_default_base_folder(), self._model_id)
-        return self._cls._build(d, self._devices, self._dtype, self._max_batch, **self._opts)
+        return self._cls._build(d, self._devices, self._dtype, self._max_batch, engine_opts=dict(self._engine),
+                                **self._opts)
 
 
 class VisionEmbedder:
@@ -94,16 +107,16 @@ class VisionEmbedder:
         return _Builder(cls, model_id=model_id)
 
     @classmethod
-    def _build(cls, model_dir, devices, dtype, max_batch, resize_impl="fast_image_resize"):
+    def _build(cls, model_dir, devices, dtype, max_batch, resize_impl="fast_image_resize", engine_opts=None):
         verify_model_dir(model_dir)
         config = OpenClipConfig.from_file(os.path.join(model_dir, "open_clip_config.json"))
         model_config = ModelConfig.from_file(os.path.join(model_dir, "model_config.json"))
-        engine = Engine(model_dir, _lib.TOWER_VISION, devices, dtype, max_batch or 256)
+        engine = Engine(model_dir, _lib.TOWER_VISION, devices, dtype, max_batch or 256, **(engine_opts or {}))
         return cls(engine, config, model_config, model_dir, resize_impl)
 
     def duplicate(self) -> "VisionEmbedder":  # src/vision.rs:86-91
         e = self.session
-        return self._build(self.model_dir, e.devices, e.dtype, e.max_batch, self.resize_impl)
+        return self._build(self.model_dir, e.devices, e.dtype, e.max_batch, self.resize_impl, e.opts)
 
     # -- embedding (src/vision.rs:93-117) --
     def embed_image(self, image) -> np.ndarray:

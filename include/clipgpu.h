@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define CLIPGPU_ABI_VERSION 1
+#define CLIPGPU_ABI_VERSION 2
 
 enum clipgpu_status {
   CLIPGPU_OK = 0,
@@ -70,6 +70,32 @@ const char* clipgpu_build_source_hash(void);
 int clipgpu_create(const char* model_dir, int tower, const int* device_ids, int n_devices, int dtype,
                    int max_batch, clipgpu_engine** out);
 void clipgpu_destroy(clipgpu_engine* e);
+
+/* Per-engine options (clipgpu_create_ex; clipgpu_create == clipgpu_create_ex with opts = NULL).
+ * The reference builds each tower's session with its own SessionBuilder settings
+ * (src/onnx.rs:13-30); these are this engine's equivalents, per handle, so one process can hold
+ * e.g. an fp8 vision tower beside a bf16 text tower with different MX splits. */
+#define CLIPGPU_MX_QKV 1u  /* fp8 engines: the QKV projection runs as an MX-fp8 GEMM */
+#define CLIPGPU_MX_FC 2u   /* c_fc */
+#define CLIPGPU_MX_PROJ 4u /* c_proj (needs CLIPGPU_MX_FC: c_fc's epilogue quantizes the hidden rows) */
+typedef struct clipgpu_options {
+  uint32_t struct_size; /* sizeof(clipgpu_options) (set by clipgpu_options_init) */
+  uint32_t mx_sites;    /* fp8 engines: CLIPGPU_MX_* bits; 0 = default (all three; the
+                           CLIPGPU_MX_SITES environment variable, if set, replaces the default) */
+  int32_t lanes;        /* concurrent sub-batch lanes per device, 1..4; 0 = the tile table's choice */
+  int32_t tuning;       /* 0 = GEMM tiles and lanes from the committed MI355X tile table
+                           (deterministic, default); 1 = time the candidates at creation (the choice
+                           then depends on the timings; never changes the output bits) */
+  int32_t communicator; /* handles over > 1 distinct devices: 1 = create the RCCL communicator at
+                           creation; 0 (default) = on the first gathered call */
+} clipgpu_options;
+/* Fills *opts with the defaults. */
+int clipgpu_options_init(clipgpu_options* opts);
+int clipgpu_create_ex(const char* model_dir, int tower, const int* device_ids, int n_devices, int dtype,
+                      int max_batch, const clipgpu_options* opts, clipgpu_engine** out);
+/* The engine's resolved choices: tiles[4] = GemmTile per trunk site (qkv, out_proj, c_fc, c_proj),
+ * *lanes = concurrent lanes of a device-side forward, *mx_sites = CLIPGPU_MX_* bits in use. */
+int clipgpu_engine_info(const clipgpu_engine* e, int tiles[4], int* lanes, uint32_t* mx_sites);
 
 int clipgpu_embed_dim(const clipgpu_engine* e);      /* E */
 int clipgpu_input_size(const clipgpu_engine* e);     /* vision: image_size S; text: context length T */
@@ -181,7 +207,9 @@ int clipgpu_similarity_device(const float* d_img, int64_t n_img, const float* d_
  * (src/vision.rs:100-117, src/text.rs:148-169) keep their signatures; these entry points are
  * what a multi-GPU caller of them binds.
  * Communicator: a handle created over n > 1 DISTINCT devices owns one (ncclCommInitAll, rank i =
- * device_ids[i]); a one-device handle in a one-process-per-GPU deployment joins one with
+ * device_ids[i]), created on its first gathered call (or at creation with
+ * clipgpu_options.communicator = 1), so creation and the host-buffer entry points never depend
+ * on RCCL; a one-device handle in a one-process-per-GPU deployment joins one with
  * clipgpu_comm_init_rank (rank 0 calls clipgpu_comm_unique_id and sends the 128 bytes to every
  * rank out of band; every rank then calls init_rank, collectively).  clipgpu_comm_info gives
  * (nranks, first rank of this handle); nranks 0 = no communicator.

@@ -109,6 +109,13 @@ int clipgpu_test_engine_tiles(const struct clipgpu_engine* e, int tiles[4]);
 /* Concurrent sub-batches the engine's device-side forwards run (the creation-time tuning's pick,
  * or CLIPGPU_LANES). */
 int clipgpu_test_engine_lanes(const struct clipgpu_engine* e, int* dev_lanes);
+/* Gathered calls of this handle take the ragged branch (one ncclBroadcast per block) even when
+ * every block has the same size (on != 0), so a one-rank or equal-shard run exercises it. */
+int clipgpu_test_force_broadcast(struct clipgpu_engine* e, int on);
+/* The host-side plan of a gathered call (no GPU): off[0..nranks] = first output row of each rank's
+ * block (off[nranks] = total rows), *equal = 1 when every block has the same size.  Errors as the
+ * gathered entry points: a negative count, or zero rows in all ("Empty batch"). */
+int clipgpu_test_gather_plan(int nranks, const int64_t* rows, int64_t* off, int* equal);
 
 #ifdef __cplusplus
 }

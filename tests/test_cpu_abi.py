@@ -35,7 +35,7 @@ def test_library_exports_every_declared_symbol():
     missing = [n for n in names if not hasattr(L, n)]
     assert not missing, missing
     assert set(_lib.SYMBOLS) == names  # the ctypes binding covers exactly the headers
-    assert L.clipgpu_abi_version() == 1
+    assert L.clipgpu_abi_version() == 2
 
 
 def test_no_oracle_in_product():
@@ -186,3 +186,76 @@ def test_bench_names_every_gemm_tile():
     bench = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(bench)
     assert set(range(0, last + 1)) <= set(bench.TILE_NAMES)
+
+
+def test_options_init_and_validation():
+    """clipgpu_options (per-engine MX split, lanes, tuning, communicator): clipgpu_options_init
+    fills the defaults; bad values are refused by clipgpu_create_ex before any device call."""
+    from open_clip_inference import _lib
+    from open_clip_inference.engine import Engine, Options, mx_site_bits
+    from open_clip_inference.error import ClipError, ConfigError
+    o = Options()
+    _lib.check(_lib.lib().clipgpu_options_init(ctypes.byref(o)))
+    assert o.struct_size == ctypes.sizeof(Options) and o.mx_sites == 0 and o.lanes == 0
+    assert o.tuning == 0 and o.communicator == 0
+    assert mx_site_bits("qkv") == 1 and mx_site_bits(["fc", "proj"]) == 6 and mx_site_bits(None) == 0
+    with pytest.raises(ValueError):
+        mx_site_bits("attn")
+    d = make_model_dir(TINY_CFG)
+    for kw, msg in (({"lanes": 5}, "lanes"), ({"mx_sites": "qkv"}, "needs dtype")):
+        with pytest.raises(ClipError, match=msg):
+            Engine(d, 0, [0], "bf16", 8, **kw)
+    with pytest.raises(ClipError, match="proj in MX needs fc"):
+        Engine(d, 0, [0], "fp8", 8, mx_sites="qkv,proj")
+    # a struct_size the library does not know is refused
+    o.struct_size = 1
+    h = ctypes.c_void_p()
+    devs = (ctypes.c_int * 1)(0)
+    rc = _lib.lib().clipgpu_create_ex(d.encode(), 0, devs, 1, 0, 8, ctypes.byref(o), ctypes.byref(h))
+    assert rc != 0 and b"struct_size" in _lib.lib().clipgpu_last_error()
+
+
+@pytest.mark.parametrize("rows,off,equal", [([256, 256], [0, 256, 512], 1),
+                                            ([3, 0, 5], [0, 3, 3, 8], 0),
+                                            ([0, 7], [0, 0, 7], 0),
+                                            ([1000, 1000, 1000], [0, 1000, 2000, 3000], 1),
+                                            ([5], [0, 5], 1)])
+def test_gather_plan(rows, off, equal):
+    """The gathered entry points' host-side plan (engine.hip plan_gather): rank-order offsets of
+    every rank's block, and the all-gather (equal blocks) vs one-broadcast-per-block choice, incl.
+    zero-row ranks and blocks larger than max_batch (chunked per rank; offsets are per rank)."""
+    from open_clip_inference import _lib
+    n = len(rows)
+    r = (ctypes.c_int64 * n)(*rows)
+    o = (ctypes.c_int64 * (n + 1))()
+    e = ctypes.c_int()
+    _lib.check(_lib.lib().clipgpu_test_gather_plan(n, r, o, ctypes.byref(e)))
+    assert list(o) == off and e.value == equal
+
+
+def test_gather_plan_errors():
+    from open_clip_inference import _lib
+    from open_clip_inference.error import ClipError
+    o = (ctypes.c_int64 * 3)()
+    e = ctypes.c_int()
+    with pytest.raises(ClipError, match="Empty batch"):
+        _lib.check(_lib.lib().clipgpu_test_gather_plan(2, (ctypes.c_int64 * 2)(0, 0), o, ctypes.byref(e)))
+    with pytest.raises(ClipError, match="negative"):
+        _lib.check(_lib.lib().clipgpu_test_gather_plan(2, (ctypes.c_int64 * 2)(4, -1), o, ctypes.byref(e)))
+
+
+def test_facade_math_loads_without_hip():
+    """Clip.softmax / Clip.sigmoid (host math in the reference, src/clip.rs:172-185) run from the
+    host-only library (no HIP, no RCCL in its dependencies), bit-exact to the main library."""
+    import subprocess
+    from open_clip_inference import _lib
+    from open_clip_inference.clip import Clip
+    deps = subprocess.run(["ldd", _lib.HOST_LIB_PATH], capture_output=True, text=True).stdout
+    assert "amdhip" not in deps and "rccl" not in deps, deps
+    x = np.array([1.5, -2.0, 0.25, 3.0], np.float32)
+    got = Clip.softmax(x)
+    ref = np.empty(4, np.float32)
+    one = np.ones(1, np.float32)
+    _lib.check(_lib.lib().clipgpu_facade_scores(x.ctypes.data, 4, one.ctypes.data, 1, 1.0, 0.0, 0, ref.ctypes.data))
+    assert np.array_equal(got, ref)
+    assert Clip.sigmoid(0.0) == 0.5

@@ -292,6 +292,35 @@ def test_rccl_communicator_and_gathered_entry_points(monkeypatch):
         got = out.cpu().numpy()
         ref = e.embed_pixels(x) if tower == 0 else e.embed_tokens(x)
         assert np.array_equal(got, ref)
+        # the ragged branch (one ncclBroadcast per non-empty block, rank offsets) forced on the
+        # equal one-rank block: the same bits
+        _lib.check(_lib.lib().clipgpu_test_force_broadcast(e.handle, 1))
+        out.fill_(float("nan"))
+        gather([d_in.data_ptr()], [B], [out.data_ptr()], [s.cuda_stream])
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy(), ref)
+        _lib.check(_lib.lib().clipgpu_test_force_broadcast(e.handle, 0))
         e.close()
     multi = Engine(d, 0, [0, 0], "bf16", 4)
     assert multi.comm_info() == (0, 0)
+
+
+def test_tile_table_is_deterministic_and_bit_invisible(monkeypatch):
+    """The default tile choice is the committed table (engine.hip table_tiles): two engines of
+    the bench's configuration pick the same tiles and one lane on any box; a creation-time timing
+    tuner (clipgpu_options.tuning) may pick others, with the same output bits."""
+    from oracle.model_spec import VIT_B_32_CFG
+    from open_clip_inference.engine import Engine
+    from tests.helpers import normalized_pixels
+    for var in ("CLIPGPU_LANES", "CLIPGPU_GEMM_TILES", "CLIPGPU_GEMM_AUTOTUNE"):
+        monkeypatch.delenv(var, raising=False)
+    d = make_model_dir(VIT_B_32_CFG, seed=1234)
+    a = Engine(d, 0, [0], "bf16", 256)
+    b = Engine(d, 0, [0], "bf16", 256)
+    assert a.info() == b.info() == ([18, 17, 18, 17], 1, [])
+    t = Engine(d, 0, [0], "bf16", 256, tuning=True)
+    v = vision_spec_from_cfg(VIT_B_32_CFG["model_cfg"])
+    x = normalized_pixels(weights.synth_images_u8(31, 64, v.image_size), OPENAI_MEAN, OPENAI_STD)
+    assert np.array_equal(a.embed_pixels(x), t.embed_pixels(x))
+    small = Engine(d, 0, [0], "bf16", 8)  # rows < 2048: the shape heuristic
+    assert small.info()[0] == [0, 0, 0, 0]

@@ -2,10 +2,13 @@
 
 `bench.py`'s headline (BASELINE.json configs[1]) and its text leg (configs[2]) run engines
 built exactly as the bench builds them: the bench's own model folder and seeded inputs,
-max_batch 256 / 1024, the default lane split (2), the default two-pass tile autotune, the
-hipGraph-replayed device entry point on the caller's stream.  Sampled rows cover both lanes
-and the lane boundary; every row of the batch is checked for unit norm, and a second replay
-must give the same bits.  Tolerance: cosine >= 0.9999 per row (north_star, tests/helpers.py).
+max_batch 256 / 1024, the committed tile table (engine.hip table_tiles: one lane, 256x256
+half-tile qkv / c_fc, 160x128 8-wave RS out_proj / c_proj), the hipGraph-replayed device entry
+point on the caller's stream.  Sampled rows spread over the batch: the first and last rows, the
+rows around the 128 / 512 midpoints (where a two-lane split would cut) and rows whose tokens
+straddle GEMM row-tile boundaries; every row of the batch is checked for unit norm, and a second
+replay must give the same bits.  Tolerance: cosine >= 0.9999 per row (north_star,
+tests/helpers.py).
 """
 import numpy as np
 import pytest

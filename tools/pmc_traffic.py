@@ -1,7 +1,10 @@
 #!/usr/bin/env python3
 """HBM traffic per launch of the bench's roofline kernel from two rocprofv3 --pmc passes.
 
-Usage: python tools/pmc_traffic.py FETCH_DIR WRITE_DIR OUT_JSON [ROWS_PER_LAUNCH [SOURCE_LABEL]]
+Usage: python tools/pmc_traffic.py FETCH_DIR WRITE_DIR OUT_JSON [ROWS_PER_LAUNCH [SOURCE_LABEL [TILES]]]
+
+TILES: the engine's gemm_tiles_env of the profiled run ("q,o,f,p"); bench.py only takes a record
+whose tiles equal its own run's.
 
 FETCH_DIR / WRITE_DIR hold `rocprofv3 --pmc FETCH_SIZE` and `--pmc WRITE_SIZE`
 counter_collection CSVs of the same `bench.py --no-text` command (separate passes: the
@@ -51,6 +54,7 @@ def main():
         "source": sys.argv[5] if len(sys.argv) > 5 else "rocprofv3 --pmc passes of bench.py",
         "compulsory_bytes_per_launch": compulsory,
         "correction": "FETCH_SIZE x2 (gfx950 wide streaming reads), KB x 1024; WRITE_SIZE as reported",
+        "tiles": sys.argv[6] if len(sys.argv) > 6 else None,
     }
     # one record per rows-per-launch (the lane split the creation-time tuning picks sets it):
     # merged into OUT_JSON's "by_rows", the latest also at the top level
