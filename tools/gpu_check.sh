@@ -19,8 +19,13 @@ run() {  # name, limit, cmd...
 for s in $STEPS; do
   case $s in
     tests)
-      run pytest_gpu 900 python -m pytest tests -m gpu -q -rf -p no:cacheprovider
+      run pytest_gpu 900 python -u -m pytest tests -m gpu -q -rf -p no:cacheprovider --timeout 300 --timeout-method thread
       rc=$?; [ $rc -le 1 ] || exit $rc ;;
+    tests_sel)  # PYTEST_SEL: test files / node ids
+      run pytest_sel 900 python -u -m pytest ${PYTEST_SEL} -m gpu -v -s -rf -p no:cacheprovider --timeout 300 --timeout-method thread
+      rc=$?; [ $rc -le 1 ] || exit $rc ;;
+    host)  # host facts the CPU baseline reads (num_cpus rule: affinity capped by the cgroup quota)
+      { nproc; cat /sys/fs/cgroup/cpu.max 2>&1; cat /sys/fs/cgroup/cpu/cpu.cfs_quota_us 2>&1; echo "OMP=$OMP_NUM_THREADS"; } > gpurun_out/host.txt; cat gpurun_out/host.txt ;;
     sweep)
       run gemm_sweep 600 python tools/gemm_sweep.py || exit $? ;;
     smoke)
