@@ -1308,6 +1308,8 @@ ResizeBatch plan_resize_batch(int S, const std::string& interp, const std::strin
     d.need_v = p.need_v;
     d.h_ksize = p.h.ksize;
     d.v_ksize = p.v.ksize;
+    d.h_prec = p.h.prec;
+    d.v_prec = p.v.prec;
     auto put = [&](const std::vector<int>& v) {
       const long off = (long)b.ints.size();
       b.ints.insert(b.ints.end(), v.begin(), v.end());

@@ -7,16 +7,20 @@
 //       crop_x = (W - crop_w) / 2; crop_y = (H - crop_h) / 2      (src/vision.rs:184-192)
 //   * resampling: "bicubic" -> CatmullRom (Keys cubic, a = -0.5, support 2),
 //     "bilinear" -> triangle (support 1), anything else -> nearest   (src/vision.rs:176-180)
-//     as a separable convolution with the filter support scaled by the
-//     downscale factor, horizontal pass then vertical pass, fixed-point
-//     coefficients and a u8 intermediate (the convolution scheme
-//     fast_image_resize 6.0.0 shares with Pillow's Resample.c; this file
-//     follows Pillow's rounding: 22-bit coefficients, round-half-up).
+//     as fast_image_resize 6.0.0's u8 convolution (the crate the reference's default feature
+//     builds, Cargo.toml; restated from its published algorithm, a port of Pillow-SIMD's
+//     Resample): per output pixel in_center = in0 + (i + 0.5) * scale, taps
+//     floor(in_center - r) .. ceil(in_center + r) clamped to the image, r = support * max(scale,
+//     1), weights filter((x - (in_center - 0.5)) / max(scale, 1)) divided by their sum; the
+//     axis's weights become i16 fixed point at precision p (the largest p < 22 with
+//     round(max weight * 2^(p+1)) < 2^15; Normalizer16), each rounded half away from zero;
+//     a pass sums 2^(p-1) + pixel * k in i32 and stores clamp(sum >> p, 0, 255); horizontal
+//     pass first, over the source rows the vertical pass reads, into a u8 intermediate.
 //   * normalize_pixels: out[c][i] = (px[i*3+c] / 255 - mean[c]) / std[c]   in f32
 //     (src/vision.rs:235-259; divide, not reciprocal-multiply).
-// Parity: bit-exact vs oracle/preprocess_ref.py; vs Pillow 12.2 within 1 u8 level
-// (Pillow rounds the crop box to f32); vs fast_image_resize's 16-bit
-// coefficients ±1 level, unpinned (no Rust toolchain here).
+// Parity: bit-exact vs oracle/preprocess_ref.py (the same restatement in Python); vs Pillow 12.2
+// within 1 u8 level (Pillow's 22-bit coefficients, f32 crop box).  The crate itself cannot be
+// built here (no Rust toolchain), so the restatement is pinned by its published algorithm.
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
@@ -33,8 +37,6 @@ namespace clipgpu {
 
 namespace {
 
-constexpr int PRECISION_BITS = kResizePrecisionBits;
-
 double bicubic_filter(double x) {  // Keys cubic, a = -0.5 (CatmullRom)
   const double a = -0.5;
   if (x < 0.0) x = -x;
@@ -48,36 +50,54 @@ double bilinear_filter(double x) {
   return 0.0;
 }
 
+// Rust's f64::round (half away from zero) then `as i16` (saturating).
+int32_t round_i16(double v) {
+  const double r = std::round(v);
+  return (int32_t)std::min(32767.0, std::max(-32768.0, r));
+}
+
+// precompute_coefficients + Normalizer16::new of fast_image_resize (header above).
 AxisPlan precompute(int in_size, double in0, double in1, int out_size, double (*filter)(double), double support0) {
   AxisPlan c;
   const double scale = (in1 - in0) / out_size;
-  const double filterscale = scale < 1.0 ? 1.0 : scale;
-  const double support = support0 * filterscale;
-  c.ksize = (int)std::ceil(support) * 2 + 1;
+  const double filter_scale = scale < 1.0 ? 1.0 : scale;
+  const double radius = support0 * filter_scale;
+  const double recip = 1.0 / filter_scale;
+  c.ksize = (int)std::ceil(radius) * 2 + 1;
   c.bounds.resize((size_t)out_size * 2);
-  c.k.assign((size_t)out_size * c.ksize, 0);
-  std::vector<double> w((size_t)c.ksize);
+  std::vector<double> w((size_t)out_size * c.ksize, 0.0);
   for (int xx = 0; xx < out_size; ++xx) {
-    const double center = in0 + (xx + 0.5) * scale;
-    const double ss = 1.0 / filterscale;
-    int xmin = (int)(center - support + 0.5);
-    if (xmin < 0) xmin = 0;
-    int xmax = (int)(center + support + 0.5);
-    if (xmax > in_size) xmax = in_size;
-    xmax -= xmin;
+    const double in_center = in0 + (xx + 0.5) * scale;
+    const int xmin = (int)std::max(std::floor(in_center - radius), 0.0);
+    const int xmax = std::min((int)std::ceil(in_center + radius), in_size);
+    const double center = in_center - 0.5;
+    double* wx = &w[(size_t)xx * c.ksize];
     double ww = 0.0;
-    for (int x = 0; x < xmax; ++x) {
-      w[x] = filter((x + xmin - center + 0.5) * ss);
-      ww += w[x];
+    for (int x = xmin; x < xmax; ++x) {
+      wx[x - xmin] = filter(((double)x - center) * recip);
+      ww += wx[x - xmin];
     }
-    for (int x = 0; x < xmax; ++x) {
-      const double v = ww != 0.0 ? w[x] / ww : w[x];
-      c.k[(size_t)xx * c.ksize + x] =
-          v < 0 ? (int32_t)(-0.5 + v * (1 << PRECISION_BITS)) : (int32_t)(0.5 + v * (1 << PRECISION_BITS));
-    }
+    if (ww != 0.0)
+      for (int x = 0; x < xmax - xmin; ++x) wx[x] /= ww;
     c.bounds[(size_t)xx * 2] = xmin;
-    c.bounds[(size_t)xx * 2 + 1] = xmax;
+    c.bounds[(size_t)xx * 2 + 1] = xmax - xmin;
   }
+  double wmax = 0.0;
+  bool first = true;
+  for (double v : w)
+    if (first || v > wmax) {
+      wmax = v;
+      first = false;
+    }
+  int prec = 0;
+  for (int p = 0; p < kResizeMaxPrecision; ++p) {
+    prec = p;
+    if ((int64_t)std::round(wmax * (double)(1 << (p + 1))) >= (1 << kResizeCoefBits)) break;
+  }
+  c.prec = prec;
+  c.k.resize(w.size());
+  const double sc = (double)(1 << prec);
+  for (size_t i = 0; i < w.size(); ++i) c.k[i] = round_i16(w[i] * sc);
   return c;
 }
 
@@ -86,7 +106,7 @@ AxisPlan nearest_axis(int in_size, double in0, double in1, int out_size) {
   AxisPlan c;
   c.ksize = 1;
   c.bounds.resize((size_t)out_size * 2);
-  c.k.assign((size_t)out_size, 1 << PRECISION_BITS);
+  c.k.assign((size_t)out_size, 1 << c.prec);
   const double sc = (in1 - in0) / out_size;
   for (int i = 0; i < out_size; ++i) {
     int x = (int)(in0 + (i + 0.5) * sc);
@@ -97,10 +117,9 @@ AxisPlan nearest_axis(int in_size, double in0, double in1, int out_size) {
   return c;
 }
 
-inline uint8_t clip8(int64_t in) {
-  if (in >= ((int64_t)1 << PRECISION_BITS << 8)) return 255;
-  if (in <= 0) return 0;
-  return (uint8_t)(in >> PRECISION_BITS);
+inline uint8_t clip8(int32_t in, int prec) {
+  const int32_t q = in >> prec;  // arithmetic shift (i32, as the crate)
+  return (uint8_t)(q < 0 ? 0 : (q > 255 ? 255 : q));
 }
 
 }  // namespace
@@ -161,17 +180,17 @@ void apply_resize_plan(const ResizePlan& p, const uint8_t* src, uint8_t* dst) {
       for (int xx = 0; xx < S; ++xx) {
         const int xmin = p.h.bounds[(size_t)xx * 2], cnt = p.h.bounds[(size_t)xx * 2 + 1];
         const int32_t* k = &p.h.k[(size_t)xx * p.h.ksize];
-        int64_t s0 = 1 << (PRECISION_BITS - 1), s1 = s0, s2 = s0;
+        int32_t s0 = 1 << (p.h.prec - 1), s1 = s0, s2 = s0;
         for (int x = 0; x < cnt; ++x) {
           const uint8_t* q = row + (size_t)(x + xmin) * 3;
-          s0 += (int64_t)q[0] * k[x];
-          s1 += (int64_t)q[1] * k[x];
-          s2 += (int64_t)q[2] * k[x];
+          s0 += (int32_t)q[0] * k[x];
+          s1 += (int32_t)q[1] * k[x];
+          s2 += (int32_t)q[2] * k[x];
         }
         uint8_t* o = &tmp[((size_t)yy * S + xx) * 3];
-        o[0] = clip8(s0);
-        o[1] = clip8(s1);
-        o[2] = clip8(s2);
+        o[0] = clip8(s0, p.h.prec);
+        o[1] = clip8(s1, p.h.prec);
+        o[2] = clip8(s2, p.h.prec);
       }
     }
     vin = tmp.data();
@@ -182,17 +201,17 @@ void apply_resize_plan(const ResizePlan& p, const uint8_t* src, uint8_t* dst) {
       const int ymin = p.v.bounds[(size_t)yy * 2], cnt = p.v.bounds[(size_t)yy * 2 + 1];
       const int32_t* k = &p.v.k[(size_t)yy * p.v.ksize];
       for (int xx = 0; xx < S; ++xx) {
-        int64_t s0 = 1 << (PRECISION_BITS - 1), s1 = s0, s2 = s0;
+        int32_t s0 = 1 << (p.v.prec - 1), s1 = s0, s2 = s0;
         for (int y = 0; y < cnt; ++y) {
           const uint8_t* q = vin + ((size_t)(y + ymin) * vin_w + xx) * 3;
-          s0 += (int64_t)q[0] * k[y];
-          s1 += (int64_t)q[1] * k[y];
-          s2 += (int64_t)q[2] * k[y];
+          s0 += (int32_t)q[0] * k[y];
+          s1 += (int32_t)q[1] * k[y];
+          s2 += (int32_t)q[2] * k[y];
         }
         uint8_t* o = dst + ((size_t)yy * S + xx) * 3;
-        o[0] = clip8(s0);
-        o[1] = clip8(s1);
-        o[2] = clip8(s2);
+        o[0] = clip8(s0, p.v.prec);
+        o[1] = clip8(s1, p.v.prec);
+        o[2] = clip8(s2, p.v.prec);
       }
     }
   } else {

@@ -9,12 +9,18 @@
 
 namespace clipgpu {
 
-constexpr int kResizePrecisionBits = 32 - 8 - 2;  // Pillow's 22-bit coefficients
+// fast_image_resize 6.0.0's u8 convolution (its Normalizer16, a port of Pillow-SIMD): the
+// normalised f64 weights of an axis become i16 fixed point at the largest precision p < 22 for
+// which round(max weight * 2^(p+1)) still fits under 2^15; a pass sums 2^(p-1) + pixel * k in
+// i32 and stores clamp(sum >> p, 0, 255).
+constexpr int kResizeMaxPrecision = 32 - 8 - 2;  // PRECISION_BITS (the precision search's bound)
+constexpr int kResizeCoefBits = 16 - 1;          // MAX_COEFS_PRECISION (i16 coefficients)
 
 // One separable axis: output i reads input [bounds[2i], bounds[2i] + bounds[2i+1]) with
-// weights k[i*ksize ..] (fixed point, sum ~= 1 << kResizePrecisionBits).
+// weights k[i*ksize ..] (fixed point at `prec` bits, sum ~= 1 << prec).
 struct AxisPlan {
   int ksize = 0;
+  int prec = kResizeMaxPrecision;
   std::vector<int> bounds;
   std::vector<int32_t> k;
 };
@@ -23,7 +29,7 @@ struct AxisPlan {
 // vertical pass (need_v): tmp (or the source when !need_h) -> out [S][S][3], with v.bounds
 // relative to the pass input.  A pass that is not needed is a straight copy (the source
 // already has that axis at S with an identity box).  Nearest is the same two passes with
-// one unit tap per output (exact: (p << 22 + 2^21) >> 22 == p).
+// one unit tap per output (exact: (p << prec + 2^(prec-1)) >> prec == p).
 struct ResizePlan {
   int W = 0, H = 0, S = 0;
   bool need_h = false, need_v = false;

@@ -28,6 +28,7 @@
 // be a multiple of 64.
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 #include <utility>
 
 #include <hip/hip_ext.h>
@@ -447,7 +448,7 @@ struct PipeBounds {
 // 2 + 11 / 32 rounds of work paid as 3 before).  No K split: every output is the same MFMA chain
 // as in the whole tile.
 template <typename T, int BM, int BN, int WGM, int WGN, int EPI, int ACT, int NS = 2, int OCC = 2, int RS = 0,
-          int HM = 0>
+          int HM = 0, int DRAIN = 0>
 __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_per_eu)) void gemm_pipe_kernel(
     GemmParams p) {
   typedef typename Vec8<T>::type V8;
@@ -883,7 +884,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
 #if CLIPGPU_GEMM_POISON_SELFTEST  // (the race check's own test: drop the wait on the 2-stage path)
         (void)EW;
 #else
-        if (after_full_epi) vm_wait<EW>();
+        if (after_full_epi && !DRAIN) vm_wait<EW>();
         else vm_wait<0>();
 #endif
       }
@@ -931,7 +932,7 @@ hipError_t launch_cfg(const GemmParams& p, hipStream_t s) {
 
 // OCC: resident blocks per CU the tile's registers allow (4-wave tiles: up to 3 by LDS; 8-wave
 // tiles: 1, or 2 when built for 4 waves per SIMD).
-template <typename T, int BM, int BN, int WGM, int WGN, int EPI, int ACT, int OCC = 3, int RS = 0>
+template <typename T, int BM, int BN, int WGM, int WGN, int EPI, int ACT, int OCC = 3, int RS = 0, int DRAIN = 0>
 hipError_t launch_pipe(const GemmParams& p, hipStream_t s) {
   constexpr int NW = WGM * WGN;
   constexpr int KOCC = NW == 8 ? (OCC >= 2 ? 2 : 1) : 2;  // kernel template's OCC (launch bounds)
@@ -949,13 +950,13 @@ hipError_t launch_pipe(const GemmParams& p, hipStream_t s) {
   if constexpr (FITS3) {
     const int nk = p.K / BK / (p.ksplit > 1 ? p.ksplit : 1);
     if (p.pipe3 == 1 && p.K >= 1024 && nk >= 3 && ntiles <= device_cus() * per_cu(3)) {
-      gemm_launch(gemm_pipe_kernel<T, BM, BN, WGM, WGN, EPI, ACT, 3, KOCC, RS>, ntiles, NW * 64, s, p);
+      gemm_launch(gemm_pipe_kernel<T, BM, BN, WGM, WGN, EPI, ACT, 3, KOCC, RS, 0, DRAIN>, ntiles, NW * 64, s, p);
       return hipGetLastError();
     }
   }
   const int resident = device_cus() * per_cu(2);
   const int grid = ntiles <= resident ? ntiles : resident;
-  gemm_launch(gemm_pipe_kernel<T, BM, BN, WGM, WGN, EPI, ACT, 2, KOCC, RS>, grid, NW * 64, s, p);
+  gemm_launch(gemm_pipe_kernel<T, BM, BN, WGM, WGN, EPI, ACT, 2, KOCC, RS, 0, DRAIN>, grid, NW * 64, s, p);
   return hipGetLastError();
 }
 
@@ -1115,10 +1116,18 @@ hipError_t launch_tile(const GemmParams& p, hipStream_t s) {
       case TILE_128x64_RS: return launch_pipe<T, 128, 64, 2, 2, EPI, ACT, 3, 1>(p, s);
       case TILE_160x128_W8_RS: return launch_pipe<T, 160, 128, 2, 4, EPI, ACT, 2, 1>(p, s);
       case TILE_256x256_HALF: return launch_pipe_half<T, EPI, ACT>(p, s);
+      case TILE_256x256_PP: return launch_gemm_pp(std::is_same<T, __bf16>::value ? DT_BF16 : DT_F16, 256, EPI, ACT, p, s);
+      case TILE_192x256_PP: return launch_gemm_pp(std::is_same<T, __bf16>::value ? DT_BF16 : DT_F16, 192, EPI, ACT, p, s);
 #if CLIPGPU_GEMM_DIAG_224
-      // (diagnostic build only, tools/check_lds_waits.py: the dropped 224x256 8-wave tile)
-      case 19:
+      // (diagnostic build only, tools/poison_diag.py: the dropped 224x256 8-wave tile)
+      case 99:
         if constexpr (EPI == EPI_STORE32 || EPI == EPI_RESID) return launch_pipe<T, 224, 256, 2, 4, EPI, ACT, 1>(p, s);
+        break;
+      case 98:  // the same with vmcnt(0) after a full epilogue instead of the counted wait
+        if constexpr (EPI == EPI_STORE32 || EPI == EPI_RESID) return launch_pipe<T, 224, 256, 2, 4, EPI, ACT, 1, 0, 1>(p, s);
+        break;
+      case 97:  // the shipped 256x256 RS f32-store instantiation with vmcnt(0) after a full epilogue
+        if constexpr (EPI == EPI_STORE32) return launch_pipe<T, 256, 256, 2, 4, EPI, ACT, 3, 1, 1>(p, s);
         break;
 #endif
       default: break;

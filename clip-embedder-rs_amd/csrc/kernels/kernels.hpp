@@ -70,7 +70,11 @@ enum GemmTile {
   TILE_128x64_RS = 16,
   TILE_160x128_W8_RS = 17,
   TILE_256x256_HALF = 18,  // 256x256 RS with the partial last round as half tiles (gemm_pipe_kernel HM = 1)
-  TILE_LAST = TILE_256x256_HALF,  // (last of the tiled kernels: the range the tuners and pins take)
+  // ping-pong schedule (gemm_pp.hip): two 4-wave row groups one section apart, so one wave of each
+  // SIMD issues MFMAs while the other reads fragments / issues DMA / runs its epilogue
+  TILE_256x256_PP = 19,   // 8 waves of 128x64, 130 KiB LDS, 1 block / CU
+  TILE_192x256_PP = 20,   // 8 waves of 96x64, 114 KiB LDS: the N = 768 GEMMs at M = 12800 are 201 tiles
+  TILE_LAST = TILE_192x256_PP,  // (last of the tiled kernels: the range the tuners and pins take)
   TILE_SKINNY = 100,      // gemm_skinny_kernel: one wave per 16x16 block, M <= 256 (TILE_AUTO's pick there);
                           // a fixed id outside the tunable range, so new tiles append without renumbering
 };
@@ -79,6 +83,9 @@ int device_cus();  // CUs of the current device (cached)
 
 // act: Act enum from common.hpp (only used with EPI_STORE16)
 hipError_t launch_gemm(DType dt, int asrc, int epi, int act, const GemmParams& p, hipStream_t s);
+// The ping-pong kernel (gemm_pp.hip; TILE_256x256_PP / TILE_192x256_PP through launch_gemm): bm = 256
+// or 192 rows per tile, 256 columns.
+hipError_t launch_gemm_pp(DType dt, int bm, int epi, int act, const GemmParams& p, hipStream_t s);
 
 // Row-complete residual GEMM + LayerNorm (gemm_rowln.hip): x[m] += A[m] . W^T + bias (f32,
 // in place) and h[m] = LN(x[m]) * ln_w + ln_b (16-bit; skipped when h is null) for the
@@ -164,7 +171,7 @@ struct ResizeImage {
   long src, tmp;            // byte offsets: source [H][W][3] in raw, pass-1 output [th][S][3] in tmp
   long h_bounds, h_coef;    // int offsets in ints: [S][2] (first, count), [S][h_ksize]
   long v_bounds, v_coef;    // [S][2] (relative to the pass input rows), [S][v_ksize]
-  int W, th, yfirst, h_ksize, v_ksize, need_h, need_v, pad;
+  int W, th, yfirst, h_ksize, v_ksize, need_h, need_v, h_prec, v_prec, pad[3];  // *_prec: fixed-point bits
 };
 hipError_t launch_resize(const uint8_t* raw, uint8_t* tmp, const int* ints, const ResizeImage* d_imgs, int n,
                          int max_th, int S, uint8_t* out, hipStream_t s);

@@ -6,8 +6,8 @@
 // to the host path: a separable convolution, horizontal pass into a u8 intermediate
 // holding only the source rows the vertical pass reads, then the vertical pass into
 // u8 NHWC [n][S][S][3] -- the input of the u8 embedding path, which normalises
-// (normalize_pixels) while staging the patch rows.  Pillow-scheme integer rounding:
-// 2^21 + sum(p * k), clipped to [0, 255 << 22], >> 22 (|sum| < 2^31: int32 as Pillow).
+// (normalize_pixels) while staging the patch rows.  fast_image_resize's integer rounding
+// (resize_plan.hpp): 2^(p-1) + sum(pixel * k) in i32, clamp(sum >> p, 0, 255), p per axis.
 //
 // One thread = one output pixel (3 channels); grid.y = image.  Memory-bound: a
 // 224 x 224 output reads its source rows once per tap column, from L2.
@@ -18,12 +18,9 @@ namespace clipgpu {
 
 namespace {
 
-constexpr int kPrec = 22;
-
-__device__ __forceinline__ uint8_t clip8(int v) {
-  if (v >= (256 << kPrec)) return 255;
-  if (v <= 0) return 0;
-  return (uint8_t)(v >> kPrec);
+__device__ __forceinline__ uint8_t clip8(int v, int prec) {
+  const int q = v >> prec;  // arithmetic shift, as the crate's i32 `>>`
+  return (uint8_t)(q < 0 ? 0 : (q > 255 ? 255 : q));
 }
 
 __global__ __launch_bounds__(256) void resize_h_kernel(const uint8_t* __restrict__ raw, uint8_t* __restrict__ tmp,
@@ -38,7 +35,7 @@ __global__ __launch_bounds__(256) void resize_h_kernel(const uint8_t* __restrict
   const int xmin = b[0], cnt = b[1];
   const int* k = ints + d.h_coef + (long)xx * d.h_ksize;
   const uint8_t* row = raw + d.src + ((long)(yy + d.yfirst) * d.W + xmin) * 3;
-  int s0 = 1 << (kPrec - 1), s1 = s0, s2 = s0;
+  int s0 = 1 << (d.h_prec - 1), s1 = s0, s2 = s0;
   for (int x = 0; x < cnt; ++x) {
     const int kx = k[x];
     s0 += (int)row[3 * x] * kx;
@@ -46,9 +43,9 @@ __global__ __launch_bounds__(256) void resize_h_kernel(const uint8_t* __restrict
     s2 += (int)row[3 * x + 2] * kx;
   }
   uint8_t* o = tmp + d.tmp + t * 3;
-  o[0] = clip8(s0);
-  o[1] = clip8(s1);
-  o[2] = clip8(s2);
+  o[0] = clip8(s0, d.h_prec);
+  o[1] = clip8(s1, d.h_prec);
+  o[2] = clip8(s2, d.h_prec);
 }
 
 __global__ __launch_bounds__(256) void resize_v_kernel(const uint8_t* __restrict__ raw,
@@ -75,7 +72,7 @@ __global__ __launch_bounds__(256) void resize_v_kernel(const uint8_t* __restrict
   const int* k = ints + d.v_coef + (long)yy * d.v_ksize;
   const uint8_t* col = in + ((long)ymin * in_w + xx) * 3;
   const long stride = (long)in_w * 3;
-  int s0 = 1 << (kPrec - 1), s1 = s0, s2 = s0;
+  int s0 = 1 << (d.v_prec - 1), s1 = s0, s2 = s0;
   for (int y = 0; y < cnt; ++y) {
     const int ky = k[y];
     const uint8_t* q = col + y * stride;
@@ -83,9 +80,9 @@ __global__ __launch_bounds__(256) void resize_v_kernel(const uint8_t* __restrict
     s1 += (int)q[1] * ky;
     s2 += (int)q[2] * ky;
   }
-  o[0] = clip8(s0);
-  o[1] = clip8(s1);
-  o[2] = clip8(s2);
+  o[0] = clip8(s0, d.v_prec);
+  o[1] = clip8(s1, d.v_prec);
+  o[2] = clip8(s2, d.v_prec);
 }
 
 }  // namespace

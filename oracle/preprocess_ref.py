@@ -2,11 +2,15 @@
 
 src/vision.rs:119-259: crop box (f64) of resize_with_fast_image_resize (:184-192),
 separable convolution resize (CatmullRom for "bicubic", triangle for "bilinear",
-:176-180), normalize_pixels (:235-259).  The convolution restates the scheme
-fast_image_resize 6.0.0 shares with Pillow's Resample.c (filter support scaled by
-the downscale factor, normalised coefficients, fixed point, horizontal pass then
-vertical pass through a u8 intermediate) with Pillow's 22-bit rounding; pinned
-against Pillow 12.2 (tests/test_cpu_preprocess.py).  Small images only (Python loops).
+:176-180), normalize_pixels (:235-259).  The convolution restates fast_image_resize
+6.0.0's u8 path (the crate is not installable here; restated from its published
+algorithm, a port of Pillow-SIMD): precompute_coefficients (taps floor(c - r) ..
+ceil(c + r), weights filter((x - (c - 0.5)) / max(scale, 1)) normalised by their sum)
+then Normalizer16 (i16 coefficients at the largest precision p < 22 with
+round(max weight * 2^(p+1)) < 2^15, rounded half away from zero), i32 sums from
+2^(p-1), clamp(sum >> p, 0, 255), horizontal pass then vertical pass through a u8
+intermediate.  Pinned against Pillow 12.2 within one level (its 22-bit scheme;
+tests/test_cpu_preprocess.py).  Small images only (Python loops).
 """
 from __future__ import annotations
 
@@ -14,7 +18,8 @@ import math
 
 import numpy as np
 
-PRECISION_BITS = 32 - 8 - 2
+PRECISION_BITS = 32 - 8 - 2  # fast_image_resize / Pillow-SIMD: the precision search's bound
+MAX_COEFS_PRECISION = 16 - 1  # i16 coefficients
 
 
 def _cubic(x, a=-0.5):
@@ -41,24 +46,44 @@ def crop_box(W, H, S, mode="shortest"):
 
 
 def _coeffs(in_size, in0, in1, out_size, filt, support0):
+    """[(first tap, i16 coefficients)] per output and the axis precision p (see header)."""
     scale = (in1 - in0) / out_size
     fs = max(scale, 1.0)
-    support = support0 * fs
-    out = []
+    radius = support0 * fs
+    recip = 1.0 / fs
+    rows = []
     for xx in range(out_size):
-        center = in0 + (xx + 0.5) * scale
-        xmin = max(int(center - support + 0.5), 0)
-        xmax = min(int(center + support + 0.5), in_size) - xmin
-        w = [filt((x + xmin - center + 0.5) / fs) for x in range(xmax)]
-        ww = sum(w)
-        w = [v / ww if ww != 0.0 else v for v in w]
-        k = [int(-0.5 + v * (1 << PRECISION_BITS)) if v < 0 else int(0.5 + v * (1 << PRECISION_BITS)) for v in w]
-        out.append((xmin, np.array(k, np.int64)))
-    return out
+        in_center = in0 + (xx + 0.5) * scale
+        xmin = int(max(math.floor(in_center - radius), 0.0))
+        xmax = min(int(math.ceil(in_center + radius)), in_size)
+        center = in_center - 0.5
+        w = [filt((x - center) * recip) for x in range(xmin, xmax)]
+        ww = 0.0
+        for v in w:
+            ww += v
+        if ww != 0.0:
+            w = [v / ww for v in w]
+        rows.append((xmin, w))
+    wmax = max(max(w) if w else 0.0 for _, w in rows)
+    if any(len(w) < int(math.ceil(radius)) * 2 + 1 for _, w in rows):
+        wmax = max(wmax, 0.0)  # the zero padding of short windows takes part in the max
+    prec = 0
+    for p in range(PRECISION_BITS):
+        prec = p
+        if _round_half_away(wmax * (1 << (p + 1))) >= (1 << MAX_COEFS_PRECISION):
+            break
+    out = [(xmin, np.array([max(-32768, min(32767, _round_half_away(v * (1 << prec)))) for v in w], np.int64))
+           for xmin, w in rows]
+    return out, prec
 
 
-def _clip8(v):
-    v = v >> PRECISION_BITS
+def _round_half_away(v):
+    """Rust f64::round: half away from zero."""
+    return int(math.floor(abs(v) + 0.5)) * (1 if v >= 0 else -1)
+
+
+def _clip8(v, prec):
+    v = v >> prec
     return np.clip(v, 0, 255).astype(np.uint8)
 
 
@@ -66,27 +91,27 @@ def resize(rgb: np.ndarray, S: int, interpolation="bicubic", mode="shortest") ->
     H, W = rgb.shape[:2]
     x0, y0, x1, y1 = crop_box(W, H, S, mode)
     filt, sup = (_cubic, 2.0) if interpolation == "bicubic" else (_triangle, 1.0)
-    ch = _coeffs(W, x0, x1, S, filt, sup)
-    cv = _coeffs(H, y0, y1, S, filt, sup)
+    ch, ph = _coeffs(W, x0, x1, S, filt, sup)
+    cv, pv = _coeffs(H, y0, y1, S, filt, sup)
     need_h = S != W or x0 != 0.0 or x1 != S
     need_v = S != H or y0 != 0.0 or y1 != S
     src = rgb.astype(np.int64)
     if need_h:
         yfirst = cv[0][0]
-        ylast = cv[-1][0] + len(cv[-1][1])
+        ylast = max(ymin + len(k) for ymin, k in cv)
         rows = src[yfirst:ylast]
         tmp = np.empty((ylast - yfirst, S, 3), np.uint8)
         for xx, (xmin, k) in enumerate(ch):
-            acc = (rows[:, xmin:xmin + len(k)] * k[None, :, None]).sum(1) + (1 << (PRECISION_BITS - 1))
-            tmp[:, xx] = _clip8(acc)
+            acc = (rows[:, xmin:xmin + len(k)] * k[None, :, None]).sum(1) + (1 << (ph - 1))
+            tmp[:, xx] = _clip8(acc, ph)
         src = tmp.astype(np.int64)
         cv = [(ymin - yfirst, k) for ymin, k in cv]
     if not need_v:
         return src[:S].astype(np.uint8)
     out = np.empty((S, S, 3), np.uint8)
     for yy, (ymin, k) in enumerate(cv):
-        acc = (src[ymin:ymin + len(k)] * k[:, None, None]).sum(0) + (1 << (PRECISION_BITS - 1))
-        out[yy] = _clip8(acc)
+        acc = (src[ymin:ymin + len(k)] * k[:, None, None]).sum(0) + (1 << (pv - 1))
+        out[yy] = _clip8(acc, pv)
     return out
 
 

@@ -1,7 +1,10 @@
 """Host preprocessing (csrc/host/preprocess.cpp, the product) vs the oracle restatement
 (oracle/preprocess_ref.py, bit-exact) and vs Pillow 12.2 (the independent pin of the
-convolution scheme: within 1 u8 level, >= 99% of samples exact).  normalize_pixels is
-bit-exact (f32 divide as src/vision.rs:254-255)."""
+convolution scheme: within 1 u8 level).  The product follows fast_image_resize 6.0.0's u8
+convolution (a5, the reference's default feature): i16 coefficients at the adaptive precision
+of its Normalizer16, where Pillow 12.2 keeps 22-bit coefficients -- the two differ by at most one
+level on under 1 % of samples.  normalize_pixels is bit-exact (f32 divide as
+src/vision.rs:254-255)."""
 import os
 
 import numpy as np
@@ -143,3 +146,25 @@ def test_preprocess_batch_image_backend():
         assert np.array_equal(got[i], ref)
     with pytest.raises(InferenceError, match="Empty batch"):
         preprocess_batch_rgb8([], 64, "bicubic", "shortest", OPENAI_MEAN, OPENAI_STD, resize_impl="image")
+
+
+@pytest.mark.parametrize("in_size,out_size,filt", [(517, 64, "bicubic"), (389, 224, "bicubic"), (120, 224, "bicubic"),
+                                                   (224, 224, "bicubic"), (97, 48, "bilinear"), (50, 400, "bilinear")])
+def test_fast_image_resize_coefficient_precision(in_size, out_size, filt):
+    """Normalizer16 (fast_image_resize 6.0.0, ported from Pillow-SIMD): the axis precision p is the
+    largest p < 22 with round(max weight * 2^(p+1)) >= 2^15 only at p itself (i16 headroom), every
+    coefficient is round-half-away(w * 2^p) and fits an i16, and each output's coefficients sum to
+    2^p within the rounding of its taps."""
+    f, sup = (preprocess_ref._cubic, 2.0) if filt == "bicubic" else (preprocess_ref._triangle, 1.0)
+    rows, p = preprocess_ref._coeffs(in_size, 0.0, float(in_size), out_size, f, sup)
+    wmax = 0.0
+    for _, k in rows:
+        wmax = max(wmax, float(k.max()) / (1 << p))
+    assert 4 <= p < 22
+    assert round(wmax * (1 << (p + 1))) >= (1 << 15) or p == 21
+    assert round(wmax * (1 << p)) < (1 << 15)
+    for _, k in rows:
+        assert np.all(np.abs(k) < 32768)
+        assert abs(int(k.sum()) - (1 << p)) <= len(k)
+    if in_size == out_size:  # identity: one unit tap per output, exact copy
+        assert p == 14 and all(int(k.max()) == 1 << 14 for _, k in rows)
