@@ -381,6 +381,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
     if (nk == 1) compute(std::true_type{}, cur1 ? sA1 : sA0, cur1 ? sB1 : sB0);
     else compute(std::false_type{}, cur1 ? sA1 : sA0, cur1 ? sB1 : sB0);
     GEMM_STAMP(4 + ti * 4);
+    vm_wait<0>();  // the next tile's stage 0 lands before the epilogue's stores (see gemm_pipe_kernel)
     epilogue(m0, n0, bias_par);
     // Retire the next tile's stage-0 glds but not this tile's output stores
     // (issued after them; in-order vmcnt): a full tile issues exactly MI*NI
@@ -448,7 +449,7 @@ struct PipeBounds {
 // 2 + 11 / 32 rounds of work paid as 3 before).  No K split: every output is the same MFMA chain
 // as in the whole tile.
 template <typename T, int BM, int BN, int WGM, int WGN, int EPI, int ACT, int NS = 2, int OCC = 2, int RS = 0,
-          int HM = 0, int DRAIN = 0>
+          int HM = 0>
 __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_per_eu)) void gemm_pipe_kernel(
     GemmParams p) {
   typedef typename Vec8<T>::type V8;
@@ -884,7 +885,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
 #if CLIPGPU_GEMM_POISON_SELFTEST  // (the race check's own test: drop the wait on the 2-stage path)
         (void)EW;
 #else
-        if (after_full_epi && !DRAIN) vm_wait<EW>();
+        if (after_full_epi) vm_wait<EW>();
         else vm_wait<0>();
 #endif
       }
@@ -898,6 +899,14 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
       if (ti == 0 && kt + 1 < nk) GEMM_STAMP(34 + kt);
     }
     GEMM_STAMP(4 + ti * 4);
+    // Retire this wave's LDS-DMA of the next step(s) before the epilogue's stores (in the 3-stage
+    // schedule all but the youngest step's pieces).  The counted waits after the epilogue count
+    // its stores, and a store can retire AHEAD of an older LDS-DMA: with the counted wait alone
+    // the 224x256 f32-store tile read steps before they landed (poison diagnosis, DESIGN.md §5
+    // "vmcnt and stores"), so no wait below may be the only one between a DMA and its readers
+    // while younger stores are in flight.
+    if constexpr (NS == 3) vm_wait<NP>();
+    else vm_wait<0>();
     epilogue(m0, n0, ti & 1, slice);
     // partial tiles, half tiles and slab units issue fewer vm ops than EPI_VM: drain them
     after_full_epi = slice == 0 && m0 + BM <= p.M && n0 + BN <= p.N && (!HM || t < hm_F);
@@ -932,7 +941,7 @@ hipError_t launch_cfg(const GemmParams& p, hipStream_t s) {
 
 // OCC: resident blocks per CU the tile's registers allow (4-wave tiles: up to 3 by LDS; 8-wave
 // tiles: 1, or 2 when built for 4 waves per SIMD).
-template <typename T, int BM, int BN, int WGM, int WGN, int EPI, int ACT, int OCC = 3, int RS = 0, int DRAIN = 0>
+template <typename T, int BM, int BN, int WGM, int WGN, int EPI, int ACT, int OCC = 3, int RS = 0>
 hipError_t launch_pipe(const GemmParams& p, hipStream_t s) {
   constexpr int NW = WGM * WGN;
   constexpr int KOCC = NW == 8 ? (OCC >= 2 ? 2 : 1) : 2;  // kernel template's OCC (launch bounds)
@@ -950,13 +959,13 @@ hipError_t launch_pipe(const GemmParams& p, hipStream_t s) {
   if constexpr (FITS3) {
     const int nk = p.K / BK / (p.ksplit > 1 ? p.ksplit : 1);
     if (p.pipe3 == 1 && p.K >= 1024 && nk >= 3 && ntiles <= device_cus() * per_cu(3)) {
-      gemm_launch(gemm_pipe_kernel<T, BM, BN, WGM, WGN, EPI, ACT, 3, KOCC, RS, 0, DRAIN>, ntiles, NW * 64, s, p);
+      gemm_launch(gemm_pipe_kernel<T, BM, BN, WGM, WGN, EPI, ACT, 3, KOCC, RS>, ntiles, NW * 64, s, p);
       return hipGetLastError();
     }
   }
   const int resident = device_cus() * per_cu(2);
   const int grid = ntiles <= resident ? ntiles : resident;
-  gemm_launch(gemm_pipe_kernel<T, BM, BN, WGM, WGN, EPI, ACT, 2, KOCC, RS, 0, DRAIN>, grid, NW * 64, s, p);
+  gemm_launch(gemm_pipe_kernel<T, BM, BN, WGM, WGN, EPI, ACT, 2, KOCC, RS>, grid, NW * 64, s, p);
   return hipGetLastError();
 }
 
@@ -1122,12 +1131,6 @@ hipError_t launch_tile(const GemmParams& p, hipStream_t s) {
       // (diagnostic build only, tools/poison_diag.py: the dropped 224x256 8-wave tile)
       case 99:
         if constexpr (EPI == EPI_STORE32 || EPI == EPI_RESID) return launch_pipe<T, 224, 256, 2, 4, EPI, ACT, 1>(p, s);
-        break;
-      case 98:  // the same with vmcnt(0) after a full epilogue instead of the counted wait
-        if constexpr (EPI == EPI_STORE32 || EPI == EPI_RESID) return launch_pipe<T, 224, 256, 2, 4, EPI, ACT, 1, 0, 1>(p, s);
-        break;
-      case 97:  // the shipped 256x256 RS f32-store instantiation with vmcnt(0) after a full epilogue
-        if constexpr (EPI == EPI_STORE32) return launch_pipe<T, 256, 256, 2, 4, EPI, ACT, 3, 1, 1>(p, s);
         break;
 #endif
       default: break;

@@ -390,6 +390,7 @@ void gemm_mx_kernel(MxGemmParams p) {
       __builtin_amdgcn_s_barrier();
       phase1(kt + 1 < nk, lds0 + ((g + 1) & 1) * STAGE);
     }
+    vm_wait<0>();  // the next step's LDS-DMA lands before the epilogue's stores (gemm.hip gemm_pipe_kernel)
     epilogue(m0, n0, ti & 1);
     after_full_epi = m0 + BM <= p.M && n0 + BN <= p.N;
     if (!after_full_epi) vm_wait<0>();
