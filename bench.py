@@ -75,7 +75,8 @@ def text_flops(B, T=77, executed=False):
 TILE_NAMES = {0: "heuristic", 1: "128x128", 2: "256x128", 3: "256x256", 4: "128x128pipe", 5: "128x64pipe",
               6: "64x128pipe", 7: "160x128pipe", 8: "160x64pipe", 9: "160x128w8", 10: "128x128w8",
               11: "192x128w8", 12: "160x256w8", 13: "192x256w8", 14: "256x256rs", 15: "160x128rs", 16: "128x64rs",
-              17: "160x128w8rs", 18: "256x256half", 19: "256x256pp", 20: "192x256pp"}
+              17: "160x128w8rs", 18: "256x256half", 19: "256x256pp", 20: "192x256pp",
+              21: "256x256m32", 22: "192x256m32", 23: "256x192m32", 24: "128x128w8m32", 25: "256x128m32"}
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md chip table)
 B_VISION = 256
 B_TEXT = 1024

@@ -67,11 +67,7 @@ namespace {
 #if CLIPGPU_GEMM_POISON
 // (race-check build) NaN bytes over the 1 KiB an LDS-DMA of this wave is about to fill; the
 // store is complete before the DMA is issued
-__device__ __forceinline__ void poison_lds(char* dst) {
-  const int lane = threadIdx.x & 63;
-  *(uint4*)(dst + lane * 16) = make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-}
+__device__ __forceinline__ void poison_lds(char* dst) { gemm_detail::lds_poison_piece(dst); }
 #define GEMM_POISON(dst) poison_lds(dst)
 #else
 #define GEMM_POISON(dst) do {} while (0)
@@ -90,6 +86,9 @@ constexpr int BK = 64;
 #endif
 #ifndef CLIPGPU_GEMM_SPREAD_ALL
 #define CLIPGPU_GEMM_SPREAD_ALL 0
+#endif
+#ifndef CLIPGPU_GEMM_EPI_DMA_WAIT
+#define CLIPGPU_GEMM_EPI_DMA_WAIT 1
 #endif
 
 template <typename T>
@@ -449,7 +448,7 @@ struct PipeBounds {
 // 2 + 11 / 32 rounds of work paid as 3 before).  No K split: every output is the same MFMA chain
 // as in the whole tile.
 template <typename T, int BM, int BN, int WGM, int WGN, int EPI, int ACT, int NS = 2, int OCC = 2, int RS = 0,
-          int HM = 0>
+          int HM = 0, int M32 = 0>
 __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_per_eu)) void gemm_pipe_kernel(
     GemmParams p) {
   typedef typename Vec8<T>::type V8;
@@ -461,11 +460,18 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
   constexpr bool WSPLIT = PW % NW == 0;     // piece i of every wave is a W piece iff i < PW / NW
   constexpr int TM = BM / WGM, TN = BN / WGN, MI = TM / 16, NI = TN / 16;
   constexpr int LG = NI == 2 ? 1 : NI == 4 ? 2 : 3;
+  // M32 = 1: v_mfma_f32_32x32x16 instead of 16x16x32 (same operand roles, the same k -> lane map
+  // within each 16-k half and the same K order: bit-identical sums, tools/mfma_order_probe.hip).
+  // The 32x32 MFMA holds the SIMD's issue for 8 of its 32 cycles instead of 8 of 16.  A phase then
+  // runs NG = MI / 2 MFMA groups of 32 rows, each over both 16-k halves of the phase's 32 k.
+  constexpr int NG = M32 ? MI / 2 : MI;
+  static_assert(!M32 || (TM % 32 == 0 && TN % 32 == 0 && RS), "32x32 MFMA: 32-multiple wave tiles, RS schedule");
   // DMA pieces spread between MFMA groups of phase 1 (>= 32 MFMAs per phase), else issued up front
   // (CLIPGPU_GEMM_SPREAD_ALL=1 at build time spreads them on every tile: an experiment switch)
   constexpr bool SPREAD = MI * NI >= 32 || CLIPGPU_GEMM_SPREAD_ALL;
+  (void)LG;
   static_assert(BM % 8 == 0 && BN % 8 == 0 && MI >= 1 && BN <= 256 && PT >= NW, "bad tile");
-  static_assert(NI == 2 || NI == 4 || NI == 8, "column permutation needs NI in {2,4,8}");
+  static_assert(M32 || NI == 2 || NI == 4 || NI == 8, "column permutation needs NI in {2,4,8}");
   static_assert(NS == 2 || (NS == 3 && EVEN), "2 LDS stages, or 3 with an even piece split");
   __shared__ __attribute__((aligned(16))) char smem[NS * STAGE + 2048];
 
@@ -526,7 +532,12 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
     tile_coords(u / ks, nTm, nTn, BM, BN, m0, n0);
   };
 
-  auto swW = [](int r) { return (r & 2) | (((r >> (2 + LG)) & 1) << 2); };
+  // W image swizzle: the 16x16 path reads W rows in a permuted order (rowB below), the 32x32 path
+  // uses the A image's (r >> 1) & 7 (conflict-free for its row order, tools comment at offB)
+  auto swW = [](int r) {
+    if constexpr (M32) return (r >> 1) & 7;
+    else return (r & 2) | (((r >> (2 + LG)) & 1) << 2);
+  };
 
   // ---- LDS-DMA cursor (global step d_g = tile d_ti, K-step d_kt) -----------
   // poff[i]: per-lane source byte offset of this wave's piece i (q = wave + NW * i) from the
@@ -605,65 +616,118 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
   // ---- fragments -------------------------------------------------------------
   const int wm = (wave / WGN) * TM, wn = (wave % WGN) * TN;
   const int fr = lane & 15, fq = lane >> 4;
-  const int rowB = wn + (fr >> 2) * (4 * NI) + (fr & 3);  // + 4*ni
-  uint32_t offA[2], offB[2];
+  // offA / offB [kk][h]: base of the phase-kk fragment reads (h: the 16-k half, 32x32 path only).
+  // 16x16: lane (fr, fq) reads row fr, k chunk 4 kk + fq; W rows permuted (rowB, + 4 ni) so a lane
+  // owns 4 NI consecutive output columns.
+  // 32x32: lane (i = lane & 31, hl = lane >> 5) reads row i of each 32-row block, k chunk
+  // 4 kk + 2 h + hl; the W fragment row of MFMA row i is wn + 16 NI32 ((i >> 2) & 1) +
+  // 4 (i >> 3) + (i & 3) (+ 16 nb), which makes D register r of lane (j, hl) output column
+  // wn + 16 NI32 hl + 16 nb + r: every lane owns 16 NI32 consecutive columns of one row.  Both
+  // images are read conflict-free with the (r >> 1) & 7 swizzle in that order.
+  uint32_t offA[2][2], offB[2][2];
+  if constexpr (M32) {
+    const int i = lane & 31, hl = lane >> 5;
+    const int rowA = wm + i;
+    const int rowW = wn + 16 * (NI / 2) * ((i >> 2) & 1) + 4 * (i >> 3) + (i & 3);
 #pragma unroll
-  for (int kk = 0; kk < 2; ++kk) {
-    offA[kk] = (uint32_t)((wm + fr) * 128 + (((kk * 4 + fq) ^ (fr >> 1)) << 4));
-    offB[kk] = (uint32_t)(A_BYTES + rowB * 128 + (((kk * 4 + fq) ^ swW(rowB)) << 4));
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int c = kk * 4 + 2 * h + hl;
+        offA[kk][h] = (uint32_t)(rowA * 128 + ((c ^ ((rowA >> 1) & 7)) << 4));
+        offB[kk][h] = (uint32_t)(A_BYTES + rowW * 128 + ((c ^ ((rowW >> 1) & 7)) << 4));
+      }
+  } else {
+    const int rowB = wn + (fr >> 2) * (4 * NI) + (fr & 3);  // + 4*ni
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      offA[kk][0] = offA[kk][1] = (uint32_t)((wm + fr) * 128 + (((kk * 4 + fq) ^ (fr >> 1)) << 4));
+      offB[kk][0] = offB[kk][1] = (uint32_t)(A_BYTES + rowB * 128 + (((kk * 4 + fq) ^ swW(rowB)) << 4));
+    }
   }
   // the current unit's row layout (HM half tiles: row offset (wave / WGN) * TM / 2, MI / 2 groups)
   int wm_cur = wm, mi_lim = MI;
-  uint32_t offA_cur[2] = {offA[0], offA[1]};
+  uint32_t offA_cur[2][2] = {{offA[0][0], offA[0][1]}, {offA[1][0], offA[1][1]}};
   auto set_layout = [&](int u) {
     if constexpr (HM) {
       const bool half = u >= hm_F;
       wm_cur = half ? (wave / WGN) * (TM / 2) : wm;
       mi_lim = half ? MI / 2 : MI;
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) offA_cur[kk] = offA[kk] - (uint32_t)((wm - wm_cur) * 128);
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) offA_cur[kk][h] = offA[kk][h] - (uint32_t)((wm - wm_cur) * 128);
     }
     (void)u;
   };
   const uint32_t lds0 = lds_addr(smem);
   f32x4 acc[NI][MI];
+  // (32x32 path) acc32[nb][mb]: the 32 x 32 block of rows wm + 32 mb, columns of group nb
+  f32x16 acc32[NI / 2 > 0 ? NI / 2 : 1][MI / 2 > 0 ? MI / 2 : 1];
+  // fragments of one phase: 16x16: a[mi], b[ni]; 32x32: a[2 mb + h], b[2 nb + h] (h: 16-k half)
   V8 a0[MI], b0[NI], a1[MI], b1[NI];
 
-  auto read_b = [&](V8(&b)[NI], uint32_t base) {
-    static_for<NI>([&](auto ni) { ds_read_b128<(int)ni * 512>(b[ni], base); });
-  };
-  auto read_a = [&](V8(&a)[MI], uint32_t base) {
-    static_for<MI>([&](auto mi) { ds_read_b128<(int)mi * 2048>(a[mi], base); });
-  };
-  // RS = 1 (read schedule): a phase's NI + MI fragment reads for the next phase go out after the
-  // first RG = MI - 2 MFMA groups, RPG per group, instead of NI up front and one A read after every
-  // group, so the last read has two MFMA groups to land before the phase-end lgkmcnt wait.
-  constexpr int NR = NI + MI, RG = RS ? (MI > 2 ? MI - 2 : 1) : MI, RPG = (NR + RG - 1) / RG;
-  auto read_k = [&](auto kc, V8(&a)[MI], V8(&b)[NI], uint32_t base_b, uint32_t base_a) {
+  auto rd_b = [&](auto kc, V8(&b)[NI], uint32_t buf, int kk) {
     constexpr int k = decltype(kc)::value;
-    if constexpr (k < NI) ds_read_b128<k * 512>(b[k], base_b);
-    else ds_read_b128<(k - NI) * 2048>(a[k - NI], base_a);
+    if constexpr (M32) ds_read_b128<(k >> 1) * 2048>(b[k], buf + offB[kk][k & 1]);
+    else ds_read_b128<k * 512>(b[k], buf + offB[kk][0]);
   };
-  auto reads_after_group = [&](auto mi, V8(&a)[MI], V8(&b)[NI], uint32_t base_b, uint32_t base_a) {
+  auto rd_a = [&](auto kc, V8(&a)[MI], uint32_t buf, int kk) {
+    constexpr int k = decltype(kc)::value;
+    if constexpr (M32) ds_read_b128<(k >> 1) * 4096>(a[k], buf + offA_cur[kk][k & 1]);
+    else ds_read_b128<k * 2048>(a[k], buf + offA_cur[kk][0]);
+  };
+  auto read_b = [&](V8(&b)[NI], uint32_t buf, int kk) { static_for<NI>([&](auto k) { rd_b(k, b, buf, kk); }); };
+  auto read_a = [&](V8(&a)[MI], uint32_t buf, int kk) { static_for<MI>([&](auto k) { rd_a(k, a, buf, kk); }); };
+  // RS = 1 (read schedule): a phase's NI + MI fragment reads for the next phase go out after the
+  // first RG = NG - 2 MFMA groups, RPG per group, instead of NI up front and one A read after every
+  // group, so the last read has two MFMA groups to land before the phase-end lgkmcnt wait.
+  constexpr int NR = NI + MI, RG = RS ? (NG > 2 ? NG - 2 : 1) : NG, RPG = (NR + RG - 1) / RG;
+  auto read_k = [&](auto kc, V8(&a)[MI], V8(&b)[NI], uint32_t buf, int kk) {
+    constexpr int k = decltype(kc)::value;
+    if constexpr (k < NI) rd_b(kc, b, buf, kk);
+    else rd_a(std::integral_constant<int, k - NI>{}, a, buf, kk);
+  };
+  auto reads_after_group = [&](auto gc, V8(&a)[MI], V8(&b)[NI], uint32_t buf, int kk) {
     static_for<RPG>([&](auto j) {
-      constexpr int k = (int)decltype(mi)::value * RPG + (int)decltype(j)::value;
-      if constexpr ((int)decltype(mi)::value < RG && k < NR) read_k(std::integral_constant<int, k>{}, a, b, base_b, base_a);
+      constexpr int k = (int)decltype(gc)::value * RPG + (int)decltype(j)::value;
+      if constexpr ((int)decltype(gc)::value < RG && k < NR) read_k(std::integral_constant<int, k>{}, a, b, buf, kk);
     });
   };
-  auto phase0 = [&](auto zero, uint32_t buf) {
-    if constexpr (!RS) read_b(b1, buf + offB[1]);
-    static_for<MI>([&](auto mi) {
-      if (!HM || (int)mi < mi_lim) {
+  // MFMA group g of a phase: 16 rows x all NI column blocks (16x16), or 32 rows x all NI / 2 column
+  // blocks over both 16-k halves (32x32); zero: the unit's first MFMA of each accumulator
+  auto mfma_group = [&](auto gc, V8(&a)[MI], V8(&b)[NI], auto zero) {
+    constexpr int g = decltype(gc)::value;
+    constexpr bool Z = decltype(zero)::value;
+    if constexpr (M32) {
+      if (!HM || 2 * g < mi_lim) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int nb = 0; nb < NI / 2; ++nb) {
+            f32x16 c = acc32[nb][g];
+            if (Z && h == 0) c = f32x16{};
+            acc32[nb][g] = mfma_32x32x16(b[2 * nb + h], a[2 * g + h], c);
+          }
+      }
+    } else {
+      if (!HM || g < mi_lim) {
 #pragma unroll
         for (int ni = 0; ni < NI; ++ni)
-          acc[ni][mi] = mfma_16x16x32(b0[ni], a0[mi], decltype(zero)::value ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[ni][mi]);
+          acc[ni][g] = mfma_16x16x32(b[ni], a[g], Z ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[ni][g]);
       }
+    }
+  };
+  auto phase0 = [&](auto zero, uint32_t buf) {
+    if constexpr (!RS) read_b(b1, buf, 1);
+    static_for<NG>([&](auto g) {
+      mfma_group(g, a0, b0, zero);
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (RS) {
-        reads_after_group(mi, a1, b1, buf + offB[1], buf + offA_cur[1]);
+        reads_after_group(g, a1, b1, buf, 1);
         __builtin_amdgcn_sched_barrier(0);
       } else {
-        ds_read_b128<(int)mi * 2048>(a1[mi], buf + offA_cur[1]);
+        rd_a(g, a1, buf, 1);
       }
     });
     lgkm_wait_all(a1, b1);
@@ -674,22 +738,19 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
     // the other buffer, unused): a conditional read made the compiler keep a second copy
     // of the fragment registers across the branch
     (void)next;
-    if constexpr (!RS) read_b(b0, nbuf + offB[0]);
+    if constexpr (!RS) read_b(b0, nbuf, 0);
     if (dma) {
       dma_bias();
       if constexpr (!SPREAD) static_for<NP>([&](auto j) { dma_piece(j); });
     }
-    static_for<MI>([&](auto mi) {
-      if (!HM || (int)mi < mi_lim) {
-#pragma unroll
-        for (int ni = 0; ni < NI; ++ni) acc[ni][mi] = mfma_16x16x32(b1[ni], a1[mi], acc[ni][mi]);
-      }
+    static_for<NG>([&](auto g) {
+      mfma_group(g, a1, b1, std::false_type{});
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr (RS) reads_after_group(mi, a0, b0, nbuf + offB[0], nbuf + offA_cur[0]);
-      else ds_read_b128<(int)mi * 2048>(a0[mi], nbuf + offA_cur[0]);
+      if constexpr (RS) reads_after_group(g, a0, b0, nbuf, 0);
+      else rd_a(g, a0, nbuf, 0);
       if constexpr (SPREAD) {
         static_for<NP>([&](auto j) {
-          if constexpr (((int)j * MI) / NP == (int)mi) {
+          if constexpr (((int)j * NG) / NP == (int)g) {
             if (dma) dma_piece(j);
           }
         });
@@ -846,7 +907,131 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
       }
     }
   };
-  // vm ops a full tile's epilogue leaves in flight behind the DMA of the step after it
+  // ---- epilogue, 32x32 path: lane (i, hl) owns row wm + 32 mb + i, the CW = 16 NI / 2 consecutive
+  // columns from nc; column nc + 16 nb + r is acc32[nb][mb][r].  The float ops per element are the
+  // 16x16 epilogue's ((acc + bias) (+ x), act), so the outputs are bit-identical to it.
+  auto epilogue32 = [&](int m0, int n0, int bpar, int slice) {
+    constexpr int MI2 = MI / 2 > 0 ? MI / 2 : 1, CW = 16 * (NI / 2), CQ = CW / 4;
+    const int i = lane & 31, hl = lane >> 5;
+    const int nc = n0 + wn + hl * CW;
+    const bool nfull = nc + CW <= p.N;
+    auto val = [&](int mb, int q, int e) -> float { return acc32[q >> 2][mb][(q & 3) * 4 + e]; };
+    if (slice > 0) {
+      float* const slab = p.slab + (long)(slice - 1) * p.M * p.ldo;
+#pragma unroll
+      for (int mb = 0; mb < MI2; ++mb) {
+        const int m = m0 + wm_cur + mb * 32 + i;
+        if (m >= p.M) continue;
+        float* o = slab + (long)m * p.ldo + nc;
+        if (nfull) {
+#pragma unroll
+          for (int q = 0; q < CQ; ++q) *(float4*)(o + q * 4) = make_float4(val(mb, q, 0), val(mb, q, 1), val(mb, q, 2), val(mb, q, 3));
+        } else {
+#pragma unroll
+          for (int q = 0; q < CQ; ++q)
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              if (nc + q * 4 + e < p.N) o[q * 4 + e] = val(mb, q, e);
+        }
+      }
+      return;
+    }
+    f32x4 bias[CQ];
+#pragma unroll
+    for (int q = 0; q < CQ; ++q) bias[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (p.bias != nullptr) {
+      const uint32_t ba = lds0 + NS * STAGE + bpar * 1024 + (wn + hl * CW) * 4;
+      static_for<CQ>([&](auto q) { ds_read_b128<(int)q * 16>(bias[q], ba); });
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int q = 0; q < CQ; ++q) asm volatile("" : "+v"(bias[q]));
+    }
+    constexpr bool ADDX = EPI == EPI_RESID || EPI == EPI_PATCH;
+    const int G2 = p.G * p.G;
+    auto out_row = [&](int m) -> long {
+      if constexpr (EPI == EPI_PATCH) {
+        const int b = m / G2;
+        return ((long)b * (G2 + p.cls) + p.cls + (m - b * G2)) * p.ldo;
+      } else {
+        return (long)m * p.ldo;
+      }
+    };
+    auto add_src = [&](int m) -> const float* {
+      if constexpr (EPI == EPI_PATCH) return p.pos + (long)(p.cls + m % G2) * p.N + nc;
+      else return (const float*)p.out + (long)m * p.ldo + nc;
+    };
+    // the added rows (residual x / positional embedding): a ring of 2 row blocks loaded one ahead
+    // when the registers allow it (accumulators + bias + 2 rows + ~40 addresses within the wave's
+    // share), else each row block loaded just before its use
+    constexpr int REG_BUDGET = NW == 8 && OCC >= 2 ? 128 : 256;
+    constexpr int XR = ADDX && MI2 > 1 && MI * NI * 4 + 12 * CQ + 40 <= REG_BUDGET ? 2 : 1;
+    float4 xr[XR][CQ];
+    auto load_x = [&](int mb, float4(&dst)[CQ]) {
+      const int m = m0 + wm_cur + mb * 32 + i;
+      if (m < p.M && nfull && (!HM || 2 * mb < mi_lim)) {
+        const float* src = add_src(m);
+#pragma unroll
+        for (int q = 0; q < CQ; ++q) dst[q] = *(const float4*)(src + q * 4);
+      }
+    };
+    if constexpr (ADDX) load_x(0, xr[0]);
+#pragma unroll
+    for (int mb = 0; mb < MI2; ++mb) {
+      if constexpr (ADDX && XR > 1) {
+        if (mb + 1 < MI2) load_x(mb + 1, xr[(mb + 1) % XR]);
+      }
+      const int m = m0 + wm_cur + mb * 32 + i;
+      if (m >= p.M || (HM && 2 * mb >= mi_lim)) continue;
+      if constexpr (EPI == EPI_STORE16) {
+        T* o = (T*)p.out + (long)m * p.ldo + nc;
+        if (nfull) {
+#pragma unroll
+          for (int h = 0; h < CW / 8; ++h) {
+            V8 w;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const int q = 2 * h + e / 4, j = e % 4;
+              w[e] = to16<T>(apply_act<ACT>(val(mb, q, j) + bias[q][j]));
+            }
+            *(V8*)(o + h * 8) = w;
+          }
+        } else {
+#pragma unroll
+          for (int q = 0; q < CQ; ++q)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if (nc + q * 4 + j < p.N) o[q * 4 + j] = to16<T>(apply_act<ACT>(val(mb, q, j) + bias[q][j]));
+        }
+      } else {
+        float* o = (float*)p.out + out_row(m) + nc;
+        if (nfull) {
+#pragma unroll
+          for (int q = 0; q < CQ; ++q) {
+            float4 w = make_float4(val(mb, q, 0) + bias[q][0], val(mb, q, 1) + bias[q][1], val(mb, q, 2) + bias[q][2],
+                                   val(mb, q, 3) + bias[q][3]);
+            if constexpr (ADDX) {
+              const float4 x = xr[mb % XR][q];
+              w.x += x.x; w.y += x.y; w.z += x.z; w.w += x.w;
+            }
+            *(float4*)(o + q * 4) = w;
+          }
+        } else {
+          const float* xs = ADDX ? add_src(m) : nullptr;
+#pragma unroll
+          for (int q = 0; q < CQ; ++q)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              if (nc + q * 4 + j >= p.N) continue;
+              float r = val(mb, q, j) + bias[q][j];
+              if constexpr (ADDX) r += xs[q * 4 + j];
+              o[q * 4 + j] = r;
+            }
+        }
+      }
+    }
+  };
+  // vm ops a full tile's epilogue leaves in flight behind the DMA of the step after it (the same
+  // count on both paths: MI NI / 2 16-byte stores of 16-bit values, MI NI of f32, + as many loads)
   constexpr int EPI_VM = EPI == EPI_STORE16 ? MI * NI / 2 : ((EPI == EPI_RESID || EPI == EPI_PATCH) ? 2 * MI * NI : MI * NI);
 
   // ---- prologue: steps 0 and 1 in flight, step 0 landed, its kk0 fragments read
@@ -857,8 +1042,8 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
   __builtin_amdgcn_s_barrier();
   dma_step();
   if constexpr (NS == 3) dma_step();
-  read_b(b0, lds0 + offB[0]);
-  read_a(a0, lds0 + offA[0]);
+  read_b(b0, lds0, 0);
+  read_a(a0, lds0, 0);
   lgkm_wait_all(a0, b0);
   GEMM_STAMP(1);
 
@@ -899,23 +1084,25 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
       if (ti == 0 && kt + 1 < nk) GEMM_STAMP(34 + kt);
     }
     GEMM_STAMP(4 + ti * 4);
-    // Retire this wave's LDS-DMA of the next step(s) before the epilogue's stores (in the 3-stage
-    // schedule all but the youngest step's pieces).  The counted waits after the epilogue count
-    // its stores, and a store can retire AHEAD of an older LDS-DMA: with the counted wait alone
-    // the 224x256 f32-store tile read steps before they landed (poison diagnosis, DESIGN.md §5
-    // "vmcnt and stores"), so no wait below may be the only one between a DMA and its readers
-    // while younger stores are in flight.
+    // (CLIPGPU_GEMM_EPI_DMA_WAIT, default on) retire this wave's LDS-DMA of the next step(s) before
+    // the epilogue's stores (3 stages: all but the youngest step's pieces), so that the counted
+    // wait after a full epilogue never relies on a store retiring after an older LDS-DMA (the
+    // compiler's own wait insertion treats mixed pending VMEM reads and writes as unordered).
+    // DESIGN.md §5 "The 224x256 race-check failure" records what this was and was not.
+#if CLIPGPU_GEMM_EPI_DMA_WAIT
     if constexpr (NS == 3) vm_wait<NP>();
     else vm_wait<0>();
-    epilogue(m0, n0, ti & 1, slice);
+#endif
+    if constexpr (M32) epilogue32(m0, n0, ti & 1, slice);
+    else epilogue(m0, n0, ti & 1, slice);
     // partial tiles, half tiles and slab units issue fewer vm ops than EPI_VM: drain them
     after_full_epi = slice == 0 && m0 + BM <= p.M && n0 + BN <= p.N && (!HM || t < hm_F);
     if (!after_full_epi) vm_wait<0>();
     if (t + t_stride < t_end) {  // the next tile's step 0 landed at the last barrier
       const uint32_t buf = lds0 + (g % NS) * STAGE;
       set_layout(t + t_stride);
-      read_b(b0, buf + offB[0]);
-      read_a(a0, buf + offA_cur[0]);
+      read_b(b0, buf, 0);
+      read_a(a0, buf, 0);
       lgkm_wait_all(a0, b0);
     }
     GEMM_STAMP(5 + ti * 4);
@@ -941,7 +1128,7 @@ hipError_t launch_cfg(const GemmParams& p, hipStream_t s) {
 
 // OCC: resident blocks per CU the tile's registers allow (4-wave tiles: up to 3 by LDS; 8-wave
 // tiles: 1, or 2 when built for 4 waves per SIMD).
-template <typename T, int BM, int BN, int WGM, int WGN, int EPI, int ACT, int OCC = 3, int RS = 0>
+template <typename T, int BM, int BN, int WGM, int WGN, int EPI, int ACT, int OCC = 3, int RS = 0, int M32 = 0>
 hipError_t launch_pipe(const GemmParams& p, hipStream_t s) {
   constexpr int NW = WGM * WGN;
   constexpr int KOCC = NW == 8 ? (OCC >= 2 ? 2 : 1) : 2;  // kernel template's OCC (launch bounds)
@@ -959,20 +1146,20 @@ hipError_t launch_pipe(const GemmParams& p, hipStream_t s) {
   if constexpr (FITS3) {
     const int nk = p.K / BK / (p.ksplit > 1 ? p.ksplit : 1);
     if (p.pipe3 == 1 && p.K >= 1024 && nk >= 3 && ntiles <= device_cus() * per_cu(3)) {
-      gemm_launch(gemm_pipe_kernel<T, BM, BN, WGM, WGN, EPI, ACT, 3, KOCC, RS>, ntiles, NW * 64, s, p);
+      gemm_launch(gemm_pipe_kernel<T, BM, BN, WGM, WGN, EPI, ACT, 3, KOCC, RS, 0, M32>, ntiles, NW * 64, s, p);
       return hipGetLastError();
     }
   }
   const int resident = device_cus() * per_cu(2);
   const int grid = ntiles <= resident ? ntiles : resident;
-  gemm_launch(gemm_pipe_kernel<T, BM, BN, WGM, WGN, EPI, ACT, 2, KOCC, RS>, grid, NW * 64, s, p);
+  gemm_launch(gemm_pipe_kernel<T, BM, BN, WGM, WGN, EPI, ACT, 2, KOCC, RS, 0, M32>, grid, NW * 64, s, p);
   return hipGetLastError();
 }
 
 // Half-tile last round for the 256x256 RS tile (gemm_pipe_kernel HM = 1, one block per CU): when the
 // tiles leave a partial last round of at most nbx / 2 tiles per XCD after >= 1 whole round; else the
 // plain RS launch (the same sums, bit for bit).
-template <typename T, int EPI, int ACT>
+template <typename T, int EPI, int ACT, int M32 = 0>
 hipError_t launch_pipe_half(const GemmParams& p, hipStream_t s) {
   const int nb = device_cus();
   const int ntiles = ((p.N + 255) / 256) * ((p.M + 255) / 256);
@@ -982,8 +1169,8 @@ hipError_t launch_pipe_half(const GemmParams& p, hipStream_t s) {
     const int cnt = q + (x < r ? 1 : 0);
     ok = cnt >= nbx && 2 * (cnt % nbx) <= nbx;
   }
-  if (!ok) return launch_pipe<T, 256, 256, 2, 4, EPI, ACT, 3, 1>(p, s);
-  gemm_launch(gemm_pipe_kernel<T, 256, 256, 2, 4, EPI, ACT, 2, 2, 1, 1>, nb, 512, s, p);
+  if (!ok) return launch_pipe<T, 256, 256, 2, 4, EPI, ACT, 3, 1, M32>(p, s);
+  gemm_launch(gemm_pipe_kernel<T, 256, 256, 2, 4, EPI, ACT, 2, 2, 1, 1, M32>, nb, 512, s, p);
   return hipGetLastError();
 }
 
@@ -1103,6 +1290,11 @@ hipError_t launch_tile(const GemmParams& p, hipStream_t s) {
       case TILE_160x128_RS: return launch_pipe<T, 160, 128, 2, 2, EPI, ACT, 3, 1>(p, s);
       case TILE_128x64_RS: return launch_pipe<T, 128, 64, 2, 2, EPI, ACT, 3, 1>(p, s);
       case TILE_160x128_W8_RS: return launch_pipe<T, 160, 128, 2, 4, EPI, ACT, 2, 1>(p, s);
+      case TILE_256x256_M32: return launch_pipe<T, 256, 256, 2, 4, EPI, ACT, 3, 1, 1>(p, s);
+      case TILE_192x256_M32: return launch_pipe<T, 192, 256, 2, 4, EPI, ACT, 1, 1, 1>(p, s);
+      case TILE_256x192_M32: return launch_pipe<T, 256, 192, 4, 2, EPI, ACT, 1, 1, 1>(p, s);
+      case TILE_128x128_W8_M32: return launch_pipe<T, 128, 128, 2, 4, EPI, ACT, 2, 1, 1>(p, s);
+      case TILE_256x128_M32: return launch_pipe<T, 256, 128, 4, 2, EPI, ACT, 1, 1, 1>(p, s);
       default: return launch_pipe<T, 128, 128, 2, 2, EPI, ACT>(p, s);
     }
   }
@@ -1125,6 +1317,11 @@ hipError_t launch_tile(const GemmParams& p, hipStream_t s) {
       case TILE_128x64_RS: return launch_pipe<T, 128, 64, 2, 2, EPI, ACT, 3, 1>(p, s);
       case TILE_160x128_W8_RS: return launch_pipe<T, 160, 128, 2, 4, EPI, ACT, 2, 1>(p, s);
       case TILE_256x256_HALF: return launch_pipe_half<T, EPI, ACT>(p, s);
+      case TILE_256x256_M32: return launch_pipe_half<T, EPI, ACT, 1>(p, s);
+      case TILE_192x256_M32: return launch_pipe<T, 192, 256, 2, 4, EPI, ACT, 1, 1, 1>(p, s);
+      case TILE_256x192_M32: return launch_pipe<T, 256, 192, 4, 2, EPI, ACT, 1, 1, 1>(p, s);
+      case TILE_128x128_W8_M32: return launch_pipe<T, 128, 128, 2, 4, EPI, ACT, 2, 1, 1>(p, s);
+      case TILE_256x128_M32: return launch_pipe<T, 256, 128, 4, 2, EPI, ACT, 1, 1, 1>(p, s);
       case TILE_256x256_PP: return launch_gemm_pp(std::is_same<T, __bf16>::value ? DT_BF16 : DT_F16, 256, EPI, ACT, p, s);
       case TILE_192x256_PP: return launch_gemm_pp(std::is_same<T, __bf16>::value ? DT_BF16 : DT_F16, 192, EPI, ACT, p, s);
 #if CLIPGPU_GEMM_DIAG_224

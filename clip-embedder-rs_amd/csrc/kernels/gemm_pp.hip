@@ -47,10 +47,7 @@ constexpr int PBK = 64;
 // CLIPGPU_GEMM_POISON): every wave fills the 1 KiB destination of each of its LDS-DMAs with NaN
 // bytes before issuing it, so a fragment read ahead of its DMA reads NaN (test_gpu_kernels.py).
 #if CLIPGPU_GEMM_POISON
-__device__ __forceinline__ void pp_poison(char* dst) {
-  *(uint4*)(dst + (threadIdx.x & 63) * 16) = make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-}
+__device__ __forceinline__ void pp_poison(char* dst) { gemm_detail::lds_poison_piece(dst); }
 #define PP_POISON(dst) pp_poison(dst)
 #else
 #define PP_POISON(dst) do {} while (0)

@@ -57,6 +57,18 @@ __device__ __forceinline__ void lgkm_wait_all(V (&a)[MI], V (&b)[NI]) {
   for (int i = 0; i < NI; ++i) asm volatile("" : "+v"(b[i]));
 }
 
+// Race-check builds only: NaN bytes over this lane's 16 bytes of an LDS-DMA destination (dst: the
+// wave's 1 KiB piece), complete before the DMA is issued.  Inline asm on purpose: a plain C++ LDS
+// store makes the compiler's wait insertion drain vmcnt first (it may alias the wave's pending
+// LDS-DMAs), which would add exactly the synchronisation the race check exists to verify, and its
+// extra live registers pushed a tile into spills once.
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void lds_poison_piece(const char* dst) {
+  const uint32_t a = lds_addr(dst) + (uint32_t)(threadIdx.x & 63) * 16u;
+  const u32x4_t nan = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
+  asm volatile("ds_write_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" ::"v"(a), "v"(nan) : "memory");
+}
+
 template <int N>
 __device__ __forceinline__ void vm_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");

@@ -74,7 +74,13 @@ enum GemmTile {
   // SIMD issues MFMAs while the other reads fragments / issues DMA / runs its epilogue
   TILE_256x256_PP = 19,   // 8 waves of 128x64, 130 KiB LDS, 1 block / CU
   TILE_192x256_PP = 20,   // 8 waves of 96x64, 114 KiB LDS: the N = 768 GEMMs at M = 12800 are 201 tiles
-  TILE_LAST = TILE_192x256_PP,  // (last of the tiled kernels: the range the tuners and pins take)
+  // gemm_pipe_kernel with v_mfma_f32_32x32x16 (M32 = 1; bit-identical to the 16x16x32 tiles):
+  TILE_256x256_M32 = 21,   // tile 18's schedule (RS, half-tile last round), 2x4 waves of 128x64
+  TILE_192x256_M32 = 22,   // 2x4 waves of 96x64, RS, 1 block / CU
+  TILE_256x192_M32 = 23,   // 4x2 waves of 64x96, RS, 114 KiB LDS, 1 block / CU: N = 768 is 4 column tiles
+  TILE_128x128_W8_M32 = 24,  // 2x4 waves of 64x32, RS, 66 KiB LDS, 2 blocks / CU
+  TILE_256x128_M32 = 25,   // 4x2 waves of 64x64, RS, 98 KiB LDS, 1 block / CU
+  TILE_LAST = TILE_256x128_M32,  // (last of the tiled kernels: the range the tuners and pins take)
   TILE_SKINNY = 100,      // gemm_skinny_kernel: one wave per 16x16 block, M <= 256 (TILE_AUTO's pick there);
                           // a fixed id outside the tunable range, so new tiles append without renumbering
 };

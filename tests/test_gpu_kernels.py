@@ -48,11 +48,12 @@ def run_gemm(dtype, mode, act, A, W, bias=None, resid=None):
     return out
 
 
-@pytest.fixture(params=[1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20],
+@pytest.fixture(params=[1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25],
                 ids=["t128x128", "pipe256x128", "pipe256x256", "pipe128x128", "pipe128x64", "pipe64x128",
                      "pipe160x128", "pipe160x64", "w8_160x128", "w8_128x128", "w8_192x128", "w8_160x256",
                      "w8_192x256", "rs_256x256", "rs_160x128", "rs_128x64",
-                     "rs_w8_160x128", "half_256x256", "pp_256x256", "pp_192x256"])
+                     "rs_w8_160x128", "half_256x256", "pp_256x256", "pp_192x256", "m32_256x256",
+                     "m32_192x256", "m32_256x192", "m32_w8_128x128", "m32_256x128"])
 def tile(request, monkeypatch):
     """Every GEMM tile configuration (GemmTile) through the same numerics checks."""
     monkeypatch.setenv("CLIPGPU_TEST_TILE", str(request.param))
@@ -176,7 +177,7 @@ def test_gemm_pipelines_never_read_a_stage_before_its_dma_lands(M, N, K, mode, a
     W = np.ascontiguousarray(round16(rng.standard_normal((N, K)) / np.sqrt(K), BF16))
     bias = rng.standard_normal(N).astype(np.float32)
     resid = rng.standard_normal((M, N)).astype(np.float32) if mode == 1 else None
-    for t in range(2, 21):
+    for t in range(2, 26):
         for p3 in ("0", "1"):
             monkeypatch.setenv("CLIPGPU_TEST_TILE", str(t))
             monkeypatch.setenv("CLIPGPU_GEMM_PIPE3", p3)
