@@ -979,6 +979,8 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
     for (int mb = 0; mb < MI2; ++mb) {
       if constexpr (ADDX && XR > 1) {
         if (mb + 1 < MI2) load_x(mb + 1, xr[(mb + 1) % XR]);
+      } else if constexpr (ADDX) {
+        if (mb > 0) load_x(mb, xr[0]);  // no ring: each row block's x just before its use
       }
       const int m = m0 + wm_cur + mb * 32 + i;
       if (m >= p.M || (HM && 2 * mb >= mi_lim)) continue;
