@@ -57,9 +57,18 @@ __device__ unsigned long long g_gemm_stamps[kStampBlocks * kStampSlots];
     if (threadIdx.x == 0 && blockIdx.x < kStampBlocks)                                          \
       g_gemm_stamps[blockIdx.x * kStampSlots + (slot)] = __builtin_amdgcn_s_memrealtime();    \
   } while (0)
+// slot 61: where the block runs, (XCC_ID << 32) | HW_ID (cu_id bits 11:8, sh 12, se 15:13)
+#define GEMM_STAMP_HWID()                                                                       \
+  do {                                                                                          \
+    if (threadIdx.x == 0 && blockIdx.x < kStampBlocks)                                          \
+      g_gemm_stamps[blockIdx.x * kStampSlots + 61] =                                            \
+          ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |              \
+          (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);                                  \
+  } while (0)
 #else
 #define GEMM_STAMP(slot) do {} while (0)
 #define GEMM_STAMP_REAL(slot) do {} while (0)
+#define GEMM_STAMP_HWID() do {} while (0)
 #endif
 
 namespace {
@@ -1038,6 +1047,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
 
   // ---- prologue: steps 0 and 1 in flight, step 0 landed, its kk0 fragments read
   GEMM_STAMP_REAL(62);
+  GEMM_STAMP_HWID();
   GEMM_STAMP(0);
   dma_step();
   vm_wait<0>();

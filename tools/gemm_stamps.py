@@ -43,6 +43,11 @@ CASES = [
     ("b256_c_proj 192x256w8", 1, 0, 12800, 768, 3072, 13),
     ("b256_out 192x256w8", 1, 0, 12800, 768, 768, 13),
     ("b256_out 128x64p", 1, 0, 12800, 768, 768, 5),
+    # the committed table's tiles (engine.hip table_tile) at the bench's one-lane rows
+    ("t17_out 160x128w8rs", 1, 0, 12800, 768, 768, 17),
+    ("t17_c_proj 160x128w8rs", 1, 0, 12800, 768, 3072, 17),
+    ("t18_c_fc 256x256half", 0, 1, 12800, 3072, 768, 18),
+    ("t18_qkv 256x256half", 0, 0, 12800, 2304, 768, 18),
 ]
 if len(sys.argv) > 1:
     CASES = [c for c in CASES if any(a in c[0] for a in sys.argv[1:])]
