@@ -372,7 +372,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
       if (kt == 0) compute(std::true_type{}, cur1 ? sA1 : sA0, cur1 ? sB1 : sB0);
       else compute(std::false_type{}, cur1 ? sA1 : sA0, cur1 ? sB1 : sB0);
       step_sync();
-      if (ti == 0) GEMM_STAMP(34 + kt);
+      if (ti == 0 && 34 + kt < 61) GEMM_STAMP(34 + kt);  // (slots 61-63: HW_ID, realtime)
     }
     GEMM_STAMP(3 + ti * 4);
     // last K-step: prefetch the next tile's first K-step under it and the epilogue
@@ -487,6 +487,15 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // The DMA row strides, fetched with the other kernel arguments up front.  Read lazily inside
+  // set_tile's per-piece (wave-dependent) branches, each became its own kernel-argument round trip:
+  // five serialized s_load + s_waitcnt in the prologue (round-3 stamps; ~0.25 us per round trip,
+  // tools/dispatch_probe.hip).
+  const int lda_i = (int)p.lda, ldw_i = (int)p.ldw, nb = gridDim.x;
+  const char* const Ab = (const char*)p.A;
+  const char* const Wb = (const char*)p.W;
+  const float* const bias_p = p.bias;
+  asm volatile("" ::"s"(lda_i), "s"(ldw_i), "s"(nb), "s"(Ab), "s"(Wb), "s"(bias_p));
   const int nTn = (p.N + BN - 1) / BN;
   const int nTm = (p.M + BM - 1) / BM;
   // Work unit u = (tile u / ks, K-slice u % ks): slice 0 runs the epilogue EPI, slices
@@ -496,7 +505,6 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
   const int ntiles = nTn * nTm * ks;
   const int nk = p.K / BK / ks;  // K-steps per unit
 
-  const int nb = gridDim.x;
   static_assert(!HM || (NS == 2 && WGM == 2), "half tiles: 2 x N waves, 2-stage schedule");
   int t_first, t_stride, t_end;
   int hm_F = 0, hm_start = 0, hm_nbx = 1, hm_j = 0;  // HM: whole rounds, XCD range start, blocks, index
@@ -552,8 +560,6 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
   // poff[i]: per-lane source byte offset of this wave's piece i (q = wave + NW * i) from the
   // kernel-argument base pointer (A or W), for the current unit's first K-step.
   uint32_t poff[NP];
-  const char* const Wb = (const char*)p.W;
-  const char* const Ab = (const char*)p.A;
   auto piece_is_w = [&](int i, int q) { return WSPLIT ? (i < PW / NW) : (q < PW); };
   auto set_tile = [&](int m0, int n0, int slice) {
     const int k0 = slice * nk * BK;  // first k of the unit's K-slice
@@ -565,11 +571,11 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
       } else if (piece_is_w(i, q)) {
         const int r = q * 8 + (lane >> 3);
         const int c = (lane & 7) ^ swW(r);
-        poff[i] = (uint32_t)(min(n0 + r, p.N - 1) * (int)p.ldw + k0 + c * 8) * 2u;
+        poff[i] = (uint32_t)(min(n0 + r, p.N - 1) * ldw_i + k0 + c * 8) * 2u;
       } else {
         const int r = (q - PW) * 8 + (lane >> 3);
         const int c = (lane & 7) ^ ((r >> 1) & 7);
-        poff[i] = (uint32_t)(min(m0 + r, p.M - 1) * (int)p.lda + k0 + c * 8) * 2u;
+        poff[i] = (uint32_t)(min(m0 + r, p.M - 1) * lda_i + k0 + c * 8) * 2u;
       }
     }
   };
@@ -594,10 +600,10 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
     else glds16(Ab + (size_t)d_kt * (BK * 2) + poff[i], dst);
   };
   auto dma_bias = [&]() {  // the tile's bias slice, with its first K-step (tile-parity buffer)
-    if (p.bias != nullptr && wave == 0 && d_kt == 0) {
+    if (bias_p != nullptr && wave == 0 && d_kt == 0) {
       const int n = min(d_n0 + lane * 4, ((p.N - 1) / 4) * 4);
       GEMM_POISON(smem + NS * STAGE + (d_ti & 1) * 1024);
-      glds16(p.bias + n, smem + NS * STAGE + (d_ti & 1) * 1024);
+      glds16(bias_p + n, smem + NS * STAGE + (d_ti & 1) * 1024);
     }
   };
   auto dma_advance = [&]() {
@@ -799,7 +805,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
       }
       return;
     }
-    if (p.bias != nullptr) {
+    if (bias_p != nullptr) {
       const uint32_t ba = lds0 + NS * STAGE + bpar * 1024 + (wn + fq * (4 * NI)) * 4;
       static_for<NI>([&](auto ni) { ds_read_b128<(int)ni * 16>(bias[ni], ba); });
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -948,7 +954,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
     f32x4 bias[CQ];
 #pragma unroll
     for (int q = 0; q < CQ; ++q) bias[q] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (p.bias != nullptr) {
+    if (bias_p != nullptr) {
       const uint32_t ba = lds0 + NS * STAGE + bpar * 1024 + (wn + hl * CW) * 4;
       static_for<CQ>([&](auto q) { ds_read_b128<(int)q * 16>(bias[q], ba); });
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1093,7 +1099,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
       __builtin_amdgcn_s_barrier();
 #endif
       phase1(kt + 1 < nk, lds0 + ((g + 1) % NS) * STAGE);
-      if (ti == 0 && kt + 1 < nk) GEMM_STAMP(34 + kt);
+      if (ti == 0 && kt + 1 < nk && 34 + kt < 61) GEMM_STAMP(34 + kt);  // (slots 61-63: HW_ID, realtime)
     }
     GEMM_STAMP(4 + ti * 4);
     // (CLIPGPU_GEMM_EPI_DMA_WAIT, default on) retire this wave's LDS-DMA of the next step(s) before

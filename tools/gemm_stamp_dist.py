@@ -3,7 +3,8 @@
 
     python tools/gemm_stamp_dist.py M N K epi act tile [iters]
 
-The stamp build records per block (wave 0): s_memrealtime at start / end (slots 62 / 63, one
+K <= 27 * 64 + 64 only (the K-step stamps of longer K reach slots 61-63 in builds before the
+guard).  The stamp build records per block (wave 0): s_memrealtime at start / end (slots 62 / 63, one
 100 MHz clock for the whole chip), s_memtime phase stamps (slots 0-5: per-XCD clock) and the
 block's XCC_ID / HW_ID (slot 61).  Prints the launch span, the spread of block start times
 (dispatch) and block durations, the durations split by how many blocks shared the block's CU
@@ -58,7 +59,7 @@ for it in range(iters):
         print(f"   blocks on CUs holding {c} of this launch's blocks: {sel.sum():4d}, duration {pct(dur[sel])}, "
               f"start p50 {np.median(start[sel]):.1f}")
     per_x = " ".join(f"x{x}:{np.median(dur[xcc == x]):.1f}/{dur[xcc == x].max():.1f}({(xcc == x).sum()})"
-                     for x in range(8))
+                     for x in range(8) if (xcc == x).any())
     print(f"   per XCD duration p50/max(blocks): {per_x}")
     slow = np.argsort(-end)[:6]
     print("   latest-ending blocks: " + "; ".join(
