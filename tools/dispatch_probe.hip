@@ -88,6 +88,47 @@ int run_args(int blocks, int threads, unsigned long long* d, std::vector<unsigne
   return 0;
 }
 
+// A straight-line preamble of NI 4-byte VALU instructions between two stamps: t1 - t0 is what a
+// cold (first launch) or warm (repeat launch) instruction cache costs for NI * 4 bytes of code.
+#define PRE_16 "v_add_u32_e32 v1, v1, v2\n v_add_u32_e32 v1, v1, v2\n v_add_u32_e32 v1, v1, v2\n v_add_u32_e32 v1, v1, v2\n" \
+               "v_add_u32_e32 v1, v1, v2\n v_add_u32_e32 v1, v1, v2\n v_add_u32_e32 v1, v1, v2\n v_add_u32_e32 v1, v1, v2\n" \
+               "v_add_u32_e32 v1, v1, v2\n v_add_u32_e32 v1, v1, v2\n v_add_u32_e32 v1, v1, v2\n v_add_u32_e32 v1, v1, v2\n" \
+               "v_add_u32_e32 v1, v1, v2\n v_add_u32_e32 v1, v1, v2\n v_add_u32_e32 v1, v1, v2\n v_add_u32_e32 v1, v1, v2\n"
+#define PRE_128 PRE_16 PRE_16 PRE_16 PRE_16 PRE_16 PRE_16 PRE_16 PRE_16
+template <int REPS128>
+__global__ void probe_pre(unsigned long long* out) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int r = 0; r < REPS128; ++r) asm volatile(PRE_128 ::: "v1", "v2");
+  unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if (threadIdx.x == 0) {
+    out[2 * blockIdx.x] = t0;
+    out[2 * blockIdx.x + 1] = t1;
+  }
+  while (__builtin_amdgcn_s_memrealtime() - t0 < HOLD_TICKS) __builtin_amdgcn_s_sleep(8);
+}
+
+template <int REPS128>
+int run_pre(int blocks, int threads, unsigned long long* d, std::vector<unsigned long long>& h) {
+  for (int rep = 0; rep < 3; ++rep) {
+    CK(hipMemset(d, 0, blocks * 16));
+    CK(hipDeviceSynchronize());
+    hipLaunchKernelGGL(probe_pre<REPS128>, dim3(blocks), dim3(threads), 0, nullptr, d);
+    CK(hipGetLastError());
+    CK(hipDeviceSynchronize());
+    CK(hipMemcpy(h.data(), d, blocks * 16, hipMemcpyDeviceToHost));
+    std::vector<double> dl(blocks);
+    for (int i = 0; i < blocks; ++i) dl[i] = (double)(h[2 * i + 1] - h[2 * i]) / 100.0;
+    std::sort(dl.begin(), dl.end());
+    printf("preamble of %4d VALU instrs (%5d B), %4d x %4d thr, launch %d (%s): t1 - t0 p50 %.2f max %.2f us\n",
+           REPS128 * 128, REPS128 * 512, blocks, threads, rep, rep == 0 ? "cold" : "repeat", dl[blocks / 2],
+           dl[blocks - 1]);
+  }
+  return 0;
+}
+
 template <int VG>
 int run(const char* name, int blocks, int threads, int lds, unsigned long long* d, std::vector<unsigned long long>& h) {
   if (lds > 65536) CK(hipFuncSetAttribute((const void*)probe<VG>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
@@ -124,5 +165,9 @@ int main() {
   rc |= run<0>("3072 x 256, 18 KiB LDS (attention)", 3072, 256, 18432, d, h);
   rc |= run_args(480, 512, d, h);
   rc |= run_args(256, 512, d, h);
+  rc |= run_pre<1>(480, 512, d, h);
+  rc |= run_pre<4>(480, 512, d, h);
+  rc |= run_pre<8>(480, 512, d, h);
+  rc |= run_pre<16>(480, 512, d, h);
   return rc;
 }
