@@ -746,18 +746,20 @@ PoolSrc trunk(const clipgpu_engine& e, const Replica& r, int B, int causal, cons
 // bits (every tile computes the same K-ordered sums, test_gemm_tile_choice_is_bit_exact).
 //   qkv / c_fc (N = 3D / MLP wide, K = D): 256x256 with the half-tile last round (tile 18, which
 //     falls back to plain 256x256 RS where the half round does not apply);
-//   out_proj / c_proj (N = D, + residual): 160x128 8-wave RS (tile 17), two blocks per CU;
+//   out_proj / c_proj (N = D, + residual): 160x128 8-wave RS (tile 17), two blocks per CU; except
+//     the wide, K-long c_proj of ViT-H/14 (N >= 1280, K >= 5120): 192x256 8-wave (tile 13), 681-685
+//     vs 725-740 us at 46720 x 1280 x 5120 in two interleaved A/B sessions
+//     (profiles/r03_v2_gemm_ab_pp.txt, r03_v7_tile_256x128_half_ab.txt); at every other N = D shape
+//     of the BASELINE models tile 17 is the fastest or within 1 %;
 //   rows < 2048 (small max_batch): the shape heuristic (TILE_AUTO; skinny kernel <= 256 rows).
 // One lane: the full-batch GEMMs quantize better over 256 CUs than two half-batch lanes (the
 // tuner's lane choice at the BASELINE batches).
 int table_tile(int site, int rows, int N, int K) {
-  (void)N;
-  (void)K;
   if (rows < 2048) return TILE_AUTO;
   switch (site) {
     case GS_QKV: return TILE_256x256_HALF;
     case GS_FC: return TILE_256x256_HALF;
-    default: return TILE_160x128_W8_RS;
+    default: return N >= 1280 && K >= 5120 ? TILE_192x256_W8 : TILE_160x128_W8_RS;
   }
 }
 
