@@ -51,8 +51,10 @@ for s in $STEPS; do
             python3 bench.py --steps 3 --warmup 1 --no-text --no-cpu-baseline --no-fp8 --no-e2e || exit $?
       done
       ROWS=$(python3 -c "import json;print([json.loads(l) for l in open('gpurun_out/bench.log') if l.startswith('{')][-1]['roofline']['rows_per_launch'])") || exit 1
+      cp profiles/pmc_c_fc.json gpurun_out/pmc_c_fc.json  # merged into (copy back to profiles/ after the call)
       python3 tools/pmc_traffic.py gpurun_out/pmc_bench/FETCH_SIZE gpurun_out/pmc_bench/WRITE_SIZE \
-          gpurun_out/pmc_c_fc.json $ROWS "${PMC_LABEL:-this run}: --pmc FETCH_SIZE and --pmc WRITE_SIZE passes of bench.py --no-text, tiles $CLIPGPU_GEMM_TILES" || exit $?
+          gpurun_out/pmc_c_fc.json $ROWS "${PMC_LABEL:-this run}: --pmc FETCH_SIZE and --pmc WRITE_SIZE passes of bench.py --no-text, tiles $CLIPGPU_GEMM_TILES" \
+          "$CLIPGPU_GEMM_TILES" || exit $?
       unset CLIPGPU_GEMM_TILES CLIPGPU_LANES ;;
   esac
 done
