@@ -281,6 +281,30 @@ def test_attention(dtype, B, N, H, causal):
 
 
 @pytest.mark.parametrize("dtype", [BF16, F16])
+@pytest.mark.parametrize("B,N,H,causal", [(300, 50, 12, 0), (700, 77, 8, 1), (1500, 9, 3, 1)])
+def test_attention_large_batch(dtype, B, N, H, causal):
+    """Bench-sized short-sequence launches (thousands of (sequence, head) workgroups, several
+    rounds over the CUs): checked against the float64 reference, and bit for bit against calls on
+    3-sequence slices at the start, middle and end of the batch (a sequence's result must not
+    depend on the batch around it; profiles/r03_v11_attn_persistent_ab.txt ran this test against
+    a persistent prefetching variant of the kernel as well)."""
+    L = _lib()
+    rng = np.random.default_rng(B + N)
+    D = H * 64
+    qkv = round16(rng.standard_normal((B * N, 3 * D)) * 1.5, dtype)
+    out = np.empty((B * N, D), np.float32)
+    L.check(L.lib().clipgpu_test_attention(dtype, B, N, H, 64, causal, qkv.ctypes.data, out.ctypes.data))
+    ref = ref_attention(qkv, B, N, H, causal)
+    tol = (2 ** -7 if dtype == BF16 else 2 ** -10) * np.abs(qkv).max()
+    assert np.abs(out - ref).max() < tol
+    for s0 in (0, B // 2, B - 3):
+        sub = np.ascontiguousarray(qkv[s0 * N:(s0 + 3) * N])
+        o3 = np.empty((3 * N, D), np.float32)
+        L.check(L.lib().clipgpu_test_attention(dtype, 3, N, H, 64, causal, sub.ctypes.data, o3.ctypes.data))
+        assert np.array_equal(o3, out[s0 * N:(s0 + 3) * N]), s0
+
+
+@pytest.mark.parametrize("dtype", [BF16, F16])
 @pytest.mark.parametrize("B,N,H,HD,causal", [(2, 300, 2, 64, 0), (2, 300, 2, 64, 1), (2, 577, 2, 72, 0),
                                              (2, 730, 2, 80, 0), (3, 130, 3, 80, 1), (2, 64, 1, 72, 0),
                                              (1, 1025, 1, 64, 1)])
