@@ -17,6 +17,7 @@ import os
 import statistics
 import sys
 import tempfile
+import time
 
 import torch  # noqa: F401  (one HIP runtime per process: torch before the native lib)
 
@@ -78,15 +79,16 @@ def main():
             for _ in range(3):
                 fwd(e)
         torch.cuda.synchronize()
-        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        # wall clock around a device-wide synchronize: a multi-lane engine forks its lanes onto
+        # its own streams, so events recorded on the caller's stream do not bracket the work
         for _ in range(args.rounds):
             for k, e in engines:
-                ev0.record(s)
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
                 for _ in range(5):
                     fwd(e)
-                ev1.record(s)
-                ev1.synchronize()
-                times[k].append(ev0.elapsed_time(ev1) / 5)
+                torch.cuda.synchronize()
+                times[k].append((time.perf_counter() - t0) * 1e3 / 5)
         for k, e in engines:
             tiles, lanes, _ = e.info()
             med = statistics.median(times[k])
