@@ -409,6 +409,9 @@ def main():
                 "ms_per_step": round(tdt * 1e3 / tsteps, 3),
                 "mfma_tflops": round(text_flops(B_TEXT, executed=True) * world * tsteps / tdt / 1e12 / world, 1)}
         text["frac_of_peak"] = round(text["mfma_tflops"] / PEAK_BF16_TFLOPS, 4)
+        t_lanes = ctypes.c_int()
+        _lib.check(_lib.lib().clipgpu_test_engine_lanes(te._h, ctypes.byref(t_lanes)))
+        text["lanes"] = t_lanes.value
         tout_host = tout.cpu().numpy()
         if world == 1 and not args.no_e2e:
             text_e2e = host_leg(te, "tokens", ids.cpu().numpy(), max(3, args.steps // 4))

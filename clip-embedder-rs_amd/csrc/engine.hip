@@ -752,8 +752,8 @@ PoolSrc trunk(const clipgpu_engine& e, const Replica& r, int B, int causal, cons
 //     (profiles/r03_v2_gemm_ab_pp.txt, r03_v7_tile_256x128_half_ab.txt); at every other N = D shape
 //     of the BASELINE models tile 17 is the fastest or within 1 %;
 //   rows < 2048 (small max_batch): the shape heuristic (TILE_AUTO; skinny kernel <= 256 rows).
-// One lane: the full-batch GEMMs quantize better over 256 CUs than two half-batch lanes (the
-// tuner's lane choice at the BASELINE batches).
+// One lane for vision: the full-batch GEMMs quantize better over 256 CUs than two half-batch lanes
+// (the tuner's lane choice at the BASELINE vision batches); large text batches: table_lanes below.
 int table_tile(int site, int rows, int N, int K) {
   if (rows < 2048) return TILE_AUTO;
   switch (site) {
@@ -763,8 +763,17 @@ int table_tile(int site, int rows, int N, int K) {
   }
 }
 
+// Device lanes of the committed table.  One lane, except a large-batch text tower (>= 32768 token
+// rows: configs[2]'s 1024 x 77), which takes two: its LayerNorms and causal attention are a larger
+// share of the layer than in the vision trunk (0.7 + 0.7 ms of 9.3 ms at one lane) and overlap the
+// other lane's GEMMs, while 39424-row lanes still fill the 256x256 / 160x128 rounds (round 2's
+// two-lane text leg: 117k seq/s; round 3's one-lane table: 110k; profiles/r03_v12_text_lanes_ab.txt).
+int table_lanes(const clipgpu_engine& e) {
+  return e.spec.tower == TOWER_TEXT && (long)e.max_batch * e.spec.tokens() >= 32768 ? 2 : 1;
+}
+
 void table_tiles(clipgpu_engine& e) {
-  if (!e.lanes_pinned) e.dev_lanes = 1;
+  if (!e.lanes_pinned) e.dev_lanes = table_lanes(e);
   const int rows = (e.max_batch + e.dev_lanes - 1) / e.dev_lanes * e.spec.tokens();
   e.tuned_rows = rows;
   const int D = e.spec.width, MLP = mlp_pad(e.spec);
@@ -1857,7 +1866,7 @@ int clipgpu_embed_pixels_device(clipgpu_engine* e, const float* d_nchw, int64_t 
     std::lock_guard<std::mutex> lk(e->mu);  // one enqueue per handle at a time (graph cache, workspace)
     Replica& r = e->reps[0];
     HIP_CHECK(hipSetDevice(r.device));
-    run_graph(*e, r, {1, (uint64_t)d_nchw, (uint64_t)d_out, (uint64_t)B}, stream ? (hipStream_t)stream : r.stream,
+    run_graph(*e, r, {1, (uint64_t)d_nchw, (uint64_t)d_out, (uint64_t)B}, (hipStream_t)stream,
               [&](hipStream_t gs) { vision_forward_lanes(*e, r, d_nchw, A_IMG_F32, nullptr, nullptr, (int)B, d_out, gs); });
   });
 }
@@ -1875,7 +1884,7 @@ int clipgpu_embed_u8_device(clipgpu_engine* e, const uint8_t* d_nhwc, int64_t B,
     run_graph(*e, r,
               {2, (uint64_t)d_nhwc, (uint64_t)d_out, (uint64_t)B, fbits(mean, 0), fbits(mean, 1), fbits(mean, 2),
                fbits(stdv, 0), fbits(stdv, 1), fbits(stdv, 2)},
-              stream ? (hipStream_t)stream : r.stream,
+              (hipStream_t)stream,
               [&](hipStream_t gs) { vision_forward_lanes(*e, r, d_nhwc, A_IMG_U8, mean, stdv, (int)B, d_out, gs); });
   });
 }
@@ -1947,7 +1956,7 @@ int clipgpu_embed_tokens_device(clipgpu_engine* e, const int64_t* d_ids, int64_t
     std::lock_guard<std::mutex> lk(e->mu);  // one enqueue per handle at a time (graph cache, workspace)
     Replica& r = e->reps[0];
     HIP_CHECK(hipSetDevice(r.device));
-    run_graph(*e, r, {3, (uint64_t)d_ids, (uint64_t)d_out, (uint64_t)B}, stream ? (hipStream_t)stream : r.stream,
+    run_graph(*e, r, {3, (uint64_t)d_ids, (uint64_t)d_out, (uint64_t)B}, (hipStream_t)stream,
               [&](hipStream_t gs) { text_forward_lanes(*e, r, d_ids, (int)B, d_out, gs); });
   });
 }

@@ -123,9 +123,12 @@ int clipgpu_embed_tokens(clipgpu_engine* e, const int64_t* ids, const int64_t* m
                          float* out);
 
 /* ---- device-resident entry points (benchmarks, zero-copy pipelines) ----------------------
- * Inputs/outputs are device pointers on the handle's first device; work is enqueued on
- * `stream` (a hipStream_t; NULL = the handle's own stream) and the call returns without
- * synchronising.  B <= max_batch. */
+ * Inputs/outputs are device pointers on the handle's first device; work is ordered on
+ * `stream` (a hipStream_t; NULL = the legacy default stream, as in HIP's own APIs, which is
+ * also torch's default stream) and the call returns without synchronising: work enqueued on
+ * `stream` before the call is complete before the forward reads its input, and work enqueued
+ * after it sees the finished embeddings.  The forward itself runs as a hipGraph on the
+ * handle's stream, forked from and joined back to `stream` by events.  B <= max_batch. */
 int clipgpu_embed_pixels_device(clipgpu_engine* e, const float* d_nchw, int64_t B, float* d_out, void* stream);
 int clipgpu_embed_u8_device(clipgpu_engine* e, const uint8_t* d_nhwc, int64_t B, const float mean[3],
                             const float std[3], float* d_out, void* stream);

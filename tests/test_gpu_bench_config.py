@@ -2,10 +2,11 @@
 
 `bench.py`'s headline (BASELINE.json configs[1]) and its text leg (configs[2]) run engines
 built exactly as the bench builds them: the bench's own model folder and seeded inputs,
-max_batch 256 / 1024, the committed tile table (engine.hip table_tiles: one lane, 256x256
-half-tile qkv / c_fc, 160x128 8-wave RS out_proj / c_proj), the hipGraph-replayed device entry
-point on the caller's stream.  Sampled rows spread over the batch: the first and last rows, the
-rows around the 128 / 512 midpoints (where a two-lane split would cut) and rows whose tokens
+max_batch 256 / 1024, the committed tile table (engine.hip table_tiles: 256x256 half-tile qkv /
+c_fc, 160x128 8-wave RS out_proj / c_proj; one lane for vision, two lanes for the 1024-sequence
+text batch), the hipGraph-replayed device entry point on the caller's stream.  Sampled rows
+spread over the batch: the first and last rows, the rows around the 128 / 512 midpoints (where
+the text batch's two lanes cut, and a two-lane vision split would) and rows whose tokens
 straddle GEMM row-tile boundaries; every row of the batch is checked for unit norm, and a second
 replay must give the same bits.  Tolerance: cosine >= 0.9999 per row (north_star,
 tests/helpers.py).
@@ -98,3 +99,38 @@ def test_bench_text_config_matches_oracle(bench_mod, monkeypatch):
     host = te.embed_tokens(ids[:64].cpu().numpy())
     assert np.array_equal(host, got[:64])
     te.close()
+
+
+@pytest.mark.parametrize("tower", ["vision", "text"])
+@pytest.mark.parametrize("which", ["default", "side"])
+def test_device_entry_is_ordered_on_the_callers_stream(bench_mod, tower, which, monkeypatch):
+    """include/clipgpu.h: the *_device entry points are stream-ordered on the caller's stream.
+    The output is filled with NaN, the forward is enqueued, and a copy of the output is enqueued
+    right behind it on the same stream with no synchronization in between: the copy must see the
+    finished embeddings -- for torch's default (legacy null) stream and for a created stream, at
+    the bench's batch (milliseconds of work, so a missing join would be caught)."""
+    import torch
+    from open_clip_inference import _lib
+    from open_clip_inference.engine import Engine
+    for var in ("CLIPGPU_LANES", "CLIPGPU_GEMM_TILES", "CLIPGPU_GEMM_AUTOTUNE", "CLIPGPU_GRAPHS"):
+        monkeypatch.delenv(var, raising=False)
+    dev = torch.device("cuda", 0)
+    px, ids = bench_mod.synth_inputs(0, dev)
+    B = bench_mod.B_VISION if tower == "vision" else bench_mod.B_TEXT
+    e = Engine(bench_mod.make_model_dir(), _lib.TOWER_VISION if tower == "vision" else _lib.TOWER_TEXT,
+               [0], "bf16", B)
+    s = torch.cuda.current_stream(dev) if which == "default" else torch.cuda.Stream(dev)
+    out = torch.empty((B, 512), device=dev, dtype=torch.float32)
+    with torch.cuda.stream(s):
+        for rep in range(3):  # capture, then replays of the graph
+            out.fill_(float("nan"))
+            if tower == "vision":
+                e.embed_pixels_device(px.data_ptr(), B, out.data_ptr(), s.cuda_stream)
+            else:
+                e.embed_tokens_device(ids.data_ptr(), B, out.data_ptr(), s.cuda_stream)
+            snap = out.clone()
+            s.synchronize()
+            got = snap.cpu().numpy()
+            assert not np.isnan(got).any(), (tower, which, rep)
+            assert np.all(np.abs(np.linalg.norm(got, axis=1) - 1) < 1e-5)
+    e.close()
