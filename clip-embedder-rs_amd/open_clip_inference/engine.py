@@ -137,7 +137,8 @@ class Engine:
                                          x.shape[0], x.shape[1], out.ctypes.data))
         return out
 
-    # Device-resident variants: raw device pointers (ints), stream = hipStream_t or 0.
+    # Device-resident variants: raw device pointers (ints), stream = hipStream_t or 0 (the legacy
+    # default stream, torch's default: the forward is ordered on it, include/clipgpu.h).
     def embed_pixels_device(self, d_in: int, B: int, d_out: int, stream: int = 0) -> None:
         check(lib().clipgpu_embed_pixels_device(self.handle, c_void_p(d_in), B, c_void_p(d_out),
                                                 c_void_p(stream or None)))
