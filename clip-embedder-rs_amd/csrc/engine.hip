@@ -742,7 +742,7 @@ PoolSrc trunk(const clipgpu_engine& e, const Replica& r, int B, int causal, cons
 // a function of its GEMM shape at the rows one lane runs at max_batch, so an engine's kernels --
 // and the profiles and PMC records taken of them -- are the same on every box and every run.  The
 // entries are the timing tuner's (below) majority choice over repeated runs on MI355X
-// (tools/tile_table.py, profiles/r03_tile_table.jsonl); the tile choice never changes the output
+// (tools/tile_table.py, profiles/r03_v13_tile_table.jsonl); the tile choice never changes the output
 // bits (every tile computes the same K-ordered sums, test_gemm_tile_choice_is_bit_exact).
 //   qkv / c_fc (N = 3D / MLP wide, K = D): 256x256 with the half-tile last round (tile 18, which
 //     falls back to plain 256x256 RS where the half round does not apply);
