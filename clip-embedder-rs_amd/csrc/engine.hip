@@ -780,6 +780,10 @@ void table_tiles(clipgpu_engine& e) {
   const int shape[GS_N][2] = {{3 * D, D}, {D, D}, {MLP, D}, {D, MLP}};
   for (int site = 0; site < GS_N; ++site)
     e.tile[site] = e.mx_site[site] ? MX_TILE_AUTO : table_tile(site, rows, shape[site][0], shape[site][1]);
+  // Large text batches: c_proj (N = 512, K = 2048) on the 4-wave 160x128 RS tile, two blocks per CU
+  // beside the other lane's work: 113.2-113.7k -> 116.6-116.8k seq/s in a same-box A/B against
+  // the 8-wave tile 17 (profiles/r03_v13_text_tiles_ab.txt; the tuner's pick was 15 as well)
+  if (e.spec.tower == TOWER_TEXT && rows >= 16384 && !e.mx_site[GS_PROJ]) e.tile[GS_PROJ] = TILE_160x128_RS;
   // the patch-embedding GEMM has the c_proj shape class (N = D, K = 3 P^2 padded)
   const int G = e.spec.grid();
   const int prow = e.spec.tower == TOWER_VISION ? rows / e.spec.tokens() * G * G : 0;

@@ -324,3 +324,14 @@ def test_tile_table_is_deterministic_and_bit_invisible(monkeypatch):
     assert np.array_equal(a.embed_pixels(x), t.embed_pixels(x))
     small = Engine(d, 0, [0], "bf16", 8)  # rows < 2048: the shape heuristic
     assert small.info()[0] == [0, 0, 0, 0]
+    # the text tower at the bench's 1024 x 77 batch: two lanes, c_proj on the 4-wave 160x128 RS
+    # tile (table_lanes / table_tiles); same bits as a small engine on the heuristic tiles
+    ta = Engine(d, 1, [0], "bf16", 1024)
+    tb = Engine(d, 1, [0], "bf16", 1024)
+    assert ta.info() == tb.info() == ([18, 17, 18, 15], 2, [])
+    ts = Engine(d, 1, [0], "bf16", 8)
+    rng = np.random.default_rng(5)
+    ids = rng.integers(1, 49406, size=(8, 77)).astype(np.int64)
+    ids[:, 0] = 49406
+    ids[np.arange(8), rng.integers(5, 77, size=8)] = 49407
+    assert np.array_equal(ta.embed_tokens(ids), ts.embed_tokens(ids))
