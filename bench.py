@@ -51,8 +51,8 @@ MODEL_CONFIG = {"logit_scale": 100.0, "logit_bias": 0.0, "activation_function": 
 
 # Algorithmic work per unit: 2 x MAC over all matmuls.
 # The engine prunes the last layer to the pooled token after attention (engine.hip trunk,
-# CLIPGPU_PRUNE_LAST, bit-identical embeddings): `executed` counts the MFMA work that runs.
-PRUNE_LAST = os.environ.get("CLIPGPU_PRUNE_LAST", "1") != "0"
+# clipgpu_options.prune_last, bit-identical embeddings): `executed` counts the MFMA work that runs.
+PRUNE_LAST = True  # the engine default (clipgpu_options.prune_last)
 
 
 def vit_flops(B, executed=False):
@@ -71,12 +71,9 @@ def text_flops(B, T=77, executed=False):
     return L * (2 * B * T * (3 * D * D + D * D + 2 * D * M) + 2 * 2 * B * T * T * D) + 2 * B * D * E - pruned
 
 
-# GemmTile ids (csrc/kernels/kernels.hpp)
-TILE_NAMES = {0: "heuristic", 1: "128x128", 2: "256x128", 3: "256x256", 4: "128x128pipe", 5: "128x64pipe",
-              6: "64x128pipe", 7: "160x128pipe", 8: "160x64pipe", 9: "160x128w8", 10: "128x128w8",
-              11: "192x128w8", 12: "160x256w8", 13: "192x256w8", 14: "256x256rs", 15: "160x128rs", 16: "128x64rs",
-              17: "160x128w8rs", 18: "256x256half", 19: "256x256pp", 20: "192x256pp",
-              21: "256x256m32", 22: "192x256m32", 23: "256x192m32", 24: "128x128w8m32", 25: "256x128m32"}
+# GemmTile ids the library builds (csrc/kernels/kernels.hpp kGemmTiles)
+TILE_NAMES = {0: "heuristic", 1: "128x128", 2: "256x128", 3: "256x256", 13: "192x256w8", 14: "256x256rs",
+              15: "160x128rs", 17: "160x128w8rs", 18: "256x256half", 26: "224x192w8", 28: "256x192w8"}
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md chip table)
 B_VISION = 256
 B_TEXT = 1024
@@ -217,6 +214,71 @@ def load_traffic(rows_per_launch, tiles):
     return None, None
 
 
+def measure_windows(step, engine, n, steps, dt_first, dev):
+    """Repeated windows after the timed one (N = 1), so a few-% change can be told from box-to-box
+    and run-to-run spread: each window is `steps` forward steps timed like `value`, with a one-wave
+    clock probe (clipgpu_test_clock_probe: s_memtime ticks over s_memrealtime's 100 MHz, sleeping,
+    on a side stream, for 60 % of the first window's wall time) running beside it, which reads the
+    shader clock the chip holds under the forward's load (MI355X_MICROARCH.md, DVFS give-back);
+    then as many profiled windows give the mean c_fc launch time (HIP events at the kernel
+    boundaries, lanes serialized, no graphs), each with its own clock probe."""
+    import statistics
+    L = _lib.lib()
+    side = torch.cuda.Stream(dev)
+    probe = torch.zeros(2, dtype=torch.int64, device=dev)
+    probe_us = max(1000, int(0.6 * dt_first * 1e6))
+
+    def clocked(fn, with_probe=True):
+        torch.cuda.synchronize()
+        if with_probe:
+            _lib.check(L.clipgpu_test_clock_probe(ctypes.c_void_p(side.cuda_stream), probe_us,
+                                                  ctypes.c_void_p(probe.data_ptr())))
+        t0 = time.perf_counter()
+        out = fn()
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - t0
+        if not with_probe:
+            return wall, None, out
+        t = probe.cpu().tolist()
+        return wall, (100.0 * t[0] / t[1] if t[1] > 0 else None), out
+
+    def run_steps():
+        for _ in range(steps):
+            step()
+
+    rates, rates_probe, clocks = [], [], []
+    for _ in range(n):  # alternating: a plain window, then one with the probe beside it
+        wall, _, _ = clocked(run_steps, with_probe=False)
+        rates.append(B_VISION * steps / wall)
+        wall, mhz, _ = clocked(run_steps)
+        rates_probe.append(B_VISION * steps / wall)
+        clocks.append(mhz)
+    fc_us, fc_clk = [], []
+    for _ in range(max(1, min(n, 3))):
+        profile_enable(engine, ["c_fc"])
+
+        def prof_steps():
+            run_steps()
+            return profile_read(engine, "c_fc")
+        _, mhz, (ms, cnt) = clocked(prof_steps)
+        profile_enable(engine, [])
+        fc_us.append(1e3 * ms / max(cnt, 1))
+        fc_clk.append(mhz)
+    good = [c for c in clocks if c]
+    return {"n": n, "steps": steps,
+            "images_s": [round(r, 1) for r in rates],
+            "min": round(min(rates), 1), "median": round(statistics.median(rates), 1), "max": round(max(rates), 1),
+            "sclk_mhz": [round(c, 1) if c else None for c in clocks],
+            "sclk_mhz_median": round(statistics.median(good), 1) if good else None,
+            "images_s_probed": [round(r, 1) for r in rates_probe],
+            "images_s_per_ghz_median": round(statistics.median(r / (c / 1e3) for r, c in zip(rates_probe, clocks) if c), 1)
+            if good else None,
+            "c_fc_us": [round(u, 2) for u in fc_us], "c_fc_sclk_mhz": [round(c, 1) if c else None for c in fc_clk],
+            "note": "windows after the timed one (same steps each), alternating plain (images_s) and clock-probed "
+                    "(images_s_probed: a one-wave s_memtime / s_memrealtime probe on a side stream, sclk_mhz); c_fc "
+                    "from profiled windows (lanes serialized)"}
+
+
 def host_leg(engine, kind, host, steps):
     """Host-buffer throughput through the C ABI (pinned staging + H2D + forward + D2H, PCIe
     included), units per second over `steps` calls after one warm call."""
@@ -245,6 +307,13 @@ def main():
     ap.add_argument("--no-fp8", action="store_true", help="skip the fp8 side measurement")
     ap.add_argument("--breakdown", action="store_true", help="per-kernel-class ms per step (serialized lanes)")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-buffer (PCIe-inclusive) legs")
+    ap.add_argument("--tiles", default="",
+                    help="vision engine: pin the GEMM tiles q,o,f,p (clipgpu_options.gemm_tiles; PMC passes and "
+                         "A/B runs pin the un-profiled bench's tiles); the patch GEMM takes p's")
+    ap.add_argument("--lanes", type=int, default=0, help="vision engine: pin the device lanes (0 = the table's)")
+    ap.add_argument("--windows", type=int, default=5,
+                    help="N = 1: repeated K-step windows after the timed one (min / median / max images/s, the "
+                         "shader clock of each window, and the c_fc launch time per window); 0 skips them")
     ap.add_argument("--gather", action="store_true",
                     help="N = 1: run the data-parallel path anyway (gloo control plane, the engine's RCCL "
                          "communicator, gathered entry points) -- a one-GPU rehearsal of N > 1")
@@ -270,7 +339,11 @@ def main():
     dev = torch.device("cuda", local)
 
     mdir = make_model_dir()
-    ve = Engine(mdir, _lib.TOWER_VISION, [local], args.dtype, B_VISION)
+    vopts = {"lanes": args.lanes}
+    if args.tiles:
+        pins = [int(t) for t in args.tiles.split(",")]
+        vopts.update(gemm_tiles=pins, patch_tile=pins[3])
+    ve = Engine(mdir, _lib.TOWER_VISION, [local], args.dtype, B_VISION, **vopts)
     if dp:
         init_engine_comm(ve)
     px, ids = synth_inputs(rank, dev)
@@ -329,6 +402,9 @@ def main():
     # Profiling runs the engine's two lanes (half-batch sub-forwards) one after the other
     # instead of concurrently, so it is kept out of the timed loop; launch shapes are the same.
     _, (fc_ms, fc_n) = timed(vision_step, max(3, args.steps // 2), 1, ve, "c_fc")
+    windows = None
+    if world == 1 and args.windows > 0:
+        windows = measure_windows(vision_step, ve, args.windows, args.steps, dt, dev)
 
     # roofline of the dominant kernel: c_fc GEMM (+QuickGELU epilogue), M=rows per launch,
     # N=3072, K=768; fc_n counts the full-row launches (12 layers, or 11 when the last one
@@ -467,6 +543,8 @@ def main():
             "whole_forward_mfma_tflops_per_gpu": round(whole_tflops, 1),
             "whole_forward_frac_of_peak": round(whole_tflops / PEAK_BF16_TFLOPS, 4),
             "last_layer_pruned": PRUNE_LAST,
+            "windows": windows,
+            "sclk_mhz": windows["sclk_mhz_median"] if windows else None,
             **({"breakdown_serialized": breakdown} if breakdown is not None else {}),
             "text": text,
             "end_to_end": e2e,

@@ -87,7 +87,6 @@ struct Replica {
   char* work = nullptr;   // activations
   DevWeights w;
   float* x = nullptr;     // [rows][D] f32 residual stream
-  float* slab = nullptr;  // [rows][D] f32 split-K partial of out_proj / c_proj (engine.ksplit == 2)
   void* h = nullptr;      // [rows][D] 16-bit (LN output / attention output); fp8 engines: LN output as e4m3
   uint8_t* hs = nullptr;   // fp8 engines: [rows][D/32] scales of the LN output in h
   uint8_t* bigs = nullptr; // fp8 engines: [rows][MLP/32] scales of the c_fc output (e4m3 in big)
@@ -123,6 +122,7 @@ struct Replica {
   // the embedding rows over xGMI): ncclCommInitAll over a multi-device handle's devices, or
   // ncclCommInitRank for one-process-per-GPU deployments (clipgpu_comm_init_rank).
   ncclComm_t comm = nullptr;
+  hipEvent_t coll = nullptr;  // recorded behind this replica's last collective (destroy_comms waits for it)
 };
 
 // Replayable forwards: one hipGraphExec per (entry point, input / output buffers, batch,
@@ -178,43 +178,31 @@ struct clipgpu_engine {
   // GEMM tile per trunk call site (clipgpu::GemmSite), autotuned at creation for
   // max_batch rows; batches under half of that use the shape heuristic.
   int tile[4] = {0, 0, 0, 0};
+  int mxtile[4] = {0, 0, 0, 0};  // fp8 engines: MxTile of the MX sites (tile[] then holds the 16-bit tile
+                                 // the site runs on layers outside mx_layers)
   int tile_patch = 0;  // vision: the patch-embedding GEMM (tuned with the trunk sites)
   int tuned_rows = 0;
-  int lanes = 1;  // lane streams / host-path slots per device (CLIPGPU_LANES, default 2)
-  // Concurrent sub-batches of a device-side forward: `lanes`, or 1 when the creation-time tuning
-  // measures the whole batch on one stream faster (full-batch GEMMs quantize better over the CUs
-  // than two half-batch ones; the lanes overlap LayerNorm / attention with GEMMs).  CLIPGPU_LANES
-  // pins it.
+  int lanes = 1;  // lane streams / host-path slots per device (clipgpu_options.lanes, default 2)
+  // Concurrent sub-batches of a device-side forward: the tile table's choice, or `lanes` when
+  // clipgpu_options.lanes pins it (full-batch GEMMs quantize better over the CUs than two
+  // half-batch ones; the lanes overlap LayerNorm / attention with GEMMs).
   int dev_lanes = 1;
   bool lanes_pinned = false;
-  bool graphs = true;  // replay forwards as hipGraphs (CLIPGPU_GRAPHS=0 disables)
-  bool prune = true;   // last layer on the pooled rows only (CLIPGPU_PRUNE_LAST=0 disables; see trunk)
-  bool trim = true;    // host-ids text batches run on their first max(EOT)+1 tokens (CLIPGPU_TRIM_TEXT=0)
-  // K-slices of the N = width GEMMs (out_proj, c_proj): CLIPGPU_GEMM_SPLIT=1 -> 2, else 1.
-  // Fixed per engine, independent of the batch and lane split, so outputs stay
-  // bit-identical across both; the second slice's partial is added by the next LayerNorm.
-  // Off by default: measured slower at ViT-B/32 lane sizes (profiles/r01_v6_split_sweep.txt:
-  // the extra f32 slab round trip costs more than the better CU fill returns).
-  int ksplit = 1;
-  int pipe3 = 0;  // CLIPGPU_GEMM_PIPE3=1: 3-stage LDS schedule for K-long one-round GEMMs (GemmParams::pipe3)
-  // Row-complete residual GEMM + LayerNorm (gemm_rowln.hip) for out_proj -> ln_2 / c_proj ->
-  // next ln_1, decided per engine at creation (bit-identical across batch and lane splits).
-  // Eligible: 16-bit sites without split-K whose following LN feeds a 16-bit GEMM, width
-  // 512/768/1024.  CLIPGPU_FUSE_LN=1 fuses every eligible site; unset / 0: off.  Its LayerNorm
-  // reduces in another order than ln_rows_kernel (last-bit differences in h), so the choice is
-  // explicit, never a timing outcome.  Off by default: at the ViT-B/32 shapes the fused kernel's
-  // 64-row x full-width tiles (one 156 KiB block per CU, K-steps of 32) measure slower than the
-  // tiled GEMM + LayerNorm pair (profiles/r02_rowln.txt).
-  bool fuse_ok_out = false, fuse_ok_proj = false;
-  bool fuse_out = false, fuse_proj = false;
-  int fuse_mode = 0;  // CLIPGPU_FUSE_LN: 0 off, 1 on
-  bool tuning = false;  // clipgpu_options.tuning / CLIPGPU_GEMM_AUTOTUNE=1: timing tuner instead of the table
+  bool graphs = true;  // replay forwards as hipGraphs (clipgpu_options.graphs = -1 disables)
+  bool prune = true;   // last layer on the pooled rows only (clipgpu_options.prune_last = -1 disables; trunk)
+  bool trim = true;    // host-ids text batches run on their first max(EOT)+1 tokens (options.trim_text = -1: off)
+  int tuning = 0;  // clipgpu_options.tuning: 1 = timing tuner (+ whole-forward pass), 2 = per-site pass only
+  // clipgpu_options.gemm_tiles / patch_tile pins (0 = the table's tile, -1 = the shape heuristic)
+  int pin_tiles[4] = {0, 0, 0, 0};
+  int pin_patch = 0;
+  // fp8 engines: layer l runs its MX sites in MX-fp8 iff bit l is set (clipgpu_options.mx_layers; 0 =
+  // every layer); the other layers run bf16 at every site
+  uint64_t mx_layers = ~0ull;
   // Multi-device handles over distinct devices: the RCCL communicator is created on the first
   // gathered call (comm_pending), or at creation when clipgpu_options.communicator = 1.
   bool comm_pending = false;
   std::vector<int> comm_devs;
   bool force_bcast = false;  // test hook: gathered calls take the ragged (broadcast) branch
-  int rowln_pf = 8;  // its L2 prefetch distance in K-steps (CLIPGPU_ROWLN_PF; 0 off)
   clipgpu::TowerSpec spec;
   clipgpu::PreprocessCfg pre;
   clipgpu::DType dt = clipgpu::DT_BF16;
@@ -222,7 +210,7 @@ struct clipgpu_engine {
   // activations, E8M0 block scales, v_mfma_scale_f32_32x32x64_f8f6f4); attention, out_proj,
   // the stems and heads stay bf16.
   bool mx = false;
-  // The MX sites of an fp8 engine (CLIPGPU_MX_SITES, a subset of "qkv,fc,proj"; c_proj in MX
+  // The MX sites of an fp8 engine (clipgpu_options.mx_sites, a subset of qkv / fc / proj; c_proj in MX
   // needs c_fc in MX, whose epilogue quantizes the hidden activations).  Default: all three.
   bool mx_site[4] = {false, false, false, false};  // indexed by GemmSite (GS_OUT stays bf16)
   int max_batch = 0;
@@ -238,6 +226,12 @@ namespace clipgpu {
 namespace {
 
 enum GemmSite { GS_QKV = 0, GS_OUT, GS_FC, GS_PROJ, GS_N };
+
+// fp8 engines: does layer l run `site` as an MX-fp8 GEMM (the engine's MX sites, on the layers of
+// clipgpu_options.mx_layers)?
+inline bool mx_at(const clipgpu_engine& e, int l, int site) {
+  return e.mx_site[site] && l >= 0 && l < 64 && ((e.mx_layers >> l) & 1ull);
+}
 
 inline size_t align256(size_t n) { return (n + 255) & ~size_t(255); }
 inline int round64(int n) { return (n + 63) / 64 * 64; }
@@ -433,11 +427,11 @@ void upload_weights(clipgpu_engine& e, Replica& r, const TensorMap& m) {
     L.ln1_w = f32(p + n_ln1w);
     L.ln1_b = f32(p + n_ln1b);
     L.wqkv = L.w1 = L.w2 = nullptr;
-    if (e.mx_site[GS_QKV]) L.mqkv = wmx_pad(p + n_qkvw, 3 * D, D);
+    if (mx_at(e, l, GS_QKV)) L.mqkv = wmx_pad(p + n_qkvw, 3 * D, D);
     else L.wqkv = w16(p + n_qkvw);
-    if (e.mx_site[GS_FC]) L.m1 = wmx_pad(p + n_fc1w, mlp_pad(s), D);
+    if (mx_at(e, l, GS_FC)) L.m1 = wmx_pad(p + n_fc1w, mlp_pad(s), D);
     else L.w1 = w16_pad(p + n_fc1w, mlp_pad(s), D);
-    if (e.mx_site[GS_PROJ]) L.m2 = wmx_pad(p + n_fc2w, D, mlp_pad(s));
+    if (mx_at(e, l, GS_PROJ)) L.m2 = wmx_pad(p + n_fc2w, D, mlp_pad(s));
     else L.w2 = w16_pad(p + n_fc2w, D, mlp_pad(s));
     L.bqkv = f32(p + n_qkvb);
     L.wo = w16(p + n_ow);
@@ -498,8 +492,7 @@ void alloc_workspace(clipgpu_engine& e, Replica& r) {
   const size_t E = s.embed_dim;
   const size_t MLP = (size_t)mlp_pad(s);
   const size_t sizes[] = {rows * D * 4, rows * D * 2, rows * wide * 2, B * D * 2, B * E * 4, B * E * 4,
-                          B * e.in_bytes_per_row, e.ksplit > 1 ? rows * D * 4 : 0,
-                          e.mx ? rows * D / 32 : 0, e.mx ? rows * MLP / 32 : 0};
+                          B * e.in_bytes_per_row, e.mx ? rows * D / 32 : 0, e.mx ? rows * MLP / 32 : 0};
   size_t total = 0;
   for (size_t z : sizes) total += align256(z);
   HIP_CHECK(hipMalloc(&r.work, total));
@@ -512,9 +505,8 @@ void alloc_workspace(clipgpu_engine& e, Replica& r) {
   r.emb = (float*)a.take(sizes[4]);
   r.out = (float*)a.take(sizes[5]);
   r.in = a.take(sizes[6]);
-  r.slab = e.ksplit > 1 ? (float*)a.take(sizes[7]) : nullptr;
-  r.hs = e.mx ? (uint8_t*)a.take(sizes[8]) : nullptr;
-  r.bigs = e.mx ? (uint8_t*)a.take(sizes[9]) : nullptr;
+  r.hs = e.mx ? (uint8_t*)a.take(sizes[7]) : nullptr;
+  r.bigs = e.mx ? (uint8_t*)a.take(sizes[8]) : nullptr;
   for (int i = 0; i < e.lanes; ++i) {
     HIP_CHECK(hipStreamCreateWithFlags(&r.lane[i], hipStreamNonBlocking));
     HIP_CHECK(hipEventCreateWithFlags(&r.join[i], hipEventDisableTiming));
@@ -583,11 +575,6 @@ GemmParams rows_gemm(const void* A, long lda, const void* W, const float* bias, 
 }
 
 int site_epi(int site) { return (site == GS_OUT || site == GS_PROJ) ? EPI_RESID : EPI_STORE16; }
-inline bool site_split(const clipgpu_engine& e, int site) {
-  if (e.ksplit < 2 || (site != GS_OUT && site != GS_PROJ)) return false;
-  const int K = site == GS_OUT ? e.spec.width : mlp_pad(e.spec);
-  return K % (64 * e.ksplit) == 0 && K / e.ksplit >= 128;  // >= 2 K-steps per slice
-}
 
 GemmParams site_gemm(const clipgpu_engine& e, const Replica& r, const LayerW& L, int site, int rows) {
   const int D = e.spec.width, MLP = mlp_pad(e.spec);
@@ -598,23 +585,18 @@ GemmParams site_gemm(const clipgpu_engine& e, const Replica& r, const LayerW& L,
     case GS_FC: g = rows_gemm(r.h, D, L.w1, L.b1, r.big, MLP, rows, MLP, D); break;
     default: g = rows_gemm(r.big, MLP, L.w2, L.b2, r.x, D, rows, D, MLP); break;
   }
-  if (site_split(e, site)) {
-    g.ksplit = e.ksplit;
-    g.slab = r.slab;
-  }
-  g.pipe3 = e.pipe3;
   return g;
 }
 
 // fp8 engines: the MX-fp8 GEMM of a trunk site (QKV: LN e4m3 -> 16-bit qkv; c_fc: LN e4m3 ->
 // act -> e4m3 hidden in `big` + scales; c_proj: e4m3 hidden -> residual stream).
-// c_fc quantizes its output (EPI_STOREQ) only when c_proj consumes MX; else it stores 16-bit.
-int site_epi_mx(const clipgpu_engine& e, int site) {
-  return site == GS_PROJ ? EPI_RESID : (site == GS_FC && e.mx_site[GS_PROJ] ? EPI_STOREQ : EPI_STORE16);
+// c_fc quantizes its output (EPI_STOREQ) only when the layer's c_proj consumes MX; else it stores 16-bit.
+int site_epi_mx(const clipgpu_engine& e, int l, int site) {
+  return site == GS_PROJ ? EPI_RESID : (site == GS_FC && mx_at(e, l, GS_PROJ) ? EPI_STOREQ : EPI_STORE16);
 }
-// LN output feeding an MX GEMM is written as MX-fp8 (scales in hs), else 16-bit.
-inline uint8_t* ln_q(const clipgpu_engine& e, int consumer_site, uint8_t* hs) {
-  return e.mx_site[consumer_site] ? hs : nullptr;
+// LN output feeding an MX GEMM (layer l's consumer site) is written as MX-fp8 (scales in hs), else 16-bit.
+inline uint8_t* ln_q(const clipgpu_engine& e, int l, int consumer_site, uint8_t* hs) {
+  return mx_at(e, l, consumer_site) ? hs : nullptr;
 }
 
 MxGemmParams site_gemm_mx(const clipgpu_engine& e, const Replica& r, const LayerW& L, int site, int rows) {
@@ -653,8 +635,8 @@ struct PoolSrc {
 // every token's K/V, then the pooled token's residual row and attention output are gathered
 // to a compact [B][D] pair and out_proj .. c_proj run at M = B.  Each kept row goes through
 // the same kernels with the same K-ordered sums, so the embeddings are bit-identical to the
-// full last layer (test_last_layer_pruning_is_bit_exact).  Off with CLIPGPU_PRUNE_LAST=0; not
-// for the SigLIP MAP head (pools every token) or split-K engines (slab rows are per token).
+// full last layer (test_last_layer_pruning_is_bit_exact).  Off with clipgpu_options.prune_last = -1;
+// not for the SigLIP MAP head (pools every token).
 // The compact pair lives in the tail of `big`, past the M = B MLP hidden.
 inline size_t prune_off_x(const TowerSpec& s, int B) { return align256((size_t)B * mlp_pad(s) * 2); }
 inline size_t prune_off_h(const TowerSpec& s, int B) {
@@ -662,7 +644,7 @@ inline size_t prune_off_h(const TowerSpec& s, int B) {
 }
 inline bool prune_last(const clipgpu_engine& e, int B, int T) {
   const TowerSpec& s = e.spec;
-  return e.prune && e.ksplit < 2 && s.family != FAMILY_SIGLIP && s.layers > 0 &&
+  return e.prune && s.family != FAMILY_SIGLIP && s.layers > 0 &&
          prune_off_h(s, B) + (size_t)B * s.width * 2 <= (size_t)B * T * big_wide(s) * 2;
 }
 
@@ -683,10 +665,10 @@ PoolSrc trunk(const clipgpu_engine& e, const Replica& r, int B, int causal, cons
     auto gemm = [&](int site, int cat, const char* what) {
       ProfScope ps(e, rows == B * T ? cat : PC_TAIL, st, /*gemm=*/true);
       const bool tuned = 2 * rows > e.tuned_rows;
-      if (e.mx_site[site]) {
+      if (mx_at(e, l, site)) {
         MxGemmParams g = site_gemm_mx(e, c, L, site, rows);
-        g.tile = tuned ? e.tile[site] : MX_TILE_AUTO;
-        check(launch_gemm_mx(e.dt, site_epi_mx(e, site), site == GS_FC ? s.act : ACT_NONE, g, st), what);
+        g.tile = tuned ? e.mxtile[site] : MX_TILE_AUTO;
+        check(launch_gemm_mx(e.dt, site_epi_mx(e, l, site), site == GS_FC ? s.act : ACT_NONE, g, st), what);
         return;
       }
       GemmParams g = site_gemm(e, c, L, site, rows);
@@ -703,35 +685,17 @@ PoolSrc trunk(const clipgpu_engine& e, const Replica& r, int B, int causal, cons
       ProfScope ps(e, PC_TAIL, st);
       check(launch_gather_pooled(r.x, r.h, ids, T, c.x, c.h, B, D, st), "gather pooled rows");
     }
-    // out_proj + residual + ln_2 (c_proj + residual + the next ln_1) in one kernel when fused
-    auto rowln = [&](const void* A, int K, const void* W, const float* bias, float* x, const float* lw,
-                     const float* lb, void* h, int cat, const char* what) {
-      ProfScope ps(e, rows == B * T ? cat : PC_TAIL, st, /*gemm=*/true);
-      RowLnParams p;
-      p.A = A; p.lda = K; p.W = W; p.ldw = K; p.bias = bias; p.x = x;
-      p.ln_w = lw; p.ln_b = lb; p.eps = s.ln_eps; p.h = h;
-      p.M = rows; p.D = D; p.K = K; p.pf = e.rowln_pf;
-      check(launch_gemm_rowln(e.dt, p, st), what);
-    };
-    if (e.fuse_out) {
-      rowln(c.h, D, L.wo, L.bo, c.x, L.ln2_w, L.ln2_b, c.h, PC_OUT_PROJ, "out_proj + ln_2");
-    } else {
-      gemm(GS_OUT, PC_OUT_PROJ, "out_proj gemm");
+    gemm(GS_OUT, PC_OUT_PROJ, "out_proj gemm");
+    {
       ProfScope ps(e, compact ? PC_TAIL : PC_LN, st);
-      check(launch_ln_rows_add(e.dt, c.x, site_split(e, GS_OUT) ? c.slab : nullptr, L.ln2_w, L.ln2_b, s.ln_eps, c.h,
-                               rows, D, st, ln_q(e, GS_FC, c.hs)), "ln_2");
+      check(launch_ln_rows(e.dt, c.x, L.ln2_w, L.ln2_b, s.ln_eps, c.h, rows, D, st, ln_q(e, l, GS_FC, c.hs)), "ln_2");
     }
     gemm(GS_FC, PC_C_FC, "c_fc gemm");
-    if (e.fuse_proj && l + 1 < s.layers) {
-      const LayerW& N1 = r.w.layers[l + 1];
-      rowln(r.big, mlp_pad(s), L.w2, L.b2, r.x, N1.ln1_w, N1.ln1_b, r.h, PC_C_PROJ, "c_proj + ln_1");
-      continue;
-    }
     gemm(GS_PROJ, PC_C_PROJ, "c_proj gemm");
-    if (l + 1 < s.layers) {  // (the last c_proj's slab is added by the head's first LayerNorm)
+    if (l + 1 < s.layers) {
       ProfScope ps(e, PC_LN, st);
-      check(launch_ln_rows_add(e.dt, r.x, site_split(e, GS_PROJ) ? r.slab : nullptr, r.w.layers[l + 1].ln1_w,
-                               r.w.layers[l + 1].ln1_b, s.ln_eps, r.h, rows, D, st, ln_q(e, GS_QKV, r.hs)), "ln_1");
+      check(launch_ln_rows(e.dt, r.x, r.w.layers[l + 1].ln1_w, r.w.layers[l + 1].ln1_b, s.ln_eps, r.h, rows, D, st,
+                           ln_q(e, l + 1, GS_QKV, r.hs)), "ln_1");
     }
     if (compact) return PoolSrc{c.x, 1, nullptr};
   }
@@ -778,55 +742,47 @@ void table_tiles(clipgpu_engine& e) {
   e.tuned_rows = rows;
   const int D = e.spec.width, MLP = mlp_pad(e.spec);
   const int shape[GS_N][2] = {{3 * D, D}, {D, D}, {MLP, D}, {D, MLP}};
-  for (int site = 0; site < GS_N; ++site)
-    e.tile[site] = e.mx_site[site] ? MX_TILE_AUTO : table_tile(site, rows, shape[site][0], shape[site][1]);
+  for (int site = 0; site < GS_N; ++site) {
+    e.tile[site] = table_tile(site, rows, shape[site][0], shape[site][1]);
+    e.mxtile[site] = MX_TILE_AUTO;
+  }
   // Large text batches: c_proj (N = 512, K = 2048) on the 4-wave 160x128 RS tile, two blocks per CU
   // beside the other lane's work: 113.2-113.7k -> 116.6-116.8k seq/s in a same-box A/B against
   // the 8-wave tile 17 (profiles/r03_v13_text_tiles_ab.txt; the tuner's pick was 15 as well)
-  if (e.spec.tower == TOWER_TEXT && rows >= 16384 && !e.mx_site[GS_PROJ]) e.tile[GS_PROJ] = TILE_160x128_RS;
+  // (measured for the two-lane regime only, so tied to it)
+  if (e.spec.tower == TOWER_TEXT && e.dev_lanes == 2 && rows >= 16384) e.tile[GS_PROJ] = TILE_160x128_RS;
   // the patch-embedding GEMM has the c_proj shape class (N = D, K = 3 P^2 padded)
   const int G = e.spec.grid();
   const int prow = e.spec.tower == TOWER_VISION ? rows / e.spec.tokens() * G * G : 0;
   e.tile_patch = prow >= 2048 ? TILE_160x128_W8_RS : TILE_AUTO;
 }
 
-// Tool / test overrides of the tile choice: CLIPGPU_GEMM_TILES="q,o,f,p" pins every site,
-// CLIPGPU_GEMM_AUTOTUNE=0 leaves every site to the shape heuristic.  Returns true when one applied.
-bool tile_env_override(clipgpu_engine& e) {
-  const char* env = getenv("CLIPGPU_GEMM_AUTOTUNE");
-  if (env && env[0] == '0') {
-    for (int& t : e.tile) t = TILE_AUTO;
-    e.tile_patch = TILE_AUTO;
-    return true;
-  }
-  if (const char* fixed = getenv("CLIPGPU_GEMM_TILES")) {  // "q,o,f,p": pin every site (tests)
-    int v[4];
-    if (sscanf(fixed, "%d,%d,%d,%d", &v[0], &v[1], &v[2], &v[3]) != 4)
-      throw ClipErr(CLIPGPU_ERR_INVALID, "CLIPGPU_GEMM_TILES must be 'q,o,f,p'");
-    for (int i = 0; i < 4; ++i) {
-      if (v[i] < TILE_AUTO || v[i] > TILE_LAST) throw ClipErr(CLIPGPU_ERR_INVALID, "bad CLIPGPU_GEMM_TILES entry");
-      e.tile[i] = v[i];
-      if (e.mx_site[i]) e.tile[i] = MX_TILE_AUTO;  // the pins name 16-bit tiles
-    }
-    return true;
-  }
-  return false;
+// clipgpu_options.gemm_tiles / patch_tile pins over the table's (or the tuner's) choice: a GemmTile
+// id, or -1 = the shape heuristic (TILE_AUTO).  Validated at creation (built tiles only).
+void apply_tile_pins(clipgpu_engine& e) {
+  for (int i = 0; i < GS_N; ++i)
+    if (e.pin_tiles[i]) e.tile[i] = e.pin_tiles[i] < 0 ? TILE_AUTO : e.pin_tiles[i];
+  if (e.pin_patch) e.tile_patch = e.pin_patch < 0 ? TILE_AUTO : e.pin_patch;
+}
+bool tiles_pinned(const clipgpu_engine& e) {
+  bool any = e.pin_patch != 0;
+  for (int t : e.pin_tiles) any = any || t != 0;
+  return any;
 }
 
-// Timing tuner (clipgpu_options.tuning = 1, or CLIPGPU_GEMM_AUTOTUNE=1; tools/tile_table.py uses
-// it to regenerate the table): times each candidate tile on every trunk GEMM site at max_batch
-// rows (workspace contents are scratch at this point) and keeps the fastest.  Tile choice changes
-// speed only: every tile computes the same sums in the same K order.
+// The tiles both timing passes choose from (the per-site autotune and tune_forward's coordinate
+// descent): every tile the library builds (kGemmTiles).
+const auto& kTuneCands = kGemmTiles;
+
+// Timing tuner (clipgpu_options.tuning = 1 / 2; tools/tile_table.py uses it to regenerate the table):
+// times each candidate tile on every trunk GEMM site at max_batch rows (workspace contents are
+// scratch at this point) and keeps the fastest.  Tile choice changes speed only: every tile computes
+// the same sums in the same K order.
 void autotune_tiles(clipgpu_engine& e, Replica& r) {
   // tuned for the rows one lane runs at max_batch
   const int rows = (e.max_batch + e.dev_lanes - 1) / e.dev_lanes * e.spec.tokens();
   e.tuned_rows = rows;
-  if (tile_env_override(e)) return;
-  const int cands[] = {TILE_128x128,      TILE_128x128_PIPE, TILE_256x128,    TILE_256x256,
-                       TILE_128x64_PIPE,  TILE_64x128_PIPE,  TILE_160x128_PIPE, TILE_160x64_PIPE,
-                       TILE_160x128_W8,   TILE_128x128_W8,   TILE_192x128_W8,  TILE_160x256_W8,
-                       TILE_192x256_W8,   TILE_256x256_RS,   TILE_160x128_RS,  TILE_128x64_RS,
-                       TILE_160x128_W8_RS, TILE_256x256_HALF};
+  const auto& cands = kTuneCands;
   hipEvent_t a, b;
   HIP_CHECK(hipEventCreate(&a));
   HIP_CHECK(hipEventCreate(&b));
@@ -834,7 +790,6 @@ void autotune_tiles(clipgpu_engine& e, Replica& r) {
     float best = 1e30f;
     int best_tile = TILE_AUTO;
     for (int t : cands) {
-      if (g.ksplit > 1 && t == TILE_128x128) continue;  // split-K runs pipelined tiles only
       g.tile = t;
       check(launch_gemm(e.dt, A_ROWS, epi, act, g, r.stream), "autotune gemm");
       HIP_CHECK(hipEventRecord(a, r.stream));
@@ -853,9 +808,9 @@ void autotune_tiles(clipgpu_engine& e, Replica& r) {
   };
   const LayerW& L = r.w.layers[0];
   for (int site = 0; site < GS_N; ++site) {
-    if (e.mx_site[site]) {  // MX sites: the built MX tiles (same timing loop)
+    if (mx_at(e, 0, site)) {  // MX sites: the built MX tiles (same timing loop)
       MxGemmParams g = site_gemm_mx(e, r, L, site, rows);
-      const int epi = site_epi_mx(e, site), act = site == GS_FC ? e.spec.act : ACT_NONE;
+      const int epi = site_epi_mx(e, 0, site), act = site == GS_FC ? e.spec.act : ACT_NONE;
       float best = 1e30f;
       for (int t : {MX_TILE_256x128, MX_TILE_128x128}) {
         g.tile = t;
@@ -868,15 +823,15 @@ void autotune_tiles(clipgpu_engine& e, Replica& r) {
         HIP_CHECK(hipEventElapsedTime(&ms, a, b));
         if (ms < best) {
           best = ms;
-          e.tile[site] = t;
+          e.mxtile[site] = t;
         }
       }
-      continue;
     }
-    // fused sites run gemm_rowln; c_proj's plain GEMM then only runs in the last layer, at full
-    // rows only when that layer is not pruned
-    if ((site == GS_OUT && e.fuse_out) || (site == GS_PROJ && e.fuse_proj && e.prune)) {
-      e.tile[site] = TILE_AUTO;
+    if (e.mx && (e.mx_layers & 1ull) && e.mx_site[site]) {
+      // a 16-bit GEMM runs at this site only on layers outside mx_layers: the table's tile there
+      const int D = e.spec.width, MLP = mlp_pad(e.spec);
+      const int shape[GS_N][2] = {{3 * D, D}, {D, D}, {MLP, D}, {D, MLP}};
+      e.tile[site] = table_tile(site, rows, shape[site][0], shape[site][1]);
       continue;
     }
     e.tile[site] = tune(site_gemm(e, r, L, site, rows), site_epi(site), site == GS_FC ? e.spec.act : ACT_NONE);
@@ -898,8 +853,8 @@ void head(const clipgpu_engine& e, const Replica& r, int B, const PoolSrc& src, 
   const TowerSpec& s = e.spec;
   const int D = s.width, E = s.embed_dim;
   ProfScope ps(e, PC_HEAD, st);
-  check(launch_pool_ln(e.dt, src.x, site_split(e, GS_PROJ) ? r.slab : nullptr, src.ids, src.tokens, r.w.lnpost_w,
-                       r.w.lnpost_b, s.ln_eps, r.pooled, B, D, st), "pool+ln");
+  check(launch_pool_ln(e.dt, src.x, src.ids, src.tokens, r.w.lnpost_w, r.w.lnpost_b, s.ln_eps, r.pooled, B, D, st),
+        "pool+ln");
   check(launch_gemm(e.dt, A_ROWS, EPI_STORE32, ACT_NONE, rows_gemm(r.pooled, D, r.w.proj_t, nullptr, r.emb, E, B, E, D), st), "proj gemm");
   check(launch_l2norm(r.emb, d_out, B, E, st), "l2norm");
 }
@@ -913,8 +868,7 @@ void head_map(const clipgpu_engine& e, const Replica& r, int B, float* d_out, hi
   const int D = s.width, T = s.tokens(), M = mlp_pad(s);
   const MapHeadW& mw = r.w.map;
   ProfScope ps(e, PC_HEAD, st);
-  check(launch_ln_rows_add(e.dt, r.x, site_split(e, GS_PROJ) ? r.slab : nullptr, r.w.lnpost_w, r.w.lnpost_b,
-                           s.ln_eps, r.h, B * T, D, st), "norm");
+  check(launch_ln_rows(e.dt, r.x, r.w.lnpost_w, r.w.lnpost_b, s.ln_eps, r.h, B * T, D, st), "norm");
   check(launch_gemm(e.dt, A_ROWS, EPI_STORE16, ACT_NONE, rows_gemm(r.h, D, mw.wkv, mw.bkv, r.big, 2 * D, B * T, 2 * D, D),
                     st), "attn_pool kv gemm");
   check(launch_map_attention(e.dt, mw.q, r.big, r.pooled, B, T, s.heads, D, st), "attn_pool attention");
@@ -946,7 +900,7 @@ void vision_forward(const clipgpu_engine& e, const Replica& r, const void* pixel
   if (s.family == FAMILY_SIGLIP) {  // no class token, no pre-norm: x = patches + bias + pos
     { ProfScope ps(e, PC_STEM, st);
       check(launch_ln_rows(e.dt, r.x, r.w.layers[0].ln1_w, r.w.layers[0].ln1_b, s.ln_eps, r.h, B * s.tokens(), D, st,
-                           ln_q(e, GS_QKV, r.hs)),
+                           ln_q(e, 0, GS_QKV, r.hs)),
             "ln_1"); }
     trunk(e, r, B, 0, nullptr, st, s.tokens());
     head_map(e, r, B, d_out, st);
@@ -955,7 +909,7 @@ void vision_forward(const clipgpu_engine& e, const Replica& r, const void* pixel
   {
   ProfScope ps(e, PC_STEM, st);
   check(launch_vision_embed_ln(e.dt, r.x, r.w.cls, r.w.pos, r.w.lnpre_w, r.w.lnpre_b, r.w.layers[0].ln1_w,
-                               r.w.layers[0].ln1_b, s.ln_eps, r.h, B, s.tokens(), D, st, ln_q(e, GS_QKV, r.hs)),
+                               r.w.layers[0].ln1_b, s.ln_eps, r.h, B, s.tokens(), D, st, ln_q(e, 0, GS_QKV, r.hs)),
         "embed+ln_pre");
   }
   head(e, r, B, trunk(e, r, B, 0, nullptr, st, s.tokens()), d_out, st);
@@ -971,7 +925,7 @@ void text_forward(const clipgpu_engine& e, const Replica& r, const int64_t* d_id
   {
   ProfScope ps(e, PC_STEM, st);
   check(launch_text_embed_ln(e.dt, d_ids, r.w.tok, r.w.pos, r.w.layers[0].ln1_w, r.w.layers[0].ln1_b, s.ln_eps,
-                             r.x, r.h, B, T, s.width, s.vocab_size, st, ln_q(e, GS_QKV, r.hs)),
+                             r.x, r.h, B, T, s.width, s.vocab_size, st, ln_q(e, 0, GS_QKV, r.hs)),
         "token embed+ln_1");
   }
   head(e, r, B, trunk(e, r, B, 1, d_ids, st, T), d_out, st);
@@ -985,7 +939,6 @@ Replica lane_view(const clipgpu_engine& e, const Replica& r, int b0) {
   const size_t wide = big_wide(s);
   Replica v = r;
   v.x = r.x + rows * D;
-  if (r.slab) v.slab = r.slab + rows * D;
   v.h = (char*)r.h + rows * D * 2;
   v.big = (char*)r.big + rows * wide * 2;
   if (r.hs) v.hs = r.hs + rows * D / 32;
@@ -1118,12 +1071,9 @@ void text_forward_lanes(const clipgpu_engine& e, const Replica& r, const int64_t
 // in the forward two lanes' kernels share the chip, so a tile that wins alone can lose there.
 // Coordinate descent: for each trunk site, try every other tile with the rest fixed and keep
 // it if the concurrent-lane forward at max_batch gets >= 1 % faster.  Inputs are the zeroed
-// staging buffer (timing only).  CLIPGPU_TUNE_FORWARD=0 skips it; pinned tiles skip it.
+// staging buffer (timing only).  clipgpu_options.tuning = 2 skips it; pinned tiles skip it.
 void tune_forward(clipgpu_engine& e, Replica& r) {
-  const char* env = getenv("CLIPGPU_TUNE_FORWARD");
-  if ((env && env[0] == '0') || getenv("CLIPGPU_GEMM_TILES") || e.max_batch < 64 || e.mx) return;
-  const char* at = getenv("CLIPGPU_GEMM_AUTOTUNE");
-  if (at && at[0] == '0') return;
+  if (e.tuning != 1 || tiles_pinned(e) || e.max_batch < 64 || e.mx) return;
   const int B = e.max_batch;
   hipEvent_t a, b;
   HIP_CHECK(hipEventCreate(&a));
@@ -1163,10 +1113,9 @@ void tune_forward(clipgpu_engine& e, Replica& r) {
     }
   }
   for (int site = 0; site < GS_N; ++site) {
-    if ((site == GS_OUT && e.fuse_out) || (site == GS_PROJ && e.fuse_proj && e.prune)) continue;
     const int keep = e.tile[site];
-    for (int t = TILE_128x128; t <= TILE_LAST; ++t) {
-      if (t == keep || (site_split(e, site) && t == TILE_128x128)) continue;
+    for (int t : kTuneCands) {
+      if (t == keep) continue;
       const int prev = e.tile[site];
       e.tile[site] = t;
       const float ms = time_fwd();
@@ -1510,7 +1459,9 @@ void sharded_gather(clipgpu_engine& e, const int64_t* rows, float* const* d_out,
   for (int i = 0; i < G; ++i) {
     Replica& r = e.reps[i];
     if (!d_out[i]) throw ClipErr(CLIPGPU_ERR_INVALID, "NULL buffer");
-    sts[i] = streams && streams[i] ? (hipStream_t)streams[i] : r.stream;
+    // NULL array / entry: the legacy default stream of the replica's device, as in the single-device
+    // entry points (run_graph forks the forward from it and joins it back; the collective runs on it)
+    sts[i] = streams ? (hipStream_t)streams[i] : nullptr;
     const int rank = e.comm_rank0 + i;
     HIP_CHECK(hipSetDevice(r.device));
     for (int64_t c0 = 0; c0 < rows[rank]; c0 += e.max_batch)
@@ -1531,17 +1482,29 @@ void sharded_gather(clipgpu_engine& e, const int64_t* rows, float* const* d_out,
     }
   }
   NCCL_CHECK(ncclGroupEnd());
+  // destroy_comms waits for these (the collective runs on the caller's stream, not the handle's)
+  for (int i = 0; i < G; ++i) {
+    Replica& r = e.reps[i];
+    HIP_CHECK(hipSetDevice(r.device));
+    if (!r.coll) HIP_CHECK(hipEventCreateWithFlags(&r.coll, hipEventDisableTiming));
+    HIP_CHECK(hipEventRecord(r.coll, sts[i]));
+  }
 }
 
-// The handle's communicators: collectives may still be in flight on callers' streams, so every
-// device is drained first; then all of the clique's communicators are finalized inside one group
-// (a one-by-one finalize from one thread can block on peers) and destroyed.
+// The handle's communicators: collectives may still be in flight on callers' streams, so each
+// replica's last collective (the event recorded behind it on the caller's stream) and the handle's own
+// streams are waited for first -- not the whole device, which may run unrelated work (torch, other
+// engines); then all of the clique's communicators are finalized inside one group (a one-by-one
+// finalize from one thread can block on peers) and destroyed.
 void destroy_comms(clipgpu_engine& e) {
   bool any = false;
   for (auto& r : e.reps)
     if (r.comm) {
       (void)hipSetDevice(r.device);
-      (void)hipDeviceSynchronize();
+      if (r.coll) (void)hipEventSynchronize(r.coll);
+      if (r.stream) (void)hipStreamSynchronize(r.stream);
+      for (int i = 0; i < 4; ++i)
+        if (r.lane[i]) (void)hipStreamSynchronize(r.lane[i]);
       any = true;
     }
   if (!any) return;
@@ -1573,6 +1536,7 @@ void destroy_replica(Replica& r) {
   if (r.fork) (void)hipEventDestroy(r.fork);
   if (r.gin) (void)hipEventDestroy(r.gin);
   if (r.gout) (void)hipEventDestroy(r.gout);
+  if (r.coll) (void)hipEventDestroy(r.coll);
   if (r.graphs) {
     r.graphs->clear();
     delete r.graphs;
@@ -1623,7 +1587,17 @@ int clipgpu_create_ex(const char* model_dir, int tower, const int* device_ids, i
     if (opts.mx_sites & ~(CLIPGPU_MX_QKV | CLIPGPU_MX_FC | CLIPGPU_MX_PROJ))
       throw ClipErr(CLIPGPU_ERR_INVALID, "clipgpu_options.mx_sites: unknown bits");
     if (opts.lanes < 0 || opts.lanes > 4) throw ClipErr(CLIPGPU_ERR_INVALID, "clipgpu_options.lanes must be 0..4");
-    if (opts.tuning < 0 || opts.tuning > 1) throw ClipErr(CLIPGPU_ERR_INVALID, "clipgpu_options.tuning must be 0 or 1");
+    if (opts.tuning < 0 || opts.tuning > 2) throw ClipErr(CLIPGPU_ERR_INVALID, "clipgpu_options.tuning must be 0, 1 or 2");
+    for (int32_t v : {opts.graphs, opts.prune_last, opts.trim_text})
+      if (v < -1 || v > 1) throw ClipErr(CLIPGPU_ERR_INVALID, "clipgpu_options graphs / prune_last / trim_text: -1, 0 or 1");
+    for (int i = 0; i < 5; ++i) {
+      const int t = i < 4 ? opts.gemm_tiles[i] : opts.patch_tile;
+      if (t != 0 && t != -1 && !gemm_tile_built(t))
+        throw ClipErr(CLIPGPU_ERR_INVALID, "clipgpu_options.gemm_tiles / patch_tile: " + std::to_string(t) +
+                                               " is not a GEMM tile this library builds");
+    }
+    if (opts.mx_layers != 0 && dtype != CLIPGPU_DTYPE_FP8)
+      throw ClipErr(CLIPGPU_ERR_INVALID, "clipgpu_options.mx_layers needs dtype CLIPGPU_DTYPE_FP8");
     if (opts.communicator < 0 || opts.communicator > 1)
       throw ClipErr(CLIPGPU_ERR_INVALID, "clipgpu_options.communicator must be 0 or 1");
     if (!model_dir) throw ClipErr(CLIPGPU_ERR_INVALID, "model_dir is NULL");
@@ -1649,28 +1623,14 @@ int clipgpu_create_ex(const char* model_dir, int tower, const int* device_ids, i
     e->pre = oc.pre;
     e->dt = dtype == CLIPGPU_DTYPE_F16 ? DT_F16 : DT_BF16;  // fp8 engines keep bf16 outside the MX GEMMs
     e->mx = dtype == CLIPGPU_DTYPE_FP8;
-    if (e->mx) {  // the MX split: the options' bits, else CLIPGPU_MX_SITES, else all three sites
-      uint32_t bits = opts.mx_sites;
-      if (bits == 0) {
-        const char* ms = getenv("CLIPGPU_MX_SITES");
-        const std::string sites = ms ? ms : "qkv,fc,proj";
-        auto has = [&](const char* k) {
-          size_t p = 0;
-          while ((p = sites.find(k, p)) != std::string::npos) {
-            const size_t q = p + strlen(k);
-            if ((p == 0 || sites[p - 1] == ',') && (q == sites.size() || sites[q] == ',')) return true;
-            p = q;
-          }
-          return false;
-        };
-        bits = (has("qkv") ? CLIPGPU_MX_QKV : 0u) | (has("fc") ? CLIPGPU_MX_FC : 0u) |
-               (has("proj") ? CLIPGPU_MX_PROJ : 0u);
-      }
+    if (e->mx) {  // the MX split: the options' bits, else all three sites
+      const uint32_t bits = opts.mx_sites ? opts.mx_sites : (CLIPGPU_MX_QKV | CLIPGPU_MX_FC | CLIPGPU_MX_PROJ);
       e->mx_site[GS_QKV] = (bits & CLIPGPU_MX_QKV) != 0;
       e->mx_site[GS_FC] = (bits & CLIPGPU_MX_FC) != 0;
       e->mx_site[GS_PROJ] = (bits & CLIPGPU_MX_PROJ) != 0;
       if (e->mx_site[GS_PROJ] && !e->mx_site[GS_FC])
         throw ClipErr(CLIPGPU_ERR_INVALID, "MX sites: proj in MX needs fc in MX");
+      e->mx_layers = opts.mx_layers ? (uint64_t)opts.mx_layers : ~0ull;
     } else if (opts.mx_sites) {
       throw ClipErr(CLIPGPU_ERR_INVALID, "clipgpu_options.mx_sites needs dtype CLIPGPU_DTYPE_FP8");
     }
@@ -1678,34 +1638,18 @@ int clipgpu_create_ex(const char* model_dir, int tower, const int* device_ids, i
     if (opts.lanes > 0) {
       e->lanes = opts.lanes;
       e->lanes_pinned = true;
-    } else if (const char* ln = getenv("CLIPGPU_LANES")) {
-      e->lanes = std::max(1, std::min(4, atoi(ln)));
-      e->lanes_pinned = true;
     } else {
       e->lanes = 2;  // host-path staging slots (run_host_shard); the device-side lane count is the table's
     }
-    {
-      const char* at = getenv("CLIPGPU_GEMM_AUTOTUNE");
-      e->tuning = opts.tuning == 1 || (at && at[0] == '1');
-    }
+    e->tuning = opts.tuning;
     e->dev_lanes = e->lanes;
-    if (const char* gr = getenv("CLIPGPU_GRAPHS")) e->graphs = gr[0] != '0';
-    if (const char* pl = getenv("CLIPGPU_PRUNE_LAST")) e->prune = pl[0] != '0';
-    if (const char* tt = getenv("CLIPGPU_TRIM_TEXT")) e->trim = tt[0] != '0';
+    e->graphs = opts.graphs != -1;
+    e->prune = opts.prune_last != -1;
+    e->trim = opts.trim_text != -1;
+    for (int i = 0; i < 4; ++i) e->pin_tiles[i] = opts.gemm_tiles[i];
+    e->pin_patch = opts.patch_tile;
     const TowerSpec& s = e->spec;
     if (!s.unsupported.empty()) throw ClipErr(CLIPGPU_ERR_CONFIG, s.unsupported);
-    if (const char* sp = getenv("CLIPGPU_GEMM_SPLIT")) e->ksplit = sp[0] == '1' ? 2 : 1;
-    if (const char* p3 = getenv("CLIPGPU_GEMM_PIPE3")) e->pipe3 = p3[0] == '1' ? 1 : 0;
-    {
-      if (const char* fl = getenv("CLIPGPU_FUSE_LN")) e->fuse_mode = fl[0] == '1' ? 1 : 0;
-      if (const char* pf = getenv("CLIPGPU_ROWLN_PF")) e->rowln_pf = std::max(0, atoi(pf));
-      e->fuse_ok_out = e->fuse_mode != 0 && gemm_rowln_supported(s.width, s.width) && !site_split(*e, GS_OUT) &&
-                       !e->mx_site[GS_FC];
-      e->fuse_ok_proj = e->fuse_mode != 0 && gemm_rowln_supported(s.width, mlp_pad(s)) &&
-                        !site_split(*e, GS_PROJ) && !e->mx_site[GS_PROJ] && !e->mx_site[GS_QKV];
-      e->fuse_out = e->fuse_mode == 1 && e->fuse_ok_out;
-      e->fuse_proj = e->fuse_mode == 1 && e->fuse_ok_proj;
-    }
     if (s.heads <= 0 || s.width % s.heads || s.width % 64)
       throw ClipErr(CLIPGPU_ERR_CONFIG, "Configuration error: width must be a multiple of 64 and of heads");
     const int hd = s.width / s.heads;
@@ -1747,10 +1691,11 @@ int clipgpu_create_ex(const char* model_dir, int tower, const int* device_ids, i
       if (i == 0) {  // one tile choice, shared by identical devices
         if (e->tuning) {
           autotune_tiles(*e, r);
+          apply_tile_pins(*e);
           tune_forward(*e, r);
         } else {
           table_tiles(*e);
-          tile_env_override(*e);
+          apply_tile_pins(*e);
         }
       }
     }
@@ -2086,7 +2031,7 @@ int clipgpu_test_read_weights(const char* model_dir, int tower, const char* name
 int clipgpu_test_engine_tiles(const clipgpu_engine* e, int tiles[4]) {
   return guarded([&]() {
     if (!e || !tiles) throw ClipErr(CLIPGPU_ERR_INVALID, "NULL argument");
-    for (int i = 0; i < 4; ++i) tiles[i] = e->tile[i];
+    for (int i = 0; i < 4; ++i) tiles[i] = e->mx_site[i] ? e->mxtile[i] : e->tile[i];
   });
 }
 
@@ -2094,7 +2039,7 @@ int clipgpu_engine_info(const clipgpu_engine* e, int tiles[4], int* lanes, uint3
   return guarded([&]() {
     if (!e) throw ClipErr(CLIPGPU_ERR_INVALID, "engine is NULL");
     if (tiles)
-      for (int i = 0; i < 4; ++i) tiles[i] = e->tile[i];
+      for (int i = 0; i < 4; ++i) tiles[i] = e->mx_site[i] ? e->mxtile[i] : e->tile[i];
     if (lanes) *lanes = e->dev_lanes;
     if (mx_sites)
       *mx_sites = (e->mx_site[GS_QKV] ? CLIPGPU_MX_QKV : 0u) | (e->mx_site[GS_FC] ? CLIPGPU_MX_FC : 0u) |

@@ -13,7 +13,7 @@
 //     floor(in_center - r) .. ceil(in_center + r) clamped to the image, r = support * max(scale,
 //     1), weights filter((x - (in_center - 0.5)) / max(scale, 1)) divided by their sum; the
 //     axis's weights become i16 fixed point at precision p (the largest p < 22 with
-//     round(max weight * 2^(p+1)) < 2^15; Normalizer16), each rounded half away from zero;
+//     round(max weight * 2^p) < 2^15, p = 14 for a unit tap; Normalizer16), each rounded half away from zero;
 //     a pass sums 2^(p-1) + pixel * k in i32 and stores clamp(sum >> p, 0, 255); horizontal
 //     pass first, over the source rows the vertical pass reads, into a u8 intermediate.
 //   * normalize_pixels: out[c][i] = (px[i*3+c] / 255 - mean[c]) / std[c]   in f32

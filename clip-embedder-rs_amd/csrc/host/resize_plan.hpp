@@ -11,8 +11,9 @@ namespace clipgpu {
 
 // fast_image_resize 6.0.0's u8 convolution (its Normalizer16, a port of Pillow-SIMD): the
 // normalised f64 weights of an axis become i16 fixed point at the largest precision p < 22 for
-// which round(max weight * 2^(p+1)) still fits under 2^15; a pass sums 2^(p-1) + pixel * k in
-// i32 and stores clamp(sum >> p, 0, 255).
+// which round(max weight * 2^p) still fits under 2^15 (the identity's unit tap: p = 14;
+// test_fast_image_resize_coefficient_precision); a pass sums 2^(p-1) + pixel * k in i32 and stores
+// clamp(sum >> p, 0, 255).
 constexpr int kResizeMaxPrecision = 32 - 8 - 2;  // PRECISION_BITS (the precision search's bound)
 constexpr int kResizeCoefBits = 16 - 1;          // MAX_COEFS_PRECISION (i16 coefficients)
 

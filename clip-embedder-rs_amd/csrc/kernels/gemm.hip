@@ -93,9 +93,6 @@ constexpr int BK = 64;
 #ifndef CLIPGPU_GEMM_POISON
 #define CLIPGPU_GEMM_POISON 0
 #endif
-#ifndef CLIPGPU_GEMM_SPREAD_ALL
-#define CLIPGPU_GEMM_SPREAD_ALL 0
-#endif
 #ifndef CLIPGPU_GEMM_EPI_DMA_WAIT
 #define CLIPGPU_GEMM_EPI_DMA_WAIT 1
 #endif
@@ -457,7 +454,7 @@ struct PipeBounds {
 // 2 + 11 / 32 rounds of work paid as 3 before).  No K split: every output is the same MFMA chain
 // as in the whole tile.
 template <typename T, int BM, int BN, int WGM, int WGN, int EPI, int ACT, int NS = 2, int OCC = 2, int RS = 0,
-          int HM = 0, int M32 = 0>
+          int HM = 0>
 __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_per_eu)) void gemm_pipe_kernel(
     GemmParams p) {
   typedef typename Vec8<T>::type V8;
@@ -465,23 +462,17 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
   constexpr int PW = BN / 8, PA = BM / 8, PT = PW + PA;
   constexpr int NP = (PT + NW - 1) / NW;    // DMA pieces per wave and K-step
-  constexpr bool EVEN = PT % NW == 0;       // every wave issues NP pieces
+  constexpr bool EVEN = PT % NW == 0;       // every wave issues NP pieces (else waves < PT % NW issue NP, the rest NP - 1)
   constexpr bool WSPLIT = PW % NW == 0;     // piece i of every wave is a W piece iff i < PW / NW
   constexpr int TM = BM / WGM, TN = BN / WGN, MI = TM / 16, NI = TN / 16;
-  constexpr int LG = NI == 2 ? 1 : NI == 4 ? 2 : 3;
-  // M32 = 1: v_mfma_f32_32x32x16 instead of 16x16x32 (same operand roles, the same k -> lane map
-  // within each 16-k half and the same K order: bit-identical sums, tools/mfma_order_probe.hip).
-  // The 32x32 MFMA holds the SIMD's issue for 8 of its 32 cycles instead of 8 of 16.  A phase then
-  // runs NG = MI / 2 MFMA groups of 32 rows, each over both 16-k halves of the phase's 32 k.
-  constexpr int NG = M32 ? MI / 2 : MI;
-  static_assert(!M32 || (TM % 32 == 0 && TN % 32 == 0 && RS), "32x32 MFMA: 32-multiple wave tiles, RS schedule");
+  constexpr int LG = NI == 2 ? 1 : NI == 4 ? 2 : 3;  // (swW: NI in {2, 4, 8})
+  constexpr int NG = MI;  // MFMA groups per phase: 16 rows x all NI column blocks each
   // DMA pieces spread between MFMA groups of phase 1 (>= 32 MFMAs per phase), else issued up front
-  // (CLIPGPU_GEMM_SPREAD_ALL=1 at build time spreads them on every tile: an experiment switch)
-  constexpr bool SPREAD = MI * NI >= 32 || CLIPGPU_GEMM_SPREAD_ALL;
+  constexpr bool SPREAD = MI * NI >= 32;
   (void)LG;
   static_assert(BM % 8 == 0 && BN % 8 == 0 && MI >= 1 && BN <= 256 && PT >= NW, "bad tile");
-  static_assert(M32 || NI == 2 || NI == 4 || NI == 8, "column permutation needs NI in {2,4,8}");
-  static_assert(NS == 2 || (NS == 3 && EVEN), "2 LDS stages, or 3 with an even piece split");
+  static_assert(NI == 2 || NI == 3 || NI == 4 || NI == 6 || NI == 8, "column permutation: NI in {2,3,4,6,8}");
+  static_assert(NS == 2 || NS == 3, "2 or 3 LDS stages");
   __shared__ __attribute__((aligned(16))) char smem[NS * STAGE + 2048];
 
   const int tid = threadIdx.x;
@@ -498,12 +489,8 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
   asm volatile("" ::"s"(lda_i), "s"(ldw_i), "s"(nb), "s"(Ab), "s"(Wb), "s"(bias_p));
   const int nTn = (p.N + BN - 1) / BN;
   const int nTm = (p.M + BM - 1) / BM;
-  // Work unit u = (tile u / ks, K-slice u % ks): slice 0 runs the epilogue EPI, slices
-  // >= 1 store their f32 partial to p.slab + (slice - 1) * M * ldo (split-K; combined
-  // by the consumer of the output in a fixed order).
-  const int ks = p.ksplit > 1 ? p.ksplit : 1;
-  const int ntiles = nTn * nTm * ks;
-  const int nk = p.K / BK / ks;  // K-steps per unit
+  const int ntiles = nTn * nTm;
+  const int nk = p.K / BK;  // K-steps per tile
 
   static_assert(!HM || (NS == 2 && WGM == 2), "half tiles: 2 x N waves, 2-stage schedule");
   int t_first, t_stride, t_end;
@@ -534,9 +521,8 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
   }
   if (t_first >= t_end) return;
   const int total = ((t_end - t_first + t_stride - 1) / t_stride) * nk;  // this block's K-steps
-  auto unit_coords = [&](int u, int& m0, int& n0, int& slice) {
+  auto unit_coords = [&](int u, int& m0, int& n0) {
     if constexpr (HM) {  // u < F: whole tile j + u nbx; u == F: half (j & 1) of tile F nbx + j / 2
-      slice = 0;
       if (u < hm_F) {
         tile_coords(hm_start + hm_j + u * hm_nbx, nTm, nTn, BM, BN, m0, n0);
       } else {
@@ -545,15 +531,22 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
       }
       return;
     }
-    slice = u % ks;
-    tile_coords(u / ks, nTm, nTn, BM, BN, m0, n0);
+    tile_coords(u, nTm, nTn, BM, BN, m0, n0);
   };
 
-  // W image swizzle: the 16x16 path reads W rows in a permuted order (rowB below), the 32x32 path
-  // uses the A image's (r >> 1) & 7 (conflict-free for its row order, tools comment at offB)
+  // W image swizzle for the permuted W-row reads (rowB below)
+  // The swizzle must be the same for the NI rows a lane reads (rowB + 4 ni, read at immediate
+  // offsets).  NI = 3 / 6: lane (fr, fq) reads rows 4 NI j + i + 4 ni of its wave's 16 NI (j = fr >> 2,
+  // i = fr & 3), so swW = c(j) ^ (2 j + (i >> 1)) with c(j) = 1 for j in {1, 2} (the lanes of one
+  // ds_read_b128 group pair fq with j that way) gives every group 16 distinct 16-byte slots
+  // (tools/lds_swizzle_check.py checks every wave, column block and k half).
   auto swW = [](int r) {
-    if constexpr (M32) return (r >> 1) & 7;
-    else return (r & 2) | (((r >> (2 + LG)) & 1) << 2);
+    if constexpr (NI == 3 || NI == 6) {
+      const int j = (r % (16 * NI)) / (4 * NI);
+      return ((j == 1 || j == 2) ? 1 : 0) ^ (2 * j + ((r & 3) >> 1));
+    } else {
+      return (r & 2) | (((r >> (2 + LG)) & 1) << 2);
+    }
   };
 
   // ---- LDS-DMA cursor (global step d_g = tile d_ti, K-step d_kt) -----------
@@ -561,8 +554,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
   // kernel-argument base pointer (A or W), for the current unit's first K-step.
   uint32_t poff[NP];
   auto piece_is_w = [&](int i, int q) { return WSPLIT ? (i < PW / NW) : (q < PW); };
-  auto set_tile = [&](int m0, int n0, int slice) {
-    const int k0 = slice * nk * BK;  // first k of the unit's K-slice
+  auto set_tile = [&](int m0, int n0) {
 #pragma unroll
     for (int i = 0; i < NP; ++i) {
       const int q = wave + NW * i;
@@ -571,19 +563,19 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
       } else if (piece_is_w(i, q)) {
         const int r = q * 8 + (lane >> 3);
         const int c = (lane & 7) ^ swW(r);
-        poff[i] = (uint32_t)(min(n0 + r, p.N - 1) * ldw_i + k0 + c * 8) * 2u;
+        poff[i] = (uint32_t)(min(n0 + r, p.N - 1) * ldw_i + c * 8) * 2u;
       } else {
         const int r = (q - PW) * 8 + (lane >> 3);
         const int c = (lane & 7) ^ ((r >> 1) & 7);
-        poff[i] = (uint32_t)(min(m0 + r, p.M - 1) * lda_i + k0 + c * 8) * 2u;
+        poff[i] = (uint32_t)(min(m0 + r, p.M - 1) * lda_i + c * 8) * 2u;
       }
     }
   };
   int d_g = 0, d_kt = 0, d_t = t_first, d_n0 = 0, d_ti = 0;
   {
-    int m0, n0, sl;
-    unit_coords(d_t, m0, n0, sl);
-    set_tile(m0, n0, sl);
+    int m0, n0;
+    unit_coords(d_t, m0, n0);
+    set_tile(m0, n0);
     d_n0 = n0;
   }
   auto dma_piece = [&](auto ic) {
@@ -613,9 +605,9 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
       d_t += t_stride;
       ++d_ti;
       if (d_t < t_end) {
-        int m0, n0, sl;
-        unit_coords(d_t, m0, n0, sl);
-        set_tile(m0, n0, sl);
+        int m0, n0;
+        unit_coords(d_t, m0, n0);
+        set_tile(m0, n0);
         d_n0 = n0;
       }
     }
@@ -631,66 +623,42 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
   // ---- fragments -------------------------------------------------------------
   const int wm = (wave / WGN) * TM, wn = (wave % WGN) * TN;
   const int fr = lane & 15, fq = lane >> 4;
-  // offA / offB [kk][h]: base of the phase-kk fragment reads (h: the 16-k half, 32x32 path only).
-  // 16x16: lane (fr, fq) reads row fr, k chunk 4 kk + fq; W rows permuted (rowB, + 4 ni) so a lane
-  // owns 4 NI consecutive output columns.
-  // 32x32: lane (i = lane & 31, hl = lane >> 5) reads row i of each 32-row block, k chunk
-  // 4 kk + 2 h + hl; the W fragment row of MFMA row i is wn + 16 NI32 ((i >> 2) & 1) +
-  // 4 (i >> 3) + (i & 3) (+ 16 nb), which makes D register r of lane (j, hl) output column
-  // wn + 16 NI32 hl + 16 nb + r: every lane owns 16 NI32 consecutive columns of one row.  Both
-  // images are read conflict-free with the (r >> 1) & 7 swizzle in that order.
-  uint32_t offA[2][2], offB[2][2];
-  if constexpr (M32) {
-    const int i = lane & 31, hl = lane >> 5;
-    const int rowA = wm + i;
-    const int rowW = wn + 16 * (NI / 2) * ((i >> 2) & 1) + 4 * (i >> 3) + (i & 3);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int c = kk * 4 + 2 * h + hl;
-        offA[kk][h] = (uint32_t)(rowA * 128 + ((c ^ ((rowA >> 1) & 7)) << 4));
-        offB[kk][h] = (uint32_t)(A_BYTES + rowW * 128 + ((c ^ ((rowW >> 1) & 7)) << 4));
-      }
-  } else {
+  // offA / offB [kk]: base of the phase-kk fragment reads.  Lane (fr, fq) reads row fr, k chunk
+  // 4 kk + fq; the W rows are permuted (rowB, + 4 ni) so that a lane owns 4 NI consecutive output
+  // columns.
+  uint32_t offA[2], offB[2];
+  {
     const int rowB = wn + (fr >> 2) * (4 * NI) + (fr & 3);  // + 4*ni
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      offA[kk][0] = offA[kk][1] = (uint32_t)((wm + fr) * 128 + (((kk * 4 + fq) ^ (fr >> 1)) << 4));
-      offB[kk][0] = offB[kk][1] = (uint32_t)(A_BYTES + rowB * 128 + (((kk * 4 + fq) ^ swW(rowB)) << 4));
+      offA[kk] = (uint32_t)((wm + fr) * 128 + (((kk * 4 + fq) ^ (fr >> 1)) << 4));
+      offB[kk] = (uint32_t)(A_BYTES + rowB * 128 + (((kk * 4 + fq) ^ swW(rowB)) << 4));
     }
   }
   // the current unit's row layout (HM half tiles: row offset (wave / WGN) * TM / 2, MI / 2 groups)
   int wm_cur = wm, mi_lim = MI;
-  uint32_t offA_cur[2][2] = {{offA[0][0], offA[0][1]}, {offA[1][0], offA[1][1]}};
+  uint32_t offA_cur[2] = {offA[0], offA[1]};
   auto set_layout = [&](int u) {
     if constexpr (HM) {
       const bool half = u >= hm_F;
       wm_cur = half ? (wave / WGN) * (TM / 2) : wm;
       mi_lim = half ? MI / 2 : MI;
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-        for (int h = 0; h < 2; ++h) offA_cur[kk][h] = offA[kk][h] - (uint32_t)((wm - wm_cur) * 128);
+      for (int kk = 0; kk < 2; ++kk) offA_cur[kk] = offA[kk] - (uint32_t)((wm - wm_cur) * 128);
     }
     (void)u;
   };
   const uint32_t lds0 = lds_addr(smem);
   f32x4 acc[NI][MI];
-  // (32x32 path) acc32[nb][mb]: the 32 x 32 block of rows wm + 32 mb, columns of group nb
-  f32x16 acc32[NI / 2 > 0 ? NI / 2 : 1][MI / 2 > 0 ? MI / 2 : 1];
-  // fragments of one phase: 16x16: a[mi], b[ni]; 32x32: a[2 mb + h], b[2 nb + h] (h: 16-k half)
-  V8 a0[MI], b0[NI], a1[MI], b1[NI];
+  V8 a0[MI], b0[NI], a1[MI], b1[NI];  // fragments of one phase
 
   auto rd_b = [&](auto kc, V8(&b)[NI], uint32_t buf, int kk) {
     constexpr int k = decltype(kc)::value;
-    if constexpr (M32) ds_read_b128<(k >> 1) * 2048>(b[k], buf + offB[kk][k & 1]);
-    else ds_read_b128<k * 512>(b[k], buf + offB[kk][0]);
+    ds_read_b128<k * 512>(b[k], buf + offB[kk]);
   };
   auto rd_a = [&](auto kc, V8(&a)[MI], uint32_t buf, int kk) {
     constexpr int k = decltype(kc)::value;
-    if constexpr (M32) ds_read_b128<(k >> 1) * 4096>(a[k], buf + offA_cur[kk][k & 1]);
-    else ds_read_b128<k * 2048>(a[k], buf + offA_cur[kk][0]);
+    ds_read_b128<k * 2048>(a[k], buf + offA_cur[kk]);
   };
   auto read_b = [&](V8(&b)[NI], uint32_t buf, int kk) { static_for<NI>([&](auto k) { rd_b(k, b, buf, kk); }); };
   auto read_a = [&](V8(&a)[MI], uint32_t buf, int kk) { static_for<MI>([&](auto k) { rd_a(k, a, buf, kk); }); };
@@ -709,28 +677,15 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
       if constexpr ((int)decltype(gc)::value < RG && k < NR) read_k(std::integral_constant<int, k>{}, a, b, buf, kk);
     });
   };
-  // MFMA group g of a phase: 16 rows x all NI column blocks (16x16), or 32 rows x all NI / 2 column
-  // blocks over both 16-k halves (32x32); zero: the unit's first MFMA of each accumulator
+  // MFMA group g of a phase: 16 rows x all NI column blocks; zero: the unit's first MFMA of each
+  // accumulator
   auto mfma_group = [&](auto gc, V8(&a)[MI], V8(&b)[NI], auto zero) {
     constexpr int g = decltype(gc)::value;
     constexpr bool Z = decltype(zero)::value;
-    if constexpr (M32) {
-      if (!HM || 2 * g < mi_lim) {
+    if (!HM || g < mi_lim) {
 #pragma unroll
-        for (int h = 0; h < 2; ++h)
-#pragma unroll
-          for (int nb = 0; nb < NI / 2; ++nb) {
-            f32x16 c = acc32[nb][g];
-            if (Z && h == 0) c = f32x16{};
-            acc32[nb][g] = mfma_32x32x16(b[2 * nb + h], a[2 * g + h], c);
-          }
-      }
-    } else {
-      if (!HM || g < mi_lim) {
-#pragma unroll
-        for (int ni = 0; ni < NI; ++ni)
-          acc[ni][g] = mfma_16x16x32(b[ni], a[g], Z ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[ni][g]);
-      }
+      for (int ni = 0; ni < NI; ++ni)
+        acc[ni][g] = mfma_16x16x32(b[ni], a[g], Z ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[ni][g]);
     }
   };
   auto phase0 = [&](auto zero, uint32_t buf) {
@@ -777,34 +732,12 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
   };
 
   // ---- epilogue: lane owns row wm+mi*16+fr, columns nc .. nc+4*NI-1 ------------
-  // slice > 0 (split-K partial): plain f32 store of acc to the slab, no bias / residual.
-  auto epilogue = [&](int m0, int n0, int bpar, int slice) {
+  auto epilogue = [&](int m0, int n0, int bpar) {
     const int nc = n0 + wn + fq * (4 * NI);
     const bool nfull = nc + 4 * NI <= p.N;
     f32x4 bias[NI];
 #pragma unroll
     for (int ni = 0; ni < NI; ++ni) bias[ni] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (slice > 0) {
-      float* const slab = p.slab + (long)(slice - 1) * p.M * p.ldo;
-#pragma unroll
-      for (int mi = 0; mi < MI; ++mi) {
-        const int m = m0 + wm + mi * 16 + fr;
-        if (m >= p.M) continue;
-        float* o = slab + (long)m * p.ldo + nc;
-        if (nfull) {
-#pragma unroll
-          for (int ni = 0; ni < NI; ++ni)
-            *(float4*)(o + ni * 4) = make_float4(acc[ni][mi][0], acc[ni][mi][1], acc[ni][mi][2], acc[ni][mi][3]);
-        } else {
-#pragma unroll
-          for (int ni = 0; ni < NI; ++ni)
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-              if (nc + ni * 4 + j < p.N) o[ni * 4 + j] = acc[ni][mi][j];
-        }
-      }
-      return;
-    }
     if (bias_p != nullptr) {
       const uint32_t ba = lds0 + NS * STAGE + bpar * 1024 + (wn + fq * (4 * NI)) * 4;
       static_for<NI>([&](auto ni) { ds_read_b128<(int)ni * 16>(bias[ni], ba); });
@@ -881,12 +814,22 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
       if constexpr (EPI == EPI_STORE16) {
         T* o = (T*)p.out + (long)m * p.ldo + nc;
         if (nfull) {
+          if constexpr (NI % 2 == 0) {
 #pragma unroll
-          for (int h = 0; h < NI / 2; ++h) {
-            V8 w;
+            for (int h = 0; h < NI / 2; ++h) {
+              V8 w;
 #pragma unroll
-            for (int e = 0; e < 8; ++e) w[e] = to16<T>(apply_act<ACT>(v[2 * h + e / 4][e % 4]));
-            *(V8*)(o + h * 8) = w;
+              for (int e = 0; e < 8; ++e) w[e] = to16<T>(apply_act<ACT>(v[2 * h + e / 4][e % 4]));
+              *(V8*)(o + h * 8) = w;
+            }
+          } else {  // odd NI: the lane's 4 NI columns start 8-byte aligned only -> 8-byte stores
+#pragma unroll
+            for (int ni = 0; ni < NI; ++ni) {
+              typename Vec4<T>::type w;
+#pragma unroll
+              for (int j = 0; j < 4; ++j) w[j] = to16<T>(apply_act<ACT>(v[ni][j]));
+              *(typename Vec4<T>::type*)(o + ni * 4) = w;
+            }
           }
         } else {
 #pragma unroll
@@ -922,134 +865,17 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
       }
     }
   };
-  // ---- epilogue, 32x32 path: lane (i, hl) owns row wm + 32 mb + i, the CW = 16 NI / 2 consecutive
-  // columns from nc; column nc + 16 nb + r is acc32[nb][mb][r].  The float ops per element are the
-  // 16x16 epilogue's ((acc + bias) (+ x), act), so the outputs are bit-identical to it.
-  auto epilogue32 = [&](int m0, int n0, int bpar, int slice) {
-    constexpr int MI2 = MI / 2 > 0 ? MI / 2 : 1, CW = 16 * (NI / 2), CQ = CW / 4;
-    const int i = lane & 31, hl = lane >> 5;
-    const int nc = n0 + wn + hl * CW;
-    const bool nfull = nc + CW <= p.N;
-    auto val = [&](int mb, int q, int e) -> float { return acc32[q >> 2][mb][(q & 3) * 4 + e]; };
-    if (slice > 0) {
-      float* const slab = p.slab + (long)(slice - 1) * p.M * p.ldo;
-#pragma unroll
-      for (int mb = 0; mb < MI2; ++mb) {
-        const int m = m0 + wm_cur + mb * 32 + i;
-        if (m >= p.M) continue;
-        float* o = slab + (long)m * p.ldo + nc;
-        if (nfull) {
-#pragma unroll
-          for (int q = 0; q < CQ; ++q) *(float4*)(o + q * 4) = make_float4(val(mb, q, 0), val(mb, q, 1), val(mb, q, 2), val(mb, q, 3));
-        } else {
-#pragma unroll
-          for (int q = 0; q < CQ; ++q)
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-              if (nc + q * 4 + e < p.N) o[q * 4 + e] = val(mb, q, e);
-        }
-      }
-      return;
-    }
-    f32x4 bias[CQ];
-#pragma unroll
-    for (int q = 0; q < CQ; ++q) bias[q] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (bias_p != nullptr) {
-      const uint32_t ba = lds0 + NS * STAGE + bpar * 1024 + (wn + hl * CW) * 4;
-      static_for<CQ>([&](auto q) { ds_read_b128<(int)q * 16>(bias[q], ba); });
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-      for (int q = 0; q < CQ; ++q) asm volatile("" : "+v"(bias[q]));
-    }
-    constexpr bool ADDX = EPI == EPI_RESID || EPI == EPI_PATCH;
-    const int G2 = p.G * p.G;
-    auto out_row = [&](int m) -> long {
-      if constexpr (EPI == EPI_PATCH) {
-        const int b = m / G2;
-        return ((long)b * (G2 + p.cls) + p.cls + (m - b * G2)) * p.ldo;
-      } else {
-        return (long)m * p.ldo;
-      }
-    };
-    auto add_src = [&](int m) -> const float* {
-      if constexpr (EPI == EPI_PATCH) return p.pos + (long)(p.cls + m % G2) * p.N + nc;
-      else return (const float*)p.out + (long)m * p.ldo + nc;
-    };
-    // the added rows (residual x / positional embedding): a ring of 2 row blocks loaded one ahead
-    // when the registers allow it (accumulators + bias + 2 rows + ~40 addresses within the wave's
-    // share), else each row block loaded just before its use
-    constexpr int REG_BUDGET = NW == 8 && OCC >= 2 ? 128 : 256;
-    constexpr int XR = ADDX && MI2 > 1 && MI * NI * 4 + 12 * CQ + 40 <= REG_BUDGET ? 2 : 1;
-    float4 xr[XR][CQ];
-    auto load_x = [&](int mb, float4(&dst)[CQ]) {
-      const int m = m0 + wm_cur + mb * 32 + i;
-      if (m < p.M && nfull && (!HM || 2 * mb < mi_lim)) {
-        const float* src = add_src(m);
-#pragma unroll
-        for (int q = 0; q < CQ; ++q) dst[q] = *(const float4*)(src + q * 4);
-      }
-    };
-    if constexpr (ADDX) load_x(0, xr[0]);
-#pragma unroll
-    for (int mb = 0; mb < MI2; ++mb) {
-      if constexpr (ADDX && XR > 1) {
-        if (mb + 1 < MI2) load_x(mb + 1, xr[(mb + 1) % XR]);
-      } else if constexpr (ADDX) {
-        if (mb > 0) load_x(mb, xr[0]);  // no ring: each row block's x just before its use
-      }
-      const int m = m0 + wm_cur + mb * 32 + i;
-      if (m >= p.M || (HM && 2 * mb >= mi_lim)) continue;
-      if constexpr (EPI == EPI_STORE16) {
-        T* o = (T*)p.out + (long)m * p.ldo + nc;
-        if (nfull) {
-#pragma unroll
-          for (int h = 0; h < CW / 8; ++h) {
-            V8 w;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-              const int q = 2 * h + e / 4, j = e % 4;
-              w[e] = to16<T>(apply_act<ACT>(val(mb, q, j) + bias[q][j]));
-            }
-            *(V8*)(o + h * 8) = w;
-          }
-        } else {
-#pragma unroll
-          for (int q = 0; q < CQ; ++q)
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-              if (nc + q * 4 + j < p.N) o[q * 4 + j] = to16<T>(apply_act<ACT>(val(mb, q, j) + bias[q][j]));
-        }
-      } else {
-        float* o = (float*)p.out + out_row(m) + nc;
-        if (nfull) {
-#pragma unroll
-          for (int q = 0; q < CQ; ++q) {
-            float4 w = make_float4(val(mb, q, 0) + bias[q][0], val(mb, q, 1) + bias[q][1], val(mb, q, 2) + bias[q][2],
-                                   val(mb, q, 3) + bias[q][3]);
-            if constexpr (ADDX) {
-              const float4 x = xr[mb % XR][q];
-              w.x += x.x; w.y += x.y; w.z += x.z; w.w += x.w;
-            }
-            *(float4*)(o + q * 4) = w;
-          }
-        } else {
-          const float* xs = ADDX ? add_src(m) : nullptr;
-#pragma unroll
-          for (int q = 0; q < CQ; ++q)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              if (nc + q * 4 + j >= p.N) continue;
-              float r = val(mb, q, j) + bias[q][j];
-              if constexpr (ADDX) r += xs[q * 4 + j];
-              o[q * 4 + j] = r;
-            }
-        }
-      }
-    }
-  };
   // vm ops a full tile's epilogue leaves in flight behind the DMA of the step after it (the same
   // count on both paths: MI NI / 2 16-byte stores of 16-bit values, MI NI of f32, + as many loads)
-  constexpr int EPI_VM = EPI == EPI_STORE16 ? MI * NI / 2 : ((EPI == EPI_RESID || EPI == EPI_PATCH) ? 2 * MI * NI : MI * NI);
+  constexpr int EPI_VM = EPI == EPI_STORE16 ? (NI % 2 ? MI * NI : MI * NI / 2)
+                                            : ((EPI == EPI_RESID || EPI == EPI_PATCH) ? 2 * MI * NI : MI * NI);
+  // 3 stages: retire all but this wave's DMA pieces of the youngest step (+ X more recent vm ops):
+  // NP pieces per step on waves < PT % NW (or every wave when the split is even), else NP - 1
+  auto vm_wait_step = [&](auto xc) {
+    constexpr int X = decltype(xc)::value;
+    if (EVEN || wave < PT % NW) vm_wait<(NP + X < 63 ? NP + X : 63)>();
+    else vm_wait<(NP - 1 + X < 63 ? NP - 1 + X : 63)>();
+  };
 
   // ---- prologue: steps 0 and 1 in flight, step 0 landed, its kk0 fragments read
   GEMM_STAMP_REAL(62);
@@ -1069,8 +895,8 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
   bool after_full_epi = false;
   int ti = 0;
   for (int t = t_first; t < t_end; t += t_stride, ++ti) {
-    int m0, n0, slice;
-    unit_coords(t, m0, n0, slice);
+    int m0, n0;
+    unit_coords(t, m0, n0);
     GEMM_STAMP(2 + ti * 4);
     for (int kt = 0; kt < nk; ++kt, ++g) {
       if (kt + 1 == nk) GEMM_STAMP(3 + ti * 4);
@@ -1082,8 +908,8 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
       // and loads
       constexpr int EW = EPI_VM < 63 ? EPI_VM : 63;
       if (NS == 3 && g + 2 < total) {
-        if (after_full_epi) vm_wait<(EPI_VM + NP < 63 ? EPI_VM + NP : 63)>();
-        else vm_wait<NP>();
+        if (after_full_epi) vm_wait_step(std::integral_constant<int, EPI_VM>{});
+        else vm_wait_step(std::integral_constant<int, 0>{});
       } else {
 #if CLIPGPU_GEMM_POISON_SELFTEST  // (the race check's own test: drop the wait on the 2-stage path)
         (void)EW;
@@ -1108,13 +934,12 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
     // compiler's own wait insertion treats mixed pending VMEM reads and writes as unordered).
     // DESIGN.md §5 "The 224x256 race-check failure" records what this was and was not.
 #if CLIPGPU_GEMM_EPI_DMA_WAIT
-    if constexpr (NS == 3) vm_wait<NP>();
+    if constexpr (NS == 3) vm_wait_step(std::integral_constant<int, 0>{});
     else vm_wait<0>();
 #endif
-    if constexpr (M32) epilogue32(m0, n0, ti & 1, slice);
-    else epilogue(m0, n0, ti & 1, slice);
-    // partial tiles, half tiles and slab units issue fewer vm ops than EPI_VM: drain them
-    after_full_epi = slice == 0 && m0 + BM <= p.M && n0 + BN <= p.N && (!HM || t < hm_F);
+    epilogue(m0, n0, ti & 1);
+    // partial tiles and half tiles issue fewer vm ops than EPI_VM: drain them
+    after_full_epi = m0 + BM <= p.M && n0 + BN <= p.N && (!HM || t < hm_F);
     if (!after_full_epi) vm_wait<0>();
     if (t + t_stride < t_end) {  // the next tile's step 0 landed at the last barrier
       const uint32_t buf = lds0 + (g % NS) * STAGE;
@@ -1128,11 +953,6 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
   GEMM_STAMP_REAL(63);
 }
 
-// GemmParams::pipe3 = 1 (CLIPGPU_GEMM_PIPE3=1 at engine creation) enables the 3-stage schedule
-// (off by default).  Alone it is a little faster (ViT-B/32 c_proj 49.7 -> 48.3 us), but its
-// 110 KiB of LDS per block keeps the other lane's blocks off the CU, and the concurrent-lane
-// forward measured 83.7k vs 85.5k img/s (profiles/r01_v19_pipe3_ab.txt).
-
 template <typename T, int BM, int BN, int WGM, int WGN, int EPI, int ACT>
 hipError_t launch_cfg(const GemmParams& p, hipStream_t s) {
   const int nTn = (p.N + BN - 1) / BN, nTm = (p.M + BM - 1) / BM;
@@ -1145,50 +965,50 @@ hipError_t launch_cfg(const GemmParams& p, hipStream_t s) {
 }
 
 // OCC: resident blocks per CU the tile's registers allow (4-wave tiles: up to 3 by LDS; 8-wave
-// tiles: 1, or 2 when built for 4 waves per SIMD).
-template <typename T, int BM, int BN, int WGM, int WGN, int EPI, int ACT, int OCC = 3, int RS = 0, int M32 = 0>
+// tiles: 1, or 2 when built for 4 waves per SIMD).  2 LDS stages.
+template <typename T, int BM, int BN, int WGM, int WGN, int EPI, int ACT, int OCC = 3, int RS = 0>
 hipError_t launch_pipe(const GemmParams& p, hipStream_t s) {
   constexpr int NW = WGM * WGN;
   constexpr int KOCC = NW == 8 ? (OCC >= 2 ? 2 : 1) : 2;  // kernel template's OCC (launch bounds)
   const int nTn = (p.N + BN - 1) / BN, nTm = (p.M + BM - 1) / BM;
-  const int ntiles = nTn * nTm * (p.ksplit > 1 ? p.ksplit : 1);
-  // resident blocks per CU: by LDS (stages + 2 KiB bias) and by registers (OCC)
-  auto per_cu = [&](int ns) {
-    const int lds = ns * (BM + BN) * BK * 2 + 2048;
-    return std::max(1, std::min(NW == 8 ? KOCC : OCC, (160 * 1024) / lds));
-  };
-  // 3 stages for K-long GEMMs whose tiles fit in one round of 3-stage blocks: there the
-  // K-step is DMA-latency-bound and the extra stage costs no occupancy (>= 3 K-steps per
-  // unit keep the bias double buffer safe); even DMA piece splits only
-  constexpr bool FITS3 = 3 * (BM + BN) * BK * 2 + 2048 <= 160 * 1024 && (BM / 8 + BN / 8) % NW == 0;
-  if constexpr (FITS3) {
-    const int nk = p.K / BK / (p.ksplit > 1 ? p.ksplit : 1);
-    if (p.pipe3 == 1 && p.K >= 1024 && nk >= 3 && ntiles <= device_cus() * per_cu(3)) {
-      gemm_launch(gemm_pipe_kernel<T, BM, BN, WGM, WGN, EPI, ACT, 3, KOCC, RS, 0, M32>, ntiles, NW * 64, s, p);
-      return hipGetLastError();
-    }
-  }
-  const int resident = device_cus() * per_cu(2);
+  const int ntiles = nTn * nTm;
+  // resident blocks per CU: by LDS (2 stages + 2 KiB bias) and by registers (OCC)
+  const int lds = 2 * (BM + BN) * BK * 2 + 2048;
+  const int per_cu = std::max(1, std::min(NW == 8 ? KOCC : OCC, (160 * 1024) / lds));
+  const int resident = device_cus() * per_cu;
   const int grid = ntiles <= resident ? ntiles : resident;
-  gemm_launch(gemm_pipe_kernel<T, BM, BN, WGM, WGN, EPI, ACT, 2, KOCC, RS, 0, M32>, grid, NW * 64, s, p);
+  gemm_launch(gemm_pipe_kernel<T, BM, BN, WGM, WGN, EPI, ACT, 2, KOCC, RS, 0>, grid, NW * 64, s, p);
   return hipGetLastError();
 }
 
 // Half-tile last round for the 256x256 RS tile (gemm_pipe_kernel HM = 1, one block per CU): when the
 // tiles leave a partial last round of at most nbx / 2 tiles per XCD after >= 1 whole round; else the
 // plain RS launch (the same sums, bit for bit).
-template <typename T, int EPI, int ACT, int M32 = 0>
+template <typename T, int EPI, int ACT>
 hipError_t launch_pipe_half(const GemmParams& p, hipStream_t s) {
   const int nb = device_cus();
   const int ntiles = ((p.N + 255) / 256) * ((p.M + 255) / 256);
-  bool ok = p.ksplit <= 1 && nb % 8 == 0 && ntiles % nb != 0;
+  bool ok = nb % 8 == 0 && ntiles % nb != 0;
   const int nbx = nb >> 3, q = ntiles >> 3, r = ntiles & 7;
   for (int x = 0; ok && x < 8; ++x) {
     const int cnt = q + (x < r ? 1 : 0);
     ok = cnt >= nbx && 2 * (cnt % nbx) <= nbx;
   }
-  if (!ok) return launch_pipe<T, 256, 256, 2, 4, EPI, ACT, 3, 1, M32>(p, s);
-  gemm_launch(gemm_pipe_kernel<T, 256, 256, 2, 4, EPI, ACT, 2, 2, 1, 1, M32>, nb, 512, s, p);
+  if (!ok) return launch_pipe<T, 256, 256, 2, 4, EPI, ACT, 3, 1>(p, s);
+  gemm_launch(gemm_pipe_kernel<T, 256, 256, 2, 4, EPI, ACT, 2, 2, 1, 1>, nb, 512, s, p);
+  return hipGetLastError();
+}
+
+// 224x192, 8 waves (2 x 4 of 112 x 48), one block per CU, 3 LDS stages (156 KiB + the bias slots) when
+// every tile has >= 3 K-steps: the N = width residual GEMMs of ViT-B/32 at 12800 rows are 58 x 4 = 232
+// tiles, one round on 232 CUs, at 103 FLOP per staged byte (the 2-blocks-per-CU 160 x 128 tiles: 71) and
+// two K-steps of LDS-DMA in flight per CU (106 KiB; 160 x 128 pairs: 72 KiB).
+template <typename T, int EPI, int ACT>
+hipError_t launch_pipe_224(const GemmParams& p, hipStream_t s) {
+  const int ntiles = ((p.N + 191) / 192) * ((p.M + 223) / 224);
+  const int grid = std::min(ntiles, device_cus());
+  if (p.K / BK >= 3) gemm_launch(gemm_pipe_kernel<T, 224, 192, 2, 4, EPI, ACT, 3, 1, 1, 0>, grid, 512, s, p);
+  else gemm_launch(gemm_pipe_kernel<T, 224, 192, 2, 4, EPI, ACT, 2, 1, 1, 0>, grid, 512, s, p);
   return hipGetLastError();
 }
 
@@ -1271,7 +1091,7 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmParams p) {
 // 16-byte aligned rows, no split-K.
 inline bool skinny_ok(const GemmParams& p) {
   return p.M > 0 && p.M <= SKINNY_MAX_M && p.N % 16 == 0 && p.K % (32 * SKINNY_U) == 0 && p.lda % 8 == 0 &&
-         p.ldw % 8 == 0 && p.ldo % 4 == 0 && p.ksplit <= 1 && !(p.diag & 2);
+         p.ldw % 8 == 0 && p.ldo % 4 == 0 && !(p.diag & 2);
 }
 
 template <typename T, int EPI, int ACT>
@@ -1290,64 +1110,17 @@ hipError_t launch_tile(const GemmParams& p, hipStream_t s) {
   const int tile = p.tile == TILE_AUTO ? pick_gemm_tile(p.M, p.N, p.K) : p.tile;
   // software-pipelined kernel: K >= 128, 16-byte-aligned 16-bit output rows (diag bit 1: legacy, stamp builds)
   const bool pipe = p.K >= 2 * BK && !(p.diag & 2) && (EPI != EPI_STORE16 || p.ldo % 8 == 0);
-  if (p.ksplit > 1) {  // split-K runs on the pipelined kernel only (128x128 -> its pipelined form)
-    if (!pipe) return hipErrorInvalidValue;
-    switch (tile) {
-      case TILE_256x256: return launch_pipe<T, 256, 256, 2, 4, EPI, ACT>(p, s);
-      case TILE_256x128: return launch_pipe<T, 256, 128, 4, 2, EPI, ACT>(p, s);
-      case TILE_128x64_PIPE: return launch_pipe<T, 128, 64, 2, 2, EPI, ACT>(p, s);
-      case TILE_64x128_PIPE: return launch_pipe<T, 64, 128, 2, 2, EPI, ACT>(p, s);
-      case TILE_160x128_PIPE: return launch_pipe<T, 160, 128, 2, 2, EPI, ACT>(p, s);
-      case TILE_160x64_PIPE: return launch_pipe<T, 160, 64, 2, 2, EPI, ACT>(p, s);
-      case TILE_160x128_W8: return launch_pipe<T, 160, 128, 2, 4, EPI, ACT, 2>(p, s);
-      case TILE_128x128_W8: return launch_pipe<T, 128, 128, 2, 4, EPI, ACT, 2>(p, s);
-      case TILE_192x128_W8: return launch_pipe<T, 192, 128, 2, 4, EPI, ACT, 1>(p, s);
-      case TILE_160x256_W8: return launch_pipe<T, 160, 256, 2, 4, EPI, ACT, 1>(p, s);
-      case TILE_192x256_W8: return launch_pipe<T, 192, 256, 2, 4, EPI, ACT, 1>(p, s);
-      case TILE_256x256_RS: return launch_pipe<T, 256, 256, 2, 4, EPI, ACT, 3, 1>(p, s);
-      case TILE_160x128_RS: return launch_pipe<T, 160, 128, 2, 2, EPI, ACT, 3, 1>(p, s);
-      case TILE_128x64_RS: return launch_pipe<T, 128, 64, 2, 2, EPI, ACT, 3, 1>(p, s);
-      case TILE_160x128_W8_RS: return launch_pipe<T, 160, 128, 2, 4, EPI, ACT, 2, 1>(p, s);
-      case TILE_256x256_M32: return launch_pipe<T, 256, 256, 2, 4, EPI, ACT, 3, 1, 1>(p, s);
-      case TILE_192x256_M32: return launch_pipe<T, 192, 256, 2, 4, EPI, ACT, 1, 1, 1>(p, s);
-      case TILE_256x192_M32: return launch_pipe<T, 256, 192, 4, 2, EPI, ACT, 1, 1, 1>(p, s);
-      case TILE_128x128_W8_M32: return launch_pipe<T, 128, 128, 2, 4, EPI, ACT, 2, 1, 1>(p, s);
-      case TILE_256x128_M32: return launch_pipe<T, 256, 128, 4, 2, EPI, ACT, 1, 1, 1>(p, s);
-      default: return launch_pipe<T, 128, 128, 2, 2, EPI, ACT>(p, s);
-    }
-  }
   if (pipe) {
     switch (tile) {
-      case TILE_256x256: return launch_pipe<T, 256, 256, 2, 4, EPI, ACT>(p, s);
       case TILE_256x128: return launch_pipe<T, 256, 128, 4, 2, EPI, ACT>(p, s);
-      case TILE_128x128_PIPE: return launch_pipe<T, 128, 128, 2, 2, EPI, ACT>(p, s);
-      case TILE_128x64_PIPE: return launch_pipe<T, 128, 64, 2, 2, EPI, ACT>(p, s);
-      case TILE_64x128_PIPE: return launch_pipe<T, 64, 128, 2, 2, EPI, ACT>(p, s);
-      case TILE_160x128_PIPE: return launch_pipe<T, 160, 128, 2, 2, EPI, ACT>(p, s);
-      case TILE_160x64_PIPE: return launch_pipe<T, 160, 64, 2, 2, EPI, ACT>(p, s);
-      case TILE_160x128_W8: return launch_pipe<T, 160, 128, 2, 4, EPI, ACT, 2>(p, s);
-      case TILE_128x128_W8: return launch_pipe<T, 128, 128, 2, 4, EPI, ACT, 2>(p, s);
-      case TILE_192x128_W8: return launch_pipe<T, 192, 128, 2, 4, EPI, ACT, 1>(p, s);
-      case TILE_160x256_W8: return launch_pipe<T, 160, 256, 2, 4, EPI, ACT, 1>(p, s);
+      case TILE_256x256: return launch_pipe<T, 256, 256, 2, 4, EPI, ACT>(p, s);
       case TILE_192x256_W8: return launch_pipe<T, 192, 256, 2, 4, EPI, ACT, 1>(p, s);
       case TILE_256x256_RS: return launch_pipe<T, 256, 256, 2, 4, EPI, ACT, 3, 1>(p, s);
       case TILE_160x128_RS: return launch_pipe<T, 160, 128, 2, 2, EPI, ACT, 3, 1>(p, s);
-      case TILE_128x64_RS: return launch_pipe<T, 128, 64, 2, 2, EPI, ACT, 3, 1>(p, s);
       case TILE_160x128_W8_RS: return launch_pipe<T, 160, 128, 2, 4, EPI, ACT, 2, 1>(p, s);
       case TILE_256x256_HALF: return launch_pipe_half<T, EPI, ACT>(p, s);
-      case TILE_256x256_M32: return launch_pipe_half<T, EPI, ACT, 1>(p, s);
-      case TILE_192x256_M32: return launch_pipe<T, 192, 256, 2, 4, EPI, ACT, 1, 1, 1>(p, s);
-      case TILE_256x192_M32: return launch_pipe<T, 256, 192, 4, 2, EPI, ACT, 1, 1, 1>(p, s);
-      case TILE_128x128_W8_M32: return launch_pipe<T, 128, 128, 2, 4, EPI, ACT, 2, 1, 1>(p, s);
-      case TILE_256x128_M32: return launch_pipe<T, 256, 128, 4, 2, EPI, ACT, 1, 1, 1>(p, s);
-      case TILE_256x256_PP: return launch_gemm_pp(std::is_same<T, __bf16>::value ? DT_BF16 : DT_F16, 256, EPI, ACT, p, s);
-      case TILE_192x256_PP: return launch_gemm_pp(std::is_same<T, __bf16>::value ? DT_BF16 : DT_F16, 192, EPI, ACT, p, s);
-#if CLIPGPU_GEMM_DIAG_224
-      // (diagnostic build only, tools/poison_diag.py: the dropped 224x256 8-wave tile)
-      case 99:
-        if constexpr (EPI == EPI_STORE32 || EPI == EPI_RESID) return launch_pipe<T, 224, 256, 2, 4, EPI, ACT, 1>(p, s);
-        break;
-#endif
+      case TILE_224x192_W8: return launch_pipe_224<T, EPI, ACT>(p, s);
+      case TILE_256x192_W8: return launch_pipe<T, 256, 192, 2, 4, EPI, ACT, 1, 1>(p, s);
       default: break;
     }
   }
@@ -1422,14 +1195,7 @@ hipError_t launch_gemm(DType dt, int asrc, int epi, int act, const GemmParams& p
   // 32-bit staging offsets: W must fit whole; A is chunked by rows
   if ((long)p.N * p.ldw * 2 >= (1L << 31) || p.lda <= 0) return hipErrorInvalidValue;
   if (asrc != A_ROWS) return hipErrorInvalidValue;  // pixels go through launch_patch_rows first
-  if (p.ksplit > 1) {  // each K-slice >= 2 K-steps (pipelined kernel); f32 epilogues only; a slab
-    if (p.K % (BK * p.ksplit) != 0 || p.K / p.ksplit < 2 * BK || p.slab == nullptr ||
-        (epi != EPI_RESID && epi != EPI_STORE32) || p.ldo % 4 != 0)
-      return hipErrorInvalidValue;
-  }
   if ((long)p.M * p.lda * 2 >= (1L << 31)) {
-    // slab slices are [ksplit - 1][M][ldo]: chunk offsets hold for one extra slice only
-    if (p.ksplit > 2) return hipErrorInvalidValue;
     const int G = epi == EPI_PATCH ? p.G : 0;
     const long chunk = gemm_chunk_rows(p.lda, G);
     if (chunk <= 0) return hipErrorInvalidValue;
@@ -1440,7 +1206,6 @@ hipError_t launch_gemm(DType dt, int asrc, int epi, int act, const GemmParams& p
       q.A = (const char*)p.A + m0 * p.lda * 2;
       const long orow = G > 0 ? m0 / ((long)G * G) * ((long)G * G + p.cls) : m0;  // EPI_PATCH: token rows
       q.out = (char*)p.out + orow * p.ldo * osz;
-      if (p.slab) q.slab = p.slab + m0 * p.ldo;
       const hipError_t err = dt == DT_BF16 ? launch_typed<__bf16>(epi, act, q, s) : launch_typed<_Float16>(epi, act, q, s);
       if (err != hipSuccess) return err;
     }

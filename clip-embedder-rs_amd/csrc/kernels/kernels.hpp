@@ -34,87 +34,46 @@ struct GemmParams {
   int cls;                   // EPI_PATCH: 1 = token 0 of each image is a class token (rows / pos shifted by one)
   const float* pos;          // EPI_PATCH positional embedding [G^2+cls][N]
   int tile;                  // GemmTile (0 = pick by shape)
-  int ksplit;                // split-K slices (0/1 = none); EPI_RESID / EPI_STORE32 only: slice 0 runs the
-                             // epilogue, slice s >= 1 stores its f32 partial to slab[(s-1)*M*ldo + m*ldo + n]
-  float* slab;
   int diag;                  // stamp build only: bit 0 = skip epilogue stores (timing experiments)
-  int pipe3;                 // 1: K-long GEMMs that fit in one round of blocks take the 3-stage LDS schedule
-                             // (the engine reads CLIPGPU_GEMM_PIPE3 once at creation)
 };
 
-// Tile configurations of the MFMA GEMM.
+// Tile configurations of the MFMA GEMM.  Ids are stable across rounds; the ones not listed were
+// experiment tiles that never won a site (round 4 removed them from the library: DESIGN.md §5 keeps
+// their measurements): 4-12 and 16 (4- / 8-wave 128-192-row variants), 19-20 (ping-pong schedule),
+// 21-25 (32x32x16 MFMA), 27 (spread-DMA 224x192).
 enum GemmTile {
   TILE_AUTO = 0,
-  TILE_128x128 = 1,       // gemm_bt_kernel: 4 waves, 64 KiB LDS, 2 blocks / CU
-  TILE_256x128 = 2,       // gemm_pipe_kernel: 8 waves (4x2, 64x64 each), 96 KiB LDS
-  TILE_256x256 = 3,       // gemm_pipe_kernel: 8 waves, 128 KiB LDS
-  TILE_128x128_PIPE = 4,  // gemm_pipe_kernel: 4 waves, 64 KiB LDS, 2 blocks / CU
-  TILE_128x64_PIPE = 5,   // gemm_pipe_kernel: 4 waves (64x32 each), 48 KiB LDS, 3 blocks / CU
-  TILE_64x128_PIPE = 6,   // gemm_pipe_kernel: 4 waves (32x64 each), 48 KiB LDS, 3 blocks / CU
-  TILE_160x128_PIPE = 7,  // gemm_pipe_kernel: 4 waves (80x64 each), 74 KiB LDS, 2 blocks / CU: M = 6400
-                          // (a 128-image lane of ViT-B/32) is 40 row tiles, 960 tiles = 1.9 rounds of 512
-  TILE_160x64_PIPE = 8,   // gemm_pipe_kernel: 4 waves (80x32 each), 58 KiB LDS, 2 blocks / CU: the N = 768
-                          // GEMMs at M = 6400 are 480 tiles, one round with two blocks on most CUs
-  // 8-wave tiles (two or four waves per SIMD: one wave's fragment reads, DMA issue and barrier
-  // waits overlap another's MFMAs on the same SIMD), 2 x 4 waves:
-  TILE_160x128_W8 = 9,    // 80x32 per wave, 74 KiB LDS, 2 blocks / CU (<= 128 VGPRs); uneven DMA split
-  TILE_128x128_W8 = 10,   // 64x32 per wave, 66 KiB LDS, 2 blocks / CU
-  TILE_192x128_W8 = 11,   // 96x32 per wave, 82 KiB LDS, 1 block / CU
-  TILE_160x256_W8 = 12,   // 80x64 per wave, 106 KiB LDS, 1 block / CU; uneven DMA split
-  TILE_192x256_W8 = 13,   // 96x64 per wave, 114 KiB LDS, 1 block / CU: the N = 768 GEMMs at M = 12800
-                          // are 67 x 3 = 201 tiles (one round) at fewer LDS bytes per MFMA than 160x128
-  // the same tiles with the spread fragment-read schedule (gemm_pipe_kernel RS = 1: a phase's reads
-  // for the next phase go out over its first MI - 2 MFMA groups); bit-identical, speed only
+  TILE_128x128 = 1,       // gemm_bt_kernel: 4 waves, 64 KiB LDS, 2 blocks / CU (M < 2048, K < 128)
+  TILE_256x128 = 2,       // gemm_pipe_kernel: 8 waves (4x2, 64x64 each), 96 KiB LDS (shape heuristic)
+  TILE_256x256 = 3,       // gemm_pipe_kernel: 8 waves (2x4, 128x64 each), 128 KiB LDS (shape heuristic)
+  TILE_192x256_W8 = 13,   // 2x4 waves of 96x64, 114 KiB LDS, 1 block / CU (the table's ViT-H/14 c_proj)
+  // the spread fragment-read schedule (gemm_pipe_kernel RS = 1: a phase's reads for the next phase go
+  // out over its first MI - 2 MFMA groups); bit-identical to the others, speed only
   TILE_256x256_RS = 14,
-  TILE_160x128_RS = 15,
-  TILE_128x64_RS = 16,
-  TILE_160x128_W8_RS = 17,
-  TILE_256x256_HALF = 18,  // 256x256 RS with the partial last round as half tiles (gemm_pipe_kernel HM = 1)
-  // ping-pong schedule (gemm_pp.hip): two 4-wave row groups one section apart, so one wave of each
-  // SIMD issues MFMAs while the other reads fragments / issues DMA / runs its epilogue
-  TILE_256x256_PP = 19,   // 8 waves of 128x64, 130 KiB LDS, 1 block / CU
-  TILE_192x256_PP = 20,   // 8 waves of 96x64, 114 KiB LDS: the N = 768 GEMMs at M = 12800 are 201 tiles
-  // gemm_pipe_kernel with v_mfma_f32_32x32x16 (M32 = 1; bit-identical to the 16x16x32 tiles):
-  TILE_256x256_M32 = 21,   // tile 18's schedule (RS, half-tile last round), 2x4 waves of 128x64
-  TILE_192x256_M32 = 22,   // 2x4 waves of 96x64, RS, 1 block / CU
-  TILE_256x192_M32 = 23,   // 4x2 waves of 64x96, RS, 114 KiB LDS, 1 block / CU: N = 768 is 4 column tiles
-  TILE_128x128_W8_M32 = 24,  // 2x4 waves of 64x32, RS, 66 KiB LDS, 2 blocks / CU
-  TILE_256x128_M32 = 25,   // 4x2 waves of 64x64, RS, 98 KiB LDS, 1 block / CU
-  TILE_LAST = TILE_256x128_M32,  // (last of the tiled kernels: the range the tuners and pins take)
-  TILE_SKINNY = 100,      // gemm_skinny_kernel: one wave per 16x16 block, M <= 256 (TILE_AUTO's pick there);
-                          // a fixed id outside the tunable range, so new tiles append without renumbering
+  TILE_160x128_RS = 15,     // 4 waves of 80x64, 74 KiB LDS, 2 blocks / CU (the table's large-text c_proj)
+  TILE_160x128_W8_RS = 17,  // 2x4 waves of 80x32, 74 KiB LDS, 2 blocks / CU (the table's N = width sites)
+  TILE_256x256_HALF = 18,   // 256x256 RS with the partial last round as half tiles (HM = 1; the table's
+                            // qkv / c_fc)
+  // 2x4 waves of 112x48 (RS), 1 block / CU, 3 LDS stages (158 KiB) when K >= 192: the N = 768 residual
+  // GEMMs at 12800 rows are 232 tiles, one round
+  TILE_224x192_W8 = 26,
+  TILE_256x192_W8 = 28,   // 2x4 waves of 128x48 (RS), 114 KiB LDS, 1 block / CU: N = 768 at 12800 rows is 200 tiles
+  TILE_SKINNY = 100,      // gemm_skinny_kernel: one wave per 16x16 block, M <= 256 (TILE_AUTO's pick there)
 };
+// The GemmTile ids the library builds (pins, tests and the timing tuner take only these).
+constexpr int kGemmTiles[] = {TILE_128x128, TILE_256x128, TILE_256x256, TILE_192x256_W8, TILE_256x256_RS,
+                              TILE_160x128_RS, TILE_160x128_W8_RS, TILE_256x256_HALF, TILE_224x192_W8,
+                              TILE_256x192_W8};
+inline bool gemm_tile_built(int t) {
+  for (int k : kGemmTiles)
+    if (k == t) return true;
+  return false;
+}
 int pick_gemm_tile(int M, int N, int K);
 int device_cus();  // CUs of the current device (cached)
 
 // act: Act enum from common.hpp (only used with EPI_STORE16)
 hipError_t launch_gemm(DType dt, int asrc, int epi, int act, const GemmParams& p, hipStream_t s);
-// The ping-pong kernel (gemm_pp.hip; TILE_256x256_PP / TILE_192x256_PP through launch_gemm): bm = 256
-// or 192 rows per tile, 256 columns.
-hipError_t launch_gemm_pp(DType dt, int bm, int epi, int act, const GemmParams& p, hipStream_t s);
-
-// Row-complete residual GEMM + LayerNorm (gemm_rowln.hip): x[m] += A[m] . W^T + bias (f32,
-// in place) and h[m] = LN(x[m]) * ln_w + ln_b (16-bit; skipped when h is null) for the
-// N = width GEMMs followed by a LayerNorm (out_proj -> ln_2, c_proj -> the next ln_1).
-// A [M][lda], W [D][ldw] 16-bit; x, h [M][D].  h may alias A (each block reads its own rows
-// before it writes them).
-struct RowLnParams {
-  const void* A = nullptr;
-  long lda = 0;
-  const void* W = nullptr;
-  long ldw = 0;
-  const float* bias = nullptr;
-  float* x = nullptr;
-  const float* ln_w = nullptr;
-  const float* ln_b = nullptr;
-  float eps = 1e-5f;
-  void* h = nullptr;
-  int M = 0, D = 0, K = 0;
-  int pf = 8;  // L2 prefetch distance in K-steps (0: off); speed only
-};
-bool gemm_rowln_supported(int D, int K);
-hipError_t launch_gemm_rowln(DType dt, const RowLnParams& p, hipStream_t s);
-
 // Kernel-boundary timing of the next GEMM launch on this thread (clipgpu_profile_*): when
 // both events are set, launch_gemm launches through hipExtLaunchKernelGGL with them, so the
 // events stamp the kernel's own start and end (an event pair recorded around a launch also
@@ -136,11 +95,8 @@ hipError_t launch_attention(DType dt, const void* qkv, void* out, int B, int N, 
 // out16[r] = LN(x[r]) for r < rows.
 hipError_t launch_ln_rows(DType dt, const float* x, const float* w, const float* b, float eps,
                           void* out16, int rows, int D, hipStream_t s, uint8_t* qs = nullptr);
-// qs != nullptr (these three LN launchers): the output is MX-fp8, out16 = e4m3 bytes [rows][D],
+// qs != nullptr (these LN launchers): the output is MX-fp8, out16 = e4m3 bytes [rows][D],
 // qs = scales [rows][D/32] (gemm_mx.hip's A operand); D % 32 == 0.
-// slab != nullptr: x[r] += slab[r] (stored) first -- the split-K combine of the GEMM that wrote x.
-hipError_t launch_ln_rows_add(DType dt, float* x, const float* slab, const float* w, const float* b, float eps,
-                              void* out16, int rows, int D, hipStream_t s, uint8_t* qs = nullptr);
 
 // Vision stem tail: CLS row = cls + pos[0]; x = ln_pre(x) (in place); h = ln_1(x).
 hipError_t launch_vision_embed_ln(DType dt, float* x, const float* cls, const float* pos,
@@ -154,8 +110,7 @@ hipError_t launch_text_embed_ln(DType dt, const int64_t* ids, const float* tok, 
                                 void* h, int B, int T, int D, int vocab, hipStream_t s, uint8_t* qs = nullptr);
 
 // Pool one row per sequence (CLS: ids == nullptr; else first argmax of ids) and LN it.
-// slab (nullable): split-K partial of the last c_proj, added to the pooled row.
-hipError_t launch_pool_ln(DType dt, const float* x, const float* slab, const int64_t* ids, int tokens,
+hipError_t launch_pool_ln(DType dt, const float* x, const int64_t* ids, int tokens,
                           const float* w, const float* b, float eps, void* out16, int B, int D,
                           hipStream_t s);
 
@@ -197,7 +152,6 @@ hipError_t launch_cast_f32(DType dt, const float* in, void* out, long n, hipStre
 #ifdef CLIPGPU_GEMM_STAMPS
 // Diagnostic build: copy (or clear) the per-block s_memtime stamps of the last GEMM launch.
 hipError_t read_gemm_stamps(unsigned long long* host, int nblocks, bool clear);
-hipError_t read_rowln_stamps(unsigned long long* host, int nblocks, bool clear);
 #endif
 
 // ---- MX-fp8 path (gemm_mx.hip) ---------------------------------------------------------

@@ -125,11 +125,9 @@ __device__ __forceinline__ void add_row(Row<NV>& r, const Row<NV>& a) {
 // Every kernel issues all of its row loads (activations and LN parameters) up front, so
 // their latencies overlap instead of following the reductions one round trip at a time.
 
-// slab != nullptr: first combine the split-K partial of the GEMM that wrote x
-// (x += slab, stored back), then LN -- the launch-boundary split-K reduce.
 template <typename T, int NV>
-__global__ __launch_bounds__(256) void ln_rows_kernel(float* __restrict__ x, const float* __restrict__ slab,
-                                                      const float* w, const float* b, float eps,
+__global__ __launch_bounds__(256) void ln_rows_kernel(const float* __restrict__ x, const float* w, const float* b,
+                                                      float eps,
                                                       T* __restrict__ out, uint8_t* __restrict__ qs, int rows,
                                                       int D) {
   // one wave per row, rows strided by the grid's wave count (grid <= rows / 4 blocks); the next
@@ -146,12 +144,6 @@ __global__ __launch_bounds__(256) void ln_rows_kernel(float* __restrict__ x, con
     const int next = row + stride;
     Row<NV> nr;
     if (next < rows) load_row(x + (long)next * D, D4, lane, nr);
-    if (slab != nullptr) {
-      Row<NV> a;
-      load_row(slab + (long)row * D, D4, lane, a);
-      add_row(r, a);
-      store_row32(x + (long)row * D, r, D4, lane);
-    }
     Row<NV> o;
     layer_norm_regs(r, o, g, bb, eps, D, lane);
     store_ln_out(out, qs, row, D, o, lane);
@@ -232,7 +224,7 @@ __device__ inline int pooled_token(const int64_t* __restrict__ ids, int bi, int 
 }
 
 template <typename T, int NV>
-__global__ __launch_bounds__(256) void pool_ln_kernel(const float* __restrict__ x, const float* __restrict__ slab,
+__global__ __launch_bounds__(256) void pool_ln_kernel(const float* __restrict__ x,
                                                       const int64_t* __restrict__ ids, int tokens, const float* w,
                                                       const float* b, float eps, T* __restrict__ out, int B, int D) {
   const int bi = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -243,11 +235,6 @@ __global__ __launch_bounds__(256) void pool_ln_kernel(const float* __restrict__ 
   load_row(x + ((long)bi * tokens + src) * D, D4, lane, r);
   load_row(w, D4, lane, g);
   load_row(b, D4, lane, bb);
-  if (slab != nullptr) {  // split-K partial of the last c_proj (x itself is not updated)
-    Row<NV> a;
-    load_row(slab + ((long)bi * tokens + src) * D, D4, lane, a);
-    add_row(r, a);
-  }
   layer_norm_regs(r, y, g, bb, eps, D, lane);
   store_row16(out + (long)bi * D, y, D4, lane);
 }
@@ -308,14 +295,9 @@ inline dim3 rows_grid(int rows) { return dim3((rows + 3) / 4); }
     }                                                                                                   \
   } while (0)
 
+// (16-bit output pointers are passed as void*: the kernel parameter is T*)
 hipError_t launch_ln_rows(DType dt, const float* x, const float* w, const float* b, float eps, void* out16,
                           int rows, int D, hipStream_t s, uint8_t* qs) {
-  return launch_ln_rows_add(dt, const_cast<float*>(x), nullptr, w, b, eps, out16, rows, D, s, qs);
-}
-
-// (16-bit output pointers are passed as void*: the kernel parameter is T*)
-hipError_t launch_ln_rows_add(DType dt, float* x, const float* slab, const float* w, const float* b, float eps,
-                              void* out16, int rows, int D, hipStream_t s, uint8_t* qs) {
   if (D % 4 || D > 256 * MAXV || D <= 0 || (qs != nullptr && D % 32)) return hipErrorInvalidValue;
   // blocks: one row per wave, at most one resident round (8 blocks of 4 waves per CU); more rows
   // loop with the next row's loads in flight.  Measured against one row per wave at 12800 rows
@@ -325,9 +307,9 @@ hipError_t launch_ln_rows_add(DType dt, float* x, const float* slab, const float
   const int cap = device_cus() * 8;
   if ((int)grid.x > cap) grid.x = cap;
   if (dt == DT_BF16) {
-    CLIPGPU_ROW_LAUNCH(ln_rows_kernel, __bf16, grid, D, x, slab, w, b, eps, (__bf16*)out16, qs, rows, D);
+    CLIPGPU_ROW_LAUNCH(ln_rows_kernel, __bf16, grid, D, x, w, b, eps, (__bf16*)out16, qs, rows, D);
   } else {
-    CLIPGPU_ROW_LAUNCH(ln_rows_kernel, _Float16, grid, D, x, slab, w, b, eps, (_Float16*)out16, qs, rows, D);
+    CLIPGPU_ROW_LAUNCH(ln_rows_kernel, _Float16, grid, D, x, w, b, eps, (_Float16*)out16, qs, rows, D);
   }
   return hipGetLastError();
 }
@@ -370,13 +352,13 @@ hipError_t launch_gather_pooled(const float* x, const void* h16, const int64_t* 
   return hipGetLastError();
 }
 
-hipError_t launch_pool_ln(DType dt, const float* x, const float* slab, const int64_t* ids, int tokens,
+hipError_t launch_pool_ln(DType dt, const float* x, const int64_t* ids, int tokens,
                           const float* w, const float* b, float eps, void* out16, int B, int D, hipStream_t s) {
   if (D % 4 || D > 256 * MAXV || D <= 0) return hipErrorInvalidValue;
   if (dt == DT_BF16) {
-    CLIPGPU_ROW_LAUNCH(pool_ln_kernel, __bf16, rows_grid(B), D, x, slab, ids, tokens, w, b, eps, (__bf16*)out16, B, D);
+    CLIPGPU_ROW_LAUNCH(pool_ln_kernel, __bf16, rows_grid(B), D, x, ids, tokens, w, b, eps, (__bf16*)out16, B, D);
   } else {
-    CLIPGPU_ROW_LAUNCH(pool_ln_kernel, _Float16, rows_grid(B), D, x, slab, ids, tokens, w, b, eps, (_Float16*)out16, B, D);
+    CLIPGPU_ROW_LAUNCH(pool_ln_kernel, _Float16, rows_grid(B), D, x, ids, tokens, w, b, eps, (_Float16*)out16, B, D);
   }
   return hipGetLastError();
 }

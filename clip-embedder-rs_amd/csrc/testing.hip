@@ -36,21 +36,30 @@ DType dt_of(int dtype) {
   return dtype == CLIPGPU_DTYPE_BF16 ? DT_BF16 : DT_F16;
 }
 
-// CLIPGPU_TEST_TILE forces a GEMM tile in clipgpu_test_gemm (tile-config coverage): a GemmTile
-// id (kernels.hpp: 0 auto, 1..TILE_LAST the tiled kernels, 100 skinny); the MX hooks take MxTile ids.
-// CLIPGPU_GEMM_PIPE3=1 selects the 3-stage schedule for the hooks' launches (read per call).
+// CLIPGPU_TEST_TILE forces a GEMM tile in the kernel-level test hooks below (tile-config coverage; the
+// engine itself reads no environment): a built GemmTile id (kernels.hpp kGemmTiles), 0 auto, 100 skinny;
+// the MX hooks take MxTile ids.
 int tile_override() {
   const char* e = getenv("CLIPGPU_TEST_TILE");
-  return e ? atoi(e) : 0;
+  const int t = e ? atoi(e) : 0;
+  if (t != 0 && t != TILE_SKINNY && !gemm_tile_built(t))
+    throw ClipErr(CLIPGPU_ERR_INVALID, "CLIPGPU_TEST_TILE: " + std::to_string(t) + " is not a built GEMM tile");
+  return t;
 }
-int pipe3_override() {
-  const char* e = getenv("CLIPGPU_GEMM_PIPE3");
-  return e && e[0] == '1' ? 1 : 0;
-}
-// K-slices for the f32-epilogue GEMM hooks (CLIPGPU_TEST_KSPLIT, default 1).
-int ksplit_override() {
-  const char* e = getenv("CLIPGPU_TEST_KSPLIT");
-  return e ? atoi(e) : 1;
+
+// One wave: sleep-poll s_memrealtime (100 MHz) for `ticks`, counting shader clocks (s_memtime) over the
+// same span.  Lanes 0 / 1 store the two counts (vector stores of lane-dependent addresses).
+__global__ void clock_probe_kernel(unsigned long long* out, unsigned long long ticks) {
+  const unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  unsigned long long r = r0;
+  while (r - r0 < ticks) {
+    __builtin_amdgcn_s_sleep(32);
+    r = __builtin_amdgcn_s_memrealtime();
+  }
+  const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+  const int lane = threadIdx.x;
+  if (lane < 2) out[lane] = lane == 0 ? t1 - t0 : r - r0;
 }
 
 void up(void* d, const void* h, size_t n) { TCHECK(hipMemcpy(d, h, n, hipMemcpyHostToDevice)); }
@@ -94,7 +103,6 @@ int clipgpu_test_gemm(int dtype, int mode, int act, int64_t M, int64_t N, int64_
     if (bias) up(dB.p, bias, N * 4);
     GemmParams g{};
     g.tile = tile_override();
-    g.pipe3 = pipe3_override();
     g.A = dA.p; g.lda = K; g.W = dW.p; g.ldw = K; g.bias = bias ? dB.as<float>() : nullptr;
     g.out = dO.p; g.ldo = N; g.M = (int)M; g.N = (int)N; g.K = (int)K;
     int epi = EPI_STORE16;
@@ -104,22 +112,10 @@ int clipgpu_test_gemm(int dtype, int mode, int act, int64_t M, int64_t N, int64_
     } else if (mode == 2) {
       epi = EPI_STORE32;
     }
-    const int ks = mode == 0 ? 1 : ksplit_override();
-    DevBuf dS(ks > 1 ? (size_t)(ks - 1) * M * N * 4 : 4);
-    if (ks > 1) {
-      g.ksplit = ks;
-      g.slab = dS.as<float>();
-    }
     TCHECK(launch_gemm(dt, A_ROWS, epi, mode == 0 ? act : 0, g, nullptr));
     TCHECK(hipDeviceSynchronize());
     if (mode == 0) down16(dt, out, dO.p, M * N);
     else down(out, dO.p, M * N * 4);
-    if (ks > 1) {  // the consumer's combine, in slice order (launch_ln_rows_add's x += slab)
-      std::vector<float> part((size_t)(ks - 1) * M * N);
-      down(part.data(), dS.p, part.size() * 4);
-      for (int sl = 0; sl < ks - 1; ++sl)
-        for (size_t i = 0; i < (size_t)(M * N); ++i) out[i] += part[(size_t)sl * M * N + i];
-    }
   });
 }
 
@@ -174,7 +170,6 @@ int clipgpu_test_patch_embed(int dtype, int mode, int64_t B, int64_t S, int64_t 
     g.cls = 1;
     g.G = (int)G; g.pos = dpos.as<float>();
     g.tile = tile_override();
-    g.pipe3 = pipe3_override();
     TCHECK(launch_gemm(dt, A_ROWS, EPI_PATCH, 0, g, nullptr));
     TCHECK(hipDeviceSynchronize());
     down(x_out, dx.p, B * tokens * D * 4);
@@ -234,6 +229,15 @@ int clipgpu_test_lane_reduce(const float* in64, float* out512) {
   });
 }
 
+int clipgpu_test_clock_probe(void* stream, int64_t duration_us, uint64_t* d_out) {
+  return guarded([&]() {
+    if (!d_out || duration_us <= 0 || duration_us > 10000000) throw ClipErr(CLIPGPU_ERR_INVALID, "bad clock probe");
+    hipLaunchKernelGGL(clock_probe_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, (unsigned long long*)d_out,
+                       (unsigned long long)duration_us * 100ull);
+    TCHECK(hipGetLastError());
+  });
+}
+
 int clipgpu_test_gemm_bench(int dtype, int epi, int act, int64_t M, int64_t N, int64_t K, int tile, int iters,
                             double* us_per_launch) {
   return guarded([&]() {
@@ -250,95 +254,14 @@ int clipgpu_test_gemm_bench(int dtype, int epi, int act, int64_t M, int64_t N, i
     GemmParams g{};
     g.A = dA.p; g.lda = K; g.W = dW.p; g.ldw = K; g.bias = dB.as<float>();
     g.out = dO.p; g.ldo = N; g.M = (int)M; g.N = (int)N; g.K = (int)K; g.tile = tile;
-    g.pipe3 = pipe3_override();
+    if (tile != 0 && tile != TILE_SKINNY && !gemm_tile_built(tile)) throw ClipErr(CLIPGPU_ERR_INVALID, "not a built tile");
     const int e = epi == 1 ? EPI_RESID : (epi == 2 ? EPI_STORE32 : EPI_STORE16);
-    const int ks = e == EPI_STORE16 ? 1 : ksplit_override();
-    DevBuf dS(ks > 1 ? (size_t)(ks - 1) * M * N * 4 : 4);
-    if (ks > 1) {
-      g.ksplit = ks;
-      g.slab = dS.as<float>();
-    }
     for (int i = 0; i < 3; ++i) TCHECK(launch_gemm(dt, A_ROWS, e, epi == 0 ? act : 0, g, nullptr));
     hipEvent_t a, b;
     TCHECK(hipEventCreate(&a));
     TCHECK(hipEventCreate(&b));
     TCHECK(hipEventRecord(a, nullptr));
     for (int i = 0; i < iters; ++i) TCHECK(launch_gemm(dt, A_ROWS, e, epi == 0 ? act : 0, g, nullptr));
-    TCHECK(hipEventRecord(b, nullptr));
-    TCHECK(hipEventSynchronize(b));
-    float ms = 0.f;
-    TCHECK(hipEventElapsedTime(&ms, a, b));
-    (void)hipEventDestroy(a);
-    (void)hipEventDestroy(b);
-    *us_per_launch = (double)ms * 1000.0 / iters;
-  });
-}
-
-int clipgpu_test_gemm_rowln(int dtype, int64_t M, int64_t D, int64_t K, const float* A, const float* W,
-                            const float* bias, float* x, const float* ln_w, const float* ln_b, float eps, float* h) {
-  return guarded([&]() {
-    const DType dt = dt_of(dtype);
-    if (M <= 0 || !gemm_rowln_supported((int)D, (int)K)) throw ClipErr(CLIPGPU_ERR_INVALID, "bad rowln shape");
-    DevBuf dA(M * K * 2), dW(D * K * 2), dB(D * 4), dx(M * D * 4), dlw(D * 4), dlb(D * 4), dh(M * D * 2);
-    up16(dt, dA.p, A, M * K);
-    up16(dt, dW.p, W, D * K);
-    if (bias) up(dB.p, bias, D * 4);
-    up(dx.p, x, M * D * 4);
-    if (h) {
-      up(dlw.p, ln_w, D * 4);
-      up(dlb.p, ln_b, D * 4);
-    }
-    RowLnParams p;
-    p.A = dA.p; p.lda = K; p.W = dW.p; p.ldw = K; p.bias = bias ? dB.as<float>() : nullptr;
-    p.x = dx.as<float>(); p.ln_w = dlw.as<float>(); p.ln_b = dlb.as<float>(); p.eps = eps;
-    p.h = h ? dh.p : nullptr; p.M = (int)M; p.D = (int)D; p.K = (int)K;
-    if (const char* pf = getenv("CLIPGPU_ROWLN_PF")) p.pf = atoi(pf);
-    TCHECK(launch_gemm_rowln(dt, p, nullptr));
-    TCHECK(hipDeviceSynchronize());
-    down(x, dx.p, M * D * 4);
-    if (h) down16(dt, h, dh.p, M * D);
-  });
-}
-
-int clipgpu_test_gemm_rowln_bench(int dtype, int mode, int64_t M, int64_t D, int64_t K, int iters,
-                                  double* us_per_launch) {
-  return guarded([&]() {
-    const DType dt = dt_of(dtype);
-    if (M <= 0 || !gemm_rowln_supported((int)D, (int)K) || iters <= 0 || !us_per_launch)
-      throw ClipErr(CLIPGPU_ERR_INVALID, "bad rowln bench arguments");
-    DevBuf fA(M * K * 4), fW(D * K * 4), dA(M * K * 2), dW(D * K * 2), dB(D * 4), dx(M * D * 4), dlw(D * 4),
-        dlb(D * 4), dh(M * D * 2);
-    hipLaunchKernelGGL(fill_random, dim3(2048), dim3(256), 0, nullptr, fA.as<float>(), (long)(M * K), 1u);
-    hipLaunchKernelGGL(fill_random, dim3(2048), dim3(256), 0, nullptr, fW.as<float>(), (long)(D * K), 2u);
-    hipLaunchKernelGGL(fill_random, dim3(64), dim3(256), 0, nullptr, dB.as<float>(), (long)D, 3u);
-    hipLaunchKernelGGL(fill_random, dim3(64), dim3(256), 0, nullptr, dlw.as<float>(), (long)D, 4u);
-    hipLaunchKernelGGL(fill_random, dim3(64), dim3(256), 0, nullptr, dlb.as<float>(), (long)D, 5u);
-    TCHECK(launch_cast_f32(dt, fA.as<float>(), dA.p, (long)(M * K), nullptr));
-    TCHECK(launch_cast_f32(dt, fW.as<float>(), dW.p, (long)(D * K), nullptr));
-    TCHECK(hipDeviceSynchronize());
-    RowLnParams p;
-    p.A = dA.p; p.lda = K; p.W = dW.p; p.ldw = K; p.bias = dB.as<float>(); p.x = dx.as<float>();
-    p.ln_w = dlw.as<float>(); p.ln_b = dlb.as<float>(); p.h = mode == 2 ? nullptr : dh.p;
-    p.M = (int)M; p.D = (int)D; p.K = (int)K;
-    if (const char* pf = getenv("CLIPGPU_ROWLN_PF")) p.pf = atoi(pf);
-    GemmParams g{};  // mode 1: the unfused pair (tiled residual GEMM + ln_rows_add)
-    g.A = dA.p; g.lda = K; g.W = dW.p; g.ldw = K; g.bias = dB.as<float>();
-    g.out = dx.p; g.ldo = D; g.M = (int)M; g.N = (int)D; g.K = (int)K; g.tile = tile_override();
-    auto run = [&]() {
-      if (mode != 1) {
-        TCHECK(launch_gemm_rowln(dt, p, nullptr));
-      } else {
-        TCHECK(launch_gemm(dt, A_ROWS, EPI_RESID, 0, g, nullptr));
-        TCHECK(launch_ln_rows_add(dt, dx.as<float>(), nullptr, dlw.as<float>(), dlb.as<float>(), 1e-5f, dh.p, (int)M,
-                                  (int)D, nullptr));
-      }
-    };
-    for (int i = 0; i < 3; ++i) run();
-    hipEvent_t a, b;
-    TCHECK(hipEventCreate(&a));
-    TCHECK(hipEventCreate(&b));
-    TCHECK(hipEventRecord(a, nullptr));
-    for (int i = 0; i < iters; ++i) run();
     TCHECK(hipEventRecord(b, nullptr));
     TCHECK(hipEventSynchronize(b));
     float ms = 0.f;
@@ -508,31 +431,6 @@ int clipgpu_diag_gemm_stamps(int dtype, int epi, int act, int64_t M, int64_t N, 
   });
 }
 
-// The fused residual GEMM + LayerNorm with stamps (gemm_rowln.hip slots); with_ln 0: no LN output.
-int clipgpu_diag_rowln_stamps(int dtype, int64_t M, int64_t D, int64_t K, int pf, int with_ln,
-                              unsigned long long* out, int nblocks) {
-  return guarded([&]() {
-    const DType dt = dt_of(dtype);
-    DevBuf fA(M * K * 4), fW(D * K * 4), dA(M * K * 2), dW(D * K * 2), dB(D * 4), dx(M * D * 4), dl(D * 4),
-        dh(M * D * 2);
-    hipLaunchKernelGGL(fill_random, dim3(2048), dim3(256), 0, nullptr, fA.as<float>(), (long)(M * K), 1u);
-    hipLaunchKernelGGL(fill_random, dim3(2048), dim3(256), 0, nullptr, fW.as<float>(), (long)(D * K), 2u);
-    hipLaunchKernelGGL(fill_random, dim3(64), dim3(256), 0, nullptr, dB.as<float>(), (long)D, 3u);
-    hipLaunchKernelGGL(fill_random, dim3(64), dim3(256), 0, nullptr, dl.as<float>(), (long)D, 4u);
-    TCHECK(launch_cast_f32(dt, fA.as<float>(), dA.p, (long)(M * K), nullptr));
-    TCHECK(launch_cast_f32(dt, fW.as<float>(), dW.p, (long)(D * K), nullptr));
-    RowLnParams p;
-    p.A = dA.p; p.lda = K; p.W = dW.p; p.ldw = K; p.bias = dB.as<float>(); p.x = dx.as<float>();
-    p.ln_w = dl.as<float>(); p.ln_b = dl.as<float>(); p.h = with_ln ? dh.p : nullptr;
-    p.M = (int)M; p.D = (int)D; p.K = (int)K; p.pf = pf;
-    for (int i = 0; i < 20; ++i) TCHECK(launch_gemm_rowln(dt, p, nullptr));
-    TCHECK(hipDeviceSynchronize());
-    TCHECK(read_rowln_stamps(nullptr, nblocks, true));
-    TCHECK(launch_gemm_rowln(dt, p, nullptr));
-    TCHECK(hipDeviceSynchronize());
-    TCHECK(read_rowln_stamps(out, nblocks, false));
-  });
-}
 #endif
 
 }  // extern "C"

@@ -77,8 +77,7 @@ _PROTOS = [
     ("clipgpu_test_resize_rgb8_gpu", c_int, [POINTER(c_void_p), POINTER(c_int), POINTER(c_int), c_int64, c_int, c_char_p, c_char_p, c_void_p]),
     ("clipgpu_test_lane_reduce", c_int, [c_void_p, c_void_p]),
     ("clipgpu_test_patch_rows", c_int, [c_int, c_int, c_int64, c_int64, c_int64, c_void_p, POINTER(c_float), POINTER(c_float), c_void_p]),
-    ("clipgpu_test_gemm_rowln", c_int, [c_int, c_int64, c_int64, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_void_p]),
-    ("clipgpu_test_gemm_rowln_bench", c_int, [c_int, c_int, c_int64, c_int64, c_int64, c_int, POINTER(c_double)]),
+    ("clipgpu_test_clock_probe", c_int, [c_void_p, c_int64, c_void_p]),
     ("clipgpu_test_attention_bench", c_int, [c_int, c_int64, c_int64, c_int64, c_int64, c_int, c_int, POINTER(c_double)]),
     ("clipgpu_test_quant_rows", c_int, [c_int64, c_int64, c_void_p, c_void_p, c_void_p]),
     ("clipgpu_test_layernorm_mx", c_int, [c_int64, c_int64, c_float, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),

@@ -14,9 +14,17 @@ from ._lib import check, f3, lib
 
 
 class Options(ctypes.Structure):
-    """``clipgpu_options`` (include/clipgpu.h): per-engine settings of clipgpu_create_ex."""
+    """``clipgpu_options`` (include/clipgpu.h, ABI v3): per-engine settings of clipgpu_create_ex.  The
+    library reads no environment variables: every engine behaviour is one of these fields."""
     _fields_ = [("struct_size", ctypes.c_uint32), ("mx_sites", ctypes.c_uint32), ("lanes", ctypes.c_int32),
-                ("tuning", ctypes.c_int32), ("communicator", ctypes.c_int32)]
+                ("tuning", ctypes.c_int32), ("communicator", ctypes.c_int32),
+                ("graphs", ctypes.c_int32), ("prune_last", ctypes.c_int32), ("trim_text", ctypes.c_int32),
+                ("gemm_tiles", ctypes.c_int32 * 4), ("patch_tile", ctypes.c_int32), ("mx_layers", ctypes.c_uint32)]
+
+
+def _tristate(v) -> int:
+    """None -> 0 (the default), True -> 1, False -> -1 (clipgpu_options on/off fields)."""
+    return 0 if v is None else (1 if v else -1)
 
 
 MX_SITE_BITS = {"qkv": 1, "fc": 2, "proj": 4}  # CLIPGPU_MX_QKV / _FC / _PROJ
@@ -38,26 +46,50 @@ def mx_site_bits(sites) -> int:
 
 class Engine:
     def __init__(self, model_dir: str, tower: int, devices: Optional[Sequence[int]] = None,
-                 dtype: str = "bf16", max_batch: int = 256, mx_sites=None, lanes: int = 0, tuning: bool = False,
-                 communicator: bool = False):
+                 dtype: str = "bf16", max_batch: int = 256, mx_sites=None, lanes: int = 0, tuning=False,
+                 communicator: bool = False, graphs: Optional[bool] = None, prune_last: Optional[bool] = None,
+                 trim_text: Optional[bool] = None, gemm_tiles: Optional[Sequence[int]] = None, patch_tile: int = 0,
+                 mx_layers=None):
         """mx_sites: fp8 engines' MX split ("qkv,fc,proj" by default); lanes: concurrent sub-batch lanes
-        (0 = the tile table's); tuning: time the GEMM tiles at creation instead of the committed table;
-        communicator: create a multi-device handle's RCCL communicator now, not on the first gather."""
+        (0 = the tile table's); tuning: time the GEMM tiles at creation instead of the committed table
+        (True / 1: per site + whole forwards, 2: per site only); communicator: create a multi-device
+        handle's RCCL communicator now, not on the first gather; graphs / prune_last / trim_text: None =
+        the default (on), False = off (all bit-identical); gemm_tiles: [qkv, out_proj, c_fc, c_proj]
+        GemmTile ids (0 = the table's, -1 = the shape heuristic), patch_tile likewise; mx_layers: fp8
+        engines' layers that run their MX sites in MX-fp8 (a bit mask or a list of layer indices;
+        None = every layer)."""
         self.model_dir = model_dir
         self.tower = tower
         self.devices = list(devices) if devices else [0]
         self.dtype = dtype
         self.max_batch = int(max_batch)
-        self.opts = {"mx_sites": mx_sites, "lanes": int(lanes), "tuning": bool(tuning),
-                     "communicator": bool(communicator)}  # duplicate() rebuilds with the same
+        self.opts = {"mx_sites": mx_sites, "lanes": int(lanes), "tuning": tuning, "communicator": bool(communicator),
+                     "graphs": graphs, "prune_last": prune_last, "trim_text": trim_text,
+                     "gemm_tiles": list(gemm_tiles) if gemm_tiles else None, "patch_tile": int(patch_tile),
+                     "mx_layers": mx_layers}  # duplicate() rebuilds with the same
         dt = {"bf16": _lib.DTYPE_BF16, "f16": _lib.DTYPE_F16, "fp16": _lib.DTYPE_F16, "fp8": _lib.DTYPE_FP8}[dtype]
         devs = (c_int * len(self.devices))(*self.devices)
         opts = Options()
         check(lib().clipgpu_options_init(ctypes.byref(opts)))
         opts.mx_sites = mx_site_bits(mx_sites)
         opts.lanes = int(lanes)
-        opts.tuning = 1 if tuning else 0
+        opts.tuning = int(tuning) if not isinstance(tuning, bool) else (1 if tuning else 0)
         opts.communicator = 1 if communicator else 0
+        opts.graphs = _tristate(graphs)
+        opts.prune_last = _tristate(prune_last)
+        opts.trim_text = _tristate(trim_text)
+        if gemm_tiles:
+            if len(gemm_tiles) != 4:
+                raise ValueError("gemm_tiles: four GemmTile ids (qkv, out_proj, c_fc, c_proj)")
+            for i, t in enumerate(gemm_tiles):
+                opts.gemm_tiles[i] = int(t)
+        opts.patch_tile = int(patch_tile)
+        if mx_layers is not None:
+            if not isinstance(mx_layers, int):
+                mx_layers = sum(1 << int(l) for l in mx_layers)
+            if mx_layers == 0:
+                raise ValueError("mx_layers: at least one layer (None = every layer)")
+            opts.mx_layers = int(mx_layers)
         h = c_void_p()
         check(lib().clipgpu_create_ex(model_dir.encode(), tower, devs, len(self.devices), dt, self.max_batch,
                                       ctypes.byref(opts), ctypes.byref(h)))
@@ -176,7 +208,8 @@ class Engine:
         ins = (c_void_p * k)(*[c_void_p(p) for p in d_in])
         outs = (c_void_p * k)(*[c_void_p(p) for p in d_out])
         rs = (ctypes.c_int64 * len(rows))(*[int(r) for r in rows])
-        sts = (c_void_p * k)(*[c_void_p(s or None) for s in (streams or [0] * k)])
+        # streams None: a NULL array (every device's legacy default stream, as a NULL entry is)
+        sts = None if streams is None else (c_void_p * k)(*[c_void_p(s or None) for s in streams])
         check(fn(self.handle, ins, rs, outs, sts))
 
     def embed_pixels_gather_device(self, d_in, rows, d_out, streams=None) -> None:

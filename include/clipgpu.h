@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define CLIPGPU_ABI_VERSION 2
+#define CLIPGPU_ABI_VERSION 3
 
 enum clipgpu_status {
   CLIPGPU_OK = 0,
@@ -79,15 +79,30 @@ void clipgpu_destroy(clipgpu_engine* e);
 #define CLIPGPU_MX_FC 2u   /* c_fc */
 #define CLIPGPU_MX_PROJ 4u /* c_proj (needs CLIPGPU_MX_FC: c_fc's epilogue quantizes the hidden rows) */
 typedef struct clipgpu_options {
-  uint32_t struct_size; /* sizeof(clipgpu_options) (set by clipgpu_options_init) */
-  uint32_t mx_sites;    /* fp8 engines: CLIPGPU_MX_* bits; 0 = default (all three; the
-                           CLIPGPU_MX_SITES environment variable, if set, replaces the default) */
+  uint32_t struct_size; /* sizeof(clipgpu_options) (set by clipgpu_options_init); an older caller's
+                           smaller struct keeps the defaults of the fields it does not have */
+  uint32_t mx_sites;    /* fp8 engines: CLIPGPU_MX_* bits; 0 = default (all three) */
   int32_t lanes;        /* concurrent sub-batch lanes per device, 1..4; 0 = the tile table's choice */
   int32_t tuning;       /* 0 = GEMM tiles and lanes from the committed MI355X tile table
-                           (deterministic, default); 1 = time the candidates at creation (the choice
-                           then depends on the timings; never changes the output bits) */
+                           (deterministic, default); 1 = time the candidates at creation, per site and
+                           then over whole forwards; 2 = the per-site timing only (the choice then
+                           depends on the timings; it never changes the output bits) */
   int32_t communicator; /* handles over > 1 distinct devices: 1 = create the RCCL communicator at
                            creation; 0 (default) = on the first gathered call */
+  /* ---- ABI v3 (round 4): every engine behaviour is a field here; the library reads no
+   * environment variables.  0 is the default everywhere. */
+  int32_t graphs;       /* 0 / 1 = replay each forward as a captured hipGraph (default); -1 = launch
+                           the kernels directly (bit-identical) */
+  int32_t prune_last;   /* 0 / 1 = the last layer runs on the pooled rows only (default; bit-identical);
+                           -1 = on every token */
+  int32_t trim_text;    /* 0 / 1 = host-id text batches run on their first max(EOT index) + 1 tokens
+                           (default; bit-identical); -1 = on the full context */
+  int32_t gemm_tiles[4]; /* GEMM tile per trunk site (qkv, out_proj, c_fc, c_proj): 0 = the table's
+                           (or tuner's) choice, -1 = the shape heuristic, else a GemmTile id the library
+                           builds (csrc/kernels/kernels.hpp kGemmTiles; speed only, never the bits) */
+  int32_t patch_tile;   /* the vision patch-embedding GEMM's tile, as gemm_tiles */
+  uint32_t mx_layers;   /* fp8 engines: bit l set = layer l runs its MX sites in MX-fp8, the other layers
+                           run every GEMM in bf16; 0 = every layer (default) */
 } clipgpu_options;
 /* Fills *opts with the defaults. */
 int clipgpu_options_init(clipgpu_options* opts);
@@ -218,8 +233,9 @@ int clipgpu_similarity_device(const float* d_img, int64_t n_img, const float* d_
  * (nranks, first rank of this handle); nranks 0 = no communicator.
  * Gathered forward: rows[nranks] = every rank's block size (identical on every rank); per LOCAL
  * device i (rank = first rank + i): d_in[i] = that rank's block on device i (f32 NCHW normalised
- * pixels / i64 ids [rows][T]), d_out[i] = [sum rows][E] f32 on device i, streams[i] (NULL entry or
- * array: the handle's stream).  Each rank embeds its block into its slot, then one collective
+ * pixels / i64 ids [rows][T]), d_out[i] = [sum rows][E] f32 on device i, streams[i] (a NULL entry, or
+ * a NULL array: device i's legacy default stream, as for the single-device *_device entry points).
+ * Each rank embeds its block into its slot, then one collective
  * (in-place ncclAllGather for equal blocks; one ncclBroadcast per block otherwise) leaves the
  * whole matrix in rank order on every device.  Stream-ordered; collective over all ranks. */
 int clipgpu_comm_unique_id(uint8_t* id /* [128] */);

@@ -17,8 +17,8 @@ extern "C" {
 
 /* out[M][N] = act(A[M][K] . W[N][K]^T + bias[N]) (act: 0 none, 1 quick_gelu, 2 gelu, 3 gelu_tanh).
  * mode 0: 16-bit output (returned as f32); mode 1: residual (out = resid + ...); mode 2: f32 output.
- * bias and resid may be NULL.  CLIPGPU_TEST_TILE = a GemmTile id (kernels.hpp: 0 auto, 1..TILE_LAST
- * the tiled kernels, 100 skinny) forces the tile; CLIPGPU_GEMM_PIPE3=1 the 3-stage schedule. */
+ * bias and resid may be NULL.  CLIPGPU_TEST_TILE = a GemmTile id the library builds (kernels.hpp
+ * kGemmTiles; 0 auto, 100 skinny) forces the tile (test hooks only: the engine reads no environment). */
 int clipgpu_test_gemm(int dtype, int mode, int act, int64_t M, int64_t N, int64_t K, const float* A,
                       const float* W, const float* bias, const float* resid, float* out);
 
@@ -57,16 +57,12 @@ int clipgpu_test_patch_rows(int dtype, int mode, int64_t B, int64_t S, int64_t P
 int clipgpu_test_gemm_bench(int dtype, int epi, int act, int64_t M, int64_t N, int64_t K, int tile, int iters,
                             double* us_per_launch);
 
-/* Row-complete residual GEMM + LayerNorm (gemm_rowln.hip): x[M][D] += A[M][K] . W[D][K]^T + bias
- * (in place, f32), then h[M][D] = LN(x) * ln_w + ln_b (16-bit, returned as f32; skipped when h is
- * NULL).  D in {512, 768, 1024}, K % 32 == 0. */
-int clipgpu_test_gemm_rowln(int dtype, int64_t M, int64_t D, int64_t K, const float* A, const float* W,
-                            const float* bias, float* x, const float* ln_w, const float* ln_b, float eps, float* h);
-/* Its timing (random operands): mode 0 the fused kernel, 2 the fused kernel without the LN output,
- * 1 the unfused pair (residual GEMM with
- * CLIPGPU_TEST_TILE's tile + ln_rows_add).  Mean µs per launch (pair) over `iters`. */
-int clipgpu_test_gemm_rowln_bench(int dtype, int mode, int64_t M, int64_t D, int64_t K, int iters,
-                                  double* us_per_launch);
+/* Shader-clock probe (bench.py's per-window clock): launches ONE wave on `stream` (a hipStream_t, NULL =
+ * the legacy default stream) that sleeps for duration_us of wall time (s_memrealtime, 100 MHz) and writes
+ * d_out[0] = shader-clock ticks (s_memtime) and d_out[1] = 100 MHz ticks elapsed over that span (device
+ * uint64 buffer of 2).  Launched on a side stream beside a timed forward it reads the clock the chip holds
+ * under that load (MI355X_MICROARCH.md, DVFS give-back item 6): MHz = 100 * d_out[0] / d_out[1].  Asynchronous. */
+int clipgpu_test_clock_probe(void* stream, int64_t duration_us, uint64_t* d_out);
 
 /* Device-resident attention timing (random 16-bit qkv): mean µs per launch_attention over `iters`. */
 int clipgpu_test_attention_bench(int dtype, int64_t B, int64_t N, int64_t H, int64_t HD, int causal, int iters,
@@ -98,12 +94,9 @@ int clipgpu_test_gemm_mx_bench(int epi, int act, int64_t M, int64_t N, int64_t K
  * n = element count. */
 int clipgpu_test_read_weights(const char* model_dir, int tower, const char* name, float* out, int64_t n);
 
-/* GEMM tile chosen per trunk call site of an engine (0 qkv, 1 out_proj, 2 c_fc, 3 c_proj):
- * 1 128x128, 2 256x128, 3 256x256, 4 128x128 pipelined, 5 128x64 pipelined, 6 64x128 pipelined,
- * 0 shape heuristic; fp8 engines report MxTile ids at the qkv / c_fc / c_proj sites (2 256x128,
- * 3 128x128).  Before clipgpu_create, set
- * CLIPGPU_GEMM_AUTOTUNE=0 to skip the creation-time tuning, or CLIPGPU_GEMM_TILES="q,o,f,p"
- * to pin the four sites. */
+/* GEMM tile chosen per trunk call site of an engine (0 qkv, 1 out_proj, 2 c_fc, 3 c_proj): a GemmTile
+ * id (kernels.hpp), 0 = the shape heuristic; fp8 engines report MxTile ids at their MX sites (2 256x128,
+ * 3 128x128).  clipgpu_options.gemm_tiles pins them. */
 struct clipgpu_engine;
 int clipgpu_test_engine_tiles(const struct clipgpu_engine* e, int tiles[4]);
 /* Concurrent sub-batches the engine's device-side forwards run (the creation-time tuning's pick,

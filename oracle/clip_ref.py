@@ -6,7 +6,7 @@ model.encode_text(x, normalize=True)`` (open-clip-torch 3.2.0, ``pull_onnx.py:7`
 the crate runs them verbatim (``src/vision.rs:108-113``, ``src/text.rs:156-166``)
 and returns the graph output as the embedding (``README.md:81-82``: "already l2
 normalized").  This module restates that arithmetic in float64 (default) or
-float32 numpy.  Pinned against HF ``transformers`` CLIP (tests/test_oracle_pin.py).
+float32 numpy.  Pinned against HF ``transformers`` CLIP / Siglip (tests/test_cpu_oracle.py).
 """
 from __future__ import annotations
 

@@ -7,7 +7,7 @@ separable convolution resize (CatmullRom for "bicubic", triangle for "bilinear",
 algorithm, a port of Pillow-SIMD): precompute_coefficients (taps floor(c - r) ..
 ceil(c + r), weights filter((x - (c - 0.5)) / max(scale, 1)) normalised by their sum)
 then Normalizer16 (i16 coefficients at the largest precision p < 22 with
-round(max weight * 2^(p+1)) < 2^15, rounded half away from zero), i32 sums from
+round(max weight * 2^p) < 2^15, so p = 14 for a unit tap; rounded half away from zero), i32 sums from
 2^(p-1), clamp(sum >> p, 0, 255), horizontal pass then vertical pass through a u8
 intermediate.  Pinned against Pillow 12.2 within one level (its 22-bit scheme;
 tests/test_cpu_preprocess.py).  Small images only (Python loops).

@@ -35,7 +35,7 @@ def test_library_exports_every_declared_symbol():
     missing = [n for n in names if not hasattr(L, n)]
     assert not missing, missing
     assert set(_lib.SYMBOLS) == names  # the ctypes binding covers exactly the headers
-    assert L.clipgpu_abi_version() == 2
+    assert L.clipgpu_abi_version() == 3
 
 
 def test_no_oracle_in_product():
@@ -175,17 +175,39 @@ def test_library_provenance_is_checked(monkeypatch):
         _lib._check_provenance(L)
 
 
-def test_bench_names_every_gemm_tile():
-    """bench.py reports the autotuned tiles by name: its table covers every GemmTile id the tuners
-    can pick (kernels.hpp TILE_LAST), so a new tile cannot crash the bench line."""
-    import importlib.util
+def _built_tiles():
+    """kernels.hpp kGemmTiles: the GemmTile ids the library builds."""
     hdr = open(os.path.join(ROOT, "clip-embedder-rs_amd", "csrc", "kernels", "kernels.hpp")).read()
     ids = {m.group(1): int(m.group(2)) for m in re.finditer(r"\b(TILE_\w+)\s*=\s*(\d+)", hdr)}
-    last = ids[re.search(r"TILE_LAST\s*=\s*(TILE_\w+)", hdr).group(1)]
+    body = re.search(r"kGemmTiles\[\]\s*=\s*\{([^}]*)\}", hdr).group(1)
+    return [ids[n.strip()] for n in body.split(",") if n.strip()]
+
+
+def test_bench_names_every_gemm_tile():
+    """bench.py reports the tiles by name: its table covers every GemmTile id the library builds
+    (kernels.hpp kGemmTiles), so a new tile cannot crash the bench line; the GPU tests' tile lists
+    cover exactly the built tiles."""
+    import importlib.util
+    built = _built_tiles()
     spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
     bench = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(bench)
-    assert set(range(0, last + 1)) <= set(bench.TILE_NAMES)
+    assert set(built) | {0} <= set(bench.TILE_NAMES)
+    for f in ("test_gpu_kernels.py", "test_gpu_parity.py"):
+        src = open(os.path.join(ROOT, "tests", f)).read()
+        listed = re.search(r"BUILT_TILES = \[([^\]]*)\]", src).group(1)
+        assert sorted(int(x) for x in listed.split(",")) == sorted(built), f
+
+
+def test_engine_reads_no_environment():
+    """ABI v3: every engine behaviour is a clipgpu_options field; the product sources read no
+    environment variable (the kernel-level test hooks in testing.hip take CLIPGPU_TEST_TILE only)."""
+    csrc = os.path.join(ROOT, "clip-embedder-rs_amd", "csrc")
+    for dirpath, _, files in os.walk(csrc):
+        for f in files:
+            if f.endswith((".hip", ".cpp", ".hpp")) and f != "testing.hip":
+                src = open(os.path.join(dirpath, f)).read()
+                assert "getenv(" not in src, os.path.join(dirpath, f)
 
 
 def test_options_init_and_validation():
@@ -207,6 +229,21 @@ def test_options_init_and_validation():
             Engine(d, 0, [0], "bf16", 8, **kw)
     with pytest.raises(ClipError, match="proj in MX needs fc"):
         Engine(d, 0, [0], "fp8", 8, mx_sites="qkv,proj")
+    for kw, msg in (({"gemm_tiles": [4, 0, 0, 0]}, "not a GEMM tile"), ({"patch_tile": 19}, "not a GEMM tile"),
+                    ({"mx_layers": [0, 3]}, "mx_layers needs dtype"), ({"tuning": 3}, "tuning must be")):
+        with pytest.raises(ClipError, match=msg):
+            Engine(d, 0, [0], "bf16", 8, **kw)
+    with pytest.raises(ValueError):
+        Engine(d, 0, [0], "bf16", 8, gemm_tiles=[17, 17])
+    o2 = Options()
+    _lib.check(_lib.lib().clipgpu_options_init(ctypes.byref(o2)))
+    assert (o2.graphs, o2.prune_last, o2.trim_text, list(o2.gemm_tiles), o2.patch_tile, o2.mx_layers) == (
+        0, 0, 0, [0, 0, 0, 0], 0, 0)
+    o2.graphs = 2
+    h = ctypes.c_void_p()
+    devs = (ctypes.c_int * 1)(0)
+    rc = _lib.lib().clipgpu_create_ex(d.encode(), 0, devs, 1, 0, 8, ctypes.byref(o2), ctypes.byref(h))
+    assert rc != 0 and b"graphs" in _lib.lib().clipgpu_last_error()
     # a struct_size the library does not know is refused
     o.struct_size = 1
     h = ctypes.c_void_p()

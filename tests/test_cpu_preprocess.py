@@ -152,7 +152,7 @@ def test_preprocess_batch_image_backend():
                                                    (224, 224, "bicubic"), (97, 48, "bilinear"), (50, 400, "bilinear")])
 def test_fast_image_resize_coefficient_precision(in_size, out_size, filt):
     """Normalizer16 (fast_image_resize 6.0.0, ported from Pillow-SIMD): the axis precision p is the
-    largest p < 22 with round(max weight * 2^(p+1)) >= 2^15 only at p itself (i16 headroom), every
+    largest p < 22 with round(max weight * 2^p) < 2^15 (i16 headroom; round(max w * 2^(p+1)) no longer fits), every
     coefficient is round-half-away(w * 2^p) and fits an i16, and each output's coefficients sum to
     2^p within the rounding of its taps."""
     f, sup = (preprocess_ref._cubic, 2.0) if filt == "bicubic" else (preprocess_ref._triangle, 1.0)

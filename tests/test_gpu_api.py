@@ -305,15 +305,13 @@ def test_rccl_communicator_and_gathered_entry_points(monkeypatch):
     assert multi.comm_info() == (0, 0)
 
 
-def test_tile_table_is_deterministic_and_bit_invisible(monkeypatch):
+def test_tile_table_is_deterministic_and_bit_invisible():
     """The default tile choice is the committed table (engine.hip table_tiles): two engines of
     the bench's configuration pick the same tiles and one lane on any box; a creation-time timing
     tuner (clipgpu_options.tuning) may pick others, with the same output bits."""
     from oracle.model_spec import VIT_B_32_CFG
     from open_clip_inference.engine import Engine
     from tests.helpers import normalized_pixels
-    for var in ("CLIPGPU_LANES", "CLIPGPU_GEMM_TILES", "CLIPGPU_GEMM_AUTOTUNE"):
-        monkeypatch.delenv(var, raising=False)
     d = make_model_dir(VIT_B_32_CFG, seed=1234)
     a = Engine(d, 0, [0], "bf16", 256)
     b = Engine(d, 0, [0], "bf16", 256)

@@ -39,13 +39,10 @@ def _tiles(engine):
     return list(t)
 
 
-def test_bench_vision_config_matches_oracle(bench_mod, monkeypatch):
+def test_bench_vision_config_matches_oracle(bench_mod):
     import torch
     from open_clip_inference import _lib
     from open_clip_inference.engine import Engine
-    for var in ("CLIPGPU_LANES", "CLIPGPU_GEMM_TILES", "CLIPGPU_GEMM_AUTOTUNE", "CLIPGPU_TUNE_FORWARD",
-                "CLIPGPU_PRUNE_LAST", "CLIPGPU_GRAPHS", "CLIPGPU_GEMM_SPLIT"):
-        monkeypatch.delenv(var, raising=False)
     B = bench_mod.B_VISION
     dev = torch.device("cuda", 0)
     ve = Engine(bench_mod.make_model_dir(), _lib.TOWER_VISION, [0], "bf16", B)
@@ -69,13 +66,10 @@ def test_bench_vision_config_matches_oracle(bench_mod, monkeypatch):
     ve.close()
 
 
-def test_bench_text_config_matches_oracle(bench_mod, monkeypatch):
+def test_bench_text_config_matches_oracle(bench_mod):
     import torch
     from open_clip_inference import _lib
     from open_clip_inference.engine import Engine
-    for var in ("CLIPGPU_LANES", "CLIPGPU_GEMM_TILES", "CLIPGPU_GEMM_AUTOTUNE", "CLIPGPU_TUNE_FORWARD",
-                "CLIPGPU_PRUNE_LAST", "CLIPGPU_GRAPHS", "CLIPGPU_GEMM_SPLIT"):
-        monkeypatch.delenv(var, raising=False)
     B = bench_mod.B_TEXT
     dev = torch.device("cuda", 0)
     te = Engine(bench_mod.make_model_dir(), _lib.TOWER_TEXT, [0], "bf16", B)
@@ -102,29 +96,38 @@ def test_bench_text_config_matches_oracle(bench_mod, monkeypatch):
 
 
 @pytest.mark.parametrize("tower", ["vision", "text"])
-@pytest.mark.parametrize("which", ["default", "side"])
-def test_device_entry_is_ordered_on_the_callers_stream(bench_mod, tower, which, monkeypatch):
+@pytest.mark.parametrize("which", ["default", "side", "null_array"])
+@pytest.mark.parametrize("entry", ["plain", "gather"])
+def test_device_entry_is_ordered_on_the_callers_stream(bench_mod, tower, which, entry):
     """include/clipgpu.h: the *_device entry points are stream-ordered on the caller's stream.
     The output is filled with NaN, the forward is enqueued, and a copy of the output is enqueued
     right behind it on the same stream with no synchronization in between: the copy must see the
     finished embeddings -- for torch's default (legacy null) stream and for a created stream, at
-    the bench's batch (milliseconds of work, so a missing join would be caught)."""
+    the bench's batch (milliseconds of work, so a missing join would be caught).  The gathered
+    entry points (one-rank communicator: the forward + the in-place all-gather) likewise, where a
+    NULL entry -- or a NULL streams array ("null_array") -- is the legacy default stream too."""
     import torch
     from open_clip_inference import _lib
     from open_clip_inference.engine import Engine
-    for var in ("CLIPGPU_LANES", "CLIPGPU_GEMM_TILES", "CLIPGPU_GEMM_AUTOTUNE", "CLIPGPU_GRAPHS"):
-        monkeypatch.delenv(var, raising=False)
+    if which == "null_array" and entry == "plain":
+        pytest.skip("a NULL streams array exists only on the gathered entry points")
     dev = torch.device("cuda", 0)
     px, ids = bench_mod.synth_inputs(0, dev)
     B = bench_mod.B_VISION if tower == "vision" else bench_mod.B_TEXT
     e = Engine(bench_mod.make_model_dir(), _lib.TOWER_VISION if tower == "vision" else _lib.TOWER_TEXT,
                [0], "bf16", B)
-    s = torch.cuda.current_stream(dev) if which == "default" else torch.cuda.Stream(dev)
+    if entry == "gather":
+        e.comm_init_rank(Engine.comm_unique_id(), 1, 0)
+    s = torch.cuda.current_stream(dev) if which != "side" else torch.cuda.Stream(dev)
     out = torch.empty((B, 512), device=dev, dtype=torch.float32)
     with torch.cuda.stream(s):
         for rep in range(3):  # capture, then replays of the graph
             out.fill_(float("nan"))
-            if tower == "vision":
+            if entry == "gather":
+                gather = e.embed_pixels_gather_device if tower == "vision" else e.embed_tokens_gather_device
+                gather([(px if tower == "vision" else ids).data_ptr()], [B], [out.data_ptr()],
+                       None if which == "null_array" else [s.cuda_stream])
+            elif tower == "vision":
                 e.embed_pixels_device(px.data_ptr(), B, out.data_ptr(), s.cuda_stream)
             else:
                 e.embed_tokens_device(ids.data_ptr(), B, out.data_ptr(), s.cuda_stream)

@@ -188,10 +188,10 @@ def _fp8_check(got, ref, label, bar=None):
     return cos
 
 
-def _engine(cfg, tower, dtype, max_batch):
+def _engine(cfg, tower, dtype, max_batch, **opts):
     from open_clip_inference.engine import Engine
     from tests.helpers import make_model_dir
-    return Engine(make_model_dir(cfg, 1234), tower, [0], dtype, max_batch)
+    return Engine(make_model_dir(cfg, 1234), tower, [0], dtype, max_batch, **opts)
 
 
 def test_fp8_vit_b32_vision_and_text():
@@ -211,7 +211,7 @@ def test_fp8_vit_b32_vision_and_text():
     _fp8_check(te.embed_tokens(ids), clip_ref.encode_text(weights.text_weights(t, 1234), t, ids), "ViT-B/32 text")
 
 
-def test_fp8_lanes_and_batch_split_are_bit_exact(monkeypatch):
+def test_fp8_lanes_and_batch_split_are_bit_exact():
     """Row results do not depend on the batch composition or the lane split (no cross-row state
     in the MX quantization: scales are per row)."""
     from oracle import weights
@@ -219,10 +219,9 @@ def test_fp8_lanes_and_batch_split_are_bit_exact(monkeypatch):
     from tests.helpers import normalized_pixels, specs
     v, _ = specs(VIT_B_32_CFG)
     px = normalized_pixels(weights.synth_images_u8(8, 40, v.image_size), OPENAI_MEAN, OPENAI_STD)
-    monkeypatch.setenv("CLIPGPU_GEMM_AUTOTUNE", "0")
-    a = _engine(VIT_B_32_CFG, 0, "fp8", 64).embed_pixels(px)
-    monkeypatch.setenv("CLIPGPU_LANES", "1")
-    b = _engine(VIT_B_32_CFG, 0, "fp8", 64).embed_pixels(px)
+    heur = [-1, -1, -1, -1]
+    a = _engine(VIT_B_32_CFG, 0, "fp8", 64, gemm_tiles=heur, lanes=2).embed_pixels(px)
+    b = _engine(VIT_B_32_CFG, 0, "fp8", 64, gemm_tiles=heur, lanes=1).embed_pixels(px)
     assert np.array_equal(a, b)
 
 
@@ -291,8 +290,8 @@ def test_fp8_input_paths_agree():
 
 
 @pytest.mark.parametrize("cfg_name", ["VIT_B_32_CFG", "VIT_H_14_378_CFG"])
-def test_fp8_qkv_only_split_meets_the_north_star_bar_on_clip_vision(cfg_name, monkeypatch):
-    """CLIPGPU_MX_SITES=qkv (only the QKV projection in MX-fp8): the CLIP vision towers keep
+def test_fp8_qkv_only_split_meets_the_north_star_bar_on_clip_vision(cfg_name):
+    """mx_sites = qkv (only the QKV projection in MX-fp8): the CLIP vision towers keep
     cos >= 0.9999 against the fp64 oracle (the ablation's one split that does)."""
     from oracle import model_spec, weights
     from oracle.model_spec import OPENAI_MEAN, OPENAI_STD
@@ -300,15 +299,15 @@ def test_fp8_qkv_only_split_meets_the_north_star_bar_on_clip_vision(cfg_name, mo
     cfg = getattr(model_spec, cfg_name)
     v, _ = specs(cfg)
     px = normalized_pixels(weights.synth_images_u8(13, 2, v.image_size), OPENAI_MEAN, OPENAI_STD)
-    monkeypatch.setenv("CLIPGPU_MX_SITES", "qkv")
-    e = _engine(cfg, 0, "fp8", 2)
+    e = _engine(cfg, 0, "fp8", 2, mx_sites="qkv")
     _fp8_check(e.embed_pixels(px), clip_ref.encode_image(weights.vision_weights(v, 1234), v, px),
                f"{cfg_name} vision, MX at QKV only", bar=COS_TOL)
 
 
-def test_fp8_site_selection_is_validated(monkeypatch):
+def test_fp8_site_selection_is_validated():
     from open_clip_inference import _lib as L
     from oracle.model_spec import VIT_B_32_CFG
-    monkeypatch.setenv("CLIPGPU_MX_SITES", "proj")
     with pytest.raises(L.ClipError, match="proj in MX needs fc"):
-        _engine(VIT_B_32_CFG, 0, "fp8", 2)
+        _engine(VIT_B_32_CFG, 0, "fp8", 2, mx_sites="proj")
+    with pytest.raises(L.ClipError, match="mx_layers needs dtype"):
+        _engine(VIT_B_32_CFG, 0, "bf16", 2, mx_layers=[0])

@@ -1,5 +1,5 @@
 """End-to-end parity of the HIP engine vs the CPU oracle (fp64 restatement of the
-reference's ONNX graphs, pinned against HF transformers — tests/test_oracle_pin.py).
+reference's ONNX graphs, pinned against HF transformers — tests/test_cpu_oracle.py).
 
 Tolerance (north_star): cosine(GPU, oracle) >= 0.9999 per embedding row, and the
 GPU rows are unit-norm to 1e-5.  Weights are the seeded synthetic set (identical
@@ -18,7 +18,7 @@ from tests.helpers import COS_TOL, make_model_dir, normalized_pixels, specs
 
 pytestmark = pytest.mark.gpu
 
-TILE_LAST = 25  # kernels.hpp GemmTile: the last tiled kernel the tuners and pins take
+BUILT_TILES = [1, 2, 3, 13, 14, 15, 17, 18, 26, 28]  # kernels.hpp kGemmTiles (test_cpu_abi checks the list)
 
 _CACHE = {}
 
@@ -39,9 +39,11 @@ def oracle_text(cfg, seed, ids):
     return clip_ref.encode_text(_CACHE[key], t, ids)
 
 
-def engine(cfg, tower, seed=1234, dtype="bf16", max_batch=64):
+def engine(cfg, tower, seed=1234, dtype="bf16", max_batch=64, **opts):
+    """opts: open_clip_inference.engine.Engine's clipgpu_options keywords (gemm_tiles, lanes, graphs,
+    prune_last, trim_text, ...)."""
     from open_clip_inference.engine import Engine
-    return Engine(make_model_dir(cfg, seed), tower, [0], dtype, max_batch)
+    return Engine(make_model_dir(cfg, seed), tower, [0], dtype, max_batch, **opts)
 
 
 def check_rows(got, ref):
@@ -148,16 +150,15 @@ def test_device_entry_points():
 
 
 @pytest.mark.parametrize("tower", [0, 1])
-def test_graph_replay_reads_fresh_inputs_and_matches_direct_launches(tower, monkeypatch):
+def test_graph_replay_reads_fresh_inputs_and_matches_direct_launches(tower):
     """Forwards replayed as hipGraphs (the default) are bit-identical to direct launches
-    (CLIPGPU_GRAPHS=0), and a replay with the same buffers sees new input contents: device
+    (clipgpu_options.graphs = -1), and a replay with the same buffers sees new input contents: device
     entry points (caller stream, fork/join) and host entry points (lane-slot streams)."""
     import torch
     v, t = specs(VIT_B_32_CFG)
     outs = {}
     for graphs in ["1", "0"]:
-        monkeypatch.setenv("CLIPGPU_GRAPHS", graphs)
-        e = engine(VIT_B_32_CFG, tower, max_batch=20)
+        e = engine(VIT_B_32_CFG, tower, max_batch=20, graphs=graphs == "1")
         res = []
         for seed in (51, 52, 53):
             if tower == 0:
@@ -208,9 +209,9 @@ def test_native_library_is_loaded():
 
 
 @pytest.mark.parametrize("tower", [0, 1])
-def test_gemm_tile_choice_is_bit_exact(tower, monkeypatch):
-    """Every GEMM tile computes the same K-ordered sums: the creation-time autotune
-    changes speed, never the embeddings."""
+def test_gemm_tile_choice_is_bit_exact(tower):
+    """Every GEMM tile the library builds computes the same K-ordered sums: the tile table and the
+    creation-time tuner change speed, never the embeddings."""
     from open_clip_inference import _lib
     v, t = specs(VIT_B_32_CFG)
     if tower == 0:
@@ -219,85 +220,22 @@ def test_gemm_tile_choice_is_bit_exact(tower, monkeypatch):
         data = weights.synth_token_ids(31, 48, t.context_length, t.vocab_size, t.vocab_size - 2,
                                        t.vocab_size - 1, random_eot=True)
     outs = []
-    pins = ["1,1,1,1", "2,2,2,2", "3,3,3,3", "4,4,4,4", "5,5,5,5", "6,6,6,6", "7,7,7,7", "8,8,8,8",
-            "9,9,9,9", "10,10,10,10", "11,11,11,11", "12,12,12,12", "13,13,13,13", "14,14,14,14",
-            "15,15,15,15", "16,16,16,16", "17,17,17,17", "18,18,18,18", "19,19,19,19", "20,20,20,20", "4,8,7,7", "14,16,14,15",
-            "18,17,18,17", "19,20,19,20", "21,21,21,21", "22,22,22,22", "23,23,23,23", "24,24,24,24",
-            "25,25,25,25", "21,23,21,23", "21,24,22,25",
-            None]
+    pins = [[t] * 4 for t in BUILT_TILES] + [[18, 26, 18, 26], [18, 17, 18, 17], [14, 15, 3, 28], None]
     for tiles in pins:
-        if tiles:
-            monkeypatch.setenv("CLIPGPU_GEMM_TILES", tiles)
-        else:
-            monkeypatch.delenv("CLIPGPU_GEMM_TILES", raising=False)
-        e = engine(VIT_B_32_CFG, tower, max_batch=48)
+        e = engine(VIT_B_32_CFG, tower, max_batch=48, gemm_tiles=tiles, patch_tile=tiles[3] if tiles else 0)
         got = (c_int * 4)()
         _lib.check(_lib.lib().clipgpu_test_engine_tiles(e._h, got))
         if tiles:
-            assert list(got) == [int(x) for x in tiles.split(",")]
+            assert list(got) == tiles
         else:
-            assert all(1 <= x <= TILE_LAST for x in got), list(got)
+            assert all(x == 0 or x in BUILT_TILES for x in got), list(got)
         outs.append(e.embed_pixels(data) if tower == 0 else e.embed_tokens(data))
     bad = [(pins[i], float(np.abs(o - outs[0]).max())) for i, o in enumerate(outs) if not np.array_equal(o, outs[0])]
     assert not bad, bad
 
 
 @pytest.mark.parametrize("tower", [0, 1])
-def test_split_k_on_and_off_match_oracle(tower, monkeypatch):
-    """out_proj / c_proj with and without the K split (combined by the next LayerNorm /
-    the pooling LN) both meet the north-star tolerance; the split is fixed per engine, so
-    batch sizes inside one engine stay bit-identical."""
-    v, t = specs(VIT_B_32_CFG)
-    if tower == 0:
-        data = normalized_pixels(weights.synth_images_u8(43, 9, v.image_size), OPENAI_MEAN, OPENAI_STD)
-        ref = oracle_vision(VIT_B_32_CFG, 1234, data)
-    else:
-        data = weights.synth_token_ids(43, 9, t.context_length, t.vocab_size, t.vocab_size - 2,
-                                       t.vocab_size - 1, random_eot=True)
-        ref = oracle_text(VIT_B_32_CFG, 1234, data)
-    for split in ["0", "1"]:
-        monkeypatch.setenv("CLIPGPU_GEMM_SPLIT", split)
-        e = engine(VIT_B_32_CFG, tower, max_batch=9)
-        full = e.embed_pixels(data) if tower == 0 else e.embed_tokens(data)
-        check_rows(full, ref)
-        one = e.embed_pixels(data[3:4]) if tower == 0 else e.embed_tokens(data[3:4])
-        assert np.array_equal(one[0], full[3])
-
-
-@pytest.mark.parametrize("tower", [0, 1])
-def test_fused_residual_gemm_layernorm_matches_oracle(tower, monkeypatch):
-    """CLIPGPU_FUSE_LN=1 (out_proj + ln_2 and c_proj + the next ln_1 in gemm_rowln.hip) meets the
-    north-star tolerance, stays bit-identical across batch splits, lanes and last-layer pruning,
-    and agrees with the unfused engine to within the LayerNorm's reduction-order rounding."""
-    v, t = specs(VIT_B_32_CFG)
-    B = 37
-    if tower == 0:
-        data = normalized_pixels(weights.synth_images_u8(47, B, v.image_size), OPENAI_MEAN, OPENAI_STD)
-        ref = oracle_vision(VIT_B_32_CFG, 1234, data[:6])
-    else:
-        data = weights.synth_token_ids(47, B, t.context_length, t.vocab_size, t.vocab_size - 2,
-                                       t.vocab_size - 1, random_eot=True)
-        ref = oracle_text(VIT_B_32_CFG, 1234, data[:6])
-    emb = (lambda e, d: e.embed_pixels(d)) if tower == 0 else (lambda e, d: e.embed_tokens(d))
-    outs = {}
-    for fuse, lanes, prune in (("1", "1", "1"), ("1", "2", "1"), ("1", "2", "0"), ("0", "2", "1")):
-        monkeypatch.setenv("CLIPGPU_FUSE_LN", fuse)
-        monkeypatch.setenv("CLIPGPU_LANES", lanes)
-        monkeypatch.setenv("CLIPGPU_PRUNE_LAST", prune)
-        e = engine(VIT_B_32_CFG, tower, max_batch=B)
-        outs[(fuse, lanes, prune)] = emb(e, data)
-        if fuse == "1" and lanes == "1":
-            part = emb(e, data[5:9])
-            assert np.array_equal(part, outs[(fuse, lanes, prune)][5:9])
-    fused = outs[("1", "1", "1")]
-    assert np.array_equal(fused, outs[("1", "2", "1")])
-    assert np.array_equal(fused, outs[("1", "2", "0")])
-    check_rows(fused[:6], ref)
-    assert clip_ref.cosine_rows(fused, outs[("0", "2", "1")]).min() >= 0.99999
-
-
-@pytest.mark.parametrize("tower", [0, 1])
-def test_concurrent_lanes_are_bit_exact(tower, monkeypatch):
+def test_concurrent_lanes_are_bit_exact(tower):
     """Splitting a batch over concurrent lanes (sub-batches on their own streams)
     is invisible in the output: rows never interact outside attention."""
     v, t = specs(VIT_B_32_CFG)
@@ -306,11 +244,9 @@ def test_concurrent_lanes_are_bit_exact(tower, monkeypatch):
     else:
         data = weights.synth_token_ids(41, 37, t.context_length, t.vocab_size, t.vocab_size - 2,
                                        t.vocab_size - 1, random_eot=True)
-    monkeypatch.setenv("CLIPGPU_GEMM_TILES", "1,1,1,1")
     outs = []
-    for lanes in ["1", "2", "3", "4"]:
-        monkeypatch.setenv("CLIPGPU_LANES", lanes)
-        e = engine(VIT_B_32_CFG, tower, max_batch=37)
+    for lanes in [1, 2, 3, 4]:
+        e = engine(VIT_B_32_CFG, tower, max_batch=37, gemm_tiles=[1, 1, 1, 1], lanes=lanes)
         outs.append(e.embed_pixels(data) if tower == 0 else e.embed_tokens(data))
     for o in outs[1:]:
         assert np.array_equal(o, outs[0])
@@ -321,7 +257,7 @@ def test_concurrent_lanes_are_bit_exact(tower, monkeypatch):
 @pytest.mark.parametrize("cfg", [VIT_B_32_CFG, TINY_CFG])
 @pytest.mark.parametrize("dtype", ["bf16", "fp8"])
 @pytest.mark.parametrize("tower", [0, 1])
-def test_last_layer_pruning_is_bit_exact(cfg, dtype, tower, monkeypatch):
+def test_last_layer_pruning_is_bit_exact(cfg, dtype, tower):
     """The last layer run on the pooled rows only (CLS / EOT argmax gathered after attention,
     engine.hip trunk) gives the same bits as the full last layer: every op after attention is
     row-local and each kept row goes through the same kernels.  Random EOT positions, two
@@ -336,11 +272,9 @@ def test_last_layer_pruning_is_bit_exact(cfg, dtype, tower, monkeypatch):
     else:
         data = weights.synth_token_ids(43, B, t.context_length, t.vocab_size, t.vocab_size - 2,
                                        t.vocab_size - 1, random_eot=True)
-    monkeypatch.setenv("CLIPGPU_LANES", "2")
     outs = {}
     for prune in ["0", "1"]:
-        monkeypatch.setenv("CLIPGPU_PRUNE_LAST", prune)
-        e = engine(cfg, tower, dtype=dtype, max_batch=B)
+        e = engine(cfg, tower, dtype=dtype, max_batch=B, lanes=2, prune_last=prune == "1")
         outs[prune] = e.embed_pixels(data) if tower == 0 else e.embed_tokens(data)
         outs[prune + "s"] = e.embed_pixels(data[:3]) if tower == 0 else e.embed_tokens(data[:3])
     assert np.array_equal(outs["0"], outs["1"])
@@ -351,7 +285,7 @@ def test_last_layer_pruning_is_bit_exact(cfg, dtype, tower, monkeypatch):
 
 
 @pytest.mark.parametrize("cfg,max_eot", [(VIT_B_32_CFG, 9), (VIT_B_32_CFG, 30), (VIT_B_32_CFG, 76), (TINY_CFG, 5)])
-def test_text_trim_is_bit_exact(cfg, max_eot, monkeypatch):
+def test_text_trim_is_bit_exact(cfg, max_eot):
     """Host-ids text batches run on their first max(EOT) + 1 tokens (at least 16;
     clipgpu_embed_tokens): causal attention keeps the tokens after a sequence's EOT away from
     its pooled row, so the embeddings equal the full-context run bit for bit.  Short captions
@@ -368,8 +302,7 @@ def test_text_trim_is_bit_exact(cfg, max_eot, monkeypatch):
         ids[b, eot[b]] = t.vocab_size - 1
     outs = {}
     for trim in ["0", "1"]:
-        monkeypatch.setenv("CLIPGPU_TRIM_TEXT", trim)
-        e = engine(cfg, 1, max_batch=16)
+        e = engine(cfg, 1, max_batch=16, trim_text=trim == "1")
         outs[trim] = e.embed_tokens(ids)
     assert np.array_equal(outs["0"], outs["1"])
     check_rows(outs["1"][:4], oracle_text(cfg, 1234, ids[:4]))
@@ -454,19 +387,15 @@ def test_so400m_siglip2_384_full_dims():
     check_rows(e.embed_pixels(px), oracle_vision(SO400M_16_SIGLIP2_384_CFG, 1234, px))
 
 
-def test_graph_cache_eviction_with_varied_caption_lengths(monkeypatch):
+def test_graph_cache_eviction_with_varied_caption_lengths():
     """More distinct forwards than the hipGraph cache holds (32): host-ids text batches of varied
     size and max-EOT position (trimmed lengths bucketed to multiples of 16) evict the least
     recently used graphs after draining every replica stream; every call still equals the
     untrimmed, graph-free run bit for bit, and the engine keeps working."""
     _, t = specs(VIT_B_32_CFG)
     rng = np.random.default_rng(2024)
-    monkeypatch.delenv("CLIPGPU_GRAPHS", raising=False)
-    monkeypatch.delenv("CLIPGPU_TRIM_TEXT", raising=False)
     e = engine(VIT_B_32_CFG, 1, max_batch=24)
-    monkeypatch.setenv("CLIPGPU_GRAPHS", "0")
-    monkeypatch.setenv("CLIPGPU_TRIM_TEXT", "0")
-    ref_engine = engine(VIT_B_32_CFG, 1, max_batch=24)
+    ref_engine = engine(VIT_B_32_CFG, 1, max_batch=24, graphs=False, trim_text=False)
     for call in range(44):
         B = int(rng.integers(1, 25))
         max_eot = int(rng.integers(2, t.context_length))

@@ -94,7 +94,7 @@ def host_leg(B=256, steps=6, warmup=2):
 def captions_leg(B=1024, steps=6, warmup=2):
     """ViT-B/32 text from host token ids at caption lengths (EOT at 8..24, zero padding to
     77): sequence trimming (clipgpu_embed_tokens runs the batch on its first max(EOT)+1
-    tokens) on vs off (CLIPGPU_TRIM_TEXT=0).  Host buffers: H2D/D2H inside the timing."""
+    tokens) on vs off (Engine(trim_text=False)).  Host buffers: H2D/D2H inside the timing."""
     d = model_dir(VIT_B_32_CFG)
     rng = np.random.default_rng(0)
     V = 49408
@@ -106,8 +106,7 @@ def captions_leg(B=1024, steps=6, warmup=2):
         ids[b, eot[b]] = V - 1
     res = {}
     for trim in ("1", "0"):
-        os.environ["CLIPGPU_TRIM_TEXT"] = trim
-        e = Engine(d, 1, [0], "bf16", B)
+        e = Engine(d, 1, [0], "bf16", B, trim_text=trim == "1")
         dt = timed(lambda: e.embed_tokens(ids), steps, warmup)
         res[trim] = e.embed_tokens(ids)
         print(json.dumps({"measure": "b32_text_captions_" + ("trimmed" if trim == "1" else "full77"), "batch": B,
@@ -115,7 +114,6 @@ def captions_leg(B=1024, steps=6, warmup=2):
                           "ms_per_step": round(dt * 1e3, 3),
                           "input": "host token ids (pinned staging + H2D/D2H inside the timing)"}), flush=True)
         e.close()
-    os.environ.pop("CLIPGPU_TRIM_TEXT")
     print(json.dumps({"measure": "b32_text_captions_bit_equal", "value": bool(np.array_equal(res["1"], res["0"]))}),
           flush=True)
 

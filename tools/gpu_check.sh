@@ -28,6 +28,15 @@ for s in $STEPS; do
       { nproc; cat /sys/fs/cgroup/cpu.max 2>&1; cat /sys/fs/cgroup/cpu/cpu.cfs_quota_us 2>&1; echo "OMP=$OMP_NUM_THREADS"; } > gpurun_out/host.txt; cat gpurun_out/host.txt ;;
     sweep)
       run gemm_sweep 600 python tools/gemm_sweep.py || exit $? ;;
+    ab)  # AB_SPECS: ';'-separated "M N K epi act tiles" (tools/gemm_ab.py, interleaved rounds in one process)
+      IFS=';' read -ra SPECS <<< "${AB_SPECS}"
+      for spec in "${SPECS[@]}"; do
+        timeout -k 10 300 python3 tools/gemm_ab.py $spec ${AB_ROUNDS:-7} ${AB_ITERS:-20} >> gpurun_out/ab.log 2>&1 || exit $?
+      done
+      cat gpurun_out/ab.log ;;
+    bench_pin)  # the vision leg with PIN_TILES pinned (q,o,f,p), BENCH_PIN_ARGS extra bench args
+      run bench_pin_${PIN_TILES//,/_} 300 python bench.py --steps 20 --warmup 5 --tiles $PIN_TILES \
+          --no-cpu-baseline --no-fp8 --no-text --no-e2e ${BENCH_PIN_ARGS:-} || exit $? ;;
     smoke)
       run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
     bench)
@@ -44,18 +53,18 @@ for s in $STEPS; do
       find gpurun_out/prof -name "*kernel_stats.csv" | head -3 ;;
     pmc)  # HBM bytes of the roofline kernel: FETCH_SIZE and WRITE_SIZE in separate passes,
           # GEMM tiles pinned to the ones the un-profiled bench autotuned (profiling skews tuning)
-      export CLIPGPU_GEMM_TILES=$(python3 -c "import json;print([json.loads(l) for l in open('gpurun_out/bench.log') if l.startswith('{')][-1]['gemm_tiles_env'])") || exit 1
-      export CLIPGPU_LANES=$(python3 -c "import json;print([json.loads(l) for l in open('gpurun_out/bench.log') if l.startswith('{')][-1]['lanes_env'])") || exit 1
+      TILES=$(python3 -c "import json;print([json.loads(l) for l in open('gpurun_out/bench.log') if l.startswith('{')][-1]['gemm_tiles_env'])") || exit 1
+      LANES=$(python3 -c "import json;print([json.loads(l) for l in open('gpurun_out/bench.log') if l.startswith('{')][-1]['lanes_env'])") || exit 1
       for C in FETCH_SIZE WRITE_SIZE; do
         run pmc_$C 600 rocprofv3 --pmc $C --output-format csv -d gpurun_out/pmc_bench/$C -o run -- \
-            python3 bench.py --steps 3 --warmup 1 --no-text --no-cpu-baseline --no-fp8 --no-e2e || exit $?
+            python3 bench.py --steps 3 --warmup 1 --no-text --no-cpu-baseline --no-fp8 --no-e2e --windows 0 \
+            --tiles $TILES --lanes $LANES || exit $?
       done
       ROWS=$(python3 -c "import json;print([json.loads(l) for l in open('gpurun_out/bench.log') if l.startswith('{')][-1]['roofline']['rows_per_launch'])") || exit 1
       cp profiles/pmc_c_fc.json gpurun_out/pmc_c_fc.json  # merged into (copy back to profiles/ after the call)
       python3 tools/pmc_traffic.py gpurun_out/pmc_bench/FETCH_SIZE gpurun_out/pmc_bench/WRITE_SIZE \
-          gpurun_out/pmc_c_fc.json $ROWS "${PMC_LABEL:-this run}: --pmc FETCH_SIZE and --pmc WRITE_SIZE passes of bench.py --no-text, tiles $CLIPGPU_GEMM_TILES" \
-          "$CLIPGPU_GEMM_TILES" || exit $?
-      unset CLIPGPU_GEMM_TILES CLIPGPU_LANES ;;
+          gpurun_out/pmc_c_fc.json $ROWS "${PMC_LABEL:-this run}: --pmc FETCH_SIZE and --pmc WRITE_SIZE passes of bench.py --no-text, tiles $TILES" \
+          "$TILES" || exit $? ;;
   esac
 done
 echo "=== done"

@@ -3,7 +3,7 @@
 run in MX-fp8 and keep the north-star cosine bar (>= 0.9999 per row) against the fp32 reference.
 
 For each tower (ViT-B/32 vision + text, DFN5B ViT-H/14-378 vision + text, SO400M-16-SigLIP2-384
-vision) and each site split of CLIPGPU_MX_SITES (c_proj in MX needs c_fc in MX; out_proj,
+vision) and each site split of Engine(mx_sites=...) (c_proj in MX needs c_fc in MX; out_proj,
 attention, stems and heads are always bf16) one fp8 engine embeds a seeded batch; the rows are
 compared with the fp32 CPU port of the same graph (oracle/torch_cpu.py; SigLIP: oracle/clip_ref.py
 in fp32) and with the bf16 engine.  Also times the device-resident forward at a bench-sized batch.
@@ -68,11 +68,9 @@ def run(name, cfg, tower, n_check, B_time):
     bf16 = None
     for split in [None] + SPLITS:
         if split is None:
-            os.environ.pop("CLIPGPU_MX_SITES", None)
             e = Engine(d, tower, [0], "bf16", B_time)
         else:
-            os.environ["CLIPGPU_MX_SITES"] = split
-            e = Engine(d, tower, [0], "fp8", B_time)
+            e = Engine(d, tower, [0], "fp8", B_time, mx_sites=split)
         got = e.embed_pixels(x[:n_check]) if tower == 0 else e.embed_tokens(x[:n_check])
         fwd = (lambda: e.embed_pixels_device(d_in.data_ptr(), B_time, out.data_ptr(), s.cuda_stream)) if tower == 0 \
             else (lambda: e.embed_tokens_device(d_in.data_ptr(), B_time, out.data_ptr(), s.cuda_stream))
@@ -96,7 +94,6 @@ def run(name, cfg, tower, n_check, B_time):
             rec["cos_vs_bf16_min"] = round(float(cos_rows(got, bf16).min()), 6)
         print(json.dumps(rec), flush=True)
         e.close()
-    os.environ.pop("CLIPGPU_MX_SITES", None)
 
 
 if __name__ == "__main__":

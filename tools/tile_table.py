@@ -53,8 +53,6 @@ def main():
     ap.add_argument("--tuned", type=int, default=2)
     ap.add_argument("--only", default="")
     args = ap.parse_args()
-    for var in ("CLIPGPU_LANES", "CLIPGPU_GEMM_TILES", "CLIPGPU_GEMM_AUTOTUNE"):
-        os.environ.pop(var, None)
     names = [n for n in WORKLOADS if not args.only or n in args.only.split(",")]
     for name in names:
         cfg, tower, B = WORKLOADS[name]
