@@ -73,7 +73,7 @@ def text_flops(B, T=77, executed=False):
 
 # GemmTile ids the library builds (csrc/kernels/kernels.hpp kGemmTiles)
 TILE_NAMES = {0: "heuristic", 1: "128x128", 2: "256x128", 3: "256x256", 13: "192x256w8", 14: "256x256rs",
-              15: "160x128rs", 17: "160x128w8rs", 18: "256x256half", 26: "224x192w8", 28: "256x192w8"}
+              15: "160x128rs", 17: "160x128w8rs", 18: "256x256half", 26: "224x192w8"}
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md chip table)
 B_VISION = 256
 B_TEXT = 1024
@@ -214,31 +214,26 @@ def load_traffic(rows_per_launch, tiles):
     return None, None
 
 
-def measure_windows(step, engine, n, steps, dt_first, dev):
+def measure_windows(step, engine, n, steps, dev):
     """Repeated windows after the timed one (N = 1), so a few-% change can be told from box-to-box
-    and run-to-run spread: each window is `steps` forward steps timed like `value`, with a one-wave
-    clock probe (clipgpu_test_clock_probe: s_memtime ticks over s_memrealtime's 100 MHz, sleeping,
-    on a side stream, for 60 % of the first window's wall time) running beside it, which reads the
-    shader clock the chip holds under the forward's load (MI355X_MICROARCH.md, DVFS give-back);
-    then as many profiled windows give the mean c_fc launch time (HIP events at the kernel
-    boundaries, lanes serialized, no graphs), each with its own clock probe."""
+    and run-to-run spread: each window is `steps` forward steps timed like `value`, followed at once
+    by a 2 ms one-wave clock probe (clipgpu_test_clock_probe: s_memtime ticks over s_memrealtime's
+    100 MHz) that reads the shader clock the chip holds as the load ends (MI355X_MICROARCH.md, DVFS
+    give-back).  The probe runs after the window, not beside it: a wave resident beside the
+    one-block-per-CU GEMMs keeps one CU from hosting their block (measured: 4 % slower windows, c_fc
+    +17 %).  Then profiled windows give the mean c_fc launch time (HIP events at the kernel
+    boundaries, lanes serialized, no graphs)."""
     import statistics
     L = _lib.lib()
-    side = torch.cuda.Stream(dev)
     probe = torch.zeros(2, dtype=torch.int64, device=dev)
-    probe_us = max(1000, int(0.6 * dt_first * 1e6))
 
-    def clocked(fn, with_probe=True):
+    def clock_after(fn):
         torch.cuda.synchronize()
-        if with_probe:
-            _lib.check(L.clipgpu_test_clock_probe(ctypes.c_void_p(side.cuda_stream), probe_us,
-                                                  ctypes.c_void_p(probe.data_ptr())))
         t0 = time.perf_counter()
         out = fn()
         torch.cuda.synchronize()
         wall = time.perf_counter() - t0
-        if not with_probe:
-            return wall, None, out
+        _lib.check(L.clipgpu_test_clock_probe(None, 2000, ctypes.c_void_p(probe.data_ptr())))
         t = probe.cpu().tolist()
         return wall, (100.0 * t[0] / t[1] if t[1] > 0 else None), out
 
@@ -246,12 +241,10 @@ def measure_windows(step, engine, n, steps, dt_first, dev):
         for _ in range(steps):
             step()
 
-    rates, rates_probe, clocks = [], [], []
-    for _ in range(n):  # alternating: a plain window, then one with the probe beside it
-        wall, _, _ = clocked(run_steps, with_probe=False)
+    rates, clocks = [], []
+    for _ in range(n):
+        wall, mhz, _ = clock_after(run_steps)
         rates.append(B_VISION * steps / wall)
-        wall, mhz, _ = clocked(run_steps)
-        rates_probe.append(B_VISION * steps / wall)
         clocks.append(mhz)
     fc_us, fc_clk = [], []
     for _ in range(max(1, min(n, 3))):
@@ -260,7 +253,7 @@ def measure_windows(step, engine, n, steps, dt_first, dev):
         def prof_steps():
             run_steps()
             return profile_read(engine, "c_fc")
-        _, mhz, (ms, cnt) = clocked(prof_steps)
+        _, mhz, (ms, cnt) = clock_after(prof_steps)
         profile_enable(engine, [])
         fc_us.append(1e3 * ms / max(cnt, 1))
         fc_clk.append(mhz)
@@ -270,30 +263,43 @@ def measure_windows(step, engine, n, steps, dt_first, dev):
             "min": round(min(rates), 1), "median": round(statistics.median(rates), 1), "max": round(max(rates), 1),
             "sclk_mhz": [round(c, 1) if c else None for c in clocks],
             "sclk_mhz_median": round(statistics.median(good), 1) if good else None,
-            "images_s_probed": [round(r, 1) for r in rates_probe],
-            "images_s_per_ghz_median": round(statistics.median(r / (c / 1e3) for r, c in zip(rates_probe, clocks) if c), 1)
+            "images_s_per_ghz_median": round(statistics.median(r / (c / 1e3) for r, c in zip(rates, clocks) if c), 1)
             if good else None,
             "c_fc_us": [round(u, 2) for u in fc_us], "c_fc_sclk_mhz": [round(c, 1) if c else None for c in fc_clk],
-            "note": "windows after the timed one (same steps each), alternating plain (images_s) and clock-probed "
-                    "(images_s_probed: a one-wave s_memtime / s_memrealtime probe on a side stream, sclk_mhz); c_fc "
-                    "from profiled windows (lanes serialized)"}
+            "note": "windows after the timed one (same steps each); sclk_mhz from a 2 ms one-wave "
+                    "s_memtime / s_memrealtime probe launched right after each window; c_fc from profiled windows "
+                    "(lanes serialized)"}
 
 
-def host_leg(engine, kind, host, steps):
-    """Host-buffer throughput through the C ABI (pinned staging + H2D + forward + D2H, PCIe
-    included), units per second over `steps` calls after one warm call."""
-    call = {"u8": lambda: engine.embed_u8(host, CFG["preprocess_cfg"]["mean"], CFG["preprocess_cfg"]["std"]),
-            "f32": lambda: engine.embed_pixels(host),
-            "tokens": lambda: engine.embed_tokens(host)}[kind]
-    call()
-    t0 = time.perf_counter()
-    for _ in range(steps):
+def host_leg(engine, kind, host, steps, registered=False):
+    """Host-buffer throughput through the C ABI (H2D + forward + D2H, PCIe included), units per
+    second over `steps` calls after one warm call.  Pageable arrays go through the engine's pinned
+    staging; `registered` pins the caller's input and output arrays first (clipgpu_host_register:
+    direct DMA, vision's 1/4 + 3/4 slot split)."""
+    from open_clip_inference.engine import host_register, host_unregister
+    host = np.ascontiguousarray(host)
+    out = np.empty((len(host), engine.embed_dim), np.float32)
+    call = {"u8": lambda: engine.embed_u8(host, CFG["preprocess_cfg"]["mean"], CFG["preprocess_cfg"]["std"], out=out),
+            "f32": lambda: engine.embed_pixels(host, out=out),
+            "tokens": lambda: engine.embed_tokens(host, out=out)}[kind]
+    if registered:
+        host_register(host)
+        host_register(out)
+    try:
         call()
-    dt = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            call()
+        dt = time.perf_counter() - t0
+    finally:
+        if registered:
+            host_unregister(host)
+            host_unregister(out)
     entry = {"u8": "clipgpu_embed_u8 (u8 NHWC [256,224,224,3])", "f32": "clipgpu_embed_pixels (f32 NCHW [256,3,224,224])",
              "tokens": "clipgpu_embed_tokens (i64 ids [1024,77], full-length rows: no trimming)"}[kind]
     return {"value": round(len(host) * steps / dt, 1), "unit": "texts/s" if kind == "tokens" else "images/s",
-            "ms_per_call": round(dt * 1e3 / steps, 3), "entry": entry}
+            "ms_per_call": round(dt * 1e3 / steps, 3), "entry": entry,
+            "buffers": "caller-registered (direct DMA)" if registered else "pageable (pinned staging)"}
 
 
 def main():
@@ -404,7 +410,7 @@ def main():
     _, (fc_ms, fc_n) = timed(vision_step, max(3, args.steps // 2), 1, ve, "c_fc")
     windows = None
     if world == 1 and args.windows > 0:
-        windows = measure_windows(vision_step, ve, args.windows, args.steps, dt, dev)
+        windows = measure_windows(vision_step, ve, args.windows, args.steps, dev)
 
     # roofline of the dominant kernel: c_fc GEMM (+QuickGELU epilogue), M=rows per launch,
     # N=3072, K=768; fc_n counts the full-row launches (12 layers, or 11 when the last one
@@ -490,7 +496,9 @@ def main():
         text["lanes"] = t_lanes.value
         tout_host = tout.cpu().numpy()
         if world == 1 and not args.no_e2e:
-            text_e2e = host_leg(te, "tokens", ids.cpu().numpy(), max(3, args.steps // 4))
+            text_e2e = {"text_ids_host": host_leg(te, "tokens", ids.cpu().numpy(), max(3, args.steps // 4)),
+                        "text_ids_host_registered": host_leg(te, "tokens", ids.cpu().numpy(), max(3, args.steps // 4),
+                                                             registered=True)}
         te.close()
 
     # End-to-end legs (host buffers in, host embeddings out, PCIe included; not `value`): the
@@ -500,10 +508,13 @@ def main():
     if world == 1 and not args.no_e2e:
         g = torch.Generator(device="cpu").manual_seed(1000 + rank)
         u8_host = torch.randint(0, 256, (B_VISION, 224, 224, 3), dtype=torch.uint8, generator=g).numpy()
-        e2e = {"vision_u8_host": host_leg(ve, "u8", u8_host, max(3, args.steps // 4)),
-               "vision_f32_host": host_leg(ve, "f32", px.cpu().numpy(), max(3, args.steps // 4))}
+        n_e2e = max(3, args.steps // 4)
+        e2e = {"vision_u8_host": host_leg(ve, "u8", u8_host, n_e2e),
+               "vision_u8_host_registered": host_leg(ve, "u8", u8_host, n_e2e, registered=True),
+               "vision_f32_host": host_leg(ve, "f32", px.cpu().numpy(), n_e2e),
+               "vision_f32_host_registered": host_leg(ve, "f32", px.cpu().numpy(), n_e2e, registered=True)}
         if text is not None:
-            e2e["text_ids_host"] = text_e2e
+            e2e.update(text_e2e)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

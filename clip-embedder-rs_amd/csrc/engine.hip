@@ -987,7 +987,7 @@ void run_lanes(const clipgpu_engine& e, const Replica& r, int B, hipStream_t st,
 // and replay stream is `st` when it is one of the replica's own streams, else the replica's
 // stream, forked from and joined back to `st` by events (a caller's stream may be the
 // legacy null stream, which cannot be captured).  Profiling (per-launch events) and
-// CLIPGPU_GRAPHS=0 run the body directly.
+// clipgpu_options.graphs = -1 run the body directly.
 template <typename F>
 void run_graph(const clipgpu_engine& e, const Replica& r, const std::vector<uint64_t>& key, hipStream_t st, F body) {
   if (!e.graphs || e.prof.mask || !r.graphs) {
@@ -1162,49 +1162,95 @@ void par_memcpy(void* dst, const void* src, size_t n) {
   for (auto& t : th) t.join();
 }
 
-// Host-buffer forward over a row range of one replica.  Pipelined over sub-chunks of one
-// lane each (max_batch / lanes rows): sub-chunk j uses slot j % lanes -- its lane's stream,
-// its rows of the pinned staging / device input / output buffers and its workspace view --
-// so the host copy of sub-chunk j+1 and its H2D overlap the forward of sub-chunk j.  A slot
-// is reused after its previous sub-chunk's D2H event, whose rows are then copied out.
+// Caller-registered host ranges (clipgpu_host_register): process-wide, hipHostRegister'ed.
+struct HostRanges {
+  std::mutex mu;
+  std::vector<std::pair<uintptr_t, size_t>> r;  // (base, bytes)
+};
+HostRanges& host_ranges() {
+  static HostRanges h;
+  return h;
+}
+// Is [p, p + n) inside one registered range?
+bool host_registered(const void* p, size_t n) {
+  HostRanges& h = host_ranges();
+  std::lock_guard<std::mutex> lk(h.mu);
+  const uintptr_t a = (uintptr_t)p;
+  for (const auto& rg : h.r)
+    if (a >= rg.first && a + n <= rg.first + rg.second) return true;
+  return false;
+}
+
+// Host-buffer forward over a row range of one replica, pipelined over sub-chunks on the lane
+// streams: chunk j runs on slot j % lanes -- its lane's stream and its rows of the pinned staging /
+// device input / output buffers and of the workspace (lane_view) -- so the transfer of chunk j + 1
+// overlaps the forward of chunk j, and the lanes' forwards overlap each other.  Each round of `lanes`
+// chunks covers up to max_batch rows; chunk i of a round uses rows [part[i], part[i + 1]) of the
+// max_batch-row buffers (a fixed partition, so a chunk only ever reuses rows its own stream used).
+// Inputs are staged through pinned memory (par_memcpy), or DMA'd straight from a caller-registered
+// range (clipgpu_host_register); with two lanes and a registered vision input the partition is
+// 1/4 + 3/4, so only the small first chunk's transfer is exposed.  Outputs likewise (a registered
+// output range takes the D2H directly).  A slot is reused after its previous chunk's D2H event.
 void run_host_shard(clipgpu_engine& e, Replica& r, InKind kind, const void* in, size_t in_row_bytes, int64_t b0,
                     int64_t b1, const float* mean, const float* stdv, float* out, int tokens = 0) {
   HIP_CHECK(hipSetDevice(r.device));
-  const int E = e.spec.embed_dim, L = e.lanes;
-  const int S = (e.max_batch + L - 1) / L;  // rows per slot
+  const int E = e.spec.embed_dim, L = e.lanes, MB = e.max_batch;
+  const bool direct_in = host_registered((const char*)in + b0 * in_row_bytes, (size_t)(b1 - b0) * in_row_bytes);
+  const bool direct_out = host_registered(out + b0 * E, (size_t)(b1 - b0) * E * 4);
+  // the fixed partition of the max_batch rows over the L slots
+  std::vector<int> part((size_t)L + 1, 0);
+  const bool quarter = L == 2 && direct_in && kind != IN_IDS && MB >= 8;
+  for (int i = 1; i <= L; ++i) part[i] = quarter ? (i == 1 ? MB / 4 : MB) : (int)(((long)MB * i + L - 1) / L);
   struct Pending { int64_t c0 = -1; int n = 0; };
   Pending pend[4];
   auto drain = [&](int k) {
     if (pend[k].c0 < 0) return;
     HIP_CHECK(hipEventSynchronize(r.done[k]));
-    std::memcpy(out + pend[k].c0 * E, r.pin_out + (size_t)k * S * E, (size_t)pend[k].n * E * 4);
+    if (!direct_out) std::memcpy(out + pend[k].c0 * E, r.pin_out + (size_t)part[k] * E, (size_t)pend[k].n * E * 4);
     pend[k].c0 = -1;
   };
-  int j = 0;
-  for (int64_t c0 = b0; c0 < b1; c0 += S, ++j) {
-    const int k = j % L;
-    const int n = (int)std::min<int64_t>(S, b1 - c0);
-    drain(k);
-    hipStream_t st = r.lane[k] ? r.lane[k] : r.stream;
-    char* pin = (char*)r.pin_in + (size_t)k * S * in_row_bytes;
-    char* din = (char*)r.in + (size_t)k * S * in_row_bytes;
-    float* dout = r.out + (size_t)k * S * E;
-    par_memcpy(pin, (const char*)in + c0 * in_row_bytes, (size_t)n * in_row_bytes);
-    HIP_CHECK(hipMemcpyAsync(din, pin, (size_t)n * in_row_bytes, hipMemcpyHostToDevice, st));
-    const Replica v = lane_view(e, r, k * S);
-    run_graph(e, r,
-              {(uint64_t)(10 + kind), (uint64_t)k, (uint64_t)n, fbits(mean, 0), fbits(mean, 1), fbits(mean, 2),
-               fbits(stdv, 0), fbits(stdv, 1), fbits(stdv, 2), (uint64_t)tokens},
-              st, [&](hipStream_t gs) {
-                if (kind == IN_IDS)
-                  text_forward(e, v, (const int64_t*)din, n, dout, gs, tokens);
-                else
-                  vision_forward(e, v, din, kind == IN_F32 ? A_IMG_F32 : A_IMG_U8, mean, stdv, n, dout, gs);
-              });
-    HIP_CHECK(hipMemcpyAsync(r.pin_out + (size_t)k * S * E, dout, (size_t)n * E * 4, hipMemcpyDeviceToHost, st));
-    HIP_CHECK(hipEventRecord(r.done[k], st));
-    pend[k].c0 = c0;
-    pend[k].n = n;
+  for (int64_t c0 = b0; c0 < b1;) {
+    const int R = (int)std::min<int64_t>(MB, b1 - c0);  // rows of this round
+    int off = 0;
+    for (int k = 0; k < L && off < R; ++k) {
+      const int cap = part[k + 1] - part[k];
+      // even partition: fill the slots in order (a round that fits one slot is one chunk); the
+      // quarter partition: the round's rows spread in proportion to it, so a short round still
+      // exposes only a quarter of its transfer
+      int n = !quarter ? std::min(cap, R - off)
+                       : k + 1 == L ? R - off : (int)(((long)R * part[k + 1] + MB - 1) / MB - off);
+      n = std::max(0, std::min(n, cap));
+      if (n == 0) continue;
+      const int64_t rc = c0 + off;
+      drain(k);
+      hipStream_t st = r.lane[k] ? r.lane[k] : r.stream;
+      char* din = (char*)r.in + (size_t)part[k] * in_row_bytes;
+      float* dout = r.out + (size_t)part[k] * E;
+      const char* src = (const char*)in + rc * in_row_bytes;
+      if (!direct_in) {
+        char* pin = (char*)r.pin_in + (size_t)part[k] * in_row_bytes;
+        par_memcpy(pin, src, (size_t)n * in_row_bytes);
+        src = pin;
+      }
+      HIP_CHECK(hipMemcpyAsync(din, src, (size_t)n * in_row_bytes, hipMemcpyHostToDevice, st));
+      const Replica v = lane_view(e, r, part[k]);
+      run_graph(e, r,
+                {(uint64_t)(10 + kind), (uint64_t)k, (uint64_t)n, fbits(mean, 0), fbits(mean, 1), fbits(mean, 2),
+                 fbits(stdv, 0), fbits(stdv, 1), fbits(stdv, 2), (uint64_t)tokens, (uint64_t)part[k]},
+                st, [&](hipStream_t gs) {
+                  if (kind == IN_IDS)
+                    text_forward(e, v, (const int64_t*)din, n, dout, gs, tokens);
+                  else
+                    vision_forward(e, v, din, kind == IN_F32 ? A_IMG_F32 : A_IMG_U8, mean, stdv, n, dout, gs);
+                });
+      float* dst = direct_out ? out + rc * E : r.pin_out + (size_t)part[k] * E;
+      HIP_CHECK(hipMemcpyAsync(dst, dout, (size_t)n * E * 4, hipMemcpyDeviceToHost, st));
+      HIP_CHECK(hipEventRecord(r.done[k], st));
+      pend[k].c0 = rc;
+      pend[k].n = n;
+      off += n;
+    }
+    c0 += R;
   }
   for (int k = 0; k < L; ++k) drain(k);
 }
@@ -1763,6 +1809,34 @@ int clipgpu_embed_u8(clipgpu_engine* e, const uint8_t* nhwc, int64_t B, int64_t 
   });
 }
 
+int clipgpu_host_register(void* ptr, size_t bytes) {
+  return guarded([&]() {
+    if (!ptr || bytes == 0) throw ClipErr(CLIPGPU_ERR_INVALID, "NULL / empty host range");
+    HostRanges& h = host_ranges();
+    std::lock_guard<std::mutex> lk(h.mu);
+    const uintptr_t a = (uintptr_t)ptr;
+    for (const auto& rg : h.r)
+      if (a < rg.first + rg.second && rg.first < a + bytes)
+        throw ClipErr(CLIPGPU_ERR_INVALID, "host range overlaps a registered one");
+    HIP_CHECK(hipHostRegister(ptr, bytes, hipHostRegisterDefault));
+    h.r.emplace_back(a, bytes);
+  });
+}
+
+int clipgpu_host_unregister(void* ptr) {
+  return guarded([&]() {
+    HostRanges& h = host_ranges();
+    std::lock_guard<std::mutex> lk(h.mu);
+    for (size_t i = 0; i < h.r.size(); ++i)
+      if (h.r[i].first == (uintptr_t)ptr) {
+        HIP_CHECK(hipHostUnregister(ptr));
+        h.r.erase(h.r.begin() + (long)i);
+        return;
+      }
+    throw ClipErr(CLIPGPU_ERR_INVALID, "host range not registered");
+  });
+}
+
 int clipgpu_embed_tokens(clipgpu_engine* e, const int64_t* ids, const int64_t* mask, int64_t B, int64_t T,
                          float* out) {
   (void)mask;
@@ -1780,7 +1854,8 @@ int clipgpu_embed_tokens(clipgpu_engine* e, const int64_t* ids, const int64_t* m
     // attention is causal, so tokens past the batch's last EOT never reach an embedding.
     // The batch runs on its first Tc = max(EOT index) + 1 tokens, rounded up to a multiple of 16,
     // bit-identical
-    // (test_text_trim_is_bit_exact).  CLIPGPU_TRIM_TEXT=0 disables.
+    // (test_text_trim_is_bit_exact).  clipgpu_options.trim_text = -1 disables.  A trimmed batch is
+    // a private copy, so it is staged even when `ids` lies in a registered range.
     int64_t Tc = T;
     if (e->trim) {
       Tc = 1;

@@ -1120,7 +1120,6 @@ hipError_t launch_tile(const GemmParams& p, hipStream_t s) {
       case TILE_160x128_W8_RS: return launch_pipe<T, 160, 128, 2, 4, EPI, ACT, 2, 1>(p, s);
       case TILE_256x256_HALF: return launch_pipe_half<T, EPI, ACT>(p, s);
       case TILE_224x192_W8: return launch_pipe_224<T, EPI, ACT>(p, s);
-      case TILE_256x192_W8: return launch_pipe<T, 256, 192, 2, 4, EPI, ACT, 1, 1>(p, s);
       default: break;
     }
   }

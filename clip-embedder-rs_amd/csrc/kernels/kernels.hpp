@@ -57,13 +57,11 @@ enum GemmTile {
   // 2x4 waves of 112x48 (RS), 1 block / CU, 3 LDS stages (158 KiB) when K >= 192: the N = 768 residual
   // GEMMs at 12800 rows are 232 tiles, one round
   TILE_224x192_W8 = 26,
-  TILE_256x192_W8 = 28,   // 2x4 waves of 128x48 (RS), 114 KiB LDS, 1 block / CU: N = 768 at 12800 rows is 200 tiles
   TILE_SKINNY = 100,      // gemm_skinny_kernel: one wave per 16x16 block, M <= 256 (TILE_AUTO's pick there)
 };
 // The GemmTile ids the library builds (pins, tests and the timing tuner take only these).
 constexpr int kGemmTiles[] = {TILE_128x128, TILE_256x128, TILE_256x256, TILE_192x256_W8, TILE_256x256_RS,
-                              TILE_160x128_RS, TILE_160x128_W8_RS, TILE_256x256_HALF, TILE_224x192_W8,
-                              TILE_256x192_W8};
+                              TILE_160x128_RS, TILE_160x128_W8_RS, TILE_256x256_HALF, TILE_224x192_W8};
 inline bool gemm_tile_built(int t) {
   for (int k : kGemmTiles)
     if (k == t) return true;

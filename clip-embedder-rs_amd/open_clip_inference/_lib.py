@@ -36,6 +36,8 @@ _PROTOS = [
     ("clipgpu_num_devices", c_int, [c_void_p]),
     ("clipgpu_embed_pixels", c_int, [c_void_p, c_void_p, c_int64, c_int64, c_void_p]),
     ("clipgpu_embed_u8", c_int, [c_void_p, c_void_p, c_int64, c_int64, POINTER(c_float), POINTER(c_float), c_void_p]),
+    ("clipgpu_host_register", c_int, [c_void_p, ctypes.c_size_t]),
+    ("clipgpu_host_unregister", c_int, [c_void_p]),
     ("clipgpu_embed_tokens", c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_void_p]),
     ("clipgpu_embed_pixels_device", c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
     ("clipgpu_embed_u8_device", c_int, [c_void_p, c_void_p, c_int64, POINTER(c_float), POINTER(c_float), c_void_p, c_void_p]),

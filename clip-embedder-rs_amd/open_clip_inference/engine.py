@@ -129,18 +129,26 @@ class Engine:
     def input_size(self) -> int:
         return lib().clipgpu_input_size(self.handle)
 
-    def embed_pixels(self, nchw: np.ndarray) -> np.ndarray:
+    def _out(self, B: int, out: Optional[np.ndarray]) -> np.ndarray:
+        # `out`: an optional caller [B, embed_dim] float32 C-contiguous array (e.g. a registered one)
+        if out is None:
+            return np.empty((B, self.embed_dim), np.float32)
+        if out.dtype != np.float32 or out.shape != (B, self.embed_dim) or not out.flags["C_CONTIGUOUS"]:
+            raise ValueError(f"out must be a C-contiguous float32 [{B}, {self.embed_dim}] array")
+        return out
+
+    def embed_pixels(self, nchw: np.ndarray, out: Optional[np.ndarray] = None) -> np.ndarray:
         x = np.ascontiguousarray(nchw, dtype=np.float32)
         if x.ndim != 4 or x.shape[1] != 3 or x.shape[2] != x.shape[3]:
             from .error import ShapeError
             raise ShapeError(f"Shape error: expected [B,3,S,S], got {x.shape}")
-        out = np.empty((x.shape[0], self.embed_dim), np.float32)
+        out = self._out(x.shape[0], out)
         check(lib().clipgpu_embed_pixels(self.handle, x.ctypes.data, x.shape[0], x.shape[2], out.ctypes.data))
         return out
 
-    def embed_u8(self, nhwc: np.ndarray, mean, std) -> np.ndarray:
+    def embed_u8(self, nhwc: np.ndarray, mean, std, out: Optional[np.ndarray] = None) -> np.ndarray:
         x = np.ascontiguousarray(nhwc, dtype=np.uint8)
-        out = np.empty((x.shape[0], self.embed_dim), np.float32)
+        out = self._out(x.shape[0], out)
         check(lib().clipgpu_embed_u8(self.handle, x.ctypes.data, x.shape[0], x.shape[1], f3(mean), f3(std),
                                      out.ctypes.data))
         return out
@@ -161,10 +169,11 @@ class Engine:
         check(lib().clipgpu_embed_images_rgb8(self.handle, ptrs, ws, hs, n, out.ctypes.data))
         return out
 
-    def embed_tokens(self, ids: np.ndarray, mask: Optional[np.ndarray] = None) -> np.ndarray:
+    def embed_tokens(self, ids: np.ndarray, mask: Optional[np.ndarray] = None,
+                     out: Optional[np.ndarray] = None) -> np.ndarray:
         x = np.ascontiguousarray(ids, dtype=np.int64)
         m = None if mask is None else np.ascontiguousarray(mask, dtype=np.int64)
-        out = np.empty((x.shape[0], self.embed_dim), np.float32)
+        out = self._out(x.shape[0], out)
         check(lib().clipgpu_embed_tokens(self.handle, x.ctypes.data, None if m is None else m.ctypes.data,
                                          x.shape[0], x.shape[1], out.ctypes.data))
         return out
@@ -238,6 +247,18 @@ def profile_read(engine: "Engine", category: str):
     check(lib().clipgpu_profile_read(engine.handle, PROFILE_CATEGORIES.index(category), ctypes.byref(ms),
                                      ctypes.byref(n)))
     return ms.value, n.value
+
+
+def host_register(arr: np.ndarray) -> None:
+    """Registers a C-contiguous host array for direct DMA by the host-buffer entry points
+    (clipgpu_host_register).  Keep `arr` alive until host_unregister(arr)."""
+    if not arr.flags["C_CONTIGUOUS"]:
+        raise ValueError("host_register needs a C-contiguous array")
+    check(lib().clipgpu_host_register(arr.ctypes.data, arr.nbytes))
+
+
+def host_unregister(arr: np.ndarray) -> None:
+    check(lib().clipgpu_host_unregister(arr.ctypes.data))
 
 
 class Tokenizer:

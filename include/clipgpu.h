@@ -127,13 +127,25 @@ int clipgpu_embed_pixels(clipgpu_engine* e, const float* nchw, int64_t B, int64_
 int clipgpu_embed_u8(clipgpu_engine* e, const uint8_t* nhwc, int64_t B, int64_t S, const float mean[3],
                      const float std[3], float* out);
 
+/* ---- caller-registered host buffers ------------------------------------------------------
+ * The reference's embed_images / embed_texts hand host arrays to the session (src/vision.rs:102-113,
+ * src/text.rs:150-166).  By default the host-buffer entry points stage them through the handle's
+ * pinned buffers (a host copy, then the PCIe DMA).  A caller that reuses its buffers can pin them once
+ * (hipHostRegister): an embed_* call whose whole input (or output) lies inside a registered range then
+ * DMAs straight from (into) it, and a vision batch's first sub-batch is a quarter of the batch, so that
+ * only its transfer is exposed before the forward starts (the rest streams in under it).  Results are
+ * bit-identical either way.  Process-wide; the caller keeps the memory alive and unregisters it
+ * before freeing it.  Ranges may not overlap. */
+int clipgpu_host_register(void* ptr, size_t bytes);
+int clipgpu_host_unregister(void* ptr);
+
 /* ---- text forward ---------------------------------------------------------------------
  * Replaces session.run(input_ids [, attention_mask]) in TextEmbedder::embed_texts
  * (src/text.rs:148-169).  ids: [B,T] int64; mask may be NULL (the exported text graph has
  * no mask input, pull_onnx.py:296-302; it is accepted and ignored, as the reference does
  * when the graph lacks "attention_mask", src/text.rs:156-161).  The batch runs on its first
  * max(EOT index)+1 tokens (at least 16; bit-identical to the full context under causal
- * attention and argmax pooling; CLIPGPU_TRIM_TEXT=0 disables). */
+ * attention and argmax pooling; clipgpu_options.trim_text = -1 disables). */
 int clipgpu_embed_tokens(clipgpu_engine* e, const int64_t* ids, const int64_t* mask, int64_t B, int64_t T,
                          float* out);
 

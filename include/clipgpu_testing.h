@@ -60,8 +60,9 @@ int clipgpu_test_gemm_bench(int dtype, int epi, int act, int64_t M, int64_t N, i
 /* Shader-clock probe (bench.py's per-window clock): launches ONE wave on `stream` (a hipStream_t, NULL =
  * the legacy default stream) that sleeps for duration_us of wall time (s_memrealtime, 100 MHz) and writes
  * d_out[0] = shader-clock ticks (s_memtime) and d_out[1] = 100 MHz ticks elapsed over that span (device
- * uint64 buffer of 2).  Launched on a side stream beside a timed forward it reads the clock the chip holds
- * under that load (MI355X_MICROARCH.md, DVFS give-back item 6): MHz = 100 * d_out[0] / d_out[1].  Asynchronous. */
+ * uint64 buffer of 2): MHz = 100 * d_out[0] / d_out[1] (MI355X_MICROARCH.md, DVFS give-back item 6).
+ * Asynchronous.  bench.py launches it right after a timed window: resident beside a forward, its wave
+ * keeps one CU from hosting the one-block-per-CU GEMMs. */
 int clipgpu_test_clock_probe(void* stream, int64_t duration_us, uint64_t* d_out);
 
 /* Device-resident attention timing (random 16-bit qkv): mean µs per launch_attention over `iters`. */
@@ -100,7 +101,7 @@ int clipgpu_test_read_weights(const char* model_dir, int tower, const char* name
 struct clipgpu_engine;
 int clipgpu_test_engine_tiles(const struct clipgpu_engine* e, int tiles[4]);
 /* Concurrent sub-batches the engine's device-side forwards run (the creation-time tuning's pick,
- * or CLIPGPU_LANES). */
+ * or clipgpu_options.lanes). */
 int clipgpu_test_engine_lanes(const struct clipgpu_engine* e, int* dev_lanes);
 /* Gathered calls of this handle take the ragged branch (one ncclBroadcast per block) even when
  * every block has the same size (on != 0), so a one-rank or equal-shard run exercises it. */

@@ -281,6 +281,20 @@ def test_gather_plan_errors():
         _lib.check(_lib.lib().clipgpu_test_gather_plan(2, (ctypes.c_int64 * 2)(4, -1), o, ctypes.byref(e)))
 
 
+def test_host_register_argument_errors():
+    """clipgpu_host_register / _unregister refuse a NULL or empty range and an unknown pointer
+    before touching HIP (the registration itself needs a GPU: tests/test_gpu_api.py)."""
+    from open_clip_inference import _lib
+    from open_clip_inference.error import ClipError
+    buf = np.zeros(64, np.uint8)
+    with pytest.raises(ClipError, match="NULL / empty"):
+        _lib.check(_lib.lib().clipgpu_host_register(None, 64))
+    with pytest.raises(ClipError, match="NULL / empty"):
+        _lib.check(_lib.lib().clipgpu_host_register(buf.ctypes.data, 0))
+    with pytest.raises(ClipError, match="not registered"):
+        _lib.check(_lib.lib().clipgpu_host_unregister(buf.ctypes.data))
+
+
 def test_facade_math_loads_without_hip():
     """Clip.softmax / Clip.sigmoid (host math in the reference, src/clip.rs:172-185) run from the
     host-only library (no HIP, no RCCL in its dependencies), bit-exact to the main library."""

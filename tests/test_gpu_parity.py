@@ -18,7 +18,7 @@ from tests.helpers import COS_TOL, make_model_dir, normalized_pixels, specs
 
 pytestmark = pytest.mark.gpu
 
-BUILT_TILES = [1, 2, 3, 13, 14, 15, 17, 18, 26, 28]  # kernels.hpp kGemmTiles (test_cpu_abi checks the list)
+BUILT_TILES = [1, 2, 3, 13, 14, 15, 17, 18, 26]  # kernels.hpp kGemmTiles (test_cpu_abi checks the list)
 
 _CACHE = {}
 
@@ -197,6 +197,55 @@ def test_graph_replay_reads_fresh_inputs_and_matches_direct_launches(tower):
     check_rows(v0, ref)
 
 
+@pytest.mark.parametrize("tower,kind", [(0, "u8"), (0, "f32"), (1, "ids")])
+def test_registered_host_buffers_are_bit_exact(tower, kind):
+    """Host entry points over caller-registered ranges (clipgpu_host_register: direct DMA, and for a
+    registered vision input the 1/4 + 3/4 slot partition) give the staged path's bytes: registered
+    input, output or both; batches of 1, 5, a ragged 37 (> max_batch, not a multiple of 4) and
+    3 x max_batch.  Overlapping registration is refused."""
+    from open_clip_inference.engine import host_register, host_unregister
+    from open_clip_inference.error import ClipError
+    v, t = specs(VIT_B_32_CFG)
+    # text: trimming off, so the ids are DMA'd from the registered range (a trimmed batch is a copy)
+    e = engine(VIT_B_32_CFG, tower, max_batch=20, lanes=2, **({"trim_text": False} if tower else {}))
+    B = 60
+    if kind == "u8":
+        data = weights.synth_images_u8(61, B, v.image_size)
+        run = lambda x, out: e.embed_u8(x, OPENAI_MEAN, OPENAI_STD, out=out)
+    elif kind == "f32":
+        data = normalized_pixels(weights.synth_images_u8(61, B, v.image_size), OPENAI_MEAN, OPENAI_STD)
+        run = lambda x, out: e.embed_pixels(x, out=out)
+    else:
+        data = weights.synth_token_ids(61, B, t.context_length, t.vocab_size, t.vocab_size - 2,
+                                       t.vocab_size - 1, random_eot=True)
+        run = lambda x, out: e.embed_tokens(x, out=out)
+    data = np.ascontiguousarray(data)
+    want = {n: run(data[:n], None) for n in (1, 5, 37, 60)}
+    out = np.zeros((B, 512), np.float32)
+    for reg_in, reg_out in [(1, 0), (0, 1), (1, 1)]:
+        if reg_in:
+            host_register(data)
+        if reg_out:
+            host_register(out)
+        try:
+            for n in (1, 5, 37, 60):
+                out[:] = np.nan
+                got = run(data[:n], out[:n])
+                assert np.array_equal(got, want[n]), (reg_in, reg_out, n)
+                assert np.isnan(out[n:]).all()
+        finally:
+            if reg_in:
+                host_unregister(data)
+            if reg_out:
+                host_unregister(out)
+    host_register(data)
+    try:
+        with pytest.raises(ClipError, match="overlaps"):
+            host_register(data[1:])
+    finally:
+        host_unregister(data)
+
+
 def test_native_library_is_loaded():
     """The HIP library, not a fallback, is what ran (one libamdhip64 in-process)."""
     import re
@@ -220,7 +269,7 @@ def test_gemm_tile_choice_is_bit_exact(tower):
         data = weights.synth_token_ids(31, 48, t.context_length, t.vocab_size, t.vocab_size - 2,
                                        t.vocab_size - 1, random_eot=True)
     outs = []
-    pins = [[t] * 4 for t in BUILT_TILES] + [[18, 26, 18, 26], [18, 17, 18, 17], [14, 15, 3, 28], None]
+    pins = [[t] * 4 for t in BUILT_TILES] + [[18, 26, 18, 26], [18, 17, 18, 17], [14, 15, 3, 26], None]
     for tiles in pins:
         e = engine(VIT_B_32_CFG, tower, max_batch=48, gemm_tiles=tiles, patch_tile=tiles[3] if tiles else 0)
         got = (c_int * 4)()
