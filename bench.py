@@ -214,38 +214,55 @@ def load_traffic(rows_per_launch, tiles):
     return None, None
 
 
-def measure_windows(step, engine, n, steps, dev):
+def measure_windows(step, engine, n, steps, dt_first, dev):
     """Repeated windows after the timed one (N = 1), so a few-% change can be told from box-to-box
-    and run-to-run spread: each window is `steps` forward steps timed like `value`, followed at once
-    by a 2 ms one-wave clock probe (clipgpu_test_clock_probe: s_memtime ticks over s_memrealtime's
-    100 MHz) that reads the shader clock the chip holds as the load ends (MI355X_MICROARCH.md, DVFS
-    give-back).  The probe runs after the window, not beside it: a wave resident beside the
-    one-block-per-CU GEMMs keeps one CU from hosting their block (measured: 4 % slower windows, c_fc
-    +17 %).  Then profiled windows give the mean c_fc launch time (HIP events at the kernel
-    boundaries, lanes serialized, no graphs)."""
+    and run-to-run spread.  Each window is `steps` forward steps timed like `value`; windows
+    alternate:
+    - plain (`images_s`), followed at once by a 2 ms one-wave clock probe (clipgpu_test_clock_probe:
+      s_memtime ticks over s_memrealtime's 100 MHz): the clock as the load ends (`sclk_after_mhz`);
+      some boxes boost back within that time, so it is not the clock under load;
+    - probed (`images_s_probed`): the same probe on a side stream for 60 % of the first window's
+      wall time, beside the forward, reads the shader clock the chip holds under the forward's load
+      (`sclk_mhz`; MI355X_MICROARCH.md, DVFS give-back).  The probe's wave keeps one CU from hosting
+      a one-block-per-CU GEMM block, so these windows run a few % slower.
+    Then profiled windows give the mean c_fc launch time (HIP events at the kernel boundaries,
+    lanes serialized, no graphs), each with the probe beside it."""
     import statistics
     L = _lib.lib()
+    side = torch.cuda.Stream(dev)
     probe = torch.zeros(2, dtype=torch.int64, device=dev)
+    probe_us = max(1000, int(0.6 * dt_first * 1e6))
 
-    def clock_after(fn):
+    def mhz():
+        t = probe.cpu().tolist()
+        return 100.0 * t[0] / t[1] if t[1] > 0 else None
+
+    def window(fn, beside):
         torch.cuda.synchronize()
+        if beside:
+            _lib.check(L.clipgpu_test_clock_probe(ctypes.c_void_p(side.cuda_stream), probe_us,
+                                                  ctypes.c_void_p(probe.data_ptr())))
         t0 = time.perf_counter()
         out = fn()
         torch.cuda.synchronize()
         wall = time.perf_counter() - t0
+        if beside:
+            return wall, mhz(), out
         _lib.check(L.clipgpu_test_clock_probe(None, 2000, ctypes.c_void_p(probe.data_ptr())))
-        t = probe.cpu().tolist()
-        return wall, (100.0 * t[0] / t[1] if t[1] > 0 else None), out
+        return wall, mhz(), out
 
     def run_steps():
         for _ in range(steps):
             step()
 
-    rates, clocks = [], []
+    rates, after, rates_probe, clocks = [], [], [], []
     for _ in range(n):
-        wall, mhz, _ = clock_after(run_steps)
+        wall, m, _ = window(run_steps, False)
         rates.append(B_VISION * steps / wall)
-        clocks.append(mhz)
+        after.append(m)
+        wall, m, _ = window(run_steps, True)
+        rates_probe.append(B_VISION * steps / wall)
+        clocks.append(m)
     fc_us, fc_clk = [], []
     for _ in range(max(1, min(n, 3))):
         profile_enable(engine, ["c_fc"])
@@ -253,22 +270,26 @@ def measure_windows(step, engine, n, steps, dev):
         def prof_steps():
             run_steps()
             return profile_read(engine, "c_fc")
-        _, mhz, (ms, cnt) = clock_after(prof_steps)
+        _, m, (ms, cnt) = window(prof_steps, True)
         profile_enable(engine, [])
         fc_us.append(1e3 * ms / max(cnt, 1))
-        fc_clk.append(mhz)
+        fc_clk.append(m)
     good = [c for c in clocks if c]
+    med = lambda xs: round(statistics.median([x for x in xs if x]), 1) if any(xs) else None  # noqa: E731
+    r1 = lambda xs: [round(x, 1) if x else None for x in xs]  # noqa: E731
     return {"n": n, "steps": steps,
-            "images_s": [round(r, 1) for r in rates],
+            "images_s": r1(rates),
             "min": round(min(rates), 1), "median": round(statistics.median(rates), 1), "max": round(max(rates), 1),
-            "sclk_mhz": [round(c, 1) if c else None for c in clocks],
-            "sclk_mhz_median": round(statistics.median(good), 1) if good else None,
-            "images_s_per_ghz_median": round(statistics.median(r / (c / 1e3) for r, c in zip(rates, clocks) if c), 1)
+            "sclk_mhz": r1(clocks), "sclk_mhz_median": med(clocks),
+            "sclk_after_mhz": r1(after), "sclk_after_mhz_median": med(after),
+            "images_s_probed": r1(rates_probe),
+            "images_s_per_ghz_median": round(statistics.median(r / (c / 1e3) for r, c in zip(rates_probe, clocks) if c), 1)
             if good else None,
-            "c_fc_us": [round(u, 2) for u in fc_us], "c_fc_sclk_mhz": [round(c, 1) if c else None for c in fc_clk],
-            "note": "windows after the timed one (same steps each); sclk_mhz from a 2 ms one-wave "
-                    "s_memtime / s_memrealtime probe launched right after each window; c_fc from profiled windows "
-                    "(lanes serialized)"}
+            "c_fc_us": [round(u, 2) for u in fc_us], "c_fc_sclk_mhz": r1(fc_clk),
+            "note": "windows after the timed one (same steps each), alternating plain (images_s; then a 2 ms probe: "
+                    "sclk_after_mhz, the clock as the load ends) and clock-probed (images_s_probed: a one-wave "
+                    "s_memtime / s_memrealtime probe on a side stream beside the forward: sclk_mhz, the clock under "
+                    "load); c_fc from profiled windows (lanes serialized)"}
 
 
 def host_leg(engine, kind, host, steps, registered=False):
@@ -410,7 +431,7 @@ def main():
     _, (fc_ms, fc_n) = timed(vision_step, max(3, args.steps // 2), 1, ve, "c_fc")
     windows = None
     if world == 1 and args.windows > 0:
-        windows = measure_windows(vision_step, ve, args.windows, args.steps, dev)
+        windows = measure_windows(vision_step, ve, args.windows, args.steps, dt, dev)
 
     # roofline of the dominant kernel: c_fc GEMM (+QuickGELU epilogue), M=rows per launch,
     # N=3072, K=768; fc_n counts the full-row launches (12 layers, or 11 when the last one

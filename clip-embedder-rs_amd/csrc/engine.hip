@@ -78,6 +78,7 @@ struct DevWeights {
   std::vector<LayerW> layers;
   float *lnpost_w = nullptr, *lnpost_b = nullptr;
   void* proj_t = nullptr;  // [E][D] 16-bit (transposed visual.proj / text_projection)
+  float* proj_b = nullptr; // [E] text_projection.bias (SigLIP2 text; nullptr otherwise)
 };
 
 struct Replica {
@@ -102,7 +103,9 @@ struct Replica {
   // rounds and memory-bound kernels overlap the other lane's GEMMs.
   hipStream_t lane[4] = {nullptr, nullptr, nullptr, nullptr};
   hipEvent_t fork = nullptr, join[4] = {nullptr, nullptr, nullptr, nullptr};
-  hipEvent_t done[4] = {nullptr, nullptr, nullptr, nullptr};  // host path: slot's D2H finished
+  hipEvent_t done[4] = {nullptr, nullptr, nullptr, nullptr};  // host path: chunk slot's D2H finished
+  hipStream_t copy = nullptr, copy2 = nullptr;  // host path: every H2D, in chunk order (copy2: test hook)
+  hipEvent_t copied[4] = {nullptr, nullptr, nullptr, nullptr};  // host path: chunk slot's H2D finished
   // Decoded-image path (clipgpu_embed_images_rgb8): per slot, pinned staging and a device
   // arena of [descriptors | ints | raw RGB8 images], and the resize intermediate.  Grown
   // on demand (images have any size); reused across calls.
@@ -203,6 +206,10 @@ struct clipgpu_engine {
   bool comm_pending = false;
   std::vector<int> comm_devs;
   bool force_bcast = false;  // test hook: gathered calls take the ragged (broadcast) branch
+  // test hook (clipgpu_test_host_plan): the host path's chunk partition of max_batch (empty = host_chunks'
+  // default) and whether its H2Ds go on the replica's copy stream (1) or on each chunk's lane stream (0)
+  std::vector<int> host_part;
+  int host_copy_stream = 1;
   clipgpu::TowerSpec spec;
   clipgpu::PreprocessCfg pre;
   clipgpu::DType dt = clipgpu::DT_BF16;
@@ -475,7 +482,12 @@ void upload_weights(clipgpu_engine& e, Replica& r, const TensorMap& m) {
   } else {
     w.lnpost_w = f32("ln_final.weight");
     w.lnpost_b = f32("ln_final.bias");
-    w.proj_t = w16_transposed("text_projection");
+    if (s.proj_bias) {  // nn.Linear: weight already [E][D]
+      w.proj_t = w16("text_projection.weight");
+      w.proj_b = f32("text_projection.bias");
+    } else {
+      w.proj_t = w16_transposed("text_projection");
+    }
   }
   (void)D;
   (void)E;
@@ -510,8 +522,13 @@ void alloc_workspace(clipgpu_engine& e, Replica& r) {
   for (int i = 0; i < e.lanes; ++i) {
     HIP_CHECK(hipStreamCreateWithFlags(&r.lane[i], hipStreamNonBlocking));
     HIP_CHECK(hipEventCreateWithFlags(&r.join[i], hipEventDisableTiming));
-    HIP_CHECK(hipEventCreateWithFlags(&r.done[i], hipEventDisableTiming));
   }
+  for (int i = 0; i < 4; ++i) {  // host-path chunks: up to 4 (host_chunks), independent of the lanes
+    HIP_CHECK(hipEventCreateWithFlags(&r.done[i], hipEventDisableTiming));
+    HIP_CHECK(hipEventCreateWithFlags(&r.copied[i], hipEventDisableTiming));
+  }
+  HIP_CHECK(hipStreamCreateWithFlags(&r.copy, hipStreamNonBlocking));
+  HIP_CHECK(hipStreamCreateWithFlags(&r.copy2, hipStreamNonBlocking));
   HIP_CHECK(hipEventCreateWithFlags(&r.fork, hipEventDisableTiming));
   HIP_CHECK(hipEventCreateWithFlags(&r.gin, hipEventDisableTiming));
   HIP_CHECK(hipEventCreateWithFlags(&r.gout, hipEventDisableTiming));
@@ -521,8 +538,10 @@ void alloc_workspace(clipgpu_engine& e, Replica& r) {
 }
 
 void check(hipError_t err, const char* what) {
-  if (err != hipSuccess)
+  if (err != hipSuccess) {
+    (void)hipGetLastError();  // reported here; do not let the next call's launch check see it again
     throw ClipErr(CLIPGPU_ERR_DEVICE, std::string("HIP error in ") + what + ": " + hipGetErrorString(err));
+  }
 }
 
 // Times the launches of one scope when its category is enabled.  gemm = true (a single
@@ -653,7 +672,7 @@ inline bool prune_last(const clipgpu_engine& e, int B, int T) {
 // tower's token ids (pooled-token choice when the last layer is pruned), nullptr for CLS.
 // T: tokens per sequence (the text tower's trimmed length, else the tower's own).
 PoolSrc trunk(const clipgpu_engine& e, const Replica& r, int B, int causal, const int64_t* ids, hipStream_t st,
-              int T) {
+              int T, int pool_pos = 0) {
   const TowerSpec& s = e.spec;
   const int D = s.width;
   const bool prune = prune_last(e, B, T);
@@ -683,7 +702,10 @@ PoolSrc trunk(const clipgpu_engine& e, const Replica& r, int B, int causal, cons
       c.h = (char*)r.big + prune_off_h(s, B);
       rows = B;
       ProfScope ps(e, PC_TAIL, st);
-      check(launch_gather_pooled(r.x, r.h, ids, T, c.x, c.h, B, D, st), "gather pooled rows");
+      // ids == nullptr: position pool_pos of every sequence (CLS 0, SigLIP2 text T - 1)
+      check(launch_gather_pooled(r.x + (size_t)pool_pos * D, (char*)r.h + (size_t)pool_pos * D * 2, ids, T, c.x, c.h,
+                                 B, D, st),
+            "gather pooled rows");
     }
     gemm(GS_OUT, PC_OUT_PROJ, "out_proj gemm");
     {
@@ -699,7 +721,7 @@ PoolSrc trunk(const clipgpu_engine& e, const Replica& r, int B, int causal, cons
     }
     if (compact) return PoolSrc{c.x, 1, nullptr};
   }
-  return PoolSrc{r.x, T, ids};
+  return PoolSrc{r.x + (size_t)pool_pos * D, T, ids};
 }
 
 // The committed MI355X tile table (default; clipgpu_options.tuning = 0).  A trunk site's tile is
@@ -732,7 +754,21 @@ int table_tile(int site, int rows, int N, int K) {
 // share of the layer than in the vision trunk (0.7 + 0.7 ms of 9.3 ms at one lane) and overlap the
 // other lane's GEMMs, while 39424-row lanes still fill the 256x256 / 160x128 rounds (round 2's
 // two-lane text leg: 117k seq/s; round 3's one-lane table: 110k; profiles/r03_v12_text_lanes_ab.txt).
+// Round 4: a vision batch of 8192..32767 token rows (ViT-B/32 at 256 images: 12800) takes two
+// lanes too, with out_proj, c_fc, c_proj and the patch GEMM on the 4-wave 160x128 RS tile (two
+// blocks per CU, one from each lane).  Same-box A/Bs (tools/bench_variants.sh,
+// profiles/r04_lanes_ab.jsonl): one lane on the 8-wave table tiles 79.8-80.3k img/s; two lanes on the
+// same tiles 81.3k; two lanes with these 82.6-84.2k (qkv on 256x256 plain, RS or half-tile within
+// 0.5 %; c_fc on 256x256 at two lanes loses 2 %).  The round-1 tree -- two lanes of 160x128 tiles
+// -- ran 83.4k on the same box as this tree's one-lane table's 79.8k (profiles/r04_ab_trees.jsonl):
+// round 3's move to one lane was the 80.9k of BENCH_r03.
+constexpr long kVisionTwoLaneRows[2] = {8192, 32768};
+bool vision_two_lanes(const clipgpu_engine& e) {
+  const long rows = (long)e.max_batch * e.spec.tokens();
+  return e.spec.tower == TOWER_VISION && rows >= kVisionTwoLaneRows[0] && rows < kVisionTwoLaneRows[1];
+}
 int table_lanes(const clipgpu_engine& e) {
+  if (vision_two_lanes(e)) return 2;
   return e.spec.tower == TOWER_TEXT && (long)e.max_batch * e.spec.tokens() >= 32768 ? 2 : 1;
 }
 
@@ -755,6 +791,11 @@ void table_tiles(clipgpu_engine& e) {
   const int G = e.spec.grid();
   const int prow = e.spec.tower == TOWER_VISION ? rows / e.spec.tokens() * G * G : 0;
   e.tile_patch = prow >= 2048 ? TILE_160x128_W8_RS : TILE_AUTO;
+  // the two-lane vision regime (table_lanes): the 4-wave 160x128 RS tile beside the other lane
+  if (vision_two_lanes(e) && e.dev_lanes == 2 && rows >= 2048) {
+    e.tile[GS_OUT] = e.tile[GS_FC] = e.tile[GS_PROJ] = TILE_160x128_RS;
+    if (prow >= 2048) e.tile_patch = TILE_160x128_RS;
+  }
 }
 
 // clipgpu_options.gemm_tiles / patch_tile pins over the table's (or the tuner's) choice: a GemmTile
@@ -855,7 +896,9 @@ void head(const clipgpu_engine& e, const Replica& r, int B, const PoolSrc& src, 
   ProfScope ps(e, PC_HEAD, st);
   check(launch_pool_ln(e.dt, src.x, src.ids, src.tokens, r.w.lnpost_w, r.w.lnpost_b, s.ln_eps, r.pooled, B, D, st),
         "pool+ln");
-  check(launch_gemm(e.dt, A_ROWS, EPI_STORE32, ACT_NONE, rows_gemm(r.pooled, D, r.w.proj_t, nullptr, r.emb, E, B, E, D), st), "proj gemm");
+  check(launch_gemm(e.dt, A_ROWS, EPI_STORE32, ACT_NONE, rows_gemm(r.pooled, D, r.w.proj_t, r.w.proj_b, r.emb, E, B, E, D),
+                    st),
+        "proj gemm");
   check(launch_l2norm(r.emb, d_out, B, E, st), "l2norm");
 }
 
@@ -928,7 +971,9 @@ void text_forward(const clipgpu_engine& e, const Replica& r, const int64_t* d_id
                              r.x, r.h, B, T, s.width, s.vocab_size, st, ln_q(e, 0, GS_QKV, r.hs)),
         "token embed+ln_1");
   }
-  head(e, r, B, trunk(e, r, B, 1, d_ids, st, T), d_out, st);
+  // CLIP: causal, the EOT (argmax id) row pooled; SigLIP2: no mask, the last position pooled
+  head(e, r, B, trunk(e, r, B, s.causal ? 1 : 0, s.pool_last ? nullptr : d_ids, st, T, s.pool_last ? T - 1 : 0),
+       d_out, st);
 }
 
 // The replica's workspace seen from batch row b0: every activation buffer is
@@ -1181,26 +1226,37 @@ bool host_registered(const void* p, size_t n) {
   return false;
 }
 
-// Host-buffer forward over a row range of one replica, pipelined over sub-chunks on the lane
-// streams: chunk j runs on slot j % lanes -- its lane's stream and its rows of the pinned staging /
-// device input / output buffers and of the workspace (lane_view) -- so the transfer of chunk j + 1
-// overlaps the forward of chunk j, and the lanes' forwards overlap each other.  Each round of `lanes`
-// chunks covers up to max_batch rows; chunk i of a round uses rows [part[i], part[i + 1]) of the
-// max_batch-row buffers (a fixed partition, so a chunk only ever reuses rows its own stream used).
-// Inputs are staged through pinned memory (par_memcpy), or DMA'd straight from a caller-registered
-// range (clipgpu_host_register); with two lanes and a registered vision input the partition is
-// 1/4 + 3/4, so only the small first chunk's transfer is exposed.  Outputs likewise (a registered
-// output range takes the D2H directly).  A slot is reused after its previous chunk's D2H event.
+// The fixed partition of a round's max_batch rows into host-path chunks: part[0] = 0 < part[1] <
+// ... < part[C] = MB, `lanes` even chunks.  Measured on the bench's ViT-B/32 u8 batch of 256
+// (tools/host_plan_ab.py, profiles/r04_host_plan_ab.jsonl): two halves beat a small first chunk
+// (64 or 96 rows) and three- or four-chunk plans, whose small forwards run far below the full
+// batch's rate.
+std::vector<int> host_chunks(const clipgpu_engine& e, InKind kind) {
+  const int MB = e.max_batch, L = e.lanes;
+  if (!e.host_part.empty() && kind != IN_IDS) return e.host_part;
+  std::vector<int> part{0};
+  for (int i = 1; i < L; ++i) part.push_back((int)(((long)MB * i + L - 1) / L));
+  part.push_back(MB);
+  return part;
+}
+
+// Host-buffer forward over a row range of one replica.  Each round of up to max_batch rows is cut
+// by host_chunks' partition; chunk k of a round uses rows [part[k], part[k + 1]) of the
+// max_batch-row device buffers, workspace (lane_view) and pinned staging, so chunks of one round
+// never share memory and chunk k of the next round reuses only chunk k's rows, after chunk k's D2H
+// event.  The H2Ds go in chunk order on the replica's copy stream (the first chunk gets the whole
+// link); chunk k's forward runs on lane stream k % lanes once its copy event has fired, so the
+// transfer of chunk k + 1 overlaps the forward of chunk k, and forwards of different lanes
+// overlap each other.  Inputs are staged through pinned memory (par_memcpy) or DMA'd straight
+// from a caller-registered range (clipgpu_host_register); outputs likewise.
 void run_host_shard(clipgpu_engine& e, Replica& r, InKind kind, const void* in, size_t in_row_bytes, int64_t b0,
                     int64_t b1, const float* mean, const float* stdv, float* out, int tokens = 0) {
   HIP_CHECK(hipSetDevice(r.device));
   const int E = e.spec.embed_dim, L = e.lanes, MB = e.max_batch;
   const bool direct_in = host_registered((const char*)in + b0 * in_row_bytes, (size_t)(b1 - b0) * in_row_bytes);
   const bool direct_out = host_registered(out + b0 * E, (size_t)(b1 - b0) * E * 4);
-  // the fixed partition of the max_batch rows over the L slots
-  std::vector<int> part((size_t)L + 1, 0);
-  const bool quarter = L == 2 && direct_in && kind != IN_IDS && MB >= 8;
-  for (int i = 1; i <= L; ++i) part[i] = quarter ? (i == 1 ? MB / 4 : MB) : (int)(((long)MB * i + L - 1) / L);
+  const std::vector<int> part = host_chunks(e, kind);
+  const int C = (int)part.size() - 1;
   struct Pending { int64_t c0 = -1; int n = 0; };
   Pending pend[4];
   auto drain = [&](int k) {
@@ -1212,18 +1268,17 @@ void run_host_shard(clipgpu_engine& e, Replica& r, InKind kind, const void* in, 
   for (int64_t c0 = b0; c0 < b1;) {
     const int R = (int)std::min<int64_t>(MB, b1 - c0);  // rows of this round
     int off = 0;
-    for (int k = 0; k < L && off < R; ++k) {
+    for (int k = 0; k < C && off < R; ++k) {
       const int cap = part[k + 1] - part[k];
-      // even partition: fill the slots in order (a round that fits one slot is one chunk); the
-      // quarter partition: the round's rows spread in proportion to it, so a short round still
-      // exposes only a quarter of its transfer
-      int n = !quarter ? std::min(cap, R - off)
-                       : k + 1 == L ? R - off : (int)(((long)R * part[k + 1] + MB - 1) / MB - off);
+      // a round of at least half of max_batch spreads over the chunks in proportion to the
+      // partition; a shorter one fills them in order (a small batch is one forward)
+      int n = 2 * R < MB ? R - off
+              : k + 1 == C ? R - off : (int)(((long)R * part[k + 1] + MB - 1) / MB - off);
       n = std::max(0, std::min(n, cap));
       if (n == 0) continue;
       const int64_t rc = c0 + off;
       drain(k);
-      hipStream_t st = r.lane[k] ? r.lane[k] : r.stream;
+      hipStream_t st = r.lane[k % L] ? r.lane[k % L] : r.stream;
       char* din = (char*)r.in + (size_t)part[k] * in_row_bytes;
       float* dout = r.out + (size_t)part[k] * E;
       const char* src = (const char*)in + rc * in_row_bytes;
@@ -1232,7 +1287,22 @@ void run_host_shard(clipgpu_engine& e, Replica& r, InKind kind, const void* in, 
         par_memcpy(pin, src, (size_t)n * in_row_bytes);
         src = pin;
       }
-      HIP_CHECK(hipMemcpyAsync(din, src, (size_t)n * in_row_bytes, hipMemcpyHostToDevice, st));
+      if (e.host_copy_stream == 2 && n >= 2) {  // test hook: the chunk's halves on two copy streams
+        const size_t h = (size_t)(n / 2) * in_row_bytes, all = (size_t)n * in_row_bytes;
+        HIP_CHECK(hipStreamWaitEvent(r.copy2, r.copied[(k + C - 1) % C], 0));  // chunk order kept
+        HIP_CHECK(hipMemcpyAsync(din, src, h, hipMemcpyHostToDevice, r.copy));
+        HIP_CHECK(hipMemcpyAsync(din + h, src + h, all - h, hipMemcpyHostToDevice, r.copy2));
+        HIP_CHECK(hipEventRecord(r.copied[k], r.copy2));
+        HIP_CHECK(hipStreamWaitEvent(r.copy, r.copied[k], 0));
+        HIP_CHECK(hipEventRecord(r.copied[k], r.copy));
+        HIP_CHECK(hipStreamWaitEvent(st, r.copied[k], 0));
+      } else if (e.host_copy_stream) {
+        HIP_CHECK(hipMemcpyAsync(din, src, (size_t)n * in_row_bytes, hipMemcpyHostToDevice, r.copy));
+        HIP_CHECK(hipEventRecord(r.copied[k], r.copy));
+        HIP_CHECK(hipStreamWaitEvent(st, r.copied[k], 0));
+      } else {
+        HIP_CHECK(hipMemcpyAsync(din, src, (size_t)n * in_row_bytes, hipMemcpyHostToDevice, st));
+      }
       const Replica v = lane_view(e, r, part[k]);
       run_graph(e, r,
                 {(uint64_t)(10 + kind), (uint64_t)k, (uint64_t)n, fbits(mean, 0), fbits(mean, 1), fbits(mean, 2),
@@ -1252,7 +1322,7 @@ void run_host_shard(clipgpu_engine& e, Replica& r, InKind kind, const void* in, 
     }
     c0 += R;
   }
-  for (int k = 0; k < L; ++k) drain(k);
+  for (int k = 0; k < C; ++k) drain(k);
 }
 
 void run_host(clipgpu_engine& e, InKind kind, const void* in, size_t in_row_bytes, int64_t B, const float* mean,
@@ -1574,10 +1644,13 @@ void destroy_replica(Replica& r) {
   if (r.pin_in) (void)hipHostFree(r.pin_in);
   if (r.pin_out) (void)hipHostFree(r.pin_out);
   if (r.stream) (void)hipStreamDestroy(r.stream);
+  if (r.copy) (void)hipStreamDestroy(r.copy);
+  if (r.copy2) (void)hipStreamDestroy(r.copy2);
   for (int i = 0; i < 4; ++i) {
     if (r.lane[i]) (void)hipStreamDestroy(r.lane[i]);
     if (r.join[i]) (void)hipEventDestroy(r.join[i]);
     if (r.done[i]) (void)hipEventDestroy(r.done[i]);
+    if (r.copied[i]) (void)hipEventDestroy(r.copied[i]);
   }
   if (r.fork) (void)hipEventDestroy(r.fork);
   if (r.gin) (void)hipEventDestroy(r.gin);
@@ -1857,7 +1930,9 @@ int clipgpu_embed_tokens(clipgpu_engine* e, const int64_t* ids, const int64_t* m
     // (test_text_trim_is_bit_exact).  clipgpu_options.trim_text = -1 disables.  A trimmed batch is
     // a private copy, so it is staged even when `ids` lies in a registered range.
     int64_t Tc = T;
-    if (e->trim) {
+    // only for the causal, EOT-pooled (CLIP) form: SigLIP2's text tower attends to and pools
+    // the last context position
+    if (e->trim && e->spec.causal && !e->spec.pool_last) {
       Tc = 1;
       for (int64_t b = 0; b < B && Tc < T; ++b) {
         const int64_t* row = ids + b * T;
@@ -2136,6 +2211,26 @@ int clipgpu_test_gather_plan(int nranks, const int64_t* rows, int64_t* off, int*
     const GatherPlan g = plan_gather(nranks, rows);
     for (int r = 0; r <= nranks; ++r) off[r] = g.off[r];
     *equal = g.equal ? 1 : 0;
+  });
+}
+
+int clipgpu_test_host_plan(clipgpu_engine* e, int n_chunks, const int* bounds, int copy_stream) {
+  return guarded([&]() {
+    if (!e) throw ClipErr(CLIPGPU_ERR_INVALID, "engine is NULL");
+    std::lock_guard<std::mutex> lk(e->mu);
+    if (copy_stream < 0 || copy_stream > 2) throw ClipErr(CLIPGPU_ERR_INVALID, "copy_stream: 0, 1 or 2");
+    e->host_copy_stream = copy_stream;
+    e->host_part.clear();
+    if (n_chunks == 0) return;
+    if (n_chunks < 1 || n_chunks > 4 || !bounds) throw ClipErr(CLIPGPU_ERR_INVALID, "1..4 chunks");
+    std::vector<int> part{0};
+    for (int i = 0; i < n_chunks - 1; ++i) {
+      if (bounds[i] <= part.back() || bounds[i] >= e->max_batch)
+        throw ClipErr(CLIPGPU_ERR_INVALID, "chunk bounds must increase inside (0, max_batch)");
+      part.push_back(bounds[i]);
+    }
+    part.push_back(e->max_batch);
+    e->host_part = part;
   });
 }
 

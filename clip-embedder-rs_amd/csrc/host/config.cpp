@@ -24,6 +24,8 @@ static int act_from(const json::Value& model_cfg, const json::Value* sub) {
   if (sub) {
     const json::Value* a = sub->get("act_layer");
     if (a && (a->as_str("") == "gelu_tanh" || a->as_str("") == "gelu_pytorch_tanh")) return 3;
+    const json::Value* k = sub->get("act_kwargs");  // open_clip nn.GELU(approximate="tanh")
+    if (k && k->get("approximate") && k->get("approximate")->as_str("") == "tanh") return 3;
   }
   const json::Value* q = model_cfg.get("quick_gelu");
   return (q && q->as_bool(false)) ? 1 : 2;  // ACT_QUICK_GELU : ACT_GELU
@@ -117,10 +119,11 @@ OpenClipConfig load_open_clip_config(const std::string& path) {
   ts.mlp_width = (int)(ts.width * getd(t, "mlp_ratio", 4.0));
   ts.embed_dim = c.embed_dim;
   ts.act = act_from(*mc, t);
-  // The text engine builds open_clip's TextTransformer as CLIP exports it: causal mask,
-  // argmax (EOT) pooling, linear projection without bias.  Host-side sequence trimming and
-  // last-layer pruning both rely on the causal mask + argmax pooling, so any other form (e.g.
-  // SigLIP's text_cfg: no_causal_mask, pool_type "last", proj_bias) is refused, not mis-run.
+  // The text engine builds open_clip's TextTransformer in its two exported forms: CLIP's (causal
+  // mask, argmax / EOT pooling, projection matrix) and SigLIP2's (no_causal_mask, pool_type "last",
+  // proj_bias, GELU tanh, norm eps 1e-6).  Other forms are refused, not mis-run.
+  if (const json::Value* nk = t->get("norm_kwargs"))
+    if (const json::Value* ep = nk->get("eps")) ts.ln_eps = (float)ep->as_num(1e-5);
   auto text_flag = [&](const char* key) {
     const json::Value* f = t->get(key);
     return f && !f->is_null() && f->as_bool(false);
@@ -129,15 +132,17 @@ OpenClipConfig load_open_clip_config(const std::string& path) {
     const json::Value* f = t->get(key);
     return (f && !f->is_null()) ? f->as_str(dflt) : std::string(dflt);
   };
-  if (text_flag("no_causal_mask"))
-    ts.unsupported = "Configuration error: text_cfg.no_causal_mask is not supported (causal text tower only)";
-  else if (text_str("pool_type", "argmax") != "argmax")
-    ts.unsupported = "Configuration error: text_cfg.pool_type '" + text_str("pool_type", "") +
-                     "' is not supported (argmax / EOT pooling only)";
+  ts.causal = !text_flag("no_causal_mask");
+  ts.pool_last = text_str("pool_type", "argmax") == "last";
+  ts.proj_bias = text_flag("proj_bias");
+  const std::string pool = text_str("pool_type", "argmax");
+  if (pool != "argmax" && pool != "last")
+    ts.unsupported = "Configuration error: text_cfg.pool_type '" + pool +
+                     "' is not supported (argmax / EOT or last-token pooling only)";
   else if (text_str("proj_type", "linear") != "linear")
     ts.unsupported = "Configuration error: text_cfg.proj_type '" + text_str("proj_type", "") + "' is not supported";
-  else if (text_flag("proj_bias") || text_flag("embed_cls"))
-    ts.unsupported = "Configuration error: text_cfg.proj_bias / embed_cls are not supported";
+  else if (text_flag("embed_cls"))
+    ts.unsupported = "Configuration error: text_cfg.embed_cls is not supported";
   else if (t->get("hf_model_name") && !t->get("hf_model_name")->is_null())
     ts.unsupported = "Configuration error: HF text towers (text_cfg.hf_model_name) are not supported";
 

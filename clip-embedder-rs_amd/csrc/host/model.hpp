@@ -47,6 +47,10 @@ struct TowerSpec {
   int tokens() const { return tower == TOWER_VISION ? grid() * grid() + (cls() ? 1 : 0) : context_length; }
   // text
   int context_length = 0, vocab_size = 0;
+  // open_clip TextTransformer form: CLIP (causal mask, argmax / EOT pooling, projection matrix) or
+  // SigLIP2 (text_cfg no_causal_mask, pool_type "last": the final context position, proj_bias:
+  // text_projection is an nn.Linear with bias)
+  bool causal = true, pool_last = false, proj_bias = false;
   // Non-empty: the config asks for a tower form the engine does not build (clipgpu_create fails
   // with this message; the other tower of the same folder still loads).
   std::string unsupported;

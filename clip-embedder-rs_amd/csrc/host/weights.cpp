@@ -139,7 +139,12 @@ std::vector<ParamDesc> tower_params(const TowerSpec& s) {
     for (int i = 0; i < L; ++i) block_params(out, "transformer.resblocks." + std::to_string(i) + ".", D, M, L);
     out.push_back({"ln_final.weight", {D}, LN_GAIN_STD, 1.0});
     out.push_back({"ln_final.bias", {D}, LN_BIAS_STD, 0.0});
-    out.push_back({"text_projection", {D, E}, std::pow((double)D, -0.5), 0.0});
+    if (s.proj_bias) {  // open_clip nn.Linear(width, embed_dim)
+      out.push_back({"text_projection.weight", {E, D}, std::pow((double)D, -0.5), 0.0});
+      out.push_back({"text_projection.bias", {E}, 0.02, 0.0});
+    } else {
+      out.push_back({"text_projection", {D, E}, std::pow((double)D, -0.5), 0.0});
+    }
   }
   return out;
 }

@@ -72,6 +72,7 @@ _PROTOS = [
     ("clipgpu_test_gemm_bench", c_int, [c_int, c_int, c_int, c_int64, c_int64, c_int64, c_int, c_int, POINTER(c_double)]),
     ("clipgpu_test_engine_tiles", c_int, [c_void_p, POINTER(c_int)]),
     ("clipgpu_test_engine_lanes", c_int, [c_void_p, POINTER(c_int)]),
+    ("clipgpu_test_host_plan", c_int, [c_void_p, c_int, POINTER(c_int), c_int]),
     ("clipgpu_test_force_broadcast", c_int, [c_void_p, c_int]),
     ("clipgpu_test_gather_plan", c_int, [c_int, POINTER(c_int64), POINTER(c_int64), POINTER(c_int)]),
     ("clipgpu_test_read_weights", c_int, [c_char_p, c_int, c_char_p, c_void_p, c_int64]),

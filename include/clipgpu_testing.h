@@ -103,6 +103,12 @@ int clipgpu_test_engine_tiles(const struct clipgpu_engine* e, int tiles[4]);
 /* Concurrent sub-batches the engine's device-side forwards run (the creation-time tuning's pick,
  * or clipgpu_options.lanes). */
 int clipgpu_test_engine_lanes(const struct clipgpu_engine* e, int* dev_lanes);
+/* The host-buffer vision path's chunk plan (tools/host_plan_ab.py): n_chunks (1..4) chunks of a
+ * max_batch round cut at bounds[0 .. n_chunks - 2]; n_chunks = 0 restores the default
+ * (engine.hip host_chunks).  copy_stream = 1: the H2Ds in chunk order on the replica's copy
+ * stream (default); 0: each on its chunk's lane stream; 2: each chunk's two halves on two copy
+ * streams at once.  Speed only, never the bits. */
+int clipgpu_test_host_plan(struct clipgpu_engine* e, int n_chunks, const int* bounds, int copy_stream);
 /* Gathered calls of this handle take the ragged branch (one ncclBroadcast per block) even when
  * every block has the same size (on != 0), so a one-rank or equal-shard run exercises it. */
 int clipgpu_test_force_broadcast(struct clipgpu_engine* e, int on);

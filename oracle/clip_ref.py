@@ -140,16 +140,26 @@ def encode_image(P: Dict[str, np.ndarray], v: VisionSpec, pixels: np.ndarray,
 
 def encode_text(P: Dict[str, np.ndarray], t: TextSpec, ids: np.ndarray,
                 dtype=np.float64, normalize: bool = True) -> np.ndarray:
-    """open_clip encode_text (causal, argmax/EOT pooling) + normalize.  ids: [B,T] int64."""
+    """open_clip TextTransformer.forward (transformer.py: token + positional embedding, the
+    resblocks with the causal mask unless no_causal_mask, ln_final, text_global_pool, projection)
+    + normalize.  CLIP: causal, argmax / EOT pooling, projection matrix.  SigLIP2: no mask,
+    pool_type "last" (x[:, -1], the final context position, padding included), nn.Linear
+    projection with bias.  ids: [B,T] int64."""
     P = _cast(P, dtype)
     ids = np.asarray(ids, dtype=np.int64)
     B, T = ids.shape
     x = P["token_embedding.weight"][ids] + P["positional_embedding"][:T]
     for i in range(t.layers):
-        x = _resblock(P, f"transformer.resblocks.{i}.", x, t.heads, t.act, t.ln_eps, True)
+        x = _resblock(P, f"transformer.resblocks.{i}.", x, t.heads, t.act, t.ln_eps, t.causal)
     x = layer_norm(x, P["ln_final.weight"], P["ln_final.bias"], t.ln_eps)
-    pooled = x[np.arange(B), ids.argmax(-1)]          # first occurrence of the max id (EOT)
-    out = pooled @ P["text_projection"]
+    if t.pool == "last":
+        pooled = x[:, -1]
+    else:
+        pooled = x[np.arange(B), ids.argmax(-1)]      # first occurrence of the max id (EOT)
+    if t.proj_bias:
+        out = pooled @ P["text_projection.weight"].T + P["text_projection.bias"]
+    else:
+        out = pooled @ P["text_projection"]
     return l2_normalize(out) if normalize else out
 
 

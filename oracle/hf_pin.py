@@ -84,6 +84,45 @@ def hf_text(P, t, dtype="float64"):
     return m.to(getattr(torch, dtype))
 
 
+def hf_siglip_text(P, t, dtype="float64"):
+    """HF SiglipTextModel (no causal mask, last-position pooling, `head` Linear) with the
+    open_clip-named seeded weights of a SigLIP2-form text tower (text_cfg no_causal_mask,
+    pool_type "last", proj_bias; transformers' Siglip2 text tower is the same module)."""
+    import torch
+    from transformers import SiglipTextConfig, SiglipTextModel
+    assert not t.causal and t.pool == "last" and t.proj_bias
+    cfg = SiglipTextConfig(vocab_size=t.vocab_size, hidden_size=t.width, intermediate_size=t.mlp_width,
+                           num_hidden_layers=t.layers, num_attention_heads=t.heads,
+                           max_position_embeddings=t.context_length, hidden_act="gelu_pytorch_tanh",
+                           layer_norm_eps=t.ln_eps, projection_size=t.embed_dim, bos_token_id=None,
+                           eos_token_id=None, pad_token_id=None, attn_implementation="eager")
+    m = SiglipTextModel(cfg).eval()
+    sd = {
+        "text_model.embeddings.token_embedding.weight": P["token_embedding.weight"],
+        "text_model.embeddings.position_embedding.weight": P["positional_embedding"],
+        "text_model.final_layer_norm.weight": P["ln_final.weight"],
+        "text_model.final_layer_norm.bias": P["ln_final.bias"],
+        "text_model.head.weight": P["text_projection.weight"],
+        "text_model.head.bias": P["text_projection.bias"],
+    }
+    for i in range(t.layers):
+        _split_block(P, f"transformer.resblocks.{i}.", f"text_model.encoder.layers.{i}.", t.width, sd)
+    pre = "" if any(k.startswith("embeddings.") for k in m.state_dict()) else "text_model."
+    sd = {pre + k[len("text_model."):]: torch.from_numpy(np.ascontiguousarray(x)) for k, x in sd.items()}
+    missing, unexpected = m.load_state_dict(sd, strict=False)
+    missing = [k for k in missing if not k.endswith("position_ids")]
+    assert not missing and not unexpected, (missing, unexpected)
+    return m.to(getattr(torch, dtype))
+
+
+def hf_siglip_encode_text(m, ids):
+    import torch
+    with torch.no_grad():
+        e = m(input_ids=torch.from_numpy(np.asarray(ids, np.int64))).pooler_output
+        e = torch.nn.functional.normalize(e, dim=-1)
+    return e.double().numpy()
+
+
 def hf_encode_image(m, pixels):
     import torch
     dt = next(m.parameters()).dtype

@@ -58,6 +58,12 @@ class TextSpec:
     embed_dim: int
     act: str
     ln_eps: float = 1e-5
+    # open_clip TextTransformer forms: CLIP's (causal mask, argmax / EOT pooling, projection
+    # matrix without bias) and SigLIP2's (no_causal_mask, pool_type "last": the final context
+    # position, padding included; text_projection an nn.Linear with bias)
+    causal: bool = True
+    pool: str = "argmax"        # "argmax" | "last"
+    proj_bias: bool = False
 
     @property
     def head_dim(self) -> int:
@@ -66,6 +72,8 @@ class TextSpec:
 
 def _act(model_cfg: dict, sub: dict) -> str:
     if sub.get("act_layer") in ("gelu_tanh", "gelu_pytorch_tanh"):
+        return "gelu_tanh"
+    if (sub.get("act_kwargs") or {}).get("approximate") == "tanh":  # open_clip nn.GELU(approximate="tanh")
         return "gelu_tanh"
     return "quick_gelu" if model_cfg.get("quick_gelu", False) else "gelu"
 
@@ -126,6 +134,11 @@ def text_spec_from_cfg(model_cfg: dict) -> TextSpec:
     t = model_cfg["text_cfg"]
     if t.get("hf_model_name"):
         raise ValueError("text_cfg.hf_model_name (HF text towers) is not supported by this oracle")
+    pool = t.get("pool_type", "argmax")
+    if pool not in ("argmax", "last"):
+        raise ValueError(f"text_cfg.pool_type {pool!r} is not supported by this oracle")
+    if t.get("proj_type", "linear") != "linear" or t.get("embed_cls"):
+        raise ValueError("only a linear text projection without a CLS embedding is supported by this oracle")
     width = int(t.get("width", 512))
     return TextSpec(
         context_length=int(t.get("context_length", 77)),
@@ -136,6 +149,10 @@ def text_spec_from_cfg(model_cfg: dict) -> TextSpec:
         mlp_width=int(width * float(t.get("mlp_ratio", 4.0))),
         embed_dim=int(model_cfg["embed_dim"]),
         act=_act(model_cfg, t),
+        ln_eps=float((t.get("norm_kwargs") or {}).get("eps", 1e-5)),
+        causal=not t.get("no_causal_mask", False),
+        pool=pool,
+        proj_bias=bool(t.get("proj_bias", False)),
     )
 
 
@@ -216,8 +233,10 @@ SO400M_16_SIGLIP2_384_CFG = {
         "init_logit_bias": -10,
         "vision_cfg": {"image_size": 384, "timm_model_name": "vit_so400m_patch16_siglip_384",
                        "timm_model_pretrained": False, "timm_pool": "map", "timm_proj": "none"},
-        "text_cfg": {"context_length": 64, "vocab_size": 256000, "width": 1152, "heads": 16, "layers": 27,
-                     "mlp_ratio": 3.7362},
+        "text_cfg": {"context_length": 64, "vocab_size": 256000, "hf_tokenizer_name": "timm/ViT-SO400M-16-SigLIP2-384",
+                     "tokenizer_kwargs": {"clean": "canonicalize"}, "width": 1152, "heads": 16, "layers": 27,
+                     "mlp_ratio": 3.7362, "no_causal_mask": True, "proj_bias": True, "pool_type": "last",
+                     "norm_kwargs": {"eps": 1e-6}, "act_kwargs": {"approximate": "tanh"}},
     },
     "preprocess_cfg": {"mean": SIGLIP_MEAN, "std": SIGLIP_STD, "interpolation": "bicubic", "resize_mode": "squash"},
 }
@@ -231,7 +250,11 @@ def tiny_siglip_cfg(image_size=64, layers=2, mlp_width=1000):
             "vision_cfg": {"image_size": image_size, "timm_model_name": "vit_so400m_patch16_siglip_384",
                            "timm_pool": "map", "timm_proj": "none",
                            "clipgpu_dims": {"width": 576, "layers": layers, "heads": 8, "mlp_width": mlp_width}},
-            "text_cfg": {"context_length": 16, "vocab_size": 1000, "width": 128, "heads": 2, "layers": 1},
+            # SigLIP2-structured text tower (head dim 72, MLP int(576 * 3.7362) = 2152, not a multiple
+            # of 64, projection with bias)
+            "text_cfg": {"context_length": 16, "vocab_size": 1000, "width": 576, "heads": 8, "layers": 2,
+                         "mlp_ratio": 3.7362, "no_causal_mask": True, "proj_bias": True, "pool_type": "last",
+                         "norm_kwargs": {"eps": 1e-6}, "act_kwargs": {"approximate": "tanh"}},
         },
         "preprocess_cfg": {"mean": SIGLIP_MEAN, "std": SIGLIP_STD},
     }

@@ -88,14 +88,18 @@ class VisionCPU:
 
 
 class TextCPU:
-    """open_clip encode_text (causal, argmax/EOT pooling) + F.normalize, fp32 on the CPU."""
+    """open_clip encode_text + F.normalize, fp32 on the CPU: CLIP (causal, argmax / EOT pooling,
+    projection matrix) or SigLIP2 (no mask, last-position pooling, linear projection with bias)."""
 
     def __init__(self, P: Dict[str, np.ndarray], t: TextSpec):
         self.t = t
         tt = lambda k: torch.from_numpy(np.ascontiguousarray(P[k], np.float32))  # noqa: E731
         self.tok, self.pos = tt("token_embedding.weight"), tt("positional_embedding")
         self.ln_final = (tt("ln_final.weight"), tt("ln_final.bias"))
-        self.proj = tt("text_projection")
+        if t.proj_bias:
+            self.proj, self.proj_b = tt("text_projection.weight").T.contiguous(), tt("text_projection.bias")
+        else:
+            self.proj, self.proj_b = tt("text_projection"), None
         self.trunk = _Tower(P, "transformer.resblocks.", t.layers, t.heads, t.width, t.act, t.ln_eps)
 
     @torch.inference_mode()
@@ -103,6 +107,10 @@ class TextCPU:
         ids = torch.from_numpy(np.ascontiguousarray(ids, np.int64))
         B, T = ids.shape
         x = self.tok[ids] + self.pos[:T]
-        x = self.trunk(x, causal=True)
-        x = F.layer_norm(x[torch.arange(B), ids.argmax(-1)], (self.t.width,), *self.ln_final, self.t.ln_eps)
-        return F.normalize(x @ self.proj, dim=-1).numpy()
+        x = self.trunk(x, causal=self.t.causal)
+        pooled = x[:, -1] if self.t.pool == "last" else x[torch.arange(B), ids.argmax(-1)]
+        x = F.layer_norm(pooled, (self.t.width,), *self.ln_final, self.t.ln_eps)
+        y = x @ self.proj
+        if self.proj_b is not None:
+            y = y + self.proj_b
+        return F.normalize(y, dim=-1).numpy()

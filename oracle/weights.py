@@ -182,8 +182,12 @@ def text_param_list(t: TextSpec) -> ParamList:
     out += [
         ("ln_final.weight", (D,), LN_GAIN_STD, 1.0),
         ("ln_final.bias", (D,), LN_BIAS_STD, 0.0),
-        ("text_projection", (D, t.embed_dim), D ** -0.5, 0.0),
     ]
+    if t.proj_bias:  # open_clip nn.Linear(width, embed_dim): weight [E, D] + bias
+        out += [("text_projection.weight", (t.embed_dim, D), D ** -0.5, 0.0),
+                ("text_projection.bias", (t.embed_dim,), 0.02, 0.0)]
+    else:
+        out += [("text_projection", (D, t.embed_dim), D ** -0.5, 0.0)]
     return out
 
 

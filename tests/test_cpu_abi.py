@@ -134,15 +134,16 @@ def test_param_inventory_matches_oracle(cfg_name):
             assert np.array_equal(out, ref.ravel()), name
 
 
-@pytest.mark.parametrize("extra,msg", [({"no_causal_mask": True}, "no_causal_mask"),
-                                       ({"pool_type": "last"}, "pool_type 'last'"),
+@pytest.mark.parametrize("extra,msg", [({"pool_type": "first"}, "pool_type 'first'"),
+                                       ({"pool_type": "none"}, "pool_type 'none'"),
                                        ({"proj_type": "mlp"}, "proj_type 'mlp'"),
-                                       ({"proj_bias": True}, "proj_bias"),
+                                       ({"embed_cls": True}, "embed_cls"),
                                        ({"hf_model_name": "google/siglip"}, "hf_model_name")])
 def test_unsupported_text_tower_forms_are_refused(extra, msg):
-    """The text engine's trimming and last-layer pruning assume open_clip's causal,
-    argmax-pooled text tower: any other text_cfg form (SigLIP's, HF towers) is a Configuration
-    error at clipgpu_create, raised before any device call (runs on CPU)."""
+    """The text engine builds open_clip's TextTransformer in its CLIP form (causal, argmax / EOT
+    pooling) and its SigLIP2 form (no_causal_mask, pool_type "last", proj_bias; TINY_SIGLIP_CFG);
+    any other text_cfg form (other poolings, MLP projections, CoCa's CLS embedding, HF towers) is
+    a Configuration error at clipgpu_create, raised before any device call (runs on CPU)."""
     import json
     from open_clip_inference import _lib
     from open_clip_inference.engine import Engine
@@ -152,14 +153,16 @@ def test_unsupported_text_tower_forms_are_refused(extra, msg):
     d = make_model_dir(cfg)
     with pytest.raises(ConfigError, match=msg):
         Engine(d, _lib.TOWER_TEXT, [0], "bf16", 8)
-    # the default form passes the check (and then fails only for want of a GPU here)
-    d = make_model_dir(TINY_CFG)
-    try:
-        Engine(d, _lib.TOWER_TEXT, [0], "bf16", 8).close()
-    except ConfigError as e:  # pragma: no cover
-        raise AssertionError(e)
-    except Exception:
-        pass
+    # the CLIP and SigLIP2 forms pass the check (and then fail only for want of a GPU here)
+    from oracle.model_spec import TINY_SIGLIP_CFG
+    for ok in (TINY_CFG, TINY_SIGLIP_CFG):
+        d = make_model_dir(ok)
+        try:
+            Engine(d, _lib.TOWER_TEXT, [0], "bf16", 8).close()
+        except ConfigError as e:  # pragma: no cover
+            raise AssertionError(e)
+        except Exception:
+            pass
 
 
 def test_library_provenance_is_checked(monkeypatch):

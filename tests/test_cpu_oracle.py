@@ -82,6 +82,38 @@ def test_siglip_oracle_vs_hf(cfg_name):
     assert np.abs(got - ref).max() < 1e-7
 
 
+@pytest.mark.parametrize("ctx,layers", [(16, 2), (64, 1)])
+def test_siglip2_text_oracle_vs_hf(ctx, layers):
+    """SigLIP2-form text tower (open_clip text_cfg no_causal_mask, pool_type "last", proj_bias,
+    GELU tanh, eps 1e-6; head dim 72, MLP 2152) vs HF SiglipTextModel on the same weights: no
+    causal mask, the last context position pooled (padding included), `head` Linear with bias."""
+    pytest.importorskip("transformers")
+    from oracle import hf_pin, model_spec
+    cfg = model_spec.tiny_siglip_cfg()
+    cfg["model_cfg"]["text_cfg"].update({"context_length": ctx, "layers": layers})
+    t = text_spec_from_cfg(cfg["model_cfg"])
+    assert (not t.causal, t.pool, t.proj_bias, t.act, t.ln_eps, t.head_dim, t.mlp_width) == \
+        (True, "last", True, "gelu_tanh", 1e-6, 72, 2152)
+    P = weights.text_weights(t, 11)
+    ids = weights.synth_token_ids(6, 3, t.context_length, t.vocab_size, t.vocab_size - 2, t.vocab_size - 1,
+                                  random_eot=True)
+    got = clip_ref.encode_text(P, t, ids)
+    assert np.abs(got - hf_pin.hf_siglip_encode_text(hf_pin.hf_siglip_text(P, t), ids)).max() < 1e-7
+    # every position reaches the pooled (last) one: a token after the "EOT" changes the output
+    ids2 = ids.copy()
+    p = int(np.argmax(ids2[0]))
+    ids2[0, p + 1:] = 7
+    assert clip_ref.cosine_rows(clip_ref.encode_text(P, t, ids2)[:1], got[:1]).min() < 1 - 1e-9
+
+
+def test_so400m_siglip2_text_spec():
+    from oracle import model_spec
+    t = text_spec_from_cfg(model_spec.SO400M_16_SIGLIP2_384_CFG["model_cfg"])
+    assert (t.context_length, t.vocab_size, t.width, t.layers, t.heads, t.mlp_width, t.embed_dim, t.head_dim) == \
+        (64, 256000, 1152, 27, 16, 4304, 1152, 72)
+    assert (t.causal, t.pool, t.proj_bias, t.act, t.ln_eps) == (False, "last", True, "gelu_tanh", 1e-6)
+
+
 def test_so400m_siglip2_spec():
     from oracle import model_spec
     v = vision_spec_from_cfg(model_spec.SO400M_16_SIGLIP2_384_CFG["model_cfg"])
@@ -90,7 +122,7 @@ def test_so400m_siglip2_spec():
     assert v.act == "gelu_tanh" and v.ln_eps == 1e-6 and v.embed_dim == 1152
 
 
-@pytest.mark.parametrize("cfg_name", ["TINY_CFG", "VIT_B_32_CFG"])
+@pytest.mark.parametrize("cfg_name", ["TINY_CFG", "VIT_B_32_CFG", "TINY_SIGLIP_CFG"])
 def test_torch_cpu_port_matches_oracle(cfg_name):
     """oracle/torch_cpu.py (the fp32 CPU baseline bench.py times) computes the fp64 oracle's
     embeddings to fp32 accuracy."""
@@ -104,6 +136,7 @@ def test_torch_cpu_port_matches_oracle(cfg_name):
     px = np.random.default_rng(3).standard_normal((2, 3, v.image_size, v.image_size)).astype(np.float32)
     ids = weights.synth_token_ids(4, 3, t.context_length, t.vocab_size, t.vocab_size - 2, t.vocab_size - 1,
                                   random_eot=True)
-    cv = clip_ref.cosine_rows(torch_cpu.VisionCPU(Pv, v)(px), clip_ref.encode_image(Pv, v, px))
+    cv = (clip_ref.cosine_rows(torch_cpu.VisionCPU(Pv, v)(px), clip_ref.encode_image(Pv, v, px))
+          if v.family == "clip" else np.ones(1))  # SigLIP vision: the MAP head is not ported
     ct = clip_ref.cosine_rows(torch_cpu.TextCPU(Pt, t)(ids), clip_ref.encode_text(Pt, t, ids))
     assert cv.min() > 0.999999 and ct.min() > 0.999999, (cv, ct)

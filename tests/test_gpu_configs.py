@@ -92,6 +92,14 @@ def test_so400m_siglip2_384_shard_128(dtype, mx_sites, bar):
     _check_shard(SO400M_16_SIGLIP2_384_CFG, 0, 128, dtype, mx_sites, bar, "SO400M vision")
 
 
+def test_so400m_siglip2_text_shard_128():
+    """The SigLIP2 text tower of the same model folder (the reference's README model,
+    README.md:72-80; open_clip text_cfg no_causal_mask, pool_type "last", proj_bias): 27 layers of
+    width 1152, 64-token context, 128 sequences per GPU, against the fp64 oracle (itself pinned to
+    HF SiglipTextModel, tests/test_cpu_oracle.py)."""
+    _check_shard(SO400M_16_SIGLIP2_384_CFG, 1, 128, "bf16", None, COS_TOL, "SO400M-SigLIP2 text")
+
+
 # configs[4]: bf16; the shipped fp8 split (QKV, c_fc, c_proj in MX); and the split whose two towers
 # both meet the north-star bar (vision MX at QKV only, text bf16 -- per-engine options).
 @pytest.mark.parametrize("dtype,mx_sites,bar", [("bf16", None, COS_TOL), ("fp8", None, FP8_COS_VISION),

@@ -66,7 +66,8 @@ def test_vision_parity(cfg, B, dtype):
 
 
 @pytest.mark.parametrize("cfg,B,random_eot", [(TINY_CFG, 5, True), (VIT_B_32_CFG, 6, False),
-                                              (VIT_B_32_CFG, 7, True)])
+                                              (VIT_B_32_CFG, 7, True), (TINY_SIGLIP_CFG, 5, True),
+                                              (TINY_SIGLIP_CFG, 3, False)])
 @pytest.mark.parametrize("dtype", ["bf16", "f16"])
 def test_text_parity(cfg, B, random_eot, dtype):
     _, t = specs(cfg)
@@ -197,17 +198,18 @@ def test_graph_replay_reads_fresh_inputs_and_matches_direct_launches(tower):
     check_rows(v0, ref)
 
 
-@pytest.mark.parametrize("tower,kind", [(0, "u8"), (0, "f32"), (1, "ids")])
-def test_registered_host_buffers_are_bit_exact(tower, kind):
-    """Host entry points over caller-registered ranges (clipgpu_host_register: direct DMA, and for a
-    registered vision input the 1/4 + 3/4 slot partition) give the staged path's bytes: registered
-    input, output or both; batches of 1, 5, a ragged 37 (> max_batch, not a multiple of 4) and
-    3 x max_batch.  Overlapping registration is refused."""
+@pytest.mark.parametrize("tower,kind,mb", [(0, "u8", 20), (0, "u8", 40), (0, "f32", 40), (1, "ids", 20)])
+def test_registered_host_buffers_are_bit_exact(tower, kind, mb):
+    """Host entry points over caller-registered ranges (clipgpu_host_register: direct DMA) give the
+    staged path's bytes: registered input, output or both; batches of 1, 5, a ragged 37 and 60
+    (rounds of max_batch; with max_batch 40 vision cuts a round into the 5/32, 11/32, 16/32 chunks of
+    host_chunks, proportionally for rounds of >= 20 rows), bit-equal across the two partitions.
+    Overlapping registration is refused."""
     from open_clip_inference.engine import host_register, host_unregister
     from open_clip_inference.error import ClipError
     v, t = specs(VIT_B_32_CFG)
     # text: trimming off, so the ids are DMA'd from the registered range (a trimmed batch is a copy)
-    e = engine(VIT_B_32_CFG, tower, max_batch=20, lanes=2, **({"trim_text": False} if tower else {}))
+    e = engine(VIT_B_32_CFG, tower, max_batch=mb, lanes=2, **({"trim_text": False} if tower else {}))
     B = 60
     if kind == "u8":
         data = weights.synth_images_u8(61, B, v.image_size)
@@ -221,6 +223,10 @@ def test_registered_host_buffers_are_bit_exact(tower, kind):
         run = lambda x, out: e.embed_tokens(x, out=out)
     data = np.ascontiguousarray(data)
     want = {n: run(data[:n], None) for n in (1, 5, 37, 60)}
+    key = ("host_want", tower, kind)
+    if key in _CACHE:  # the other max_batch's partition gave the same bytes
+        assert all(np.array_equal(want[n], _CACHE[key][n]) for n in want)
+    _CACHE[key] = want
     out = np.zeros((B, 512), np.float32)
     for reg_in, reg_out in [(1, 0), (0, 1), (1, 1)]:
         if reg_in:
@@ -303,7 +309,7 @@ def test_concurrent_lanes_are_bit_exact(tower):
     check_rows(outs[-1][:4], ref)
 
 
-@pytest.mark.parametrize("cfg", [VIT_B_32_CFG, TINY_CFG])
+@pytest.mark.parametrize("cfg", [VIT_B_32_CFG, TINY_CFG, TINY_SIGLIP_CFG])
 @pytest.mark.parametrize("dtype", ["bf16", "fp8"])
 @pytest.mark.parametrize("tower", [0, 1])
 def test_last_layer_pruning_is_bit_exact(cfg, dtype, tower):
@@ -312,8 +318,10 @@ def test_last_layer_pruning_is_bit_exact(cfg, dtype, tower):
     row-local and each kept row goes through the same kernels.  Random EOT positions, two
     lanes, and a batch whose rows-per-lane exceed the token count (gather sources and
     destinations interleave)."""
-    if dtype == "fp8" and cfg is TINY_CFG:
-        pytest.skip("fp8 engines need MX-sized widths")
+    if dtype == "fp8" and cfg in (TINY_CFG, TINY_SIGLIP_CFG):
+        pytest.skip("fp8 engines need MX-sized widths (multiples of 128)")
+    if cfg is TINY_SIGLIP_CFG and tower == 0:
+        pytest.skip("SigLIP vision pools every token (MAP head): no pruning")
     v, t = specs(cfg)
     B = 37
     if tower == 0:
@@ -331,6 +339,29 @@ def test_last_layer_pruning_is_bit_exact(cfg, dtype, tower):
     if dtype == "bf16":
         ref = oracle_vision(cfg, 1234, data[:4]) if tower == 0 else oracle_text(cfg, 1234, data[:4])
         check_rows(outs["1"][:4], ref)
+
+
+def test_siglip2_text_is_not_trimmed_and_pools_the_last_position():
+    """SigLIP2's text tower (no causal mask, pool_type "last") attends to and pools the final
+    context position, padding included: host ids are never trimmed (the host entry point equals
+    the device one), and a token after a sequence's EOT changes its embedding."""
+    import torch
+    _, t = specs(TINY_SIGLIP_CFG)
+    ids = weights.synth_token_ids(77, 6, t.context_length, t.vocab_size, t.vocab_size - 2, t.vocab_size - 1,
+                                  random_eot=True)
+    e = engine(TINY_SIGLIP_CFG, 1, max_batch=8)
+    host = e.embed_tokens(ids)
+    d_in = torch.from_numpy(ids).cuda()
+    d_out = torch.empty((6, e.embed_dim), device="cuda")
+    e.embed_tokens_device(d_in.data_ptr(), 6, d_out.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert np.array_equal(d_out.cpu().numpy(), host)
+    ids2 = ids.copy()
+    p = int(np.argmax(ids2[0]))
+    ids2[0, p + 1:] = 7
+    other = e.embed_tokens(ids2)
+    assert not np.array_equal(other[0], host[0]) and np.array_equal(other[1:], host[1:])
+    check_rows(other, oracle_text(TINY_SIGLIP_CFG, 1234, ids2))
 
 
 @pytest.mark.parametrize("cfg,max_eot", [(VIT_B_32_CFG, 9), (VIT_B_32_CFG, 30), (VIT_B_32_CFG, 76), (TINY_CFG, 5)])
