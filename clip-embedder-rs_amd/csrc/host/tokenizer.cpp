@@ -1,14 +1,21 @@
-// CLIP BPE tokenizer (host, C++).
+// BPE tokenizer (host, C++).
 //
 // Replaces the HF `tokenizers` 0.22.2 pipeline the reference drives in
-// TextEmbedder (src/text.rs:62-85 setup, :110-139 tokenize) for a CLIP
-// tokenizer.json:
+// TextEmbedder (src/text.rs:62-85 setup, :110-139 tokenize) for the BPE tokenizer.json forms of
+// the models it runs -- CLIP's byte-level BPE and the SentencePiece-style BPE of SigLIP2's Gemma
+// tokenizer (README.md:72-80):
 //   added tokens split out (normalized flag honoured, leftmost-longest)
-//   normalizer     Sequence[NFC, Replace(Regex \s+ -> " "), Lowercase]
-//   pre_tokenizer  Sequence[Split(CLIP regex, Removed, invert), ByteLevel(no prefix, no regex)]
-//   model          BPE(end_of_word_suffix "</w>", unk "<|endoftext|>")  lowest-rank-first merges
-//   post_processor RobertaProcessing / BertProcessing / TemplateProcessing (cls A sep)
-//   truncation     max_length = context_length (content truncated to ctx - 2 added tokens, right)
+//   normalizer     Sequence of NFC, Lowercase, Replace (Regex \s+ or a string), Prepend, Strip
+//                  (CLIP: NFC, \s+ -> " ", Lowercase; Gemma: " " -> "▁"; Llama-2: Prepend "▁", " " -> "▁")
+//   pre_tokenizer  CLIP: Sequence[Split(CLIP regex, Removed, invert), ByteLevel(no prefix, no regex)];
+//                  none (the normalized text is one word); Metaspace(replacement, prepend_scheme
+//                  always / first / never, split)
+//   model          BPE: lowest-rank-first merges over byte-level chars or Unicode chars,
+//                  end_of_word_suffix / continuing_subword_prefix, unk (fuse_unk), byte_fallback
+//                  (<0xXX> pieces), ignore_merges
+//   post_processor RobertaProcessing / BertProcessing / TemplateProcessing (any special tokens
+//                  before and after $A)
+//   truncation     max_length = context_length (content truncated to ctx - added tokens, right)
 //   padding        Fixed(context_length), pad_id, right; attention mask 1/0
 // Optional str::to_lowercase of the input first (tokenizer_needs_lowercase,
 // src/text.rs:115-117; Rust's final-sigma rule applied).
@@ -18,6 +25,7 @@
 // by tests/test_cpu_tokenizer.py on committed fixtures.
 #include <algorithm>
 #include <cstdint>
+#include <cstdio>
 #include <cstring>
 #include <queue>
 #include <stdexcept>
@@ -213,7 +221,7 @@ struct AddedToken {
   bool normalized;
 };
 
-enum NormKind { N_NFC, N_LOWER, N_REPLACE_WS, N_REPLACE_STR, N_STRIP };
+enum NormKind { N_NFC, N_LOWER, N_REPLACE_WS, N_REPLACE_STR, N_STRIP, N_PREPEND };
 struct NormStep {
   NormKind kind;
   std::u32string from, to;
@@ -229,10 +237,17 @@ struct clipgpu_tokenizer {
   std::vector<clipgpu::NormStep> norm;
   std::string eow = "</w>", cont_prefix;
   int64_t unk = -1;
-  int64_t cls = -1, sep = -1;
+  std::vector<int64_t> tmpl_pre, tmpl_post;  // post_processor: special ids before / after $A
   int ctx = 77;
   int64_t pad_id = 0;
-  bool byte_level = true, add_prefix_space = false;
+  bool byte_level = false, add_prefix_space = false, clip_split = false;
+  bool byte_fallback = false, fuse_unk = false, ignore_merges = false;
+  // Metaspace pre-tokenizer: ' ' -> replacement, prepend_scheme 0 never / 1 first / 2 always,
+  // split on the replacement (MergedWithNext)
+  bool metaspace = false, ms_split = true;
+  int ms_prepend = 2;
+  std::u32string ms_repl = U"\u2581";
+  int64_t byte_piece[256];  // byte_fallback: id of "<0xXX>" (-1: absent)
   uint32_t byte2cp[256];
 };
 
@@ -279,13 +294,15 @@ void parse_normalizer(clipgpu_tokenizer& t, const Value* n) {
     }
   } else if (type == "Strip") {
     t.norm.push_back({N_STRIP, {}, {}});
+  } else if (type == "Prepend") {
+    t.norm.push_back({N_PREPEND, {}, utf8_decode(n->get("prepend") ? n->get("prepend")->as_str("") : "")});
   } else {
     throw ClipErr(CLIPGPU_ERR_TOKENIZER, "Tokenization error: unsupported normalizer " + type);
   }
 }
 
 void parse_pretok(clipgpu_tokenizer& t, const Value* p, bool& have_split) {
-  if (!p || p->is_null()) return;
+  if (!p || p->is_null()) return;  // none: the normalized text is one word
   const std::string type = p->get("type") ? p->get("type")->as_str("") : "";
   if (type == "Sequence") {
     const Value* list = p->get("pretokenizers");
@@ -298,10 +315,24 @@ void parse_pretok(clipgpu_tokenizer& t, const Value* p, bool& have_split) {
     if ((re != kClipPattern1 && re != kClipPattern2) || beh != "Removed" || !inv)
       throw ClipErr(CLIPGPU_ERR_TOKENIZER, "Tokenization error: unsupported Split pre-tokenizer (CLIP pattern expected)");
     have_split = true;
+    t.clip_split = true;
   } else if (type == "ByteLevel") {
     if (p->get("use_regex") && p->get("use_regex")->as_bool(true) && !have_split)
       throw ClipErr(CLIPGPU_ERR_TOKENIZER, "Tokenization error: ByteLevel(use_regex=true) without CLIP Split");
+    t.byte_level = true;
     t.add_prefix_space = p->get("add_prefix_space") ? p->get("add_prefix_space")->as_bool(false) : false;
+  } else if (type == "Metaspace") {
+    t.metaspace = true;
+    if (const Value* r = p->get("replacement")) t.ms_repl = utf8_decode(r->as_str("\xe2\x96\x81"));
+    if (t.ms_repl.size() != 1) throw ClipErr(CLIPGPU_ERR_TOKENIZER, "Tokenization error: Metaspace replacement must be one char");
+    const std::string scheme = p->get("prepend_scheme") ? p->get("prepend_scheme")->as_str("always")
+                               : (p->get("add_prefix_space") && !p->get("add_prefix_space")->as_bool(true) ? "never"
+                                                                                                         : "always");
+    if (scheme == "always") t.ms_prepend = 2;
+    else if (scheme == "first") t.ms_prepend = 1;
+    else if (scheme == "never") t.ms_prepend = 0;
+    else throw ClipErr(CLIPGPU_ERR_TOKENIZER, "Tokenization error: Metaspace prepend_scheme " + scheme);
+    t.ms_split = p->get("split") ? p->get("split")->as_bool(true) : true;
   } else {
     throw ClipErr(CLIPGPU_ERR_TOKENIZER, "Tokenization error: unsupported pre_tokenizer " + type);
   }
@@ -316,28 +347,26 @@ void parse_post(clipgpu_tokenizer& t, const Value* p) {
   if (!p || p->is_null()) return;
   const std::string type = p->get("type") ? p->get("type")->as_str("") : "";
   if (type == "RobertaProcessing" || type == "BertProcessing") {
-    t.cls = special_id(p->get("cls"));
-    t.sep = special_id(p->get("sep"));
+    const int64_t cls = special_id(p->get("cls")), sep = special_id(p->get("sep"));
+    if (cls >= 0) t.tmpl_pre.push_back(cls);
+    if (sep >= 0) t.tmpl_post.push_back(sep);
   } else if (type == "TemplateProcessing") {
     const Value* single = p->get("single");
     const Value* st = p->get("special_tokens");
     if (!single || !st) throw ClipErr(CLIPGPU_ERR_TOKENIZER, "Tokenization error: bad TemplateProcessing");
-    std::vector<std::string> seq;
+    int seen_a = 0;
     for (auto& piece : single->arr) {
-      if (const Value* sp = piece->get("SpecialToken")) seq.push_back(sp->get("id")->as_str(""));
-      else seq.push_back("$A");
+      if (const Value* sp = piece->get("SpecialToken")) {
+        const Value* e = st->get(sp->get("id") ? sp->get("id")->as_str("") : "");
+        if (!e || !e->get("ids")) throw ClipErr(CLIPGPU_ERR_TOKENIZER, "Tokenization error: TemplateProcessing special token without ids");
+        for (auto& id : e->get("ids")->arr) (seen_a ? t.tmpl_post : t.tmpl_pre).push_back((int64_t)id->as_num(-1));
+      } else if (piece->get("Sequence")) {
+        ++seen_a;
+      } else {
+        throw ClipErr(CLIPGPU_ERR_TOKENIZER, "Tokenization error: unsupported TemplateProcessing piece");
+      }
     }
-    auto id_of = [&](const std::string& k) -> int64_t {
-      const Value* e = st->get(k);
-      if (!e || !e->get("ids") || e->get("ids")->arr.empty()) return -1;
-      return (int64_t)e->get("ids")->arr[0]->as_num(-1);
-    };
-    if (seq.size() == 3 && seq[1] == "$A") {
-      t.cls = id_of(seq[0]);
-      t.sep = id_of(seq[2]);
-    } else {
-      throw ClipErr(CLIPGPU_ERR_TOKENIZER, "Tokenization error: unsupported TemplateProcessing layout");
-    }
+    if (seen_a != 1) throw ClipErr(CLIPGPU_ERR_TOKENIZER, "Tokenization error: unsupported TemplateProcessing layout");
   } else {
     throw ClipErr(CLIPGPU_ERR_TOKENIZER, "Tokenization error: unsupported post_processor " + type);
   }
@@ -372,6 +401,9 @@ std::u32string normalize(const clipgpu_tokenizer& t, const std::u32string& in) {
           }
         }
         break;
+      case N_PREPEND:  // tokenizers Prepend: non-empty strings only
+        if (!s.empty()) o = st.to + s;
+        break;
       case N_STRIP: {
         size_t a = 0, b = s.size();
         while (a < b && uni::is_space(s[a])) ++a;
@@ -385,10 +417,12 @@ std::u32string normalize(const clipgpu_tokenizer& t, const std::u32string& in) {
   return s;
 }
 
-// Pieces of text: either an added-token id (>= 0) or raw text to process.
+// Pieces of text: either an added-token id (>= 0) or raw text to process.  origin: the piece
+// starts at offset 0 of the input (Metaspace prepend_scheme "first").
 struct Piece {
   int64_t id;
   std::u32string text;
+  bool origin = false;
 };
 
 void split_added(const clipgpu_tokenizer& t, std::vector<Piece>& pieces, bool normalized_pass) {
@@ -409,15 +443,15 @@ void split_added(const clipgpu_tokenizer& t, std::vector<Piece>& pieces, bool no
         }
       }
       if (best >= 0) {
-        if (i > start) out.push_back({-1, s.substr(start, i - start)});
-        out.push_back({t.added[best].id, {}});
+        if (i > start) out.push_back({-1, s.substr(start, i - start), p.origin && start == 0});
+        out.push_back({t.added[best].id, {}, false});
         i += best_len;
         start = i;
       } else {
         ++i;
       }
     }
-    if (start < s.size()) out.push_back({-1, s.substr(start)});
+    if (start < s.size()) out.push_back({-1, s.substr(start), p.origin && start == 0});
   }
   pieces.swap(out);
 }
@@ -469,26 +503,14 @@ int64_t lookup(const clipgpu_tokenizer& t, const std::string& s) {
   return it == t.vocab.end() ? -1 : it->second;
 }
 
-void bpe_word(const clipgpu_tokenizer& t, const std::string& word_bytes, std::vector<int64_t>& out) {
-  // byte-level chars
-  std::vector<std::string> chars;
-  for (unsigned char b : word_bytes) {
-    std::string c;
-    utf8_append(c, t.byte2cp[b]);
-    chars.push_back(c);
-  }
-  if (chars.empty()) return;
-  struct Sym { int64_t id; int prev, next; size_t len; };
-  std::vector<Sym> syms;
-  for (size_t i = 0; i < chars.size(); ++i) {
-    std::string s = (i > 0 ? t.cont_prefix : std::string()) + chars[i];
-    if (i + 1 == chars.size()) s += t.eow;
-    int64_t id = lookup(t, s);
-    if (id < 0) {
-      if (t.unk < 0) throw ClipErr(CLIPGPU_ERR_TOKENIZER, "Tokenization error: unknown symbol and no unk token");
-      id = t.unk;
-    }
-    syms.push_back({id, (int)i - 1, i + 1 < chars.size() ? (int)i + 1 : -1, 1});
+struct Sym { int64_t id; int prev, next; size_t len; };
+
+// Lowest-rank-first merges over a word's symbols (tokenizers Word::merge_all without dropout).
+void bpe_merge(const clipgpu_tokenizer& t, std::vector<Sym>& syms, std::vector<int64_t>& out) {
+  if (syms.empty()) return;
+  for (size_t i = 0; i < syms.size(); ++i) {
+    syms[i].prev = (int)i - 1;
+    syms[i].next = i + 1 < syms.size() ? (int)i + 1 : -1;
   }
   struct Cand {
     int32_t rank;
@@ -528,10 +550,103 @@ void bpe_word(const clipgpu_tokenizer& t, const std::string& word_bytes, std::ve
   for (int i = 0; i >= 0 && i < (int)syms.size(); i = syms[i].next) out.push_back(syms[i].id);
 }
 
+// Byte-level BPE word (CLIP): every byte is one char of the GPT-2 byte alphabet.
+void bpe_word(const clipgpu_tokenizer& t, const std::string& word_bytes, std::vector<int64_t>& out) {
+  std::vector<std::string> chars;
+  for (unsigned char b : word_bytes) {
+    std::string c;
+    utf8_append(c, t.byte2cp[b]);
+    chars.push_back(c);
+  }
+  if (chars.empty()) return;
+  if (t.ignore_merges) {
+    std::string whole;
+    for (auto& c : chars) whole += c;
+    const int64_t id = lookup(t, whole + t.eow);
+    if (id >= 0) { out.push_back(id); return; }
+  }
+  std::vector<Sym> syms;
+  for (size_t i = 0; i < chars.size(); ++i) {
+    std::string s = (i > 0 ? t.cont_prefix : std::string()) + chars[i];
+    if (i + 1 == chars.size()) s += t.eow;
+    int64_t id = lookup(t, s);
+    if (id < 0) {
+      if (t.unk < 0) throw ClipErr(CLIPGPU_ERR_TOKENIZER, "Tokenization error: unknown symbol and no unk token");
+      id = t.unk;
+    }
+    syms.push_back({id, 0, 0, 1});
+  }
+  bpe_merge(t, syms, out);
+}
+
+// BPE word over Unicode chars (SentencePiece-style tokenizer.json, e.g. Gemma): a char missing
+// from the vocab falls back to its UTF-8 bytes as <0xXX> pieces (byte_fallback) or becomes unk
+// (consecutive unks fused with fuse_unk), as tokenizers' BPE::merge_word does.
+void bpe_chars(const clipgpu_tokenizer& t, const std::u32string& w, std::vector<int64_t>& out) {
+  if (w.empty()) return;
+  if (t.ignore_merges) {
+    const int64_t id = lookup(t, utf8_encode(w));
+    if (id >= 0) { out.push_back(id); return; }
+  }
+  std::vector<Sym> syms;
+  int64_t pend_unk = -1;  // a pending (fusable) unk symbol
+  size_t pend_len = 0;
+  for (size_t i = 0; i < w.size(); ++i) {
+    std::string c;
+    utf8_append(c, w[i]);
+    const size_t byte_len = c.size();
+    std::string sym = (i > 0 ? t.cont_prefix : std::string()) + c;
+    if (i + 1 == w.size()) sym += t.eow;
+    const int64_t id = lookup(t, sym);
+    if (id >= 0) {
+      if (pend_unk >= 0) { syms.push_back({pend_unk, 0, 0, pend_len}); pend_unk = -1; }
+      syms.push_back({id, 0, 0, byte_len});
+      continue;
+    }
+    if (t.byte_fallback) {
+      bool all = true;
+      for (unsigned char b : sym) all = all && t.byte_piece[b] >= 0;
+      if (all) {  // (tokenizers leaves a pending unk in place here)
+        for (unsigned char b : sym) syms.push_back({t.byte_piece[b], 0, 0, 1});
+        continue;
+      }
+    }
+    if (t.unk < 0) throw ClipErr(CLIPGPU_ERR_TOKENIZER, "Tokenization error: unknown symbol and no unk token");
+    if (pend_unk >= 0 && t.fuse_unk) {
+      pend_len += byte_len;
+    } else {
+      if (pend_unk >= 0) syms.push_back({pend_unk, 0, 0, pend_len});
+      pend_unk = t.unk;
+      pend_len = byte_len;
+    }
+  }
+  if (pend_unk >= 0) syms.push_back({pend_unk, 0, 0, pend_len});
+  bpe_merge(t, syms, out);
+}
+
+// Metaspace pre-tokenizer: ' ' -> replacement, the replacement prepended (scheme), then (split)
+// one word per replacement char, merged with what follows it (MergedWithNext).
+void metaspace_words(const clipgpu_tokenizer& t, std::u32string s, bool origin, std::vector<std::u32string>& words) {
+  const char32_t r = t.ms_repl[0];
+  for (auto& c : s)
+    if (c == U' ') c = r;
+  if ((t.ms_prepend == 2 || (t.ms_prepend == 1 && origin)) && (s.empty() || s[0] != r)) s.insert(s.begin(), r);
+  if (!t.ms_split) {
+    if (!s.empty()) words.push_back(s);
+    return;
+  }
+  size_t start = 0;
+  for (size_t i = 1; i <= s.size(); ++i)
+    if (i == s.size() || s[i] == r) {
+      if (i > start) words.push_back(s.substr(start, i - start));
+      start = i;
+    }
+}
+
 void encode_one(const clipgpu_tokenizer& t, const std::string& text, bool lowercase, int64_t* ids, int64_t* mask) {
   std::u32string u = utf8_decode(text);
   if (lowercase) u = rust_to_lowercase(u);
-  std::vector<Piece> pieces{{-1, u}};
+  std::vector<Piece> pieces{{-1, u, true}};
   split_added(t, pieces, false);
   for (Piece& p : pieces)
     if (p.id < 0) p.text = normalize(t, p.text);
@@ -540,18 +655,22 @@ void encode_one(const clipgpu_tokenizer& t, const std::string& text, bool lowerc
   for (const Piece& p : pieces) {
     if (p.id >= 0) { content.push_back(p.id); continue; }
     std::u32string s = p.text;
-    if (t.add_prefix_space && !s.empty() && s[0] != U' ') s.insert(s.begin(), U' ');
+    if (t.byte_level && t.add_prefix_space && !s.empty() && s[0] != U' ') s.insert(s.begin(), U' ');
     std::vector<std::u32string> words;
-    clip_pretokenize(s, words);
-    for (const auto& w : words) bpe_word(t, utf8_encode(w), content);
+    if (t.clip_split) clip_pretokenize(s, words);
+    else if (t.metaspace) metaspace_words(t, s, p.origin, words);
+    else if (!s.empty()) words.push_back(s);  // no pre-tokenizer: one word
+    for (const auto& w : words) {
+      if (t.byte_level) bpe_word(t, utf8_encode(w), content);
+      else bpe_chars(t, w, content);
+    }
   }
-  const int n_special = (t.cls >= 0) + (t.sep >= 0);
+  const int n_special = (int)(t.tmpl_pre.size() + t.tmpl_post.size());
   const size_t keep = (size_t)std::max(0, t.ctx - n_special);
   if (content.size() > keep) content.resize(keep);  // TruncationParams: LongestFirst, Right
-  std::vector<int64_t> seq;
-  if (t.cls >= 0) seq.push_back(t.cls);
+  std::vector<int64_t> seq(t.tmpl_pre);
   seq.insert(seq.end(), content.begin(), content.end());
-  if (t.sep >= 0) seq.push_back(t.sep);
+  seq.insert(seq.end(), t.tmpl_post.begin(), t.tmpl_post.end());
   if ((int)seq.size() > t.ctx) seq.resize(t.ctx);
   for (int i = 0; i < t.ctx; ++i) {
     const bool real = i < (int)seq.size();
@@ -595,6 +714,15 @@ int clipgpu_tokenizer_create(const char* path, int context_length, int64_t pad_i
     if (const Value* u = model->get("unk_token")) {
       if (u->kind == Value::STR) t->unk = lookup(*t, u->str);
     }
+    auto flag = [&](const char* k) { const Value* f = model->get(k); return f && !f->is_null() && f->as_bool(false); };
+    t->byte_fallback = flag("byte_fallback");
+    t->fuse_unk = flag("fuse_unk");
+    t->ignore_merges = flag("ignore_merges");
+    for (int b = 0; b < 256; ++b) {
+      char name[8];
+      std::snprintf(name, sizeof(name), "<0x%02X>", b);
+      t->byte_piece[b] = lookup(*t, name);
+    }
     const Value* merges = model->get("merges");
     if (merges) {
       int32_t rank = 0;
@@ -635,7 +763,6 @@ int clipgpu_tokenizer_create(const char* path, int context_length, int64_t pad_i
     parse_normalizer(*t, root->get("normalizer"));
     bool have_split = false;
     parse_pretok(*t, root->get("pre_tokenizer"), have_split);
-    if (!have_split) throw ClipErr(CLIPGPU_ERR_TOKENIZER, "Tokenization error: CLIP Split pre-tokenizer expected");
     parse_post(*t, root->get("post_processor"));
     if (pad_id >= 0) {
       t->pad_id = pad_id;

@@ -32,11 +32,11 @@ class QuickGELU(nn.Module):
 
 
 class ResidualAttentionBlock(nn.Module):
-    def __init__(self, d, heads, mlp, act):
+    def __init__(self, d, heads, mlp, act, eps=1e-5):
         super().__init__()
-        self.ln_1 = nn.LayerNorm(d)
+        self.ln_1 = nn.LayerNorm(d, eps=eps)
         self.attn = nn.MultiheadAttention(d, heads, batch_first=True)
-        self.ln_2 = nn.LayerNorm(d)
+        self.ln_2 = nn.LayerNorm(d, eps=eps)
         self.mlp = nn.Sequential(OrderedDict([("c_fc", nn.Linear(d, mlp)), ("gelu", act()),
                                               ("c_proj", nn.Linear(mlp, d))]))
 
@@ -47,9 +47,9 @@ class ResidualAttentionBlock(nn.Module):
 
 
 class Transformer(nn.Module):
-    def __init__(self, d, layers, heads, mlp, act):
+    def __init__(self, d, layers, heads, mlp, act, eps=1e-5):
         super().__init__()
-        self.resblocks = nn.ModuleList([ResidualAttentionBlock(d, heads, mlp, act) for _ in range(layers)])
+        self.resblocks = nn.ModuleList([ResidualAttentionBlock(d, heads, mlp, act, eps) for _ in range(layers)])
 
     def forward(self, x, attn_mask=None):
         for r in self.resblocks:
@@ -58,7 +58,7 @@ class Transformer(nn.Module):
 
 
 def _act(name):
-    return {"quick_gelu": QuickGELU, "gelu": nn.GELU}[name]
+    return {"quick_gelu": QuickGELU, "gelu": nn.GELU, "gelu_tanh": lambda: nn.GELU(approximate="tanh")}[name]
 
 
 class VisionTransformer(nn.Module):
@@ -238,6 +238,48 @@ def export_siglip_visual(d, v, seed, external=False):
                 "pixel_values", "image_embeddings")
     if external:
         externalize(os.path.join(d, "visual.onnx"))
+    return m
+
+
+class SiglipTextOnly(nn.Module):
+    """open_clip TextTransformer in its SigLIP2 form (text_cfg no_causal_mask, pool_type "last",
+    proj_bias, GELU tanh, norm eps 1e-6): no attention mask, x[:, -1] after ln_final, nn.Linear
+    projection."""
+
+    def __init__(self, t):
+        super().__init__()
+        self.token_embedding = nn.Embedding(t.vocab_size, t.width)
+        self.positional_embedding = nn.Parameter(torch.zeros(t.context_length, t.width))
+        self.transformer = Transformer(t.width, t.layers, t.heads, t.mlp_width, _act(t.act), t.ln_eps)
+        self.ln_final = nn.LayerNorm(t.width, eps=t.ln_eps)
+        self.text_projection = nn.Linear(t.width, t.embed_dim)
+
+    def encode_text(self, ids, normalize=False):
+        x = self.token_embedding(ids) + self.positional_embedding
+        x = self.ln_final(self.transformer(x))
+        x = self.text_projection(x[:, -1])
+        return nn.functional.normalize(x, dim=-1) if normalize else x
+
+
+def build_siglip_text(t, seed):
+    from oracle import weights
+    m = SiglipTextOnly(t).eval()
+    P = weights.text_weights(t, seed)
+    sd = m.state_dict()
+    assert set(sd) == set(P), set(sd) ^ set(P)
+    m.load_state_dict({k: torch.from_numpy(np.asarray(P[k], np.float32)) for k in sd})
+    return m
+
+
+def export_siglip_text(d, t, seed, external=False):
+    import warnings
+    m = build_siglip_text(t, seed)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        _export(TextWrapper(m), torch.randint(0, t.vocab_size, (2, t.context_length)), os.path.join(d, "text.onnx"),
+                "input_ids", "text_embeddings")
+    if external:
+        externalize(os.path.join(d, "text.onnx"))
     return m
 
 

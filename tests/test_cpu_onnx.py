@@ -119,3 +119,30 @@ def test_onnx_siglip_weights_bit_exact(tmp_path, external):
         got = m.encode_image(torch.from_numpy(px), normalize=True).double().numpy()
     ref = clip_ref.encode_image(weights.vision_weights(v, 78), v, px)
     assert clip_ref.cosine_rows(got, ref).min() > 1 - 1e-6
+
+
+@pytest.mark.parametrize("external", [False, True])
+def test_onnx_siglip2_text_weights_bit_exact(tmp_path, external):
+    """SigLIP2 text tower (no causal mask, last-position pooling, nn.Linear projection with bias):
+    every parameter of a real torch.onnx.export of the restated open_clip TextTransformer read back
+    bit-exact (the folded text_projection MatMul and its bias included); the torch tower pins the
+    oracle."""
+    from oracle.model_spec import TINY_SIGLIP_CFG
+    from tests.onnx_export import export_siglip_text
+    d = tmp_path / "siglip_text"
+    d.mkdir()
+    with open(d / "open_clip_config.json", "w") as f:
+        json.dump(TINY_SIGLIP_CFG, f)
+    with open(d / "model_config.json", "w") as f:
+        json.dump(OPENAI_MODEL_CONFIG, f)
+    _, t = specs(TINY_SIGLIP_CFG)
+    m = export_siglip_text(str(d), t, seed=79, external=external)
+    P = weights.text_weights(t, 79)
+    for name, ref in P.items():
+        got = _read(str(d), 1, name, ref.shape)
+        assert np.array_equal(got, ref.astype(np.float32)), name
+    ids = weights.synth_token_ids(6, 3, t.context_length, t.vocab_size, t.vocab_size - 2, t.vocab_size - 1,
+                                  random_eot=True)
+    with torch.no_grad():
+        got = m.encode_text(torch.from_numpy(ids), normalize=True).double().numpy()
+    assert clip_ref.cosine_rows(got, clip_ref.encode_text(P, t, ids)).min() > 1 - 1e-6

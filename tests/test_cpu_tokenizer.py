@@ -104,3 +104,54 @@ def test_cpp_matches_tokenizers_live_fuzz():
         assert mask.tolist() == [e.attention_mask for e in enc]
 
     check()
+
+
+# SentencePiece-style BPE tokenizer.json forms (SigLIP2's Gemma tokenizer, README.md:72-80;
+# Llama-2's Prepend + Replace; Metaspace): synthetic files and goldens from the tokenizers wheel
+# (tests/golden/make_sp_tokenizers.py).
+SP_FILES = ["gemma_synth_tokenizer.json", "spm_prepend_tokenizer.json", "metaspace_tokenizer.json"]
+
+
+def sp_golden():
+    with open(os.path.join(GOLD, "sp_tokenizer_golden.json"), encoding="utf-8") as f:
+        return json.load(f)
+
+
+@pytest.mark.parametrize("case", range(12))
+def test_cpp_sentencepiece_bpe_matches_tokenizers_golden(case):
+    """Byte fallback (<0xXX> pieces), fuse_unk, no / Metaspace pre-tokenizer, Prepend / Replace
+    normalizers, TemplateProcessing with <bos> before and / or <eos> after $A, truncation to
+    ctx - added tokens, Fixed(ctx) padding with pad id 0: bit-exact ids and masks."""
+    from open_clip_inference.engine import Tokenizer
+    g = sp_golden()
+    c = g["cases"][case]
+    tok = Tokenizer(os.path.join(GOLD, c["file"]), c["context_length"], 0)
+    ids, mask = tok.encode_batch(g["texts"], lowercase=c["lowercase"])
+    bad = [i for i in range(len(g["texts"])) if ids[i].tolist() != c["ids"][i]]
+    assert not bad, [(g["texts"][i][:40], ids[i].tolist()[:12], c["ids"][i][:12]) for i in bad[:3]]
+    assert mask.tolist() == c["mask"]
+
+
+@pytest.mark.parametrize("name", SP_FILES)
+def test_cpp_sentencepiece_bpe_matches_tokenizers_live_fuzz(name):
+    tokenizers = pytest.importorskip("tokenizers")
+    from hypothesis import given, settings, strategies as st
+    from open_clip_inference.engine import Tokenizer
+    path = os.path.join(GOLD, name)
+    ref = tokenizers.Tokenizer.from_file(path)
+    ref.enable_padding(length=48, pad_id=0)
+    ref.enable_truncation(max_length=48)
+    tok = Tokenizer(path, 48, 0)
+    alphabet = st.characters(blacklist_categories=("Cs",), max_codepoint=0x2FFFF)
+    words = st.sampled_from(["<bos>", "<eos>", "<mask>", " ", "  ", "▁", "the", "photo", "Straße", "日本"])
+
+    @settings(max_examples=250, deadline=None)
+    @given(st.lists(st.lists(st.one_of(st.text(alphabet=alphabet, max_size=12), words), max_size=6).map("".join),
+                    min_size=1, max_size=4))
+    def check(texts):
+        enc = ref.encode_batch(texts)
+        ids, mask = tok.encode_batch(texts)
+        assert ids.tolist() == [e.ids for e in enc], texts
+        assert mask.tolist() == [e.attention_mask for e in enc]
+
+    check()

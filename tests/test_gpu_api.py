@@ -334,3 +334,43 @@ def test_tile_table_is_deterministic_and_bit_invisible():
     ids[:, 0] = 49406
     ids[np.arange(8), rng.integers(5, 77, size=8)] = 49407
     assert np.array_equal(ta.embed_tokens(ids), ts.embed_tokens(ids))
+
+
+def test_siglip2_text_embedder_and_clip_end_to_end():
+    """The reference's README model family (README.md:72-80, timm/ViT-SO400M-16-SigLIP2-384):
+    a SigLIP2-structured folder -- SigLIP vision + SigLIP2 text tower (no causal mask, last-position
+    pooling, projection bias), a Gemma-structured tokenizer.json (SentencePiece BPE with byte
+    fallback, tests/golden/gemma_synth_tokenizer.json) and pull_onnx.py:140-150's SigLIP2
+    model_config (sigmoid, lowercase, pad id 0) -- through TextEmbedder and Clip, against the
+    tokenizers wheel + fp64 oracle chain."""
+    tokenizers = pytest.importorskip("tokenizers")
+    from oracle.model_spec import SIGLIP_MEAN, SIGLIP_STD, tiny_siglip_cfg
+    from open_clip_inference import Clip, TextEmbedder
+    path = os.path.join(GOLD, "gemma_synth_tokenizer.json")
+    with open(path, encoding="utf-8") as f:
+        tj = f.read()
+    vocab = len(json.loads(tj)["model"]["vocab"])
+    cfg = tiny_siglip_cfg()
+    cfg["model_cfg"]["text_cfg"]["vocab_size"] = vocab
+    mc = {"logit_scale": 10.0, "logit_bias": -10.0, "activation_function": "sigmoid",
+          "tokenizer_needs_lowercase": True, "pad_id": 0, "vocab_size": vocab}
+    d = make_model_dir(cfg, seed=78, tokenizer_json=tj, model_config=mc)
+    t = text_spec_from_cfg(cfg["model_cfg"])
+    ref_tok = tokenizers.Tokenizer.from_file(path)
+    ref_tok.enable_padding(length=t.context_length, pad_id=0)
+    ref_tok.enable_truncation(max_length=t.context_length)
+    ids = np.array([e.ids for e in ref_tok.encode_batch([x.lower() for x in TEXTS])], np.int64)
+    want = clip_ref.encode_text(weights.text_weights(t, 78), t, ids)
+    te = TextEmbedder.from_local_dir(d).build()
+    got_ids, _ = te.tokenize(TEXTS)
+    assert np.array_equal(got_ids, ids)
+    got = te.embed_texts(TEXTS)
+    assert clip_ref.cosine_rows(got, want).min() >= COS_TOL
+    clip = Clip.from_local_dir(d).build()
+    v = vision_spec_from_cfg(cfg["model_cfg"])
+    px = np.stack([preprocess_ref.preprocess(im, v.image_size, SIGLIP_MEAN, SIGLIP_STD, mode="shortest")
+                   for im in images()[:1]])
+    img = clip_ref.encode_image(weights.vision_weights(v, 78), v, px)[0]
+    res = clip.classify(images()[0], TEXTS[:3])
+    ref = facade_ref.classify(img, want[:3], TEXTS[:3], 10.0, -10.0, activation="sigmoid")
+    assert np.allclose(sorted(p for _, p in res), sorted(p for _, p in ref), atol=0.02)
