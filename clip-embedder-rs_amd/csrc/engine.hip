@@ -1287,7 +1287,18 @@ void run_host_shard(clipgpu_engine& e, Replica& r, InKind kind, const void* in, 
         par_memcpy(pin, src, (size_t)n * in_row_bytes);
         src = pin;
       }
-      if (e.host_copy_stream == 2 && n >= 2) {  // test hook: the chunk's halves on two copy streams
+      const void* mapped = nullptr;
+      if (e.host_copy_stream == 3 && direct_in &&
+          hipHostGetDevicePointer((void**)&mapped, (void*)src, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        mapped = nullptr;
+      }
+      if (mapped != nullptr && (((uintptr_t)src | (uintptr_t)din | ((size_t)n * in_row_bytes)) & 15) == 0) {
+        // test hook: pull the chunk through the host mapping with a copy kernel on the copy stream
+        check(launch_pull_copy(mapped, din, (size_t)n * in_row_bytes, r.copy), "pull copy");
+        HIP_CHECK(hipEventRecord(r.copied[k], r.copy));
+        HIP_CHECK(hipStreamWaitEvent(st, r.copied[k], 0));
+      } else if (e.host_copy_stream == 2 && n >= 2) {  // test hook: the chunk's halves on two copy streams
         const size_t h = (size_t)(n / 2) * in_row_bytes, all = (size_t)n * in_row_bytes;
         HIP_CHECK(hipStreamWaitEvent(r.copy2, r.copied[(k + C - 1) % C], 0));  // chunk order kept
         HIP_CHECK(hipMemcpyAsync(din, src, h, hipMemcpyHostToDevice, r.copy));
@@ -1891,7 +1902,7 @@ int clipgpu_host_register(void* ptr, size_t bytes) {
     for (const auto& rg : h.r)
       if (a < rg.first + rg.second && rg.first < a + bytes)
         throw ClipErr(CLIPGPU_ERR_INVALID, "host range overlaps a registered one");
-    HIP_CHECK(hipHostRegister(ptr, bytes, hipHostRegisterDefault));
+    HIP_CHECK(hipHostRegister(ptr, bytes, hipHostRegisterMapped));
     h.r.emplace_back(a, bytes);
   });
 }
@@ -2218,7 +2229,7 @@ int clipgpu_test_host_plan(clipgpu_engine* e, int n_chunks, const int* bounds, i
   return guarded([&]() {
     if (!e) throw ClipErr(CLIPGPU_ERR_INVALID, "engine is NULL");
     std::lock_guard<std::mutex> lk(e->mu);
-    if (copy_stream < 0 || copy_stream > 2) throw ClipErr(CLIPGPU_ERR_INVALID, "copy_stream: 0, 1 or 2");
+    if (copy_stream < 0 || copy_stream > 3) throw ClipErr(CLIPGPU_ERR_INVALID, "copy_stream: 0 .. 3");
     e->host_copy_stream = copy_stream;
     e->host_part.clear();
     if (n_chunks == 0) return;

@@ -146,6 +146,8 @@ hipError_t launch_l2norm(const float* in, float* out, int B, int E, hipStream_t 
 
 // f32 -> T16 conversion (weight upload).
 hipError_t launch_cast_f32(DType dt, const float* in, void* out, long n, hipStream_t s);
+// dst[0 .. bytes) = host-mapped src (16-byte aligned, bytes % 16 == 0), read by a grid of CUs.
+hipError_t launch_pull_copy(const void* src_mapped, void* dst, size_t bytes, hipStream_t s);
 
 #ifdef CLIPGPU_GEMM_STAMPS
 // Diagnostic build: copy (or clear) the per-block s_memtime stamps of the last GEMM launch.

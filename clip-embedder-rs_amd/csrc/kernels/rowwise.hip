@@ -368,6 +368,24 @@ hipError_t launch_l2norm(const float* in, float* out, int B, int E, hipStream_t 
   return hipGetLastError();
 }
 
+// Pull copy of a host-mapped (registered) range into device memory: every lane moves 16-byte
+// chunks, grid-stride, so many CUs keep PCIe reads in flight (the host path's alternative to an
+// SDMA H2D; clipgpu_test_host_plan copy_stream 3).  src / dst 16-byte aligned, bytes % 16 == 0.
+__global__ __launch_bounds__(256) void pull_copy_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                        long n16) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n16; i += (long)gridDim.x * 256) dst[i] = src[i];
+}
+
+hipError_t launch_pull_copy(const void* src_mapped, void* dst, size_t bytes, hipStream_t s) {
+  if (((uintptr_t)src_mapped | (uintptr_t)dst | bytes) & 15) return hipErrorInvalidValue;
+  const long n16 = (long)(bytes / 16);
+  const long blocks = (n16 + 255) / 256 < 2048 ? (n16 + 255) / 256 : 2048;
+  if (n16 == 0) return hipSuccess;
+  hipLaunchKernelGGL(pull_copy_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (const uint4*)src_mapped, (uint4*)dst,
+                     n16);
+  return hipGetLastError();
+}
+
 hipError_t launch_cast_f32(DType dt, const float* in, void* out, long n, hipStream_t s) {
   const long blocks = (n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096;
   if (dt == DT_BF16)

@@ -107,7 +107,8 @@ int clipgpu_test_engine_lanes(const struct clipgpu_engine* e, int* dev_lanes);
  * max_batch round cut at bounds[0 .. n_chunks - 2]; n_chunks = 0 restores the default
  * (engine.hip host_chunks).  copy_stream = 1: the H2Ds in chunk order on the replica's copy
  * stream (default); 0: each on its chunk's lane stream; 2: each chunk's two halves on two copy
- * streams at once.  Speed only, never the bits. */
+ * streams at once; 3: registered inputs pulled through their host mapping by a copy kernel on
+ * the copy stream (others as 1).  Speed only, never the bits. */
 int clipgpu_test_host_plan(struct clipgpu_engine* e, int n_chunks, const int* bounds, int copy_stream);
 /* Gathered calls of this handle take the ragged branch (one ncclBroadcast per block) even when
  * every block has the same size (on != 0), so a one-rank or equal-shard run exercises it. */

@@ -26,7 +26,8 @@ from open_clip_inference.engine import Engine  # noqa: E402
 from oracle.model_spec import (OPENAI_MODEL_CONFIG, SO400M_16_SIGLIP2_384_CFG, VIT_B_32_CFG,  # noqa: E402
                                VIT_H_14_378_CFG)
 
-GFLOP = {"so400m_vision": 518.9, "h14_vision": 1007.0, "h14_text": 47.1, "b32_vision": 8.818}
+# so400m_text: SigLIP2 text tower, 64 tokens x 27 layers x 2 (4 D^2 + 2 D MLP) + attention + projection
+GFLOP = {"so400m_vision": 518.9, "h14_vision": 1007.0, "h14_text": 47.1, "b32_vision": 8.818, "so400m_text": 53.1}
 
 
 def model_dir(cfg):
@@ -49,9 +50,9 @@ def timed(fn, steps, warmup):
     return (time.perf_counter() - t0) / steps
 
 
-def device_leg(name, cfg, tower, B, steps=6, warmup=2, dtype="bf16"):
+def device_leg(name, cfg, tower, B, steps=6, warmup=2, dtype="bf16", mx_sites=None):
     d = model_dir(cfg)
-    e = Engine(d, tower, [0], dtype, B)
+    e = Engine(d, tower, [0], dtype, B, mx_sites=mx_sites)
     s = torch.cuda.current_stream()
     mc = cfg["model_cfg"]
     E = mc["embed_dim"]
@@ -67,8 +68,9 @@ def device_leg(name, cfg, tower, B, steps=6, warmup=2, dtype="bf16"):
         fn = lambda: e.embed_tokens_device(ids.data_ptr(), B, out.data_ptr(), s.cuda_stream)  # noqa: E731
     dt = timed(fn, steps, warmup)
     rate = B / dt
-    gf = GFLOP[name.replace("_fp8", "")]
-    print(json.dumps({"measure": name, "dtype": dtype, "batch_per_gpu": B, "units_per_s": round(rate, 1),
+    gf = GFLOP[name.replace("_fp8", "").replace("_full", "")]
+    print(json.dumps({"measure": name, "dtype": dtype, "mx_sites": mx_sites if dtype == "fp8" else None,
+                      "batch_per_gpu": B, "units_per_s": round(rate, 1),
                       "ms_per_step": round(dt * 1e3, 3), "model_tflops": round(rate * gf / 1e3, 1),
                       "frac_of_2500": round(rate * gf / 1e3 / 2500, 4), "input": "device-resident"}),
           flush=True)
@@ -208,9 +210,17 @@ if __name__ == "__main__":
     if "h14" in which:
         device_leg("h14_vision", VIT_H_14_378_CFG, 0, 64)
         device_leg("h14_text", VIT_H_14_378_CFG, 1, 64)
-    if "h14fp8" in which:  # configs[4]'s fp8 MFMA weight path (MX-fp8 trunk GEMMs)
-        device_leg("h14_vision_fp8", VIT_H_14_378_CFG, 0, 64, dtype="fp8")
-        device_leg("h14_text_fp8", VIT_H_14_378_CFG, 1, 64, dtype="fp8")
+    if "h14fp8" in which:
+        # configs[4]'s fp8 MFMA weight path at the north-star tolerance: vision with
+        # QKV in MX-fp8 (cos >= 0.9999), text in bf16 -- no MX text split meets the bar at any
+        # speed gain (per-site and per-layer sweeps, profiles/r04_mx_layer_*.jsonl)
+        device_leg("h14_vision_fp8", VIT_H_14_378_CFG, 0, 64, dtype="fp8", mx_sites="qkv")
+        device_leg("h14_text", VIT_H_14_378_CFG, 1, 64)
+    if "h14fp8full" in which:  # the full MX split (QKV, c_fc, c_proj): throughput mode, below the bar
+        device_leg("h14_vision_fp8_full", VIT_H_14_378_CFG, 0, 64, dtype="fp8")
+        device_leg("h14_text_fp8_full", VIT_H_14_378_CFG, 1, 64, dtype="fp8")
+    if "so400mtext" in which:  # the SigLIP2 text tower of the configs[3] model folder
+        device_leg("so400m_text", SO400M_16_SIGLIP2_384_CFG, 1, 128)
     if "so400mfp8" in which:
         device_leg("so400m_vision_fp8", SO400M_16_SIGLIP2_384_CFG, 0, 128, dtype="fp8")
     if "b32fp8" in which:

@@ -22,7 +22,7 @@ from open_clip_inference.engine import Engine, host_register, host_unregister  #
 from oracle.model_spec import OPENAI_MEAN, OPENAI_STD, VIT_B_32_CFG  # noqa: E402
 from tests.helpers import make_model_dir  # noqa: E402
 
-PLANS = [([], 1), ([], 2), ([], 0), ([64], 1), ([64], 2), ([96], 1), ([96], 2), ([160], 2)]
+PLANS = [([], 1), ([], 3), ([64], 1), ([64], 3), ([96], 3), ([32], 3)]
 
 
 def main():
