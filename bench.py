@@ -338,6 +338,8 @@ def main():
                     help="vision engine: pin the GEMM tiles q,o,f,p (clipgpu_options.gemm_tiles; PMC passes and "
                          "A/B runs pin the un-profiled bench's tiles); the patch GEMM takes p's")
     ap.add_argument("--lanes", type=int, default=0, help="vision engine: pin the device lanes (0 = the table's)")
+    ap.add_argument("--text-tiles", default="", help="text engine: pin the GEMM tiles q,o,f,p (A/B runs)")
+    ap.add_argument("--text-lanes", type=int, default=0, help="text engine: pin the device lanes (0 = the table's)")
     ap.add_argument("--windows", type=int, default=5,
                     help="N = 1: repeated K-step windows after the timed one (min / median / max images/s, the "
                          "shader clock of each window, and the c_fc launch time per window); 0 skips them")
@@ -492,7 +494,10 @@ def main():
     text = None
     tout_host = None
     if not args.no_text:
-        te = Engine(mdir, _lib.TOWER_TEXT, [local], args.dtype, B_TEXT)
+        topts = {"lanes": args.text_lanes}
+        if args.text_tiles:
+            topts["gemm_tiles"] = [int(t) for t in args.text_tiles.split(",")]
+        te = Engine(mdir, _lib.TOWER_TEXT, [local], args.dtype, B_TEXT, **topts)
         if dp:
             init_engine_comm(te)
         tout_full = torch.empty((world * B_TEXT, 512), device=dev, dtype=torch.float32)

@@ -1,13 +1,16 @@
 #!/usr/bin/env python3
 """Per-kernel statistics of bench.py's timed steps only, from a rocprofv3 --kernel-trace CSV.
 
-    python tools/trace_timed.py RUN_kernel_trace.csv STEPS [OUT.txt]
+    python tools/trace_timed.py RUN_kernel_trace.csv STEPS [OUT.txt] [LANES]
 
 For a vision-only bench (`--no-text --no-fp8 --no-e2e --no-cpu-baseline`): after the engine's
 creation-time tuning, the trace ends with W warmup steps, the STEPS timed steps, then the c_fc
 profiling pass (1 warmup + P = max(3, STEPS // 2) steps, lanes serialized).  Every step issues the
 same kernel sequence, so the launches per step n is the period of the trace's tail; the timed
-block is the STEPS * n launches before the last (P + 1) * n.  Prints per-kernel calls per step,
+block is the STEPS * n launches before the last (P + 1) * n.  With LANES concurrent lanes the
+profiling pass runs them one after the other, so the tail's period is one lane's forward and a
+step is LANES * n launches; kernel durations in the timed block then overlap (the summed kernel
+time per step exceeds the wall time per step).  Prints per-kernel calls per step,
 mean / median duration and the share of the summed kernel time, plus the timed block's wall time
 per step (first start to last end), so rocprof's numbers exclude the creation-time tuning launches
 that rocprofv3 --stats mixes in.
@@ -31,6 +34,7 @@ def short(name):
 
 def main():
     path, steps = sys.argv[1], int(sys.argv[2])
+    lanes = int(sys.argv[4]) if len(sys.argv) > 4 else 1
     rows = []
     with open(path) as f:
         for r in csv.DictReader(f):
@@ -45,9 +49,10 @@ def main():
             break
     if n is None:
         raise SystemExit("no periodic tail: not a vision-only bench trace?")
+    n *= lanes  # launches per step
     end = len(rows) - prof_steps * n
     timed = rows[end - steps * n:end]
-    out = [f"# {path}: {len(rows)} launches, {n} per step; timed block = {steps} steps "
+    out = [f"# {path}: {len(rows)} launches, {n} per step ({lanes} lane(s)); timed block = {steps} steps "
            f"({len(timed)} launches) before the {prof_steps}-step profiling pass",
            f"# timed block wall time per step (first start -> last end): "
            f"{(timed[-1][1] - timed[0][0]) / steps / 1e3:.1f} us; summed kernel time per step "
