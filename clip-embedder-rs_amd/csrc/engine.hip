@@ -755,8 +755,8 @@ int table_tile(int site, int rows, int N, int K) {
 // other lane's GEMMs, while 39424-row lanes still fill the 256x256 / 160x128 rounds (round 2's
 // two-lane text leg: 117k seq/s; round 3's one-lane table: 110k; profiles/r03_v12_text_lanes_ab.txt).
 // Round 4: a vision batch of 8192..32767 token rows (ViT-B/32 at 256 images: 12800) takes two
-// lanes too, with out_proj, c_fc, c_proj and the patch GEMM on the 4-wave 160x128 RS tile (two
-// blocks per CU, one from each lane).  Same-box A/Bs (tools/bench_variants.sh,
+// lanes too, with out_proj, c_fc, c_proj and the patch GEMM off the 8-wave 160x128 tile (table_tiles
+// below: c_fc on the 4-wave 160x128 RS tile, two blocks per CU, one from each lane).  Same-box A/Bs (tools/bench_variants.sh,
 // profiles/r04_lanes_ab.jsonl): one lane on the 8-wave table tiles 79.8-80.3k img/s; two lanes on the
 // same tiles 81.3k; two lanes with these 82.6-84.2k (qkv on 256x256 plain, RS or half-tile within
 // 0.5 %; c_fc on 256x256 at two lanes loses 2 %).  The round-1 tree -- two lanes of 160x128 tiles
@@ -791,10 +791,14 @@ void table_tiles(clipgpu_engine& e) {
   const int G = e.spec.grid();
   const int prow = e.spec.tower == TOWER_VISION ? rows / e.spec.tokens() * G * G : 0;
   e.tile_patch = prow >= 2048 ? TILE_160x128_W8_RS : TILE_AUTO;
-  // the two-lane vision regime (table_lanes): the 4-wave 160x128 RS tile beside the other lane
+  // the two-lane vision regime (table_lanes): c_fc on the 4-wave 160x128 RS tile, out_proj / c_proj /
+  // the patch GEMM on the 8-wave 224x192 tile (one round of 116 tiles per 6400-row lane), beside the
+  // other lane: +0.4 % and +0.9 % over the 4-wave tile there in two same-box sessions
+  // (profiles/r04_residual26_two_lanes_ab.jsonl); c_fc on it loses 3 %
   if (vision_two_lanes(e) && e.dev_lanes == 2 && rows >= 2048) {
-    e.tile[GS_OUT] = e.tile[GS_FC] = e.tile[GS_PROJ] = TILE_160x128_RS;
-    if (prow >= 2048) e.tile_patch = TILE_160x128_RS;
+    e.tile[GS_FC] = TILE_160x128_RS;
+    e.tile[GS_OUT] = e.tile[GS_PROJ] = TILE_224x192_W8;
+    if (prow >= 2048) e.tile_patch = TILE_224x192_W8;
   }
 }
 

@@ -46,7 +46,8 @@ for s in $STEPS; do
     vtrace)  # kernel trace of the vision leg alone; per-kernel stats of the timed steps only (tools/trace_timed.py)
       run vtrace 300 rocprofv3 --kernel-trace --stats -d gpurun_out/vtrace -o run --output-format csv -- \
           python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-fp8 --no-text --no-e2e --windows 0 || exit $?
-      python3 tools/trace_timed.py gpurun_out/vtrace/run_kernel_trace.csv 10 gpurun_out/vtrace_timed_kernels.txt || exit $? ;;
+      VLANES=$(python3 -c "import json;print([json.loads(l) for l in open('gpurun_out/vtrace.log') if l.startswith('{')][-1]['lanes_env'])") || exit 1
+      python3 tools/trace_timed.py gpurun_out/vtrace/run_kernel_trace.csv 10 gpurun_out/vtrace_timed_kernels.txt $VLANES || exit $? ;;
     prof)
       run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
           python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline || exit $?
