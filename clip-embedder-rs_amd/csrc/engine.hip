@@ -1906,7 +1906,7 @@ int clipgpu_host_register(void* ptr, size_t bytes) {
     for (const auto& rg : h.r)
       if (a < rg.first + rg.second && rg.first < a + bytes)
         throw ClipErr(CLIPGPU_ERR_INVALID, "host range overlaps a registered one");
-    HIP_CHECK(hipHostRegister(ptr, bytes, hipHostRegisterMapped));
+    HIP_CHECK(hipHostRegister(ptr, bytes, hipHostRegisterMapped | hipHostRegisterPortable));  // every device
     h.r.emplace_back(a, bytes);
   });
 }

@@ -50,9 +50,9 @@ def timed(fn, steps, warmup):
     return (time.perf_counter() - t0) / steps
 
 
-def device_leg(name, cfg, tower, B, steps=6, warmup=2, dtype="bf16", mx_sites=None):
+def device_leg(name, cfg, tower, B, steps=6, warmup=2, dtype="bf16", mx_sites=None, lanes=0):
     d = model_dir(cfg)
-    e = Engine(d, tower, [0], dtype, B, mx_sites=mx_sites)
+    e = Engine(d, tower, [0], dtype, B, mx_sites=mx_sites, lanes=lanes)
     s = torch.cuda.current_stream()
     mc = cfg["model_cfg"]
     E = mc["embed_dim"]
@@ -70,6 +70,7 @@ def device_leg(name, cfg, tower, B, steps=6, warmup=2, dtype="bf16", mx_sites=No
     rate = B / dt
     gf = GFLOP[name.replace("_fp8", "").replace("_full", "")]
     print(json.dumps({"measure": name, "dtype": dtype, "mx_sites": mx_sites if dtype == "fp8" else None,
+                      "lanes": e.info()[1],
                       "batch_per_gpu": B, "units_per_s": round(rate, 1),
                       "ms_per_step": round(dt * 1e3, 3), "model_tflops": round(rate * gf / 1e3, 1),
                       "frac_of_2500": round(rate * gf / 1e3 / 2500, 4), "input": "device-resident"}),
@@ -219,6 +220,12 @@ if __name__ == "__main__":
     if "h14fp8full" in which:  # the full MX split (QKV, c_fc, c_proj): throughput mode, below the bar
         device_leg("h14_vision_fp8_full", VIT_H_14_378_CFG, 0, 64, dtype="fp8")
         device_leg("h14_text_fp8_full", VIT_H_14_378_CFG, 1, 64, dtype="fp8")
+    if "lanesab" in which:  # one vs two device lanes at the large-model shards (table tiles), interleaved
+        for rnd in range(2):
+            for lanes in (1, 2):
+                device_leg("so400m_vision", SO400M_16_SIGLIP2_384_CFG, 0, 128, lanes=lanes)
+                device_leg("h14_vision", VIT_H_14_378_CFG, 0, 64, lanes=lanes)
+                device_leg("h14_text", VIT_H_14_378_CFG, 1, 64, lanes=lanes)
     if "so400mtext" in which:  # the SigLIP2 text tower of the configs[3] model folder
         device_leg("so400m_text", SO400M_16_SIGLIP2_384_CFG, 1, 128)
     if "so400mfp8" in which:
