@@ -738,8 +738,8 @@ PoolSrc trunk(const clipgpu_engine& e, const Replica& r, int B, int causal, cons
 //     (profiles/r03_v2_gemm_ab_pp.txt, r03_v7_tile_256x128_half_ab.txt); at every other N = D shape
 //     of the BASELINE models tile 17 is the fastest or within 1 %;
 //   rows < 2048 (small max_batch): the shape heuristic (TILE_AUTO; skinny kernel <= 256 rows).
-// One lane for vision: the full-batch GEMMs quantize better over 256 CUs than two half-batch lanes
-// (the tuner's lane choice at the BASELINE vision batches); large text batches: table_lanes below.
+// `rows` is one lane's rows at max_batch; the lane count is table_lanes' (below), and the two-lane
+// ViT-B/32 regime overrides out_proj / c_fc / c_proj / patch in table_tiles.
 int table_tile(int site, int rows, int N, int K) {
   if (rows < 2048) return TILE_AUTO;
   switch (site) {
@@ -749,8 +749,8 @@ int table_tile(int site, int rows, int N, int K) {
   }
 }
 
-// Device lanes of the committed table.  One lane, except a large-batch text tower (>= 32768 token
-// rows: configs[2]'s 1024 x 77), which takes two: its LayerNorms and causal attention are a larger
+// Device lanes of the committed table.  A large-batch text tower (>= 32768 token rows: configs[2]'s
+// 1024 x 77) takes two lanes: its LayerNorms and causal attention are a larger
 // share of the layer than in the vision trunk (0.7 + 0.7 ms of 9.3 ms at one lane) and overlap the
 // other lane's GEMMs, while 39424-row lanes still fill the 256x256 / 160x128 rounds (round 2's
 // two-lane text leg: 117k seq/s; round 3's one-lane table: 110k; profiles/r03_v12_text_lanes_ab.txt).
@@ -767,9 +767,13 @@ bool vision_two_lanes(const clipgpu_engine& e) {
   const long rows = (long)e.max_batch * e.spec.tokens();
   return e.spec.tower == TOWER_VISION && rows >= kVisionTwoLaneRows[0] && rows < kVisionTwoLaneRows[1];
 }
+// Larger vision batches take two lanes on their one-lane tiles: DFN5B ViT-H/14-378 at 64 images
+// (46720 rows) 862 -> 886 img/s, SO400M-16-SigLIP2-384 at 128 (73728 rows) 1545 -> 1545
+// (tools/bench_models.py lanesab, profiles/r04_large_model_lanes_ab.jsonl, two rounds each).
 int table_lanes(const clipgpu_engine& e) {
-  if (vision_two_lanes(e)) return 2;
-  return e.spec.tower == TOWER_TEXT && (long)e.max_batch * e.spec.tokens() >= 32768 ? 2 : 1;
+  const long rows = (long)e.max_batch * e.spec.tokens();
+  if (e.spec.tower == TOWER_VISION) return rows >= kVisionTwoLaneRows[0] ? 2 : 1;
+  return e.spec.tower == TOWER_TEXT && rows >= 32768 ? 2 : 1;
 }
 
 void table_tiles(clipgpu_engine& e) {
