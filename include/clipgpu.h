@@ -131,11 +131,11 @@ int clipgpu_embed_u8(clipgpu_engine* e, const uint8_t* nhwc, int64_t B, int64_t 
  * The reference's embed_images / embed_texts hand host arrays to the session (src/vision.rs:102-113,
  * src/text.rs:150-166).  By default the host-buffer entry points stage them through the handle's
  * pinned buffers (a host copy, then the PCIe DMA).  A caller that reuses its buffers can pin them once
- * (hipHostRegister): an embed_* call whose whole input (or output) lies inside a registered range then
- * DMAs straight from (into) it, and a vision batch's first sub-batch is a quarter of the batch, so that
- * only its transfer is exposed before the forward starts (the rest streams in under it).  Results are
- * bit-identical either way.  Process-wide; the caller keeps the memory alive and unregisters it
- * before freeing it.  Ranges may not overlap. */
+ * (hipHostRegister, mapped and portable): an embed_* call whose whole input (or output) lies inside a
+ * registered range then DMAs straight from (into) it, skipping the host copy; the batch still moves
+ * in one chunk per lane, so the first chunk's transfer is what is exposed before the forward starts.
+ * Results are bit-identical either way.  Process-wide; the caller keeps the memory alive, and
+ * unregisters it only when no embed_* call is using it, before freeing it.  Ranges may not overlap. */
 int clipgpu_host_register(void* ptr, size_t bytes);
 int clipgpu_host_unregister(void* ptr);
 
