@@ -72,6 +72,9 @@ def text_flops(B, T=77, executed=False):
 
 
 # GemmTile ids the library builds (csrc/kernels/kernels.hpp kGemmTiles)
+# trunk GEMM sites of the ViT-B/32 vision tower: (N, K), and what the epilogue adds
+SITE_SHAPES = {"qkv": (2304, 768), "out_proj": (768, 768), "c_fc": (3072, 768), "c_proj": (768, 3072)}
+SITE_EPI = {"qkv": "+bias", "out_proj": "+bias, f32 residual", "c_fc": "+QuickGELU", "c_proj": "+bias, f32 residual"}
 TILE_NAMES = {0: "heuristic", 1: "128x128", 2: "256x128", 3: "256x256", 13: "192x256w8", 14: "256x256rs",
               15: "160x128rs", 17: "160x128w8rs", 18: "256x256half", 26: "224x192w8"}
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md chip table)
@@ -193,20 +196,23 @@ def cpu_baseline(px_host, ids_host, gpu_vision, gpu_text, fp8_vision=None, targe
     return res
 
 
-def load_traffic(rows_per_launch, tiles):
-    """HBM bytes per c_fc launch: NOT measured in this run -- read from the committed PMC summary
-    (separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench, gfx950 FETCH_SIZE x2
-    correction, tools/pmc_traffic.py); its `source` names the run it came from.  Only used when
-    it was measured at this run's rows per launch AND with this run's GEMM tiles (the record's
-    `tiles`); otherwise null, with the reason in traffic_source."""
+def load_traffic(site, rows_per_launch, tiles):
+    """HBM bytes per launch of the roofline kernel: NOT measured in this run -- read from the
+    committed PMC summary (separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench,
+    gfx950 FETCH_SIZE x2 correction, tools/pmc_traffic.py); its `source` names the run it came from.
+    Only used when it was measured for this site at this run's rows per launch AND with this run's
+    GEMM tiles (the record's `tiles`); otherwise null, with the reason in traffic_source."""
     p = os.path.join(ROOT, "profiles", "pmc_c_fc.json")
     if os.path.exists(p):
         with open(p) as f:
             d = json.load(f)
-        rec = d.get("by_rows", {}).get(str(int(rows_per_launch)))
+        key = f"{site}:{int(rows_per_launch)}"
+        rec = d.get("by_site_rows", {}).get(key)
+        if rec is None and site == "c_fc":
+            rec = d.get("by_rows", {}).get(str(int(rows_per_launch)))
         if rec is None:
-            return None, (f"profiles/pmc_c_fc.json has no measurement at {int(rows_per_launch)} rows per launch "
-                          f"(has {sorted(d.get('by_rows', {}))})")
+            return None, (f"profiles/pmc_c_fc.json has no {site} measurement at {int(rows_per_launch)} rows per "
+                          f"launch (has {sorted(d.get('by_site_rows', {}))})")
         if rec.get("tiles") != tiles:
             return None, (f"profiles/pmc_c_fc.json's record at {int(rows_per_launch)} rows was taken with tiles "
                           f"{rec.get('tiles')}, this run uses {tiles}: not applicable")
@@ -387,11 +393,11 @@ def main():
         else:
             ve.embed_pixels_device(px.data_ptr(), B_VISION, out.data_ptr(), stream.cuda_stream)
 
-    def timed(step, steps, warmup, prof_engine=None, prof_cat=None):
+    def timed(step, steps, warmup, prof_engine=None, prof_cats=None):
         for _ in range(warmup):
             step()
         if prof_engine is not None:
-            profile_enable(prof_engine, [prof_cat])
+            profile_enable(prof_engine, list(prof_cats))
         if dp:
             dist.barrier()
         torch.cuda.synchronize()
@@ -408,7 +414,7 @@ def main():
             dt = float(t.item())
         prof = None
         if prof_engine is not None:
-            prof = profile_read(prof_engine, prof_cat)
+            prof = {c: profile_read(prof_engine, c) for c in prof_cats}
             profile_enable(prof_engine, [])
         return dt, prof
 
@@ -427,22 +433,32 @@ def main():
     images = world * B_VISION * args.steps
     value = images / dt
     ms_per_step = dt * 1e3 / args.steps
-    # Per-launch kernel time: a separate pass with HIP events around every c_fc launch.
-    # Profiling runs the engine's two lanes (half-batch sub-forwards) one after the other
-    # instead of concurrently, so it is kept out of the timed loop; launch shapes are the same.
-    _, (fc_ms, fc_n) = timed(vision_step, max(3, args.steps // 2), 1, ve, "c_fc")
+    # Per-launch kernel time of the four trunk GEMM sites: a separate pass with HIP events at the
+    # kernel boundaries of every launch.  Profiling runs the engine's two lanes (half-batch
+    # sub-forwards) one after the other instead of concurrently, so it is kept out of the timed
+    # loop; launch shapes are the same.
+    psteps = max(3, args.steps // 2)
+    _, site_prof = timed(vision_step, psteps, 1, ve, SITE_SHAPES)
+    fc_ms, fc_n = site_prof["c_fc"]
     windows = None
     if world == 1 and args.windows > 0:
         windows = measure_windows(vision_step, ve, args.windows, args.steps, dt, dev)
 
-    # roofline of the dominant kernel: c_fc GEMM (+QuickGELU epilogue), M=rows per launch,
-    # N=3072, K=768; fc_n counts the full-row launches (12 layers, or 11 when the last one
-    # is pruned to the pooled rows and profiled as "last_layer", x lanes per step)
+    # Per-site figures (M = rows per launch; the counts are the full-row launches: 12 layers, or 11
+    # when the last one is pruned to the pooled rows and profiled as "last_layer", x lanes per
+    # step).  The roofline kernel is the dominant one: the site with the most GEMM time per step.
     fc_layers = 11 if PRUNE_LAST else 12
-    fc_rows_per_launch = B_VISION * 50 * fc_layers * max(3, args.steps // 2) / max(fc_n, 1)
-    fc_flops = 2.0 * fc_rows_per_launch * 3072 * 768
-    fc_avg_s = (fc_ms / 1e3) / max(fc_n, 1)
-    achieved = fc_flops / fc_avg_s / 1e12
+    sites = {}
+    for site, (N, K) in SITE_SHAPES.items():
+        ms, n = site_prof[site]
+        rows = B_VISION * 50 * fc_layers * psteps / max(n, 1)
+        avg_s = (ms / 1e3) / max(n, 1)
+        tf = 2.0 * rows * N * K / avg_s / 1e12 if n else 0.0
+        sites[site] = {"shape": f"{int(rows)}x{N}x{K}", "rows_per_launch": int(rows), "tile": gemm_tiles[site],
+                       "avg_launch_us": round(avg_s * 1e6, 2), "us_per_step": round(ms * 1e3 / psteps, 1),
+                       "tflops": round(tf, 1), "frac": round(tf / peak, 4)}
+    dom = max(sites, key=lambda k: sites[k]["us_per_step"])
+    fc_rows_per_launch = sites["c_fc"]["rows_per_launch"]
     whole_tflops = vit_flops(B_VISION, executed=True) * args.steps / dt / 1e12 / 1.0
 
     # Per-kernel-class time per step (lanes serialized, no graph): where the step goes.
@@ -548,7 +564,7 @@ def main():
         torch.cuda.synchronize()
         cpu = cpu_baseline(px.cpu().numpy(), ids.cpu().numpy(), out.cpu().numpy(), tout_host, fout_host)
 
-    traffic, traffic_src = (load_traffic(fc_rows_per_launch, ",".join(str(t) for t in tiles)) if not fp8
+    traffic, traffic_src = (load_traffic(dom, sites[dom]["rows_per_launch"], ",".join(str(t) for t in tiles)) if not fp8
                             else (None, None))
     if rank == 0:
         line = {
@@ -568,12 +584,16 @@ def main():
                                    "synthetic 224x224 per GPU, device-resident input",
                        "global_batch": world * B_VISION, "seq_len": 50,
                        "parallelism": f"dp{world}, {dev_lanes.value} concurrent sub-batch lane(s)/GPU (committed MI355X tile table)" + (" + the engine's RCCL all-gather (ncclAllGather in the C ABI) of the [B,512] embeddings on every rank" if dp else "")},
-            "roofline": {"bound": "mfma", "kernel": f"c_fc GEMM ({int(fc_rows_per_launch)}x3072x768, +QuickGELU, tile {gemm_tiles['c_fc']})",
-                         "rows_per_launch": int(fc_rows_per_launch),
-                         "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
-                         "frac": round(achieved / peak, 4), "traffic": traffic,
+            "roofline": {"bound": "mfma",
+                         "kernel": f"{dom} GEMM ({sites[dom]['shape']}, {SITE_EPI[dom]}, tile {sites[dom]['tile']}): the "
+                                   f"site with the most GEMM time per step",
+                         "rows_per_launch": sites[dom]["rows_per_launch"],
+                         "achieved": sites[dom]["tflops"], "peak": peak, "unit": "TFLOP/s",
+                         "frac": sites[dom]["frac"], "traffic": traffic,
                          "traffic_source": traffic_src,
-                         "launches_timed": fc_n, "avg_launch_us": round(fc_avg_s * 1e6, 2)},
+                         "launches_timed": site_prof[dom][1], "avg_launch_us": sites[dom]["avg_launch_us"]},
+            "gemm_sites": dict(sites, note="per-launch HIP-event times of each trunk GEMM site in a profiled pass "
+                                           "(lanes serialized); us_per_step sums the site's launches"),
             "gemm_tiles": gemm_tiles,
             "gemm_tiles_env": ",".join(str(t) for t in tiles),
             "lanes_env": dev_lanes.value,

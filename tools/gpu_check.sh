@@ -61,11 +61,13 @@ for s in $STEPS; do
             python3 bench.py --steps 3 --warmup 1 --no-text --no-cpu-baseline --no-fp8 --no-e2e --windows 0 \
             --tiles $TILES --lanes $LANES || exit $?
       done
-      ROWS=$(python3 -c "import json;print([json.loads(l) for l in open('gpurun_out/bench.log') if l.startswith('{')][-1]['roofline']['rows_per_launch'])") || exit 1
       cp profiles/pmc_c_fc.json gpurun_out/pmc_c_fc.json  # merged into (copy back to profiles/ after the call)
-      python3 tools/pmc_traffic.py gpurun_out/pmc_bench/FETCH_SIZE gpurun_out/pmc_bench/WRITE_SIZE \
-          gpurun_out/pmc_c_fc.json $ROWS "${PMC_LABEL:-this run}: --pmc FETCH_SIZE and --pmc WRITE_SIZE passes of bench.py --no-text, tiles $TILES" \
-          "$TILES" || exit $? ;;
+      for SITE in c_fc c_proj out_proj; do  # every site with a record; the bench reads its roofline kernel's
+        ROWS=$(python3 -c "import json;print([json.loads(l) for l in open('gpurun_out/bench.log') if l.startswith('{')][-1]['gemm_sites']['$SITE']['rows_per_launch'])") || exit 1
+        python3 tools/pmc_traffic.py gpurun_out/pmc_bench/FETCH_SIZE gpurun_out/pmc_bench/WRITE_SIZE \
+            gpurun_out/pmc_c_fc.json $ROWS "${PMC_LABEL:-this run}: --pmc FETCH_SIZE and --pmc WRITE_SIZE passes of bench.py --no-text, tiles $TILES" \
+            "$TILES" $SITE || exit $?
+      done ;;
   esac
 done
 echo "=== done"
