@@ -451,7 +451,8 @@ def main():
     sites = {}
     for site, (N, K) in SITE_SHAPES.items():
         ms, n = site_prof[site]
-        rows = B_VISION * 50 * fc_layers * psteps / max(n, 1)
+        # qkv runs on every token in every layer (the pruned last layer's attention needs all keys)
+        rows = B_VISION * 50 * (12 if site == "qkv" else fc_layers) * psteps / max(n, 1)
         avg_s = (ms / 1e3) / max(n, 1)
         tf = 2.0 * rows * N * K / avg_s / 1e12 if n else 0.0
         sites[site] = {"shape": f"{int(rows)}x{N}x{K}", "rows_per_launch": int(rows), "tile": gemm_tiles[site],
