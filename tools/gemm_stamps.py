@@ -48,6 +48,13 @@ CASES = [
     ("t17_c_proj 160x128w8rs", 1, 0, 12800, 768, 3072, 17),
     ("t18_c_fc 256x256half", 0, 1, 12800, 3072, 768, 18),
     ("t18_qkv 256x256half", 0, 0, 12800, 2304, 768, 18),
+    # round 4: the two-lane table's tiles at one lane's 6400 rows
+    ("t26_c_proj 224x192w8", 1, 0, 6400, 768, 3072, 26),
+    ("t26_out 224x192w8", 1, 0, 6400, 768, 768, 26),
+    ("t15_c_proj 160x128rs", 1, 0, 6400, 768, 3072, 15),
+    ("t15_out 160x128rs", 1, 0, 6400, 768, 768, 15),
+    ("t15_c_fc 160x128rs", 0, 1, 6400, 3072, 768, 15),
+    ("t14_qkv 256x256rs", 0, 0, 6400, 2304, 768, 14),
 ]
 if len(sys.argv) > 1:
     CASES = [c for c in CASES if any(a in c[0] for a in sys.argv[1:])]
@@ -76,7 +83,7 @@ for name, epi, act, M, N, K, tile in CASES:
             epis.append(row[b + 3] - row[b + 2])
             if i + 1 < nt:
                 gaps.append(row[b + 4] - row[b + 3])
-    ks = np.diff(s[:, 34:34 + nk - 1], axis=1) if nk > 2 else np.zeros((nb, 0))
+    ks = np.diff(s[:, 34:min(34 + nk - 1, 61)], axis=1) if nk > 2 else np.zeros((nb, 0))  # slots 34..60
     end = np.array([row[5 + 4 * (nt - 1)] for row, nt in zip(s, ntile)])
     real = (s[:, 63] - s[:, 62]).astype(np.float64)
     cyc = (end - s[:, 0]).astype(np.float64)
