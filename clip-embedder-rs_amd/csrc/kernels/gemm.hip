@@ -117,6 +117,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nTn = (p.N + BN - 1) / BN;
+  const int grp = p.group > 0 ? p.group : CLIPGPU_TILE_GROUP;
   const int nTm = (p.M + BM - 1) / BM;
   const int ntiles = nTn * nTm;
   const int nk = p.K / BK;
@@ -341,7 +342,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
   int m0, n0;
   GEMM_STAMP_REAL(62);
   GEMM_STAMP(0);
-  tile_coords(t_first, nTm, nTn, BM, BN, m0, n0);
+  tile_coords(t_first, nTm, nTn, BM, BN, m0, n0, grp);
   set_tile(m0, n0);
   stage(0, sA0, sB0);
   stage_bias(n0, 0);
@@ -378,7 +379,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
     const bool has_next = tn < t_end;
     int nm0 = m0, nn0 = n0;
     if (has_next) {
-      tile_coords(tn, nTm, nTn, BM, BN, nm0, nn0);
+      tile_coords(tn, nTm, nTn, BM, BN, nm0, nn0, grp);
       set_tile(nm0, nn0);
       stage(0, cur1 ? sA0 : sA1, cur1 ? sB0 : sB1);
       stage_bias(nn0, bias_par ^ 1);
@@ -488,6 +489,8 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
   const float* const bias_p = p.bias;
   asm volatile("" ::"s"(lda_i), "s"(ldw_i), "s"(nb), "s"(Ab), "s"(Wb), "s"(bias_p));
   const int nTn = (p.N + BN - 1) / BN;
+  const int grp = p.group > 0 ? p.group : CLIPGPU_TILE_GROUP;
+  asm volatile("" ::"s"(grp));
   const int nTm = (p.M + BM - 1) / BM;
   const int ntiles = nTn * nTm;
   const int nk = p.K / BK;  // K-steps per tile
@@ -524,14 +527,14 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
   auto unit_coords = [&](int u, int& m0, int& n0) {
     if constexpr (HM) {  // u < F: whole tile j + u nbx; u == F: half (j & 1) of tile F nbx + j / 2
       if (u < hm_F) {
-        tile_coords(hm_start + hm_j + u * hm_nbx, nTm, nTn, BM, BN, m0, n0);
+        tile_coords(hm_start + hm_j + u * hm_nbx, nTm, nTn, BM, BN, m0, n0, grp);
       } else {
-        tile_coords(hm_start + hm_F * hm_nbx + (hm_j >> 1), nTm, nTn, BM, BN, m0, n0);
+        tile_coords(hm_start + hm_F * hm_nbx + (hm_j >> 1), nTm, nTn, BM, BN, m0, n0, grp);
         m0 += (hm_j & 1) * (BM / 2);
       }
       return;
     }
-    tile_coords(u, nTm, nTn, BM, BN, m0, n0);
+    tile_coords(u, nTm, nTn, BM, BN, m0, n0, grp);
   };
 
   // W image swizzle for the permuted W-row reads (rowB below)

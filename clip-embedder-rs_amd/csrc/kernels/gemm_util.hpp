@@ -8,7 +8,7 @@
 
 #include "kernels.hpp"
 
-// Row panels per tile-order group (tile_coords); a build-time knob for schedule experiments.
+// Row panels per tile-order group (tile_coords) when GemmParams.group is 0.
 #ifndef CLIPGPU_TILE_GROUP
 #define CLIPGPU_TILE_GROUP 8
 #endif
@@ -75,14 +75,15 @@ __device__ __forceinline__ void vm_wait() {
 }
 
 
-// Tile order shared by all blocks: tiles are grouped 8 row panels at a time
-// (walk M first inside a group) so that concurrently running tiles share A and W
-// panels in L2.
-__device__ __forceinline__ void tile_coords(int t, int nTm, int nTn, int BM, int BN, int& m0, int& n0) {
-  constexpr int GROUP = CLIPGPU_TILE_GROUP;
-  const int per_group = GROUP * nTn;
-  const int first_m = (t / per_group) * GROUP;
-  const int gsize = min(nTm - first_m, GROUP);
+// Tile order shared by all blocks: tiles are grouped `group` row panels at a time (walk M first
+// inside a group) so that concurrently running tiles share A and W panels in L2.  group = 1 walks N
+// first: the tiles of one row panel are neighbours, so one XCD's blocks read each A panel once and
+// every XCD reads all of W (the order for a small W and a large A: c_proj).
+__device__ __forceinline__ void tile_coords(int t, int nTm, int nTn, int BM, int BN, int& m0, int& n0,
+                                            int group = CLIPGPU_TILE_GROUP) {
+  const int per_group = group * nTn;
+  const int first_m = (t / per_group) * group;
+  const int gsize = min(nTm - first_m, group);
   m0 = (first_m + (t % per_group) % gsize) * BM;
   n0 = ((t % per_group) / gsize) * BN;
 }

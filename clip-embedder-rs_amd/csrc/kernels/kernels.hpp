@@ -35,6 +35,7 @@ struct GemmParams {
   const float* pos;          // EPI_PATCH positional embedding [G^2+cls][N]
   int tile;                  // GemmTile (0 = pick by shape)
   int diag;                  // stamp build only: bit 0 = skip epilogue stores (timing experiments)
+  int group;                 // tile order: row panels per group (gemm_util.hpp tile_coords); 0 = 8
 };
 
 // Tile configurations of the MFMA GEMM.  Ids are stable across rounds; the ones not listed were

@@ -240,19 +240,27 @@ int clipgpu_test_clock_probe(void* stream, int64_t duration_us, uint64_t* d_out)
 
 int clipgpu_test_gemm_bench(int dtype, int epi, int act, int64_t M, int64_t N, int64_t K, int tile, int iters,
                             double* us_per_launch) {
+  return clipgpu_test_gemm_bench_ld(dtype, epi, act, M, N, K, K, K, tile, iters, us_per_launch);
+}
+
+int clipgpu_test_gemm_bench_ld(int dtype, int epi, int act, int64_t M, int64_t N, int64_t K, int64_t lda,
+                               int64_t ldw, int tile, int iters, double* us_per_launch) {
   return guarded([&]() {
     const DType dt = dt_of(dtype);
-    if (M <= 0 || N <= 0 || K <= 0 || K % 64 || iters <= 0 || !us_per_launch)
+    if (M <= 0 || N <= 0 || K <= 0 || K % 64 || iters <= 0 || !us_per_launch || lda < K || ldw < K ||
+        lda % 8 || ldw % 8)
       throw ClipErr(CLIPGPU_ERR_INVALID, "bad GEMM bench arguments");
-    DevBuf fA(M * K * 4), fW(N * K * 4), dA(M * K * 2), dW(N * K * 2), dB(N * 4), dO(M * N * 4);
-    hipLaunchKernelGGL(fill_random, dim3(2048), dim3(256), 0, nullptr, fA.as<float>(), (long)(M * K), 1u);
-    hipLaunchKernelGGL(fill_random, dim3(2048), dim3(256), 0, nullptr, fW.as<float>(), (long)(N * K), 2u);
+    // A [M][lda], W [N][ldw] (row pitch in elements; the pad columns hold random values the GEMM
+    // never reads)
+    DevBuf fA(M * lda * 4), fW(N * ldw * 4), dA(M * lda * 2), dW(N * ldw * 2), dB(N * 4), dO(M * N * 4);
+    hipLaunchKernelGGL(fill_random, dim3(2048), dim3(256), 0, nullptr, fA.as<float>(), (long)(M * lda), 1u);
+    hipLaunchKernelGGL(fill_random, dim3(2048), dim3(256), 0, nullptr, fW.as<float>(), (long)(N * ldw), 2u);
     hipLaunchKernelGGL(fill_random, dim3(64), dim3(256), 0, nullptr, dB.as<float>(), (long)N, 3u);
-    TCHECK(launch_cast_f32(dt, fA.as<float>(), dA.p, (long)(M * K), nullptr));
-    TCHECK(launch_cast_f32(dt, fW.as<float>(), dW.p, (long)(N * K), nullptr));
+    TCHECK(launch_cast_f32(dt, fA.as<float>(), dA.p, (long)(M * lda), nullptr));
+    TCHECK(launch_cast_f32(dt, fW.as<float>(), dW.p, (long)(N * ldw), nullptr));
     TCHECK(hipDeviceSynchronize());
     GemmParams g{};
-    g.A = dA.p; g.lda = K; g.W = dW.p; g.ldw = K; g.bias = dB.as<float>();
+    g.A = dA.p; g.lda = lda; g.W = dW.p; g.ldw = ldw; g.bias = dB.as<float>();
     g.out = dO.p; g.ldo = N; g.M = (int)M; g.N = (int)N; g.K = (int)K; g.tile = tile;
     if (tile != 0 && tile != TILE_SKINNY && !gemm_tile_built(tile)) throw ClipErr(CLIPGPU_ERR_INVALID, "not a built tile");
     const int e = epi == 1 ? EPI_RESID : (epi == 2 ? EPI_STORE32 : EPI_STORE16);

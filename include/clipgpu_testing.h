@@ -56,6 +56,9 @@ int clipgpu_test_patch_rows(int dtype, int mode, int64_t B, int64_t S, int64_t P
  * id (kernels.hpp; 0 auto).  Returns the mean µs per launch (HIP events). */
 int clipgpu_test_gemm_bench(int dtype, int epi, int act, int64_t M, int64_t N, int64_t K, int tile, int iters,
                             double* us_per_launch);
+/* As clipgpu_test_gemm_bench with row pitches lda >= K, ldw >= K (elements, multiples of 8). */
+int clipgpu_test_gemm_bench_ld(int dtype, int epi, int act, int64_t M, int64_t N, int64_t K, int64_t lda,
+                               int64_t ldw, int tile, int iters, double* us_per_launch);
 
 /* Shader-clock probe (bench.py's per-window clock): launches ONE wave on `stream` (a hipStream_t, NULL =
  * the legacy default stream) that sleeps for duration_us of wall time (s_memrealtime, 100 MHz) and writes

@@ -1,5 +1,5 @@
 # Interleaved same-box A/B of bench.py variants.  VARIANTS: ';'-separated "label|extra bench
-# args"; ROUNDS rounds; BV_BASE replaces the default base args (vision leg only).  One JSON summary line per run in
+# args[|library]" (library: a lib/libclipgpu_<name>.so variant, `make variant`, via CLIPGPU_LIB); ROUNDS rounds; BV_BASE replaces the default base args (vision leg only).  One JSON summary line per run in
 # gpurun_out/bench_variants.jsonl (value, ms/step, c_fc launch, tiles, lanes, clock under load).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -9,7 +9,9 @@ OUT=gpurun_out/bench_variants.jsonl
 IFS=';' read -ra VS <<< "${VARIANTS}"
 for i in $(seq 1 "$ROUNDS"); do
   for v in "${VS[@]}"; do
-    label=${v%%|*}; extra=${v#*|}
+    label=${v%%|*}; extra=${v#*|}; vlib=
+    if [[ "$extra" == *"|"* ]]; then vlib=${extra#*|}; extra=${extra%%|*}; fi
+    if [ -n "$vlib" ]; then export CLIPGPU_LIB=$PWD/clip-embedder-rs_amd/lib/libclipgpu_$vlib.so; else unset CLIPGPU_LIB; fi
     log="gpurun_out/bv_${label}_$i.log"
     timeout -k 10 300 python bench.py --steps 20 --warmup 5 ${BV_BASE:---no-cpu-baseline --no-fp8 --no-text --no-e2e --windows 3} \
         $extra > "$log" 2>&1 || { echo "variant $label failed rc=$?"; tail -5 "$log"; exit 1; }
