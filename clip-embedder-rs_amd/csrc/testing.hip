@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
+#include <cstring>
+#include <exception>
 #include <vector>
 
 #include "../../include/clipgpu.h"
@@ -410,6 +412,80 @@ int clipgpu_test_gemm_mx_bench(int epi, int act, int64_t M, int64_t N, int64_t K
     (void)hipEventDestroy(ea);
     (void)hipEventDestroy(eb);
     *us_per_launch = (double)ms * 1000.0 / iters;
+  });
+}
+
+int clipgpu_test_h2d_bench(int64_t bytes, int mode, int iters, double* us_per_copy) {
+  return guarded([&]() {
+    const int src = mode >> 2;
+    mode &= 3;
+    if (bytes <= 0 || bytes % 32 || src > 1 || iters <= 0 || !us_per_copy)
+      throw ClipErr(CLIPGPU_ERR_INVALID, "bad H2D bench arguments");
+    // src 0: hipHostMalloc; 1: page-aligned malloc'd memory registered as clipgpu_host_register does
+    void* host = nullptr;
+    if (src == 0) {
+      TCHECK(hipHostMalloc(&host, (size_t)bytes, hipHostMallocMapped | hipHostMallocPortable));
+    } else {
+      if (posix_memalign(&host, 4096, (size_t)bytes) != 0) throw ClipErr(CLIPGPU_ERR_INVALID, "host alloc");
+      std::memset(host, 1, (size_t)bytes);
+      const hipError_t e = hipHostRegister(host, (size_t)bytes, hipHostRegisterMapped | hipHostRegisterPortable);
+      if (e != hipSuccess) {
+        std::free(host);
+        TCHECK(e);
+      }
+    }
+    std::memset(host, 1, (size_t)bytes);
+    void* mapped = nullptr;
+    hipStream_t s0 = nullptr, s1 = nullptr;
+    hipEvent_t a = nullptr, b = nullptr, j = nullptr;
+    DevBuf dst(bytes);
+    auto run = [&]() {
+      const size_t h = (size_t)bytes / 2;
+      switch (mode) {
+        case 0: TCHECK(hipMemcpyAsync(dst.p, host, (size_t)bytes, hipMemcpyHostToDevice, s0)); break;
+        case 1: TCHECK(launch_pull_copy(mapped, dst.p, (size_t)bytes, s0)); break;
+        default:  // halves on two streams: 2 = two SDMA copies, 3 = the pull kernel beside one SDMA copy
+          TCHECK(hipEventRecord(j, s0));
+          TCHECK(hipStreamWaitEvent(s1, j, 0));
+          if (mode == 2) TCHECK(hipMemcpyAsync(dst.p, host, h, hipMemcpyHostToDevice, s0));
+          else TCHECK(launch_pull_copy(mapped, dst.p, h, s0));
+          TCHECK(hipMemcpyAsync((char*)dst.p + h, (char*)host + h, (size_t)bytes - h, hipMemcpyHostToDevice, s1));
+          TCHECK(hipEventRecord(j, s1));
+          TCHECK(hipStreamWaitEvent(s0, j, 0));
+      }
+    };
+    std::exception_ptr err;
+    try {
+      TCHECK(hipHostGetDevicePointer(&mapped, host, 0));
+      TCHECK(hipStreamCreateWithFlags(&s0, hipStreamNonBlocking));
+      TCHECK(hipStreamCreateWithFlags(&s1, hipStreamNonBlocking));
+      TCHECK(hipEventCreate(&a));
+      TCHECK(hipEventCreate(&b));
+      TCHECK(hipEventCreateWithFlags(&j, hipEventDisableTiming));
+      for (int i = 0; i < 3; ++i) run();
+      TCHECK(hipEventRecord(a, s0));
+      for (int i = 0; i < iters; ++i) run();
+      TCHECK(hipEventRecord(b, s0));
+      TCHECK(hipEventSynchronize(b));
+      float ms = 0.f;
+      TCHECK(hipEventElapsedTime(&ms, a, b));
+      *us_per_copy = (double)ms * 1000.0 / iters;
+    } catch (...) {
+      err = std::current_exception();
+    }
+    (void)hipStreamSynchronize(s0);
+    if (a) (void)hipEventDestroy(a);
+    if (b) (void)hipEventDestroy(b);
+    if (j) (void)hipEventDestroy(j);
+    if (s0) (void)hipStreamDestroy(s0);
+    if (s1) (void)hipStreamDestroy(s1);
+    if (src == 0) {
+      (void)hipHostFree(host);
+    } else {
+      (void)hipHostUnregister(host);
+      std::free(host);
+    }
+    if (err) std::rethrow_exception(err);
   });
 }
 

@@ -66,6 +66,12 @@ int clipgpu_test_gemm_bench_ld(int dtype, int epi, int act, int64_t M, int64_t N
  * uint64 buffer of 2): MHz = 100 * d_out[0] / d_out[1] (MI355X_MICROARCH.md, DVFS give-back item 6).
  * Asynchronous.  bench.py launches it right after a timed window: resident beside a forward, its wave
  * keeps one CU from hosting the one-block-per-CU GEMMs. */
+/* Host-to-device copy rate: `bytes` from a pinned mapped host buffer into device memory, mode 0 = one
+ * hipMemcpyAsync (SDMA), 1 = a copy kernel reading through the host mapping, 2 = the halves as two
+ * SDMA copies on two streams, 3 = the first half by the copy kernel beside the second half's SDMA
+ * copy; + 4: the host buffer is page-aligned malloc'd memory registered (hipHostRegister, as
+ * clipgpu_host_register) instead of hipHostMalloc'd.  Returns the mean µs per copy (HIP events). */
+int clipgpu_test_h2d_bench(int64_t bytes, int mode, int iters, double* us_per_copy);
 int clipgpu_test_clock_probe(void* stream, int64_t duration_us, uint64_t* d_out);
 
 /* Device-resident attention timing (random 16-bit qkv): mean µs per launch_attention over `iters`. */

@@ -7,7 +7,7 @@ per-XCD re-read.  If that excess is L2 set pressure from the 6 KiB row stride of
 and the 192-row W panel, a padded pitch moves it; this script times both (alternating, median of
 REPS) at the per-lane shapes of the ViT-B/32 bench.
 
-usage: ld_pad_ab.py [REPS] [site ...]     sites: c_proj c_fc out_proj qkv (default all)
+usage: ld_pad_ab.py [REPS] [site ...]     sites: c_proj c_fc out_proj qkv (default all); LD_PADS=0,64 (pads)
        ld_pad_ab.py one SITE PAD ITERS    (one config, for rocprofv3 --pmc passes)
 """
 import ctypes
@@ -24,7 +24,7 @@ ROWS, D, MLP = 6400, 768, 3072
 # site: (N, K, epi, act, tile) at the two-lane table (18, 26, 15, 26)
 SITES = {"qkv": (3 * D, D, 0, 0, 18), "out_proj": (D, D, 1, 0, 26), "c_fc": (MLP, D, 0, 1, 15),
          "c_proj": (D, MLP, 1, 0, 26)}
-PADS = (0, 64, 32, 8)
+PADS = tuple(int(x) for x in os.environ.get("LD_PADS", "0,64,32,8").split(","))
 
 
 def run(site, pad, iters):
