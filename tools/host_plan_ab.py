@@ -23,6 +23,8 @@ from oracle.model_spec import OPENAI_MEAN, OPENAI_STD, VIT_B_32_CFG  # noqa: E40
 from tests.helpers import make_model_dir  # noqa: E402
 
 PLANS = [([], 1), ([], 3), ([64], 1), ([64], 3), ([96], 3), ([32], 3)]
+if os.environ.get("HP_MODES"):  # e.g. "1,3": the default partition at these copy_stream modes only
+    PLANS = [([], int(m)) for m in os.environ["HP_MODES"].split(",")]
 
 
 def main():
