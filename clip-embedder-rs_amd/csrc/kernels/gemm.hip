@@ -891,6 +891,11 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
   if constexpr (NW == 8) {
     if (wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
   }
+#if CLIPGPU_ODD_BLOCK_PRIO
+  if constexpr (NW == 4) {
+    if (blockIdx.x & 1) __builtin_amdgcn_s_setprio(1);
+  }
+#endif
   dma_step();
   vm_wait<0>();
   __builtin_amdgcn_s_barrier();
