@@ -616,6 +616,8 @@ GemmParams site_gemm(const clipgpu_engine& e, const Replica& r, const LayerW& L,
     default: g = rows_gemm(r.big, MLP, L.w2, L.b2, r.x, D, rows, D, MLP); break;
   }
   g.group = kSiteGroup[site];
+  // the younger half of 8-wave blocks at priority 1: vision +0.75 %, text -0.5 % (gemm.hip)
+  g.prio = e.spec.tower == TOWER_VISION ? 1 : 0;
   return g;
 }
 

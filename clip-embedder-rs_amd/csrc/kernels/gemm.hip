@@ -884,18 +884,14 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
   GEMM_STAMP_REAL(62);
   GEMM_STAMP_HWID();
   GEMM_STAMP(0);
-  // 8-wave blocks: the younger half (waves 4-7, dispatched second) at priority 1 for the whole
-  // kernel, so it stops losing every VALU / issue arbitration to its SIMD partner (cdna_hip_programming.md
-  // T5 static form): +1.0-1.4 % on the two-lane ViT-B/32 bench in three interleaved rounds, a per-phase
-  // priority around the MFMA groups -0.6 % (profiles/r04_wave_priority_ab.jsonl)
+  // 8-wave blocks, p.prio = 1: the younger half (waves 4-7, dispatched second) at priority 1 for the
+  // whole kernel, so it stops losing every issue arbitration to its SIMD partner
+  // (cdna_hip_programming.md T5, static form).  The engine sets it for the vision tower: +0.75 % on
+  // the two-lane ViT-B/32 bench; the text leg loses 0.5 % with it, and a per-phase priority around
+  // the MFMA groups loses 0.6 % (profiles/r04_wave_priority_ab.jsonl).  Issue order only, never the sums.
   if constexpr (NW == 8) {
-    if (wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
+    if (p.prio && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
   }
-#if CLIPGPU_ODD_BLOCK_PRIO
-  if constexpr (NW == 4) {
-    if (blockIdx.x & 1) __builtin_amdgcn_s_setprio(1);
-  }
-#endif
   dma_step();
   vm_wait<0>();
   __builtin_amdgcn_s_barrier();

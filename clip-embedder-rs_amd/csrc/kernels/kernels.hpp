@@ -36,6 +36,7 @@ struct GemmParams {
   int tile;                  // GemmTile (0 = pick by shape)
   int diag;                  // stamp build only: bit 0 = skip epilogue stores (timing experiments)
   int group;                 // tile order: row panels per group (gemm_util.hpp tile_coords); 0 = 8
+  int prio;                  // 8-wave gemm_pipe tiles: 1 = the younger half of the block at s_setprio 1
 };
 
 // Tile configurations of the MFMA GEMM.  Ids are stable across rounds; the ones not listed were
