@@ -106,6 +106,14 @@ struct Replica {
   hipEvent_t done[4] = {nullptr, nullptr, nullptr, nullptr};  // host path: chunk slot's D2H finished
   hipStream_t copy = nullptr, copy2 = nullptr;  // host path: every H2D, in chunk order (copy2: test hook)
   hipEvent_t copied[4] = {nullptr, nullptr, nullptr, nullptr};  // host path: chunk slot's H2D finished
+  // Host path, second buffer set (run_host_shard): a call of more than max_batch rows alternates
+  // rounds between two sets of input / output staging, so round i + 1's host copy and H2D run under
+  // round i's forward.  Allocated on the first such call (ensure_host_set2).
+  void* in2 = nullptr;
+  void* pin_in2 = nullptr;
+  float* pin_out2 = nullptr;
+  hipEvent_t done2[4] = {nullptr, nullptr, nullptr, nullptr};
+  hipEvent_t copied2[4] = {nullptr, nullptr, nullptr, nullptr};
   // Decoded-image path (clipgpu_embed_images_rgb8): per slot, pinned staging and a device
   // arena of [descriptors | ints | raw RGB8 images], and the resize intermediate.  Grown
   // on demand (images have any size); reused across calls.
@@ -654,6 +662,21 @@ MxGemmParams site_gemm_mx(const clipgpu_engine& e, const Replica& r, const Layer
   return g;
 }
 
+#ifdef CLIPGPU_ABLATE
+// Diagnostic build only (make variant VNAME=ablate VDEFS=-DCLIPGPU_ABLATE; tools/ablate.py): skips
+// trunk ops so that each op's marginal share of the concurrent-lane step can be measured (the
+// numbers are garbage).  Bits: 0 LayerNorm, 1 attention, 2 out_proj, 3 qkv, 4 c_fc, 5 c_proj.
+// The product library has no such switch.
+static unsigned g_ablate = 0;
+#define ABLATED(bit) ((g_ablate >> (bit)) & 1u)
+extern "C" int clipgpu_test_ablate(unsigned mask) {
+  g_ablate = mask;
+  return 0;
+}
+#else
+#define ABLATED(bit) false
+#endif
+
 // Residual rows the head pools from: x at token pos(b) of each sequence (tokens = T), or the
 // compact [B][D] rows the pruned last layer leaves (tokens = 1, pos 0).
 struct PoolSrc {
@@ -696,6 +719,7 @@ PoolSrc trunk(const clipgpu_engine& e, const Replica& r, int B, int causal, cons
     Replica c = r;  // the buffers the tail of this layer runs on
     int rows = B * T;
     auto gemm = [&](int site, int cat, const char* what) {
+      if (ABLATED(site == GS_QKV ? 3 : site == GS_OUT ? 2 : site == GS_FC ? 4 : 5)) return;
       ProfScope ps(e, rows == B * T ? cat : PC_TAIL, st, /*gemm=*/true);
       const bool tuned = 2 * rows > e.tuned_rows;
       if (mx_at(e, l, site)) {
@@ -709,7 +733,7 @@ PoolSrc trunk(const clipgpu_engine& e, const Replica& r, int B, int causal, cons
       check(launch_gemm(e.dt, A_ROWS, site_epi(site), site == GS_FC ? s.act : ACT_NONE, g, st), what);
     };
     gemm(GS_QKV, PC_QKV, "qkv gemm");
-    { ProfScope ps(e, PC_ATTN, st);
+    if (!ABLATED(1)) { ProfScope ps(e, PC_ATTN, st);
       check(launch_attention(e.dt, r.big, r.h, B, T, s.heads, D, causal, st), "attention"); }
     if (compact) {  // pooled rows only from here on (QKV in `big` is dead after attention)
       c.x = (float*)((char*)r.big + prune_off_x(s, B));
@@ -722,13 +746,13 @@ PoolSrc trunk(const clipgpu_engine& e, const Replica& r, int B, int causal, cons
             "gather pooled rows");
     }
     gemm(GS_OUT, PC_OUT_PROJ, "out_proj gemm");
-    {
+    if (!ABLATED(0)) {
       ProfScope ps(e, compact ? PC_TAIL : PC_LN, st);
       check(launch_ln_rows(e.dt, c.x, L.ln2_w, L.ln2_b, s.ln_eps, c.h, rows, D, st, ln_q(e, l, GS_FC, c.hs)), "ln_2");
     }
     gemm(GS_FC, PC_C_FC, "c_fc gemm");
     gemm(GS_PROJ, PC_C_PROJ, "c_proj gemm");
-    if (l + 1 < s.layers) {
+    if (l + 1 < s.layers && !ABLATED(0)) {
       ProfScope ps(e, PC_LN, st);
       check(launch_ln_rows(e.dt, r.x, r.w.layers[l + 1].ln1_w, r.w.layers[l + 1].ln1_b, s.ln_eps, r.h, rows, D, st,
                            ln_q(e, l + 1, GS_QKV, r.hs)), "ln_1");
@@ -1056,7 +1080,7 @@ void run_lanes(const clipgpu_engine& e, const Replica& r, int B, hipStream_t st,
 // legacy null stream, which cannot be captured).  Profiling (per-launch events) and
 // clipgpu_options.graphs = -1 run the body directly.
 template <typename F>
-void run_graph(const clipgpu_engine& e, const Replica& r, const std::vector<uint64_t>& key, hipStream_t st, F body) {
+void run_graph(const clipgpu_engine& e, const Replica& r, const std::vector<uint64_t>& key_in, hipStream_t st, F body) {
   if (!e.graphs || e.prof.mask || !r.graphs) {
     body(st);
     return;
@@ -1066,6 +1090,12 @@ void run_graph(const clipgpu_engine& e, const Replica& r, const std::vector<uint
   hipStream_t gs = own ? st : r.stream;
   GraphCache& gc = *r.graphs;
   hipGraphExec_t exec = nullptr;
+#ifdef CLIPGPU_ABLATE
+  std::vector<uint64_t> key = key_in;
+  key.push_back(0xAB1A7E00u | g_ablate);
+#else
+  const std::vector<uint64_t>& key = key_in;
+#endif
   ++gc.clock;
   for (auto& en : gc.entries)
     if (en.key == key) {
@@ -1262,6 +1292,19 @@ std::vector<int> host_chunks(const clipgpu_engine& e, InKind kind) {
   return part;
 }
 
+// The second host-path buffer set of a replica (multi-round host calls), allocated once.
+void ensure_host_set2(const clipgpu_engine& e, Replica& r) {
+  if (r.in2) return;
+  const size_t B = (size_t)((e.max_batch + e.lanes - 1) / e.lanes * e.lanes);
+  HIP_CHECK(hipMalloc(&r.in2, B * e.in_bytes_per_row));
+  HIP_CHECK(hipHostMalloc(&r.pin_in2, B * e.in_bytes_per_row, hipHostMallocDefault));
+  HIP_CHECK(hipHostMalloc((void**)&r.pin_out2, B * (size_t)e.spec.embed_dim * 4, hipHostMallocDefault));
+  for (int i = 0; i < 4; ++i) {
+    HIP_CHECK(hipEventCreateWithFlags(&r.done2[i], hipEventDisableTiming));
+    HIP_CHECK(hipEventCreateWithFlags(&r.copied2[i], hipEventDisableTiming));
+  }
+}
+
 // Host-buffer forward over a row range of one replica.  Each round of up to max_batch rows is cut
 // by host_chunks' partition; chunk k of a round uses rows [part[k], part[k + 1]) of the
 // max_batch-row device buffers, workspace (lane_view) and pinned staging, so chunks of one round
@@ -1271,6 +1314,11 @@ std::vector<int> host_chunks(const clipgpu_engine& e, InKind kind) {
 // transfer of chunk k + 1 overlaps the forward of chunk k, and forwards of different lanes
 // overlap each other.  Inputs are staged through pinned memory (par_memcpy) or DMA'd straight
 // from a caller-registered range (clipgpu_host_register); outputs likewise.
+// A range of more than max_batch rows alternates its rounds between two buffer sets (device input
+// rows, pinned staging, events): round i's host copy and H2D are issued while round i - 1's forward
+// runs, and a set is reused two rounds later, after its round's D2H event -- so every round but the
+// first starts its forward with its input already on the device.  Each round
+// runs the same forward on the same rows as a call of its own: the outputs are bit-identical.
 void run_host_shard(clipgpu_engine& e, Replica& r, InKind kind, const void* in, size_t in_row_bytes, int64_t b0,
                     int64_t b1, const float* mean, const float* stdv, float* out, int tokens = 0) {
   HIP_CHECK(hipSetDevice(r.device));
@@ -1279,15 +1327,26 @@ void run_host_shard(clipgpu_engine& e, Replica& r, InKind kind, const void* in, 
   const bool direct_out = host_registered(out + b0 * E, (size_t)(b1 - b0) * E * 4);
   const std::vector<int> part = host_chunks(e, kind);
   const int C = (int)part.size() - 1;
+  const bool two_sets = b1 - b0 > MB;
+  if (two_sets) ensure_host_set2(e, r);
   struct Pending { int64_t c0 = -1; int n = 0; };
-  Pending pend[4];
-  auto drain = [&](int k) {
-    if (pend[k].c0 < 0) return;
-    HIP_CHECK(hipEventSynchronize(r.done[k]));
-    if (!direct_out) std::memcpy(out + pend[k].c0 * E, r.pin_out + (size_t)part[k] * E, (size_t)pend[k].n * E * 4);
-    pend[k].c0 = -1;
+  Pending pend[2][4];
+  float* const pin_out_set[2] = {r.pin_out, r.pin_out2};
+  hipEvent_t* const done_set[2] = {r.done, r.done2};
+  auto drain = [&](int set, int k) {
+    if (pend[set][k].c0 < 0) return;
+    HIP_CHECK(hipEventSynchronize(done_set[set][k]));
+    if (!direct_out)
+      std::memcpy(out + pend[set][k].c0 * E, pin_out_set[set] + (size_t)part[k] * E, (size_t)pend[set][k].n * E * 4);
+    pend[set][k].c0 = -1;
   };
-  for (int64_t c0 = b0; c0 < b1;) {
+  int round = 0;
+  for (int64_t c0 = b0; c0 < b1; ++round) {
+    const int set = two_sets ? (round & 1) : 0;
+    char* const in_base = (char*)(set ? r.in2 : r.in);
+    char* const pin_in_base = (char*)(set ? r.pin_in2 : r.pin_in);
+    hipEvent_t* const done = set ? r.done2 : r.done;
+    hipEvent_t* const copied = set ? r.copied2 : r.copied;
     const int R = (int)std::min<int64_t>(MB, b1 - c0);  // rows of this round
     int off = 0;
     for (int k = 0; k < C && off < R; ++k) {
@@ -1299,13 +1358,13 @@ void run_host_shard(clipgpu_engine& e, Replica& r, InKind kind, const void* in, 
       n = std::max(0, std::min(n, cap));
       if (n == 0) continue;
       const int64_t rc = c0 + off;
-      drain(k);
+      drain(set, k);  // this set's round before last: its D2H (so also its H2D and forward) done
       hipStream_t st = r.lane[k % L] ? r.lane[k % L] : r.stream;
-      char* din = (char*)r.in + (size_t)part[k] * in_row_bytes;
+      char* din = in_base + (size_t)part[k] * in_row_bytes;
       float* dout = r.out + (size_t)part[k] * E;
       const char* src = (const char*)in + rc * in_row_bytes;
       if (!direct_in) {
-        char* pin = (char*)r.pin_in + (size_t)part[k] * in_row_bytes;
+        char* pin = pin_in_base + (size_t)part[k] * in_row_bytes;
         par_memcpy(pin, src, (size_t)n * in_row_bytes);
         src = pin;
       }
@@ -1318,44 +1377,45 @@ void run_host_shard(clipgpu_engine& e, Replica& r, InKind kind, const void* in, 
       if (mapped != nullptr && (((uintptr_t)src | (uintptr_t)din | ((size_t)n * in_row_bytes)) & 15) == 0) {
         // test hook: pull the chunk through the host mapping with a copy kernel on the copy stream
         check(launch_pull_copy(mapped, din, (size_t)n * in_row_bytes, r.copy), "pull copy");
-        HIP_CHECK(hipEventRecord(r.copied[k], r.copy));
-        HIP_CHECK(hipStreamWaitEvent(st, r.copied[k], 0));
+        HIP_CHECK(hipEventRecord(copied[k], r.copy));
+        HIP_CHECK(hipStreamWaitEvent(st, copied[k], 0));
       } else if (e.host_copy_stream == 2 && n >= 2) {  // test hook: the chunk's halves on two copy streams
         const size_t h = (size_t)(n / 2) * in_row_bytes, all = (size_t)n * in_row_bytes;
-        HIP_CHECK(hipStreamWaitEvent(r.copy2, r.copied[(k + C - 1) % C], 0));  // chunk order kept
+        HIP_CHECK(hipStreamWaitEvent(r.copy2, copied[(k + C - 1) % C], 0));  // chunk order kept
         HIP_CHECK(hipMemcpyAsync(din, src, h, hipMemcpyHostToDevice, r.copy));
         HIP_CHECK(hipMemcpyAsync(din + h, src + h, all - h, hipMemcpyHostToDevice, r.copy2));
-        HIP_CHECK(hipEventRecord(r.copied[k], r.copy2));
-        HIP_CHECK(hipStreamWaitEvent(r.copy, r.copied[k], 0));
-        HIP_CHECK(hipEventRecord(r.copied[k], r.copy));
-        HIP_CHECK(hipStreamWaitEvent(st, r.copied[k], 0));
+        HIP_CHECK(hipEventRecord(copied[k], r.copy2));
+        HIP_CHECK(hipStreamWaitEvent(r.copy, copied[k], 0));
+        HIP_CHECK(hipEventRecord(copied[k], r.copy));
+        HIP_CHECK(hipStreamWaitEvent(st, copied[k], 0));
       } else if (e.host_copy_stream) {
         HIP_CHECK(hipMemcpyAsync(din, src, (size_t)n * in_row_bytes, hipMemcpyHostToDevice, r.copy));
-        HIP_CHECK(hipEventRecord(r.copied[k], r.copy));
-        HIP_CHECK(hipStreamWaitEvent(st, r.copied[k], 0));
+        HIP_CHECK(hipEventRecord(copied[k], r.copy));
+        HIP_CHECK(hipStreamWaitEvent(st, copied[k], 0));
       } else {
         HIP_CHECK(hipMemcpyAsync(din, src, (size_t)n * in_row_bytes, hipMemcpyHostToDevice, st));
       }
       const Replica v = lane_view(e, r, part[k]);
       run_graph(e, r,
                 {(uint64_t)(10 + kind), (uint64_t)k, (uint64_t)n, fbits(mean, 0), fbits(mean, 1), fbits(mean, 2),
-                 fbits(stdv, 0), fbits(stdv, 1), fbits(stdv, 2), (uint64_t)tokens, (uint64_t)part[k]},
+                 fbits(stdv, 0), fbits(stdv, 1), fbits(stdv, 2), (uint64_t)tokens, (uint64_t)part[k], (uint64_t)set},
                 st, [&](hipStream_t gs) {
                   if (kind == IN_IDS)
                     text_forward(e, v, (const int64_t*)din, n, dout, gs, tokens);
                   else
                     vision_forward(e, v, din, kind == IN_F32 ? A_IMG_F32 : A_IMG_U8, mean, stdv, n, dout, gs);
                 });
-      float* dst = direct_out ? out + rc * E : r.pin_out + (size_t)part[k] * E;
+      float* dst = direct_out ? out + rc * E : pin_out_set[set] + (size_t)part[k] * E;
       HIP_CHECK(hipMemcpyAsync(dst, dout, (size_t)n * E * 4, hipMemcpyDeviceToHost, st));
-      HIP_CHECK(hipEventRecord(r.done[k], st));
-      pend[k].c0 = rc;
-      pend[k].n = n;
+      HIP_CHECK(hipEventRecord(done[k], st));
+      pend[set][k].c0 = rc;
+      pend[set][k].n = n;
       off += n;
     }
     c0 += R;
   }
-  for (int k = 0; k < C; ++k) drain(k);
+  for (int set = 0; set < 2; ++set)
+    for (int k = 0; k < C; ++k) drain(set, k);
 }
 
 void run_host(clipgpu_engine& e, InKind kind, const void* in, size_t in_row_bytes, int64_t B, const float* mean,
@@ -1676,6 +1736,9 @@ void destroy_replica(Replica& r) {
   if (r.work) (void)hipFree(r.work);
   if (r.pin_in) (void)hipHostFree(r.pin_in);
   if (r.pin_out) (void)hipHostFree(r.pin_out);
+  if (r.in2) (void)hipFree(r.in2);
+  if (r.pin_in2) (void)hipHostFree(r.pin_in2);
+  if (r.pin_out2) (void)hipHostFree(r.pin_out2);
   if (r.stream) (void)hipStreamDestroy(r.stream);
   if (r.copy) (void)hipStreamDestroy(r.copy);
   if (r.copy2) (void)hipStreamDestroy(r.copy2);
@@ -1684,6 +1747,8 @@ void destroy_replica(Replica& r) {
     if (r.join[i]) (void)hipEventDestroy(r.join[i]);
     if (r.done[i]) (void)hipEventDestroy(r.done[i]);
     if (r.copied[i]) (void)hipEventDestroy(r.copied[i]);
+    if (r.done2[i]) (void)hipEventDestroy(r.done2[i]);
+    if (r.copied2[i]) (void)hipEventDestroy(r.copied2[i]);
   }
   if (r.fork) (void)hipEventDestroy(r.fork);
   if (r.gin) (void)hipEventDestroy(r.gin);
@@ -1732,7 +1797,9 @@ int clipgpu_create_ex(const char* model_dir, int tower, const int* device_ids, i
     std::memset(&opts, 0, sizeof(opts));
     opts.struct_size = sizeof(opts);
     if (opts_in) {  // an older caller's smaller struct: its prefix, defaults for the rest
-      if (opts_in->struct_size < 2 * sizeof(uint32_t) || opts_in->struct_size > sizeof(opts))
+      // the sizes of the struct's published versions only: v2 (through `communicator`) and v3 (ADVICE r4:
+      // a size ending inside a field would copy part of it)
+      if (opts_in->struct_size != offsetof(clipgpu_options, graphs) && opts_in->struct_size != sizeof(opts))
         throw ClipErr(CLIPGPU_ERR_INVALID, "clipgpu_options.struct_size: call clipgpu_options_init first");
       std::memcpy(&opts, opts_in, opts_in->struct_size);
     }
@@ -1782,6 +1849,9 @@ int clipgpu_create_ex(const char* model_dir, int tower, const int* device_ids, i
       e->mx_site[GS_PROJ] = (bits & CLIPGPU_MX_PROJ) != 0;
       if (e->mx_site[GS_PROJ] && !e->mx_site[GS_FC])
         throw ClipErr(CLIPGPU_ERR_INVALID, "MX sites: proj in MX needs fc in MX");
+      if (e->spec.layers < 32 && (opts.mx_layers >> e->spec.layers) != 0)
+        throw ClipErr(CLIPGPU_ERR_INVALID, "clipgpu_options.mx_layers: bit set at or beyond the tower's " +
+                                               std::to_string(e->spec.layers) + " layers");
       e->mx_layers = opts.mx_layers ? (uint64_t)opts.mx_layers : ~0ull;
     } else if (opts.mx_sites) {
       throw ClipErr(CLIPGPU_ERR_INVALID, "clipgpu_options.mx_sites needs dtype CLIPGPU_DTYPE_FP8");
@@ -1855,8 +1925,10 @@ int clipgpu_create_ex(const char* model_dir, int tower, const int* device_ids, i
     // = device_ids[i]; RCCL refuses two ranks on one GPU, so a handle that lists a device twice
     // keeps the host-buffer sharding and has no collective entry points).  It is created on the
     // first gathered call (ensure_comm) unless the options ask for it now: creation and the
-    // host-buffer entry points never depend on RCCL.
-    bool distinct = devs.size() > 1;
+    // host-buffer entry points never depend on RCCL.  A one-device handle gets a one-rank clique
+    // through the same code when clipgpu_options.communicator = 1 asks for one (else it joins a
+    // deployment's communicator with clipgpu_comm_init_rank).
+    bool distinct = devs.size() > 1 || (devs.size() == 1 && opts.communicator == 1);
     for (size_t i = 0; i < devs.size() && distinct; ++i)
       for (size_t j = i + 1; j < devs.size(); ++j) distinct = distinct && devs[i] != devs[j];
     if (distinct) {
@@ -2235,6 +2307,25 @@ int clipgpu_test_force_broadcast(clipgpu_engine* e, int on) {
     if (!e) throw ClipErr(CLIPGPU_ERR_INVALID, "engine is NULL");
     std::lock_guard<std::mutex> lk(e->mu);
     e->force_bcast = on != 0;
+  });
+}
+
+// A handle without a communicator takes the multi-device handle's lazy path: its own clique over its
+// replicas' (distinct) devices, created by ensure_comm on the first gathered call.
+int clipgpu_test_comm_lazy(clipgpu_engine* e) {
+  return guarded([&]() {
+    if (!e) throw ClipErr(CLIPGPU_ERR_INVALID, "NULL handle");
+    if (e->comm_nranks > 0) throw ClipErr(CLIPGPU_ERR_INVALID, "the handle already has a communicator");
+    std::vector<int> devs;
+    for (auto& r : e->reps) {
+      for (int d : devs)
+        if (d == r.device) throw ClipErr(CLIPGPU_ERR_INVALID, "a device listed twice has no clique");
+      devs.push_back(r.device);
+    }
+    e->comm_devs = devs;
+    e->comm_pending = true;
+    e->comm_nranks = (int)devs.size();
+    e->comm_rank0 = 0;
   });
 }
 

@@ -562,7 +562,9 @@ void bpe_word(const clipgpu_tokenizer& t, const std::string& word_bytes, std::ve
   if (t.ignore_merges) {
     std::string whole;
     for (auto& c : chars) whole += c;
-    const int64_t id = lookup(t, whole + t.eow);
+    // tokenizers' BPE::tokenize_with_cache looks up the bare word, without end_of_word_suffix
+    // (as bpe_chars does; test_ignore_merges_looks_up_the_bare_word)
+    const int64_t id = lookup(t, whole);
     if (id >= 0) { out.push_back(id); return; }
   }
   std::vector<Sym> syms;

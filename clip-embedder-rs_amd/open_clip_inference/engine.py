@@ -86,7 +86,12 @@ class Engine:
         opts.patch_tile = int(patch_tile)
         if mx_layers is not None:
             if not isinstance(mx_layers, int):
-                mx_layers = sum(1 << int(l) for l in mx_layers)
+                layers = [int(l) for l in mx_layers]
+                if any(l < 0 or l >= 32 for l in layers):
+                    raise ValueError("mx_layers: layer indices 0..31 (clipgpu_options.mx_layers is a 32-bit mask)")
+                mx_layers = sum(1 << l for l in set(layers))
+            if mx_layers < 0 or mx_layers > 0xFFFFFFFF:
+                raise ValueError("mx_layers: a 32-bit layer mask (clipgpu_options.mx_layers)")
             if mx_layers == 0:
                 raise ValueError("mx_layers: at least one layer (None = every layer)")
             opts.mx_layers = int(mx_layers)

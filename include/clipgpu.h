@@ -66,7 +66,12 @@ const char* clipgpu_build_source_hash(void);
  * {"seed": N} (seeded weights).
  * device_ids/n_devices: the GPUs this handle replicates the weights onto (data-parallel
  * batch sharding across them); NULL/0 = device 0.  max_batch: rows per device per launch
- * (larger batches are processed in chunks). */
+ * (larger batches are processed in chunks).
+ * Speed (never the output bits): the GEMM tiles and lane count come from a table measured on
+ * MI355X (engine.hip table_tiles / table_lanes) for one lane's token rows at max_batch: the
+ * measured regimes are >= 2048 rows per lane (ViT-B/32 vision 256, text 1024, SO400M 128, H/14
+ * 64 per GPU); smaller max_batch uses the shape heuristic (skinny kernel at <= 256 rows), and
+ * clipgpu_options.tuning = 1 times the candidates at creation for any other batch. */
 int clipgpu_create(const char* model_dir, int tower, const int* device_ids, int n_devices, int dtype,
                    int max_batch, clipgpu_engine** out);
 void clipgpu_destroy(clipgpu_engine* e);
@@ -102,7 +107,9 @@ typedef struct clipgpu_options {
                            builds (csrc/kernels/kernels.hpp kGemmTiles; speed only, never the bits) */
   int32_t patch_tile;   /* the vision patch-embedding GEMM's tile, as gemm_tiles */
   uint32_t mx_layers;   /* fp8 engines: bit l set = layer l runs its MX sites in MX-fp8, the other layers
-                           run every GEMM in bf16; 0 = every layer (default) */
+                           run every GEMM in bf16; 0 = every layer (default).  Layers 0..31 only (a
+                           tower's layers >= 32 run bf16 under a non-zero mask); a bit at or beyond the
+                           tower's layer count is refused (CLIPGPU_ERR_INVALID) */
 } clipgpu_options;
 /* Fills *opts with the defaults. */
 int clipgpu_options_init(clipgpu_options* opts);

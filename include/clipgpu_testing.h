@@ -122,6 +122,9 @@ int clipgpu_test_host_plan(struct clipgpu_engine* e, int n_chunks, const int* bo
 /* Gathered calls of this handle take the ragged branch (one ncclBroadcast per block) even when
  * every block has the same size (on != 0), so a one-rank or equal-shard run exercises it. */
 int clipgpu_test_force_broadcast(struct clipgpu_engine* e, int on);
+/* A handle without a communicator takes the multi-device handle's lazy path: a clique over its
+ * replicas' distinct devices, created (ncclCommInitAll) by the first gathered call. */
+int clipgpu_test_comm_lazy(struct clipgpu_engine* e);
 /* The host-side plan of a gathered call (no GPU): off[0..nranks] = first output row of each rank's
  * block (off[nranks] = total rows), *equal = 1 when every block has the same size.  Errors as the
  * gathered entry points: a negative count, or zero rows in all ("Empty batch"). */

@@ -253,6 +253,18 @@ def test_options_init_and_validation():
     devs = (ctypes.c_int * 1)(0)
     rc = _lib.lib().clipgpu_create_ex(d.encode(), 0, devs, 1, 0, 8, ctypes.byref(o), ctypes.byref(h))
     assert rc != 0 and b"struct_size" in _lib.lib().clipgpu_last_error()
+    # only the published struct sizes (v2: through `communicator`; v3): not one ending inside a field
+    for bad in (Options.graphs.offset + 2, ctypes.sizeof(Options) - 4, 8):
+        o.struct_size = bad
+        rc = _lib.lib().clipgpu_create_ex(d.encode(), 0, devs, 1, 0, 8, ctypes.byref(o), ctypes.byref(h))
+        assert rc != 0 and b"struct_size" in _lib.lib().clipgpu_last_error(), bad
+    # mx_layers: a 32-bit mask (Python refuses layer 32+, the library bits beyond the tower's layers)
+    for bad in ([32], [40], [0, 33], 1 << 32):
+        with pytest.raises(ValueError, match="mx_layers"):
+            Engine(d, 0, [0], "fp8", 8, mx_layers=bad)
+    tiny_layers = json.load(open(os.path.join(d, "open_clip_config.json")))["model_cfg"]["vision_cfg"]["layers"]
+    with pytest.raises(ClipError, match="beyond the tower"):
+        Engine(d, 0, [0], "fp8", 8, mx_layers=[tiny_layers])
 
 
 @pytest.mark.parametrize("rows,off,equal", [([256, 256], [0, 256, 512], 1),

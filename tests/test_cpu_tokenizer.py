@@ -155,3 +155,31 @@ def test_cpp_sentencepiece_bpe_matches_tokenizers_live_fuzz(name):
         assert mask.tolist() == [e.attention_mask for e in enc]
 
     check()
+
+
+def test_ignore_merges_looks_up_the_bare_word(tmp_path):
+    """Byte-level BPE with ignore_merges and an end_of_word_suffix: a word found in the vocab as is
+    (without the suffix) is one token, whatever the merges would make of it (tokenizers 0.22.2
+    BPE::tokenize_with_cache; ADVICE r4).  The CLIP-structured synthetic file with ignore_merges on
+    and bare-word entries added, live against the wheel."""
+    tokenizers = pytest.importorskip("tokenizers")
+    from open_clip_inference.engine import Tokenizer
+    with open(TOK, encoding="utf-8") as f:
+        tj = json.load(f)
+    vocab = tj["model"]["vocab"]
+    added = ["photo", "zebra", "xq"]  # bare (suffix-less) entries
+    for w in added:
+        vocab.setdefault(w, max(vocab.values()) + 1)
+    tj["model"]["ignore_merges"] = True
+    path = str(tmp_path / "tokenizer.json")
+    with open(path, "w", encoding="utf-8") as f:
+        json.dump(tj, f)
+    ref = tokenizers.Tokenizer.from_file(path)
+    ref.enable_padding(length=24, pad_id=0)
+    ref.enable_truncation(max_length=24)
+    texts = ["a photo of a zebra", "photo", "xq xqq photos", "the zebra's photo", "a photograph"]
+    enc = ref.encode_batch(texts)
+    assert vocab["photo"] in enc[1].ids  # the wheel takes the bare entry
+    ids, mask = Tokenizer(path, 24, 0).encode_batch(texts)
+    assert ids.tolist() == [e.ids for e in enc]
+    assert mask.tolist() == [e.attention_mask for e in enc]

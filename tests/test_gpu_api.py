@@ -305,6 +305,102 @@ def test_rccl_communicator_and_gathered_entry_points(monkeypatch):
     assert multi.comm_info() == (0, 0)
 
 
+def test_multi_round_host_calls_alternate_buffer_sets_bit_exactly():
+    """A host-buffer call of more than max_batch rows runs its rounds on two alternating staging sets
+    (engine.hip run_host_shard: round i + 1's H2D under round i's forward).  Every
+    round must equal the same rows embedded by a call of their own, bit for bit: u8 and f32 pixels
+    and token ids, pageable and caller-registered buffers, a ragged last round, and a second
+    multi-round call (graph replay on both sets)."""
+    from oracle.model_spec import VIT_B_32_CFG
+    from open_clip_inference.engine import Engine, host_register, host_unregister
+    from tests.helpers import normalized_pixels
+    d = make_model_dir(VIT_B_32_CFG, seed=1234)
+    v = vision_spec_from_cfg(VIT_B_32_CFG["model_cfg"])
+    t = text_spec_from_cfg(VIT_B_32_CFG["model_cfg"])
+    MB, B = 16, 71  # 5 rounds, the last one of 7 rows
+    u8 = weights.synth_images_u8(21, B, v.image_size)
+    px = normalized_pixels(u8, OPENAI_MEAN, OPENAI_STD)
+    ids = weights.synth_token_ids(21, B, t.context_length, t.vocab_size, t.vocab_size - 2, t.vocab_size - 1,
+                                  random_eot=True)
+    ve = Engine(d, 0, [0], "bf16", MB)
+    te = Engine(d, 1, [0], "bf16", MB)
+    calls = {"u8": (ve, lambda e, x, out=None: e.embed_u8(x, OPENAI_MEAN, OPENAI_STD, out=out), u8),
+             "f32": (ve, lambda e, x, out=None: e.embed_pixels(x, out=out), px),
+             "ids": (te, lambda e, x, out=None: e.embed_tokens(x, out=out), ids)}
+    for name, (e, fn, x) in calls.items():
+        ref = np.concatenate([fn(e, x[i:i + MB]) for i in range(0, B, MB)])
+        for registered in (False, True):
+            xin = np.ascontiguousarray(x)
+            out = np.full((B, 512), np.nan, np.float32)
+            if registered:
+                host_register(xin)
+                host_register(out)
+            try:
+                for _ in range(2):
+                    out.fill(np.nan)
+                    fn(e, xin, out=out)
+                    assert np.array_equal(out, ref), (name, registered)
+            finally:
+                if registered:
+                    host_unregister(xin)
+                    host_unregister(out)
+    ve.close()
+    te.close()
+
+
+def test_one_device_clique_runs_the_multi_device_comm_path():
+    """The multi-device handle's own communicator code on the one-GPU box: a
+    one-device handle with clipgpu_options.communicator = 1 builds a one-rank clique through
+    ensure_comm (ncclCommInitAll at creation), and one given the multi-device handle's lazy path
+    (clipgpu_test_comm_lazy) builds it inside sharded_gather on its first gathered call.  The
+    gathered calls equal the plain device entry point bit for bit; each handle is then destroyed
+    while its last collective is still queued behind a busy caller stream (a created stream, and
+    the legacy default stream through a NULL streams array): destroy_comms waits for
+    the collective's event before the grouped ncclCommFinalize, so the output is complete."""
+    import torch
+    from oracle.model_spec import VIT_B_32_CFG
+    from open_clip_inference import _lib
+    from open_clip_inference.engine import Engine
+    from tests.helpers import normalized_pixels
+    d = make_model_dir(VIT_B_32_CFG, seed=1234)
+    v = vision_spec_from_cfg(VIT_B_32_CFG["model_cfg"])
+    t = text_spec_from_cfg(VIT_B_32_CFG["model_cfg"])
+    B = 24
+    for tower, lazy in ((0, False), (1, True), (0, True), (1, False)):
+        if tower == 0:
+            x = normalized_pixels(weights.synth_images_u8(13, B, v.image_size), OPENAI_MEAN, OPENAI_STD)
+        else:
+            x = weights.synth_token_ids(13, B, t.context_length, t.vocab_size, t.vocab_size - 2, t.vocab_size - 1,
+                                        random_eot=True)
+        plain = Engine(d, tower, [0], "bf16", 16)
+        ref = plain.embed_pixels(x) if tower == 0 else plain.embed_tokens(x)
+        plain.close()
+        if lazy:
+            e = Engine(d, tower, [0], "bf16", 16)
+            assert e.comm_info() == (0, 0)
+            _lib.check(_lib.lib().clipgpu_test_comm_lazy(e.handle))
+        else:
+            e = Engine(d, tower, [0], "bf16", 16, communicator=True)
+        assert e.comm_info() == (1, 0)
+        d_in = torch.from_numpy(x).cuda()
+        gather = e.embed_pixels_gather_device if tower == 0 else e.embed_tokens_gather_device
+        out = torch.full((B, 512), float("nan"), device="cuda")
+        side = torch.cuda.Stream()
+        gather([d_in.data_ptr()], [B], [out.data_ptr()], [side.cuda_stream])  # the lazy clique is built here
+        side.synchronize()
+        assert np.array_equal(out.cpu().numpy(), ref)
+        # destroy with the collective still queued: behind ~50 ms of spinning on the caller's stream
+        out2 = torch.full((B, 512), float("nan"), device="cuda")
+        null_array = tower == 1
+        busy = torch.cuda.default_stream() if null_array else side
+        with torch.cuda.stream(busy):
+            torch.cuda._sleep(100_000_000)
+        gather([d_in.data_ptr()], [B], [out2.data_ptr()], None if null_array else [side.cuda_stream])
+        e.close()
+        torch.cuda.synchronize()
+        assert np.array_equal(out2.cpu().numpy(), ref)
+
+
 def test_tile_table_is_deterministic_and_bit_invisible():
     """The default tile choice is the committed table (engine.hip table_tiles): two engines of
     the bench's configuration pick the same tiles and lanes on any box (vision at 256 images: two

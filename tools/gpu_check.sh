@@ -1,5 +1,7 @@
 #!/bin/bash
-# One GPU session: kernel + parity tests, smoke, bench, rocprofv3 kernel-trace summary.
+# One GPU session, parameterised by STEPS (the steps below, in order; e.g.
+#   STEPS="bench_quick ablate" bash tools/gpu_check.sh
+# ): kernel + parity tests, smoke, bench, rocprofv3 kernel-trace summary, PMC passes, A/B runs.
 # Every GPU step has its own time limit; a crash / timeout (exit >= 2 for pytest,
 # != 0 for the others) ends the script.  Output goes to gpurun_out/.
 set -u
@@ -37,6 +39,12 @@ for s in $STEPS; do
     bench_pin)  # the vision leg with PIN_TILES pinned (q,o,f,p), BENCH_PIN_ARGS extra bench args
       run bench_pin_${PIN_TILES//,/_} 300 python bench.py --steps 20 --warmup 5 --tiles $PIN_TILES \
           --no-cpu-baseline --no-fp8 --no-text --no-e2e ${BENCH_PIN_ARGS:-} || exit $? ;;
+    ablate)  # marginal step time of each trunk op (tools/ablate.py; needs lib/libclipgpu_ablate.so:
+             # make variant VNAME=ablate VDEFS=-DCLIPGPU_ABLATE)
+      CLIPGPU_LIB=$PWD/clip-embedder-rs_amd/lib/libclipgpu_ablate.so run ablate 600 python tools/ablate.py || exit $?
+      cp gpurun_out/ablate.log gpurun_out/ablate.jsonl ;;
+    bench_quick)  # the bench without the CPU leg
+      run bench_quick 400 python bench.py --steps 20 --warmup 5 --no-cpu-baseline || exit $? ;;
     smoke)
       run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
     bench)
