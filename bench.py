@@ -421,11 +421,11 @@ def main():
         else:
             ve.embed_pixels_device(px.data_ptr(), B_VISION, out.data_ptr(), stream.cuda_stream)
 
-    def timed(step, steps, warmup, prof_engine=None, prof_cats=None):
+    def timed(step, steps, warmup, prof_engine=None, prof_cats=None, concurrent=False):
         for _ in range(warmup):
             step()
         if prof_engine is not None:
-            profile_enable(prof_engine, list(prof_cats))
+            profile_enable(prof_engine, list(prof_cats), concurrent=concurrent)
         if dp:
             dist.barrier()
         torch.cuda.synchronize()
@@ -468,6 +468,9 @@ def main():
     psteps = max(3, args.steps // 2)
     _, site_prof = timed(vision_step, psteps, 1, ve, SITE_SHAPES)
     fc_ms, fc_n = site_prof["c_fc"]
+    # The same launches timed in the timed step's regime: both lanes running (CLIPGPU_PROFILE_CONCURRENT:
+    # no serialization, no graph replay), each GEMM's event pair at its own kernel boundaries.
+    _, site_prof_cc = timed(vision_step, psteps, 1, ve, SITE_SHAPES, concurrent=True)
     windows = None
     if world == 1 and args.windows > 0:
         windows = measure_windows(vision_step, ve, args.windows, args.steps, dt, dev)
@@ -483,9 +486,25 @@ def main():
         rows = B_VISION * 50 * (12 if site == "qkv" else fc_layers) * psteps / max(n, 1)
         avg_s = (ms / 1e3) / max(n, 1)
         tf = 2.0 * rows * N * K / avg_s / 1e12 if n else 0.0
+        # blocks per launch (the launcher's persistent grid) and the CU-time view: a launch holds
+        # min(blocks, CUs) CUs for its duration beside the other lane; cu_frac = FLOPs / (that CU time x
+        # the per-CU peak), i.e. frac x CUs / min(CUs, blocks) on the concurrent duration
+        grid = ctypes.c_int()
+        _lib.check(_lib.lib().clipgpu_test_gemm_grid(int(tiles[list(SITE_SHAPES).index(site)]), int(rows), N, K,
+                                                     ctypes.byref(grid)))
+        cus = torch.cuda.get_device_properties(dev).multi_processor_count
+        held = min(grid.value, cus)
+        ms_cc, n_cc = site_prof_cc[site]
+        avg_cc = (ms_cc / 1e3) / max(n_cc, 1)
+        tf_cc = 2.0 * rows * N * K / avg_cc / 1e12 if n_cc else 0.0
         sites[site] = {"shape": f"{int(rows)}x{N}x{K}", "rows_per_launch": int(rows), "tile": gemm_tiles[site],
                        "avg_launch_us": round(avg_s * 1e6, 2), "us_per_step": round(ms * 1e3 / psteps, 1),
-                       "tflops": round(tf, 1), "frac": round(tf / peak, 4)}
+                       "tflops": round(tf, 1), "frac": round(tf / peak, 4),
+                       "blocks": grid.value, "cus_held": held,
+                       "concurrent": {"avg_launch_us": round(avg_cc * 1e6, 2), "tflops": round(tf_cc, 1),
+                                      "frac": round(tf_cc / peak, 4),
+                                      "cu_us_per_step": round(ms_cc * 1e3 / psteps * held / cus, 1),
+                                      "cu_frac": round(tf_cc / peak * cus / held, 4)}}
     dom = max(sites, key=lambda k: sites[k]["us_per_step"])
     fc_rows_per_launch = sites["c_fc"]["rows_per_launch"]
     whole_tflops = vit_flops(B_VISION, executed=True) * args.steps / dt / 1e12 / 1.0
@@ -638,9 +657,17 @@ def main():
                          "achieved": sites[dom]["tflops"], "peak": peak, "unit": "TFLOP/s",
                          "frac": sites[dom]["frac"], "traffic": traffic,
                          "traffic_source": traffic_src,
-                         "launches_timed": site_prof[dom][1], "avg_launch_us": sites[dom]["avg_launch_us"]},
+                         "launches_timed": site_prof[dom][1], "avg_launch_us": sites[dom]["avg_launch_us"],
+                         "blocks": sites[dom]["blocks"],
+                         "cu_frac": sites[dom]["concurrent"]["cu_frac"],
+                         "cu_frac_note": "the same launches timed with both lanes running (CLIPGPU_PROFILE_CONCURRENT): "
+                                         "FLOPs / (launch time x min(blocks, CUs) x the per-CU share of the peak); "
+                                         "achieved / frac are the lanes-serialized launch (as rocprofv3 traces it)"},
+            "gemm_cu_us_per_step": round(sum(v["concurrent"]["cu_us_per_step"] for v in sites.values()), 1),
             "gemm_sites": dict(sites, note="per-launch HIP-event times of each trunk GEMM site in a profiled pass "
-                                           "(lanes serialized); us_per_step sums the site's launches"),
+                                           "(lanes serialized); us_per_step sums the site's launches; concurrent: the "
+                                           "same with both lanes running, cu_us_per_step = its launches' time x "
+                                           "min(blocks, CUs) / CUs (the CU time the site takes per step)"),
             "gemm_tiles": gemm_tiles,
             "gemm_tiles_env": ",".join(str(t) for t in tiles),
             "lanes_env": dev_lanes.value,

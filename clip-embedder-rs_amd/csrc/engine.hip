@@ -1055,7 +1055,10 @@ inline int lanes_for(const clipgpu_engine& e, int B) {
 template <typename F>
 void run_lanes(const clipgpu_engine& e, const Replica& r, int B, hipStream_t st, F fwd) {
   const int L = lanes_for(e, B);
-  if (L == 1 || e.prof.mask) {
+  // profiling serializes the lanes (each event pair times one kernel alone), unless the mask asks
+  // for the concurrent regime (CLIPGPU_PROFILE_CONCURRENT)
+  const bool serial = e.prof.mask != 0 && !(e.prof.mask & CLIPGPU_PROFILE_CONCURRENT);
+  if (L == 1 || serial) {
     for (int i = 0; i < L; ++i) {
       int b0, b1;
       lane_range(B, L, i, b0, b1);

@@ -964,30 +964,52 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
   GEMM_STAMP_REAL(63);
 }
 
+// Persistent grids (the launchers below and gemm_grid use these, so the bench's per-site block counts
+// are the launches' own).
+inline int cfg_grid(int BM, int BN, int NW, int M, int N) {
+  const int ntiles = ((N + BN - 1) / BN) * ((M + BM - 1) / BM);
+  // resident blocks: one 8-wave block (96-128 KiB LDS) or two 4-wave blocks (64 KiB) per CU
+  const int resident = device_cus() * (NW == 4 ? 2 : 1);
+  return ntiles <= resident ? ntiles : resident;
+}
+// OCC: resident blocks per CU the tile's registers allow (4-wave tiles: up to 3 by LDS; 8-wave
+// tiles: 1, or 2 when built for 4 waves per SIMD).  2 LDS stages.
+constexpr int pipe_kocc(int NW, int OCC) { return NW == 8 ? (OCC >= 2 ? 2 : 1) : 2; }  // launch bounds' OCC
+inline int pipe_grid(int BM, int BN, int NW, int OCC, int M, int N) {
+  const int ntiles = ((N + BN - 1) / BN) * ((M + BM - 1) / BM);
+  // resident blocks per CU: by LDS (2 stages + 2 KiB bias) and by registers (OCC)
+  const int lds = 2 * (BM + BN) * BK * 2 + 2048;
+  const int per_cu = std::max(1, std::min(NW == 8 ? pipe_kocc(NW, OCC) : OCC, (160 * 1024) / lds));
+  const int resident = device_cus() * per_cu;
+  return ntiles <= resident ? ntiles : resident;
+}
+// Half-tile last round for the 256x256 RS tile: applies when every XCD has >= 1 whole round and at
+// most nbx / 2 remainder tiles.
+inline bool half_round_applies(int M, int N) {
+  const int nb = device_cus();
+  const int ntiles = ((N + 255) / 256) * ((M + 255) / 256);
+  bool ok = nb % 8 == 0 && ntiles % nb != 0;
+  const int nbx = nb >> 3, q = ntiles >> 3, r = ntiles & 7;
+  for (int x = 0; ok && x < 8; ++x) {
+    const int cnt = q + (x < r ? 1 : 0);
+    ok = cnt >= nbx && 2 * (cnt % nbx) <= nbx;
+  }
+  return ok;
+}
+inline int grid_224(int M, int N) { return std::min(((N + 191) / 192) * ((M + 223) / 224), device_cus()); }
+
 template <typename T, int BM, int BN, int WGM, int WGN, int EPI, int ACT>
 hipError_t launch_cfg(const GemmParams& p, hipStream_t s) {
-  const int nTn = (p.N + BN - 1) / BN, nTm = (p.M + BM - 1) / BM;
-  const int ntiles = nTn * nTm;
-  // resident blocks: one 8-wave block (96-128 KiB LDS) or two 4-wave blocks (64 KiB) per CU
-  const int resident = device_cus() * (WGM * WGN == 4 ? 2 : 1);
-  const int grid = ntiles <= resident ? ntiles : resident;
+  const int grid = cfg_grid(BM, BN, WGM * WGN, p.M, p.N);
   gemm_launch(gemm_bt_kernel<T, BM, BN, WGM, WGN, EPI, ACT>, grid, WGM * WGN * 64, s, p);
   return hipGetLastError();
 }
 
-// OCC: resident blocks per CU the tile's registers allow (4-wave tiles: up to 3 by LDS; 8-wave
-// tiles: 1, or 2 when built for 4 waves per SIMD).  2 LDS stages.
 template <typename T, int BM, int BN, int WGM, int WGN, int EPI, int ACT, int OCC = 3, int RS = 0>
 hipError_t launch_pipe(const GemmParams& p, hipStream_t s) {
   constexpr int NW = WGM * WGN;
-  constexpr int KOCC = NW == 8 ? (OCC >= 2 ? 2 : 1) : 2;  // kernel template's OCC (launch bounds)
-  const int nTn = (p.N + BN - 1) / BN, nTm = (p.M + BM - 1) / BM;
-  const int ntiles = nTn * nTm;
-  // resident blocks per CU: by LDS (2 stages + 2 KiB bias) and by registers (OCC)
-  const int lds = 2 * (BM + BN) * BK * 2 + 2048;
-  const int per_cu = std::max(1, std::min(NW == 8 ? KOCC : OCC, (160 * 1024) / lds));
-  const int resident = device_cus() * per_cu;
-  const int grid = ntiles <= resident ? ntiles : resident;
+  constexpr int KOCC = pipe_kocc(NW, OCC);
+  const int grid = pipe_grid(BM, BN, NW, OCC, p.M, p.N);
   gemm_launch(gemm_pipe_kernel<T, BM, BN, WGM, WGN, EPI, ACT, 2, KOCC, RS, 0>, grid, NW * 64, s, p);
   return hipGetLastError();
 }
@@ -997,16 +1019,8 @@ hipError_t launch_pipe(const GemmParams& p, hipStream_t s) {
 // plain RS launch (the same sums, bit for bit).
 template <typename T, int EPI, int ACT>
 hipError_t launch_pipe_half(const GemmParams& p, hipStream_t s) {
-  const int nb = device_cus();
-  const int ntiles = ((p.N + 255) / 256) * ((p.M + 255) / 256);
-  bool ok = nb % 8 == 0 && ntiles % nb != 0;
-  const int nbx = nb >> 3, q = ntiles >> 3, r = ntiles & 7;
-  for (int x = 0; ok && x < 8; ++x) {
-    const int cnt = q + (x < r ? 1 : 0);
-    ok = cnt >= nbx && 2 * (cnt % nbx) <= nbx;
-  }
-  if (!ok) return launch_pipe<T, 256, 256, 2, 4, EPI, ACT, 3, 1>(p, s);
-  gemm_launch(gemm_pipe_kernel<T, 256, 256, 2, 4, EPI, ACT, 2, 2, 1, 1>, nb, 512, s, p);
+  if (!half_round_applies(p.M, p.N)) return launch_pipe<T, 256, 256, 2, 4, EPI, ACT, 3, 1>(p, s);
+  gemm_launch(gemm_pipe_kernel<T, 256, 256, 2, 4, EPI, ACT, 2, 2, 1, 1>, device_cus(), 512, s, p);
   return hipGetLastError();
 }
 
@@ -1016,8 +1030,7 @@ hipError_t launch_pipe_half(const GemmParams& p, hipStream_t s) {
 // two K-steps of LDS-DMA in flight per CU (106 KiB; 160 x 128 pairs: 72 KiB).
 template <typename T, int EPI, int ACT>
 hipError_t launch_pipe_224(const GemmParams& p, hipStream_t s) {
-  const int ntiles = ((p.N + 191) / 192) * ((p.M + 223) / 224);
-  const int grid = std::min(ntiles, device_cus());
+  const int grid = grid_224(p.M, p.N);
   if (p.K / BK >= 3) gemm_launch(gemm_pipe_kernel<T, 224, 192, 2, 4, EPI, ACT, 3, 1, 1, 0>, grid, 512, s, p);
   else gemm_launch(gemm_pipe_kernel<T, 224, 192, 2, 4, EPI, ACT, 2, 1, 1, 0>, grid, 512, s, p);
   return hipGetLastError();
@@ -1169,6 +1182,33 @@ int device_cus() {
   return cus;
 }
 
+
+// Blocks (the persistent grid) of one launch of `tile` (a GemmTile id; TILE_AUTO resolved as launch_tile
+// does, the skinny kernel included) at M x N x K with row operands: the launchers' own grid functions.
+int gemm_grid(int tile, int M, int N, int K) {
+  GemmParams p{};
+  p.M = M;
+  p.N = N;
+  p.K = K;
+  p.lda = p.ldw = K;
+  p.ldo = N;
+  if ((tile == TILE_AUTO || tile == TILE_SKINNY) && skinny_ok(p)) return (int)((((M + 15) / 16) * (N / 16) + 3) / 4);
+  if (tile == TILE_AUTO) tile = pick_gemm_tile(M, N, K);
+  if (K >= 2 * BK) {
+    switch (tile) {
+      case TILE_256x128: return pipe_grid(256, 128, 8, 3, M, N);
+      case TILE_256x256: return pipe_grid(256, 256, 8, 3, M, N);
+      case TILE_192x256_W8: return pipe_grid(192, 256, 8, 1, M, N);
+      case TILE_256x256_RS: return pipe_grid(256, 256, 8, 3, M, N);
+      case TILE_160x128_RS: return pipe_grid(160, 128, 4, 3, M, N);
+      case TILE_160x128_W8_RS: return pipe_grid(160, 128, 8, 2, M, N);
+      case TILE_256x256_HALF: return half_round_applies(M, N) ? device_cus() : pipe_grid(256, 256, 8, 3, M, N);
+      case TILE_224x192_W8: return grid_224(M, N);
+      default: break;
+    }
+  }
+  return cfg_grid(128, 128, 4, M, N);
+}
 
 // Tile choice: large-M GEMMs use the 256-row tiles (128 FLOP per staged byte
 // instead of 64); among those, the column tile that wastes the least of the

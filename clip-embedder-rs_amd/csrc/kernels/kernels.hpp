@@ -70,6 +70,7 @@ inline bool gemm_tile_built(int t) {
   return false;
 }
 int pick_gemm_tile(int M, int N, int K);
+int gemm_grid(int tile, int M, int N, int K);  // blocks of one launch (the persistent grid)
 int device_cus();  // CUs of the current device (cached)
 
 // act: Act enum from common.hpp (only used with EPI_STORE16)

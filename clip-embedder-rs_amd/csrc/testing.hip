@@ -240,6 +240,15 @@ int clipgpu_test_clock_probe(void* stream, int64_t duration_us, uint64_t* d_out)
   });
 }
 
+int clipgpu_test_gemm_grid(int tile, int64_t M, int64_t N, int64_t K, int* grid) {
+  return guarded([&]() {
+    if (M <= 0 || N <= 0 || K <= 0 || K % 64 || !grid || M > INT32_MAX || N > INT32_MAX || K > INT32_MAX)
+      throw ClipErr(CLIPGPU_ERR_INVALID, "bad GEMM grid arguments");
+    if (tile != 0 && tile != TILE_SKINNY && !gemm_tile_built(tile)) throw ClipErr(CLIPGPU_ERR_INVALID, "not a built tile");
+    *grid = gemm_grid(tile, (int)M, (int)N, (int)K);
+  });
+}
+
 int clipgpu_test_gemm_bench(int dtype, int epi, int act, int64_t M, int64_t N, int64_t K, int tile, int iters,
                             double* us_per_launch) {
   return clipgpu_test_gemm_bench_ld(dtype, epi, act, M, N, K, K, K, tile, iters, us_per_launch);

@@ -69,6 +69,7 @@ _PROTOS = [
     ("clipgpu_test_gemm", c_int, [c_int, c_int, c_int, c_int64, c_int64, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     ("clipgpu_test_attention", c_int, [c_int, c_int64, c_int64, c_int64, c_int64, c_int, c_void_p, c_void_p]),
     ("clipgpu_test_layernorm", c_int, [c_int, c_int64, c_int64, c_float, c_void_p, c_void_p, c_void_p, c_void_p]),
+    ("clipgpu_test_gemm_grid", c_int, [c_int, c_int64, c_int64, c_int64, POINTER(c_int)]),
     ("clipgpu_test_gemm_bench", c_int, [c_int, c_int, c_int, c_int64, c_int64, c_int64, c_int, c_int, POINTER(c_double)]),
     ("clipgpu_test_h2d_bench", c_int, [c_int64, c_int, c_int, POINTER(c_double)]),
     ("clipgpu_test_gemm_bench_ld", c_int, [c_int, c_int, c_int, c_int64, c_int64, c_int64, c_int64, c_int64, c_int, c_int,

@@ -239,8 +239,11 @@ PROFILE_CATEGORIES = ["patch_embed", "stem_ln", "qkv", "attention", "out_proj", 
                       "c_proj", "head", "last_layer"]
 
 
-def profile_enable(engine: "Engine", categories) -> None:
-    mask = 0
+PROFILE_CONCURRENT = 0x80000000  # include/clipgpu.h CLIPGPU_PROFILE_CONCURRENT: keep the lanes concurrent
+
+
+def profile_enable(engine: "Engine", categories, concurrent: bool = False) -> None:
+    mask = PROFILE_CONCURRENT if concurrent and categories else 0
     for c in categories:
         mask |= 1 << PROFILE_CATEGORIES.index(c)
     check(lib().clipgpu_profile_enable(engine.handle, mask))

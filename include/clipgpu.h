@@ -285,7 +285,10 @@ int clipgpu_facade_scores(const float* embs, int64_t n, const float* query, int6
  * last layer's gather, out_proj, ln_2, c_fc and c_proj at M = batch).  enable() resets totals;
  * read() waits for the recorded events and returns the summed ms and launch count.  While a
  * mask is set, a batch's concurrent sub-batch lanes run one after another on the launch
- * stream (same launches, no overlap), so each event pair times one kernel alone. */
+ * stream (same launches, no overlap), so each event pair times one kernel alone -- unless the
+ * mask also has CLIPGPU_PROFILE_CONCURRENT: then the lanes stay concurrent (no graph replay) and
+ * each GEMM's event pair times its launch beside the other lane's kernels, as in the timed step. */
+#define CLIPGPU_PROFILE_CONCURRENT 0x80000000u
 int clipgpu_profile_enable(clipgpu_engine* e, unsigned mask);
 int clipgpu_profile_read(clipgpu_engine* e, int category, double* total_ms, int64_t* launches);
 const char* clipgpu_profile_category_name(int category);

@@ -56,6 +56,10 @@ int clipgpu_test_patch_rows(int dtype, int mode, int64_t B, int64_t S, int64_t P
  * id (kernels.hpp; 0 auto).  Returns the mean µs per launch (HIP events). */
 int clipgpu_test_gemm_bench(int dtype, int epi, int act, int64_t M, int64_t N, int64_t K, int tile, int iters,
                             double* us_per_launch);
+/* Blocks of one launch of GEMM tile `tile` (0 auto) at M x N x K (row operands): the persistent grid
+ * the launcher uses (one CU's resident blocks x CUs, or the tile count when smaller).  No GPU needed
+ * (a host without one counts 256 CUs). */
+int clipgpu_test_gemm_grid(int tile, int64_t M, int64_t N, int64_t K, int* grid);
 /* As clipgpu_test_gemm_bench with row pitches lda >= K, ldw >= K (elements, multiples of 8). */
 int clipgpu_test_gemm_bench_ld(int dtype, int epi, int act, int64_t M, int64_t N, int64_t K, int64_t lda,
                                int64_t ldw, int tile, int iters, double* us_per_launch);
