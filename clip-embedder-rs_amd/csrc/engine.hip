@@ -169,7 +169,7 @@ struct Profiler {
   unsigned mask = 0;
   std::vector<hipEvent_t> pool;
   size_t used = 0;
-  struct Rec { int cat; hipEvent_t a, b; };
+  struct Rec { int cat; hipEvent_t a, b; hipStream_t st; };
   std::vector<Rec> pending;
   double total_ms[PC_N] = {0};
   long long count[PC_N] = {0};
@@ -581,7 +581,7 @@ struct ProfScope {
     if (!a) return;
     if (gemm) g_gemm_events = GemmLaunchEvents();  // consumed by the launch (or disarm on error)
     else (void)hipEventRecord(b, st);
-    p->pending.push_back({cat, a, b});
+    p->pending.push_back({cat, a, b, st});
   }
 };
 
@@ -2397,6 +2397,42 @@ int clipgpu_profile_read(clipgpu_engine* e, int category, double* total_ms, int6
     p.used = 0;
     if (total_ms) *total_ms = p.total_ms[category];
     if (launches) *launches = p.count[category];
+  });
+}
+
+// The recorded launches as a timeline (tools/timeline.py): start / end of each in ms from the first
+// recorded start, its category and lane (index of the lane stream it ran on, -1 for another stream).
+// Consumes the records like clipgpu_profile_read (which then sees them in its totals).
+int clipgpu_test_profile_timeline(clipgpu_engine* e, int64_t n_max, double* t0, double* t1, int* cat, int* lane,
+                                  int64_t* n_out) {
+  return guarded([&]() {
+    if (!e || !n_out || n_max < 0 || (n_max > 0 && (!t0 || !t1 || !cat || !lane)))
+      throw ClipErr(CLIPGPU_ERR_INVALID, "bad timeline query");
+    std::lock_guard<std::mutex> lk(e->mu);
+    Profiler& p = e->prof;
+    int64_t n = 0;
+    for (auto& rec : p.pending) HIP_CHECK(hipEventSynchronize(rec.b));
+    for (auto& rec : p.pending) {
+      float ms = 0.f, s0 = 0.f, s1 = 0.f;
+      HIP_CHECK(hipEventElapsedTime(&ms, rec.a, rec.b));
+      p.total_ms[rec.cat] += ms;
+      p.count[rec.cat] += 1;
+      if (n < n_max) {
+        HIP_CHECK(hipEventElapsedTime(&s0, p.pending[0].a, rec.a));
+        HIP_CHECK(hipEventElapsedTime(&s1, p.pending[0].a, rec.b));
+        t0[n] = s0;
+        t1[n] = s1;
+        cat[n] = rec.cat;
+        int ln = -1;
+        for (int i = 0; i < 4 && !e->reps.empty(); ++i)
+          if (rec.st != nullptr && rec.st == e->reps[0].lane[i]) ln = i;
+        lane[n] = ln;
+      }
+      ++n;
+    }
+    p.pending.clear();
+    p.used = 0;
+    *n_out = n;
   });
 }
 

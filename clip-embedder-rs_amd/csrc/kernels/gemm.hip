@@ -96,6 +96,9 @@ constexpr int BK = 64;
 #ifndef CLIPGPU_GEMM_SPREAD_W8
 #define CLIPGPU_GEMM_SPREAD_W8 0
 #endif
+#ifndef CLIPGPU_GEMM_SPREAD_ALL
+#define CLIPGPU_GEMM_SPREAD_ALL 0
+#endif
 #ifndef CLIPGPU_GEMM_EPI_DMA_WAIT
 #define CLIPGPU_GEMM_EPI_DMA_WAIT 1
 #endif
@@ -474,7 +477,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
   // DMA pieces spread between MFMA groups of phase 1 (>= 32 MFMAs per phase; with
   // CLIPGPU_GEMM_SPREAD_W8, also the one-block-per-CU 8-wave tiles, whose pieces otherwise go out in
   // one burst after the step barrier while no MFMA issues), else issued up front
-  constexpr bool SPREAD = MI * NI >= 32 || (CLIPGPU_GEMM_SPREAD_W8 && NW == 8 && OCC < 2);
+  constexpr bool SPREAD = MI * NI >= 32 || (CLIPGPU_GEMM_SPREAD_W8 && NW == 8 && OCC < 2) || CLIPGPU_GEMM_SPREAD_ALL;
   (void)LG;
   static_assert(BM % 8 == 0 && BN % 8 == 0 && MI >= 1 && BN <= 256 && PT >= NW, "bad tile");
   static_assert(NI == 2 || NI == 3 || NI == 4 || NI == 6 || NI == 8, "column permutation: NI in {2,3,4,6,8}");

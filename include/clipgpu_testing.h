@@ -129,6 +129,12 @@ int clipgpu_test_force_broadcast(struct clipgpu_engine* e, int on);
 /* A handle without a communicator takes the multi-device handle's lazy path: a clique over its
  * replicas' distinct devices, created (ncclCommInitAll) by the first gathered call. */
 int clipgpu_test_comm_lazy(struct clipgpu_engine* e);
+/* The launches recorded by clipgpu_profile_enable as a timeline: up to n_max entries of start / end
+ * (ms from the first recorded start), category (clipgpu_profile_category_name) and lane (the device
+ * lane stream index, -1 for another stream); *n_out = the number recorded.  Consumes the records as
+ * clipgpu_profile_read does (their times then count in its totals). */
+int clipgpu_test_profile_timeline(struct clipgpu_engine* e, int64_t n_max, double* t0, double* t1, int* cat,
+                                  int* lane, int64_t* n_out);
 /* The host-side plan of a gathered call (no GPU): off[0..nranks] = first output row of each rank's
  * block (off[nranks] = total rows), *equal = 1 when every block has the same size.  Errors as the
  * gathered entry points: a negative count, or zero rows in all ("Empty batch"). */
