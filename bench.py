@@ -377,6 +377,8 @@ def main():
     ap.add_argument("--windows", type=int, default=5,
                     help="N = 1: repeated K-step windows after the timed one (min / median / max images/s, the "
                          "shader clock of each window, and the c_fc launch time per window); 0 skips them")
+    ap.add_argument("--residual", default=None, choices=["f32", "f16"],
+                    help="the residual stream's storage (clipgpu_options.residual; default: the library's)")
     ap.add_argument("--gather", action="store_true",
                     help="N = 1: run the data-parallel path anyway (gloo control plane, the engine's RCCL "
                          "communicator, gathered entry points) -- a one-GPU rehearsal of N > 1")
@@ -402,7 +404,7 @@ def main():
     dev = torch.device("cuda", local)
 
     mdir = make_model_dir()
-    vopts = {"lanes": args.lanes}
+    vopts = {"lanes": args.lanes, "residual": args.residual}
     if args.tiles:
         pins = [int(t) for t in args.tiles.split(",")]
         vopts.update(gemm_tiles=pins, patch_tile=pins[3])
@@ -558,7 +560,7 @@ def main():
     text = None
     tout_host = None
     if not args.no_text:
-        topts = {"lanes": args.text_lanes}
+        topts = {"lanes": args.text_lanes, "residual": args.residual}
         if args.text_tiles:
             topts["gemm_tiles"] = [int(t) for t in args.text_tiles.split(",")]
         te = Engine(mdir, _lib.TOWER_TEXT, [local], args.dtype, B_TEXT, **topts)

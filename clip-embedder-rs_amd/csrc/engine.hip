@@ -87,7 +87,7 @@ struct Replica {
   char* arena = nullptr;  // weights
   char* work = nullptr;   // activations
   DevWeights w;
-  float* x = nullptr;     // [rows][D] f32 residual stream
+  void* x = nullptr;      // [rows][D] residual stream: f32, or f16 (clipgpu_engine::x16)
   void* h = nullptr;      // [rows][D] 16-bit (LN output / attention output); fp8 engines: LN output as e4m3
   uint8_t* hs = nullptr;   // fp8 engines: [rows][D/32] scales of the LN output in h
   uint8_t* bigs = nullptr; // fp8 engines: [rows][MLP/32] scales of the c_fc output (e4m3 in big)
@@ -202,6 +202,11 @@ struct clipgpu_engine {
   bool graphs = true;  // replay forwards as hipGraphs (clipgpu_options.graphs = -1 disables)
   bool prune = true;   // last layer on the pooled rows only (clipgpu_options.prune_last = -1 disables; trunk)
   bool trim = true;    // host-ids text batches run on their first max(EOT)+1 tokens (options.trim_text = -1: off)
+  // The residual stream x is stored in f16 (clipgpu_options.residual): its two read-modify-writes and
+  // two LayerNorm reads per layer move half the bytes; every add into it and every LayerNorm statistic
+  // stays f32.  bf16 / f16 engines of the CLIP family only (fp8 engines' MX residual epilogue and the
+  // SigLIP MAP head take the f32 stream).
+  bool x16 = false;
   int tuning = 0;  // clipgpu_options.tuning: 1 = timing tuner (+ whole-forward pass), 2 = per-site pass only
   // clipgpu_options.gemm_tiles / patch_tile pins (0 = the table's tile, -1 = the shape heuristic)
   int pin_tiles[4] = {0, 0, 0, 0};
@@ -518,7 +523,7 @@ void alloc_workspace(clipgpu_engine& e, Replica& r) {
   HIP_CHECK(hipMalloc(&r.work, total));
   HIP_CHECK(hipMemset(r.work, 0, total));
   Bump a{r.work, 0, total};
-  r.x = (float*)a.take(sizes[0]);
+  r.x = a.take(sizes[0]);  // f32 capacity (an f16 stream uses the first half)
   r.h = a.take(sizes[1]);
   r.big = a.take(sizes[2]);
   r.pooled = a.take(sizes[3]);
@@ -601,6 +606,15 @@ GemmParams rows_gemm(const void* A, long lda, const void* W, const float* bias, 
   return g;
 }
 
+// The residual stream's element size and row offsets (f32, or f16: clipgpu_engine::x16).
+inline size_t xbytes(const clipgpu_engine& e) { return e.x16 ? 2 : 4; }
+inline void* xrows(const clipgpu_engine& e, void* x, size_t rows) {
+  return (char*)x + rows * (size_t)e.spec.width * xbytes(e);
+}
+
+// clipgpu_options.residual = 0: the residual stream's default storage
+constexpr int kResidualDefault = CLIPGPU_RESIDUAL_F32;
+
 int site_epi(int site) { return (site == GS_OUT || site == GS_PROJ) ? EPI_RESID : EPI_STORE16; }
 
 // Tile order per trunk site (GemmParams.group: row panels per group, 0 = the kernels' 8).  qkv and
@@ -624,6 +638,7 @@ GemmParams site_gemm(const clipgpu_engine& e, const Replica& r, const LayerW& L,
     default: g = rows_gemm(r.big, MLP, L.w2, L.b2, r.x, D, rows, D, MLP); break;
   }
   g.group = kSiteGroup[site];
+  g.x16 = e.x16 ? 1 : 0;
   // the younger half of 8-wave blocks at priority 1: vision +0.75 %, text -0.5 % (gemm.hip)
   g.prio = e.spec.tower == TOWER_VISION ? 1 : 0;
   return g;
@@ -680,7 +695,7 @@ extern "C" int clipgpu_test_ablate(unsigned mask) {
 // Residual rows the head pools from: x at token pos(b) of each sequence (tokens = T), or the
 // compact [B][D] rows the pruned last layer leaves (tokens = 1, pos 0).
 struct PoolSrc {
-  const float* x;
+  const void* x;  // the residual stream's type (clipgpu_engine::x16)
   int tokens;
   const int64_t* ids;
 };
@@ -736,30 +751,31 @@ PoolSrc trunk(const clipgpu_engine& e, const Replica& r, int B, int causal, cons
     if (!ABLATED(1)) { ProfScope ps(e, PC_ATTN, st);
       check(launch_attention(e.dt, r.big, r.h, B, T, s.heads, D, causal, st), "attention"); }
     if (compact) {  // pooled rows only from here on (QKV in `big` is dead after attention)
-      c.x = (float*)((char*)r.big + prune_off_x(s, B));
+      c.x = (char*)r.big + prune_off_x(s, B);
       c.h = (char*)r.big + prune_off_h(s, B);
       rows = B;
       ProfScope ps(e, PC_TAIL, st);
       // ids == nullptr: position pool_pos of every sequence (CLS 0, SigLIP2 text T - 1)
-      check(launch_gather_pooled(r.x + (size_t)pool_pos * D, (char*)r.h + (size_t)pool_pos * D * 2, ids, T, c.x, c.h,
+      check(launch_gather_pooled(xrows(e, r.x, pool_pos), e.x16, (char*)r.h + (size_t)pool_pos * D * 2, ids, T, c.x, c.h,
                                  B, D, st),
             "gather pooled rows");
     }
     gemm(GS_OUT, PC_OUT_PROJ, "out_proj gemm");
     if (!ABLATED(0)) {
       ProfScope ps(e, compact ? PC_TAIL : PC_LN, st);
-      check(launch_ln_rows(e.dt, c.x, L.ln2_w, L.ln2_b, s.ln_eps, c.h, rows, D, st, ln_q(e, l, GS_FC, c.hs)), "ln_2");
+      check(launch_ln_rows(e.dt, c.x, e.x16, L.ln2_w, L.ln2_b, s.ln_eps, c.h, rows, D, st, ln_q(e, l, GS_FC, c.hs)),
+            "ln_2");
     }
     gemm(GS_FC, PC_C_FC, "c_fc gemm");
     gemm(GS_PROJ, PC_C_PROJ, "c_proj gemm");
     if (l + 1 < s.layers && !ABLATED(0)) {
       ProfScope ps(e, PC_LN, st);
-      check(launch_ln_rows(e.dt, r.x, r.w.layers[l + 1].ln1_w, r.w.layers[l + 1].ln1_b, s.ln_eps, r.h, rows, D, st,
+      check(launch_ln_rows(e.dt, r.x, e.x16, r.w.layers[l + 1].ln1_w, r.w.layers[l + 1].ln1_b, s.ln_eps, r.h, rows, D, st,
                            ln_q(e, l + 1, GS_QKV, r.hs)), "ln_1");
     }
     if (compact) return PoolSrc{c.x, 1, nullptr};
   }
-  return PoolSrc{r.x + (size_t)pool_pos * D, T, ids};
+  return PoolSrc{xrows(e, r.x, pool_pos), T, ids};
 }
 
 // The committed MI355X tile table (default; clipgpu_options.tuning = 0).  A trunk site's tile is
@@ -930,6 +946,7 @@ void autotune_tiles(clipgpu_engine& e, Replica& r) {
     g.G = G;
     g.pos = r.w.pos;
     g.cls = s.cls() ? 1 : 0;
+    g.x16 = e.x16 ? 1 : 0;
     e.tile_patch = tune(g, EPI_PATCH, ACT_NONE);
   }
   (void)hipEventDestroy(a);
@@ -940,7 +957,8 @@ void head(const clipgpu_engine& e, const Replica& r, int B, const PoolSrc& src, 
   const TowerSpec& s = e.spec;
   const int D = s.width, E = s.embed_dim;
   ProfScope ps(e, PC_HEAD, st);
-  check(launch_pool_ln(e.dt, src.x, src.ids, src.tokens, r.w.lnpost_w, r.w.lnpost_b, s.ln_eps, r.pooled, B, D, st),
+  check(launch_pool_ln(e.dt, src.x, e.x16, src.ids, src.tokens, r.w.lnpost_w, r.w.lnpost_b, s.ln_eps, r.pooled, B, D,
+                       st),
         "pool+ln");
   check(launch_gemm(e.dt, A_ROWS, EPI_STORE32, ACT_NONE, rows_gemm(r.pooled, D, r.w.proj_t, r.w.proj_b, r.emb, E, B, E, D),
                     st),
@@ -957,18 +975,18 @@ void head_map(const clipgpu_engine& e, const Replica& r, int B, float* d_out, hi
   const int D = s.width, T = s.tokens(), M = mlp_pad(s);
   const MapHeadW& mw = r.w.map;
   ProfScope ps(e, PC_HEAD, st);
-  check(launch_ln_rows(e.dt, r.x, r.w.lnpost_w, r.w.lnpost_b, s.ln_eps, r.h, B * T, D, st), "norm");
+  check(launch_ln_rows(e.dt, r.x, 0, r.w.lnpost_w, r.w.lnpost_b, s.ln_eps, r.h, B * T, D, st), "norm");
   check(launch_gemm(e.dt, A_ROWS, EPI_STORE16, ACT_NONE, rows_gemm(r.h, D, mw.wkv, mw.bkv, r.big, 2 * D, B * T, 2 * D, D),
                     st), "attn_pool kv gemm");
   check(launch_map_attention(e.dt, mw.q, r.big, r.pooled, B, T, s.heads, D, st), "attn_pool attention");
   check(launch_gemm(e.dt, A_ROWS, EPI_STORE32, ACT_NONE, rows_gemm(r.pooled, D, mw.wproj, mw.bproj, r.x, D, B, D, D), st),
         "attn_pool proj gemm");
-  check(launch_ln_rows(e.dt, r.x, mw.norm_w, mw.norm_b, s.ln_eps, r.h, B, D, st), "attn_pool norm");
+  check(launch_ln_rows(e.dt, r.x, 0, mw.norm_w, mw.norm_b, s.ln_eps, r.h, B, D, st), "attn_pool norm");
   check(launch_gemm(e.dt, A_ROWS, EPI_STORE16, s.act, rows_gemm(r.h, D, mw.w1, mw.b1, r.big, M, B, M, D), st),
         "attn_pool fc1 gemm");
   check(launch_gemm(e.dt, A_ROWS, EPI_RESID, ACT_NONE, rows_gemm(r.big, M, mw.w2, mw.b2, r.x, D, B, D, M), st),
         "attn_pool fc2 gemm");
-  check(launch_l2norm(r.x, d_out, B, D, st), "l2norm");
+  check(launch_l2norm((const float*)r.x, d_out, B, D, st), "l2norm");
 }
 
 // asrc: A_IMG_F32 (pixels = normalised f32 NCHW) or A_IMG_U8 (NHWC u8 + mean/std)
@@ -984,11 +1002,12 @@ void vision_forward(const clipgpu_engine& e, const Replica& r, const void* pixel
     g.G = G;
     g.pos = r.w.pos;
     g.cls = s.cls() ? 1 : 0;
+    g.x16 = e.x16 ? 1 : 0;
     g.tile = 2 * B * s.tokens() > e.tuned_rows ? e.tile_patch : TILE_AUTO;
     check(launch_gemm(e.dt, A_ROWS, EPI_PATCH, ACT_NONE, g, st), "patch gemm"); }
   if (s.family == FAMILY_SIGLIP) {  // no class token, no pre-norm: x = patches + bias + pos
     { ProfScope ps(e, PC_STEM, st);
-      check(launch_ln_rows(e.dt, r.x, r.w.layers[0].ln1_w, r.w.layers[0].ln1_b, s.ln_eps, r.h, B * s.tokens(), D, st,
+      check(launch_ln_rows(e.dt, r.x, e.x16, r.w.layers[0].ln1_w, r.w.layers[0].ln1_b, s.ln_eps, r.h, B * s.tokens(), D, st,
                            ln_q(e, 0, GS_QKV, r.hs)),
             "ln_1"); }
     trunk(e, r, B, 0, nullptr, st, s.tokens());
@@ -997,7 +1016,7 @@ void vision_forward(const clipgpu_engine& e, const Replica& r, const void* pixel
   }
   {
   ProfScope ps(e, PC_STEM, st);
-  check(launch_vision_embed_ln(e.dt, r.x, r.w.cls, r.w.pos, r.w.lnpre_w, r.w.lnpre_b, r.w.layers[0].ln1_w,
+  check(launch_vision_embed_ln(e.dt, r.x, e.x16, r.w.cls, r.w.pos, r.w.lnpre_w, r.w.lnpre_b, r.w.layers[0].ln1_w,
                                r.w.layers[0].ln1_b, s.ln_eps, r.h, B, s.tokens(), D, st, ln_q(e, 0, GS_QKV, r.hs)),
         "embed+ln_pre");
   }
@@ -1014,7 +1033,7 @@ void text_forward(const clipgpu_engine& e, const Replica& r, const int64_t* d_id
   {
   ProfScope ps(e, PC_STEM, st);
   check(launch_text_embed_ln(e.dt, d_ids, r.w.tok, r.w.pos, r.w.layers[0].ln1_w, r.w.layers[0].ln1_b, s.ln_eps,
-                             r.x, r.h, B, T, s.width, s.vocab_size, st, ln_q(e, 0, GS_QKV, r.hs)),
+                             r.x, e.x16, r.h, B, T, s.width, s.vocab_size, st, ln_q(e, 0, GS_QKV, r.hs)),
         "token embed+ln_1");
   }
   // CLIP: causal, the EOT (argmax id) row pooled; SigLIP2: no mask, the last position pooled
@@ -1029,7 +1048,7 @@ Replica lane_view(const clipgpu_engine& e, const Replica& r, int b0) {
   const size_t rows = (size_t)b0 * s.tokens(), D = s.width;
   const size_t wide = big_wide(s);
   Replica v = r;
-  v.x = r.x + rows * D;
+  v.x = (char*)r.x + rows * D * xbytes(e);
   v.h = (char*)r.h + rows * D * 2;
   v.big = (char*)r.big + rows * wide * 2;
   if (r.hs) v.hs = r.hs + rows * D / 32;
@@ -1800,9 +1819,10 @@ int clipgpu_create_ex(const char* model_dir, int tower, const int* device_ids, i
     std::memset(&opts, 0, sizeof(opts));
     opts.struct_size = sizeof(opts);
     if (opts_in) {  // an older caller's smaller struct: its prefix, defaults for the rest
-      // the sizes of the struct's published versions only: v2 (through `communicator`) and v3 (ADVICE r4:
-      // a size ending inside a field would copy part of it)
-      if (opts_in->struct_size != offsetof(clipgpu_options, graphs) && opts_in->struct_size != sizeof(opts))
+      // the sizes of the struct's published versions only: v2 (through `communicator`), v3 (through
+      // `mx_layers`) and v4 (a size ending inside a field would copy part of it)
+      if (opts_in->struct_size != offsetof(clipgpu_options, graphs) &&
+          opts_in->struct_size != offsetof(clipgpu_options, residual) && opts_in->struct_size != sizeof(opts))
         throw ClipErr(CLIPGPU_ERR_INVALID, "clipgpu_options.struct_size: call clipgpu_options_init first");
       std::memcpy(&opts, opts_in, opts_in->struct_size);
     }
@@ -1820,6 +1840,8 @@ int clipgpu_create_ex(const char* model_dir, int tower, const int* device_ids, i
     }
     if (opts.mx_layers != 0 && dtype != CLIPGPU_DTYPE_FP8)
       throw ClipErr(CLIPGPU_ERR_INVALID, "clipgpu_options.mx_layers needs dtype CLIPGPU_DTYPE_FP8");
+    if (opts.residual < 0 || opts.residual > CLIPGPU_RESIDUAL_F16)
+      throw ClipErr(CLIPGPU_ERR_INVALID, "clipgpu_options.residual must be 0, 1 (f32) or 2 (f16)");
     if (opts.communicator < 0 || opts.communicator > 1)
       throw ClipErr(CLIPGPU_ERR_INVALID, "clipgpu_options.communicator must be 0 or 1");
     if (!model_dir) throw ClipErr(CLIPGPU_ERR_INVALID, "model_dir is NULL");
@@ -1871,6 +1893,13 @@ int clipgpu_create_ex(const char* model_dir, int tower, const int* device_ids, i
     e->graphs = opts.graphs != -1;
     e->prune = opts.prune_last != -1;
     e->trim = opts.trim_text != -1;
+    {  // the residual stream's storage (clipgpu_options.residual; kResidualDefault when 0)
+      const int res = opts.residual ? opts.residual : kResidualDefault;
+      const bool f16_ok = !e->mx && e->spec.family != FAMILY_SIGLIP;
+      if (opts.residual == CLIPGPU_RESIDUAL_F16 && !f16_ok)
+        throw ClipErr(CLIPGPU_ERR_INVALID, "clipgpu_options.residual = f16: bf16 / f16 engines of the CLIP family only");
+      e->x16 = res == CLIPGPU_RESIDUAL_F16 && f16_ok;
+    }
     for (int i = 0; i < 4; ++i) e->pin_tiles[i] = opts.gemm_tiles[i];
     e->pin_patch = opts.patch_tile;
     const TowerSpec& s = e->spec;

@@ -25,6 +25,20 @@ template <typename T> struct Vec4;
 template <> struct Vec4<__bf16> { typedef bf16x4 type; };
 template <> struct Vec4<_Float16> { typedef f16x4 type; };
 
+// Four consecutive residual-stream values (f32, or f16 when the stream is stored in f16:
+// clipgpu_options.residual), widened to / rounded from f32.
+__device__ __forceinline__ float4 ldx4(const float* p) { return *(const float4*)p; }
+__device__ __forceinline__ float4 ldx4(const _Float16* p) {
+  const f16x4 h = *(const f16x4*)p;
+  return make_float4((float)h[0], (float)h[1], (float)h[2], (float)h[3]);
+}
+__device__ __forceinline__ void stx4(float* p, float4 v) { *(float4*)p = v; }
+__device__ __forceinline__ void stx4(_Float16* p, float4 v) {
+  f16x4 h;
+  h[0] = (_Float16)v.x; h[1] = (_Float16)v.y; h[2] = (_Float16)v.z; h[3] = (_Float16)v.w;
+  *(f16x4*)p = h;
+}
+
 __device__ __forceinline__ f32x4 mfma_16x16x32(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }

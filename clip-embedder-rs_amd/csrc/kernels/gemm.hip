@@ -253,7 +253,9 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
     mfma_block(std::false_type{}, a1, b1);
   };
 
-  auto epilogue = [&](int m0, int n0, int bpar) {
+  // x16c: the residual stream (EPI_RESID's out, EPI_PATCH's out) is f16 (GemmParams.x16), else f32
+  auto epilogue = [&](auto x16c, int m0, int n0, int bpar) {
+    typedef typename std::conditional<decltype(x16c)::value, _Float16, float>::type XE;
     const int G2 = p.G * p.G;
     // EPI_RESID: the residual rows of column block ni+1 are loaded before block ni
     // is stored, so no load waits behind this epilogue's own stores.
@@ -263,7 +265,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
 #pragma unroll
       for (int mi = 0; mi < MI; ++mi) {
         const int m = m0 + wm + mi * 16 + fr;
-        if (m < p.M && n + 4 <= p.N) dst[mi] = *(const float4*)((const float*)p.out + (long)m * p.ldo + n);
+        if (m < p.M && n + 4 <= p.N) dst[mi] = ldx4((const XE*)p.out + (long)m * p.ldo + n);
       }
     };
     if constexpr (EPI == EPI_RESID) load_x(0, xr[0]);
@@ -310,14 +312,14 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
               if (n + j < p.N) o[j] = to16<T>(apply_act<ACT>(v[j]));
           }
         } else {
-          float* o;
+          XE* o;  // (EPI_STORE32: f32 output, x16c false)
           const float* ps = nullptr;
           if constexpr (EPI == EPI_PATCH) {
             const int b = m / G2, pp = m - b * G2;
-            o = (float*)p.out + ((long)b * (G2 + p.cls) + p.cls + pp) * p.ldo + n;
+            o = (XE*)p.out + ((long)b * (G2 + p.cls) + p.cls + pp) * p.ldo + n;
             ps = p.pos + (long)(p.cls + pp) * p.N + n;
           } else {
-            o = (float*)p.out + (long)m * p.ldo + n;
+            o = (XE*)p.out + (long)m * p.ldo + n;
           }
           if (nfull) {
             float4 w = make_float4(v[0], v[1], v[2], v[3]);
@@ -328,14 +330,14 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
               const float4 x = *(const float4*)ps;
               w.x += x.x; w.y += x.y; w.z += x.z; w.w += x.w;
             }
-            *(float4*)o = w;
+            stx4(o, w);
           } else {
             for (int j = 0; j < 4; ++j) {
               if (n + j >= p.N) continue;
               float r = v[j];
-              if constexpr (EPI == EPI_RESID) r += o[j];
+              if constexpr (EPI == EPI_RESID) r += (float)o[j];
               if constexpr (EPI == EPI_PATCH) r += ps[j];
-              o[j] = r;
+              o[j] = (XE)r;
             }
           }
         }
@@ -394,7 +396,12 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
     else compute(std::false_type{}, cur1 ? sA1 : sA0, cur1 ? sB1 : sB0);
     GEMM_STAMP(4 + ti * 4);
     vm_wait<0>();  // the next tile's stage 0 lands before the epilogue's stores (see gemm_pipe_kernel)
-    epilogue(m0, n0, bias_par);
+    if constexpr (EPI == EPI_RESID || EPI == EPI_PATCH) {
+      if (p.x16) epilogue(std::true_type{}, m0, n0, bias_par);
+      else epilogue(std::false_type{}, m0, n0, bias_par);
+    } else {
+      epilogue(std::false_type{}, m0, n0, bias_par);
+    }
     // Retire the next tile's stage-0 glds but not this tile's output stores
     // (issued after them; in-order vmcnt): a full tile issues exactly MI*NI
     // epilogue stores per lane, a partial one may issue fewer -> wait for all.
@@ -743,7 +750,9 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
   };
 
   // ---- epilogue: lane owns row wm+mi*16+fr, columns nc .. nc+4*NI-1 ------------
-  auto epilogue = [&](int m0, int n0, int bpar) {
+  // x16c: the residual stream (EPI_RESID's out, EPI_PATCH's out) is f16 (GemmParams.x16), else f32
+  auto epilogue = [&](auto x16c, int m0, int n0, int bpar) {
+    typedef typename std::conditional<decltype(x16c)::value, _Float16, float>::type XE;
     const int nc = n0 + wn + fq * (4 * NI);
     const bool nfull = nc + 4 * NI <= p.N;
     f32x4 bias[NI];
@@ -768,9 +777,10 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
         return (long)m * p.ldo;
       }
     };
-    auto add_src = [&](int m) -> const float* {
+    // the rows added in: the positional embedding (f32) for EPI_PATCH, the residual row (XE) for EPI_RESID
+    auto add_src = [&](int m) {
       if constexpr (EPI == EPI_PATCH) return p.pos + (long)(p.cls + m % G2) * p.N + nc;
-      else return (const float*)p.out + (long)m * p.ldo + nc;
+      else return (const XE*)p.out + (long)m * p.ldo + nc;
     };
     // The rows added in (residual x / positional embedding) are loaded before the epilogue math:
     // all MI row blocks at once when they fit in the fragment registers the main loop no longer
@@ -785,9 +795,9 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
     auto load_x = [&](int mi, float4(&dst)[NI]) {
       const int m = m0 + wm_cur + mi * 16 + fr;
       if (m < p.M && nfull && (!HM || mi < mi_lim)) {
-        const float* src = add_src(m);
+        const auto src = add_src(m);
 #pragma unroll
-        for (int ni = 0; ni < NI; ++ni) dst[ni] = *(const float4*)(src + ni * 4);
+        for (int ni = 0; ni < NI; ++ni) dst[ni] = ldx4(src + ni * 4);
       }
     };
     if constexpr (ADDX) {
@@ -850,7 +860,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
               if (nc + ni * 4 + j < p.N) o[ni * 4 + j] = to16<T>(apply_act<ACT>(v[ni][j]));
         }
       } else {
-        float* o = (float*)p.out + out_row(m) + nc;
+        XE* o = (XE*)p.out + out_row(m) + nc;  // (EPI_STORE32: f32, x16c false)
         if (nfull) {
 #pragma unroll
           for (int ni = 0; ni < NI; ++ni) {
@@ -859,23 +869,23 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
               const float4 x = xr[XALL ? mi : mi % XR][ni];
               w.x += x.x; w.y += x.y; w.z += x.z; w.w += x.w;
             }
-            *(float4*)(o + ni * 4) = w;
+            stx4(o + ni * 4, w);
           }
         } else {
-          const float* xs = ADDX ? add_src(m) : nullptr;
 #pragma unroll
           for (int ni = 0; ni < NI; ++ni)
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
               if (nc + ni * 4 + j >= p.N) continue;
               float r = v[ni][j];
-              if constexpr (ADDX) r += xs[ni * 4 + j];
-              o[ni * 4 + j] = r;
+              if constexpr (ADDX) r += (float)add_src(m)[ni * 4 + j];
+              o[ni * 4 + j] = (XE)r;
             }
         }
       }
     }
   };
+  constexpr bool ADDX_EPI = EPI == EPI_RESID || EPI == EPI_PATCH;  // epilogues that touch the residual stream
   // vm ops a full tile's epilogue leaves in flight behind the DMA of the step after it (the same
   // count on both paths: MI NI / 2 16-byte stores of 16-bit values, MI NI of f32, + as many loads)
   constexpr int EPI_VM = EPI == EPI_STORE16 ? (NI % 2 ? MI * NI : MI * NI / 2)
@@ -956,7 +966,12 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
     if constexpr (NS == 3) vm_wait_step(std::integral_constant<int, 0>{});
     else vm_wait<0>();
 #endif
-    epilogue(m0, n0, ti & 1);
+    if constexpr (ADDX_EPI) {
+      if (p.x16) epilogue(std::true_type{}, m0, n0, ti & 1);
+      else epilogue(std::false_type{}, m0, n0, ti & 1);
+    } else {
+      epilogue(std::false_type{}, m0, n0, ti & 1);
+    }
     // partial tiles and half tiles issue fewer vm ops than EPI_VM: drain them
     after_full_epi = m0 + BM <= p.M && n0 + BN <= p.N && (!HM || t < hm_F);
     if (!after_full_epi) vm_wait<0>();
@@ -1109,8 +1124,17 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmParams p) {
     for (int j = 0; j < 4; ++j) o[j] = to16<T>(apply_act<ACT>(v[j]));
     *(typename Vec4<T>::type*)((T*)p.out + (long)m * p.ldo + n) = o;
   } else {
-    float* o = (float*)p.out + (long)m * p.ldo + n;
     float4 r = make_float4(v[0], v[1], v[2], v[3]);
+    if constexpr (EPI == EPI_RESID) {
+      if (p.x16) {  // the residual stream in f16
+        _Float16* o = (_Float16*)p.out + (long)m * p.ldo + n;
+        const float4 x = ldx4(o);
+        r.x += x.x; r.y += x.y; r.z += x.z; r.w += x.w;
+        stx4(o, r);
+        return;
+      }
+    }
+    float* o = (float*)p.out + (long)m * p.ldo + n;
     if constexpr (EPI == EPI_RESID) {
       const float4 x = *(const float4*)o;
       r.x += x.x; r.y += x.y; r.z += x.z; r.w += x.w;

@@ -37,6 +37,7 @@ struct GemmParams {
   int diag;                  // stamp build only: bit 0 = skip epilogue stores (timing experiments)
   int group;                 // tile order: row panels per group (gemm_util.hpp tile_coords); 0 = 8
   int prio;                  // 8-wave gemm_pipe tiles: 1 = the younger half of the block at s_setprio 1
+  int x16;                   // EPI_RESID / EPI_PATCH: the residual stream `out` is f16 (else f32); the adds are f32
 };
 
 // Tile configurations of the MFMA GEMM.  Ids are stable across rounds; the ones not listed were
@@ -93,31 +94,33 @@ hipError_t launch_map_attention(DType dt, const float* q, const void* kv, void* 
 hipError_t launch_attention(DType dt, const void* qkv, void* out, int B, int N, int H, int D,
                             int causal, hipStream_t s);
 
+// The residual stream x (launchers taking `x, x16`): f32 rows, or f16 rows when x16 != 0
+// (clipgpu_options.residual); every add into it and every statistic of it is computed in f32.
 // out16[r] = LN(x[r]) for r < rows.
-hipError_t launch_ln_rows(DType dt, const float* x, const float* w, const float* b, float eps,
+hipError_t launch_ln_rows(DType dt, const void* x, int x16, const float* w, const float* b, float eps,
                           void* out16, int rows, int D, hipStream_t s, uint8_t* qs = nullptr);
 // qs != nullptr (these LN launchers): the output is MX-fp8, out16 = e4m3 bytes [rows][D],
 // qs = scales [rows][D/32] (gemm_mx.hip's A operand); D % 32 == 0.
 
 // Vision stem tail: CLS row = cls + pos[0]; x = ln_pre(x) (in place); h = ln_1(x).
-hipError_t launch_vision_embed_ln(DType dt, float* x, const float* cls, const float* pos,
+hipError_t launch_vision_embed_ln(DType dt, void* x, int x16, const float* cls, const float* pos,
                                   const float* lnpre_w, const float* lnpre_b,
                                   const float* ln1_w, const float* ln1_b, float eps,
                                   void* h, int B, int tokens, int D, hipStream_t s, uint8_t* qs = nullptr);
 
 // Text stem: x = tok[ids] + pos; h = ln_1(x).
 hipError_t launch_text_embed_ln(DType dt, const int64_t* ids, const float* tok, const float* pos,
-                                const float* ln1_w, const float* ln1_b, float eps, float* x,
+                                const float* ln1_w, const float* ln1_b, float eps, void* x, int x16,
                                 void* h, int B, int T, int D, int vocab, hipStream_t s, uint8_t* qs = nullptr);
 
 // Pool one row per sequence (CLS: ids == nullptr; else first argmax of ids) and LN it.
-hipError_t launch_pool_ln(DType dt, const float* x, const int64_t* ids, int tokens,
+hipError_t launch_pool_ln(DType dt, const void* x, int x16, const int64_t* ids, int tokens,
                           const float* w, const float* b, float eps, void* out16, int B, int D,
                           hipStream_t s);
 
-// Last-layer compaction: xc[b] = x[b*tokens + pos(b)] (f32) and hc[b] = h[same row] (16-bit),
-// pos as launch_pool_ln picks it.  x / h and xc / hc must not overlap.
-hipError_t launch_gather_pooled(const float* x, const void* h16, const int64_t* ids, int tokens, float* xc,
+// Last-layer compaction: xc[b] = x[b*tokens + pos(b)] (the residual type) and hc[b] = h[same row]
+// (16-bit), pos as launch_pool_ln picks it.  x / h and xc / hc must not overlap.
+hipError_t launch_gather_pooled(const void* x, int x16, const void* h16, const int64_t* ids, int tokens, void* xc,
                                 void* hc16, int B, int D, hipStream_t s);
 
 // Patch rows of the patch-embedding conv: out[b*G*G + p][k] (16-bit, row stride Kp) from

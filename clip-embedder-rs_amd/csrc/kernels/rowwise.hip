@@ -38,6 +38,22 @@ __device__ __forceinline__ void load_row(const float* src, int D4, int lane, Row
     r.v[i] = in_row<NV>(i, lane, D4) ? ((const float4*)src)[i * 64 + lane] : make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
+// A residual-stream row stored as f16 (clipgpu_options.residual: 4 halves per lane slot, 8-byte
+// accesses); the values are widened to f32 for every add and statistic.
+typedef _Float16 Half4 __attribute__((ext_vector_type(4)));
+template <int NV>
+__device__ __forceinline__ void load_row(const _Float16* src, int D4, int lane, Row<NV>& r) {
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    if (in_row<NV>(i, lane, D4)) {
+      const Half4 h = ((const Half4*)src)[i * 64 + lane];
+      r.v[i] = make_float4((float)h[0], (float)h[1], (float)h[2], (float)h[3]);
+    } else {
+      r.v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+}
+
 // torch LayerNorm, two-pass mean / biased variance in f32; g, b preloaded rows.
 template <int NV>
 __device__ __forceinline__ void layer_norm_regs(const Row<NV>& in, Row<NV>& out, const Row<NV>& g, const Row<NV>& b,
@@ -113,6 +129,32 @@ __device__ __forceinline__ void store_row32(float* dst, const Row<NV>& r, int D4
   for (int i = 0; i < NV; ++i)
     if (in_row<NV>(i, lane, D4)) ((float4*)dst)[i * 64 + lane] = r.v[i];
 }
+// The residual row as the stream stores it (f16: every value rounded to f16, held as f32).
+template <typename XT, int NV>
+__device__ __forceinline__ void round_rowx(Row<NV>& r) {
+  if constexpr (!std::is_same<XT, float>::value) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      r.v[i].x = (float)(_Float16)r.v[i].x; r.v[i].y = (float)(_Float16)r.v[i].y;
+      r.v[i].z = (float)(_Float16)r.v[i].z; r.v[i].w = (float)(_Float16)r.v[i].w;
+    }
+  }
+}
+// residual-stream row store: f32, or rounded to f16
+template <int NV>
+__device__ __forceinline__ void store_rowx(float* dst, const Row<NV>& r, int D4, int lane) {
+  store_row32(dst, r, D4, lane);
+}
+template <int NV>
+__device__ __forceinline__ void store_rowx(_Float16* dst, const Row<NV>& r, int D4, int lane) {
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+    if (in_row<NV>(i, lane, D4)) {
+      Half4 h;
+      h[0] = (_Float16)r.v[i].x; h[1] = (_Float16)r.v[i].y; h[2] = (_Float16)r.v[i].z; h[3] = (_Float16)r.v[i].w;
+      ((Half4*)dst)[i * 64 + lane] = h;
+    }
+}
 
 template <int NV>
 __device__ __forceinline__ void add_row(Row<NV>& r, const Row<NV>& a) {
@@ -125,8 +167,8 @@ __device__ __forceinline__ void add_row(Row<NV>& r, const Row<NV>& a) {
 // Every kernel issues all of its row loads (activations and LN parameters) up front, so
 // their latencies overlap instead of following the reductions one round trip at a time.
 
-template <typename T, int NV>
-__global__ __launch_bounds__(256) void ln_rows_kernel(const float* __restrict__ x, const float* w, const float* b,
+template <typename T, int NV, typename XT>
+__global__ __launch_bounds__(256) void ln_rows_kernel(const XT* __restrict__ x, const float* w, const float* b,
                                                       float eps,
                                                       T* __restrict__ out, uint8_t* __restrict__ qs, int rows,
                                                       int D) {
@@ -153,8 +195,8 @@ __global__ __launch_bounds__(256) void ln_rows_kernel(const float* __restrict__ 
   }
 }
 
-template <typename T, int NV>
-__global__ __launch_bounds__(256) void vision_embed_ln_kernel(float* __restrict__ x, const float* cls,
+template <typename T, int NV, typename XT>
+__global__ __launch_bounds__(256) void vision_embed_ln_kernel(XT* __restrict__ x, const float* cls,
                                                               const float* pos, const float* lnpre_w,
                                                               const float* lnpre_b, const float* ln1_w,
                                                               const float* ln1_b, float eps, T* __restrict__ h,
@@ -177,15 +219,16 @@ __global__ __launch_bounds__(256) void vision_embed_ln_kernel(float* __restrict_
   load_row(ln1_w, D4, lane, g1);
   load_row(ln1_b, D4, lane, b1);
   layer_norm_regs(r, y, g0, b0, eps, D, lane);
-  store_row32(x + (long)row * D, y, D4, lane);
+  round_rowx<XT>(y);  // ln_1 of the residual row as stored
+  store_rowx(x + (long)row * D, y, D4, lane);
   layer_norm_regs(y, z, g1, b1, eps, D, lane);
   store_ln_out(h, qs, row, D, z, lane);
 }
 
-template <typename T, int NV>
+template <typename T, int NV, typename XT>
 __global__ __launch_bounds__(256) void text_embed_ln_kernel(const int64_t* __restrict__ ids, const float* tok,
                                                             const float* pos, const float* ln1_w,
-                                                            const float* ln1_b, float eps, float* __restrict__ x,
+                                                            const float* ln1_b, float eps, XT* __restrict__ x,
                                                             T* __restrict__ h, uint8_t* __restrict__ qs, int rows,
                                                             int Tctx, int D, int vocab) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -199,7 +242,8 @@ __global__ __launch_bounds__(256) void text_embed_ln_kernel(const int64_t* __res
   load_row(ln1_w, D4, lane, g);
   load_row(ln1_b, D4, lane, bb);
   add_row(e, p);
-  store_row32(x + (long)row * D, e, D4, lane);
+  round_rowx<XT>(e);  // ln_1 of the residual row as stored
+  store_rowx(x + (long)row * D, e, D4, lane);
   layer_norm_regs(e, y, g, bb, eps, D, lane);
   store_ln_out(h, qs, row, D, y, lane);
 }
@@ -223,8 +267,8 @@ __device__ inline int pooled_token(const int64_t* __restrict__ ids, int bi, int 
   return bidx;
 }
 
-template <typename T, int NV>
-__global__ __launch_bounds__(256) void pool_ln_kernel(const float* __restrict__ x,
+template <typename T, int NV, typename XT>
+__global__ __launch_bounds__(256) void pool_ln_kernel(const XT* __restrict__ x,
                                                       const int64_t* __restrict__ ids, int tokens, const float* w,
                                                       const float* b, float eps, T* __restrict__ out, int B, int D) {
   const int bi = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -241,17 +285,18 @@ __global__ __launch_bounds__(256) void pool_ln_kernel(const float* __restrict__ 
 
 // Last-layer compaction: the pooled token's residual row x and attention-output row h
 // (16-bit, raw bits) of each sequence, copied to row bi of xc / hc.  One wave per sequence.
-__global__ __launch_bounds__(256) void gather_pooled_kernel(const float* __restrict__ x,
+__global__ __launch_bounds__(256) void gather_pooled_kernel(const char* __restrict__ x,
                                                             const uint16_t* __restrict__ h,
                                                             const int64_t* __restrict__ ids, int tokens,
-                                                            float* __restrict__ xc, uint16_t* __restrict__ hc, int B,
-                                                            int D) {
+                                                            char* __restrict__ xc, uint16_t* __restrict__ hc, int B,
+                                                            int D, int xbytes) {
   const int bi = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (bi >= B) return;
   const long src = (long)bi * tokens + pooled_token(ids, bi, tokens, lane);
-  const float4* xs = (const float4*)(x + src * D);
-  float4* xd = (float4*)(xc + (long)bi * D);
-  for (int i = lane; i < D / 4; i += 64) xd[i] = xs[i];
+  const long rb = (long)D * xbytes;  // residual row bytes (f32 or f16), a multiple of 8
+  const uint2* xs = (const uint2*)(x + src * rb);
+  uint2* xd = (uint2*)(xc + (long)bi * rb);
+  for (int i = lane; i < rb / 8; i += 64) xd[i] = xs[i];
   const uint2* hs = (const uint2*)(h + src * D);
   uint2* hd = (uint2*)(hc + (long)bi * D);
   for (int i = lane; i < D / 4; i += 64) hd[i] = hs[i];
@@ -279,12 +324,13 @@ inline dim3 rows_grid(int rows) { return dim3((rows + 3) / 4); }
 }  // namespace
 
 // NV = ceil(D / 256) float4 per lane; D % 4 == 0, D <= 1280.
-#define CLIPGPU_ROW_LAUNCH(KERNEL, T, GRID, D, ...)                                                    \
+// KERNEL<T, NV, XT>: XT the residual-stream element type (float or _Float16).
+#define CLIPGPU_ROW_LAUNCH_X(KERNEL, T, XT, GRID, D, ...)                                              \
   do {                                                                                                  \
     const int nv_ = ((D) / 4 + 63) / 64;                                                                \
     auto go_ = [&](auto nvc) {                                                                          \
       constexpr int NVC = decltype(nvc)::value;                                                         \
-      hipLaunchKernelGGL((KERNEL<T, NVC>), GRID, dim3(256), 0, s, __VA_ARGS__);                         \
+      hipLaunchKernelGGL((KERNEL<T, NVC, XT>), GRID, dim3(256), 0, s, __VA_ARGS__);                     \
     };                                                                                                  \
     switch (nv_) {                                                                                      \
       case 1: go_(std::integral_constant<int, 1>{}); break;                                             \
@@ -294,9 +340,26 @@ inline dim3 rows_grid(int rows) { return dim3((rows + 3) / 4); }
       default: go_(std::integral_constant<int, 5>{}); break;                                            \
     }                                                                                                   \
   } while (0)
+// f(T*, XT*) with T the 16-bit type of dt and XT the residual-stream type (x16: _Float16, else float):
+// the four instantiations of a row kernel that touches the residual stream.
+template <typename F>
+inline void dispatch_dx(DType dt, int x16, F f) {
+  if (dt == DT_BF16) {
+    if (x16) f((__bf16*)nullptr, (_Float16*)nullptr);
+    else f((__bf16*)nullptr, (float*)nullptr);
+  } else {
+    if (x16) f((_Float16*)nullptr, (_Float16*)nullptr);
+    else f((_Float16*)nullptr, (float*)nullptr);
+  }
+}
+#define CLIPGPU_TX_TYPES                                  \
+  using T = std::remove_pointer_t<decltype(tp_)>;          \
+  using XT = std::remove_pointer_t<decltype(xp_)>;         \
+  (void)tp_;                                              \
+  (void)xp_
 
 // (16-bit output pointers are passed as void*: the kernel parameter is T*)
-hipError_t launch_ln_rows(DType dt, const float* x, const float* w, const float* b, float eps, void* out16,
+hipError_t launch_ln_rows(DType dt, const void* x, int x16, const float* w, const float* b, float eps, void* out16,
                           int rows, int D, hipStream_t s, uint8_t* qs) {
   if (D % 4 || D > 256 * MAXV || D <= 0 || (qs != nullptr && D % 32)) return hipErrorInvalidValue;
   // blocks: one row per wave, at most one resident round (8 blocks of 4 waves per CU); more rows
@@ -306,60 +369,54 @@ hipError_t launch_ln_rows(DType dt, const float* x, const float* w, const float*
   dim3 grid = rows_grid(rows);
   const int cap = device_cus() * 8;
   if ((int)grid.x > cap) grid.x = cap;
-  if (dt == DT_BF16) {
-    CLIPGPU_ROW_LAUNCH(ln_rows_kernel, __bf16, grid, D, x, w, b, eps, (__bf16*)out16, qs, rows, D);
-  } else {
-    CLIPGPU_ROW_LAUNCH(ln_rows_kernel, _Float16, grid, D, x, w, b, eps, (_Float16*)out16, qs, rows, D);
-  }
+  dispatch_dx(dt, x16, [&](auto tp_, auto xp_) {
+    CLIPGPU_TX_TYPES;
+    CLIPGPU_ROW_LAUNCH_X(ln_rows_kernel, T, XT, grid, D, (const XT*)x, w, b, eps, (T*)out16, qs, rows, D);
+  });
   return hipGetLastError();
 }
 
-hipError_t launch_vision_embed_ln(DType dt, float* x, const float* cls, const float* pos, const float* lnpre_w,
+hipError_t launch_vision_embed_ln(DType dt, void* x, int x16, const float* cls, const float* pos, const float* lnpre_w,
                                   const float* lnpre_b, const float* ln1_w, const float* ln1_b, float eps,
                                   void* h, int B, int tokens, int D, hipStream_t s, uint8_t* qs) {
   if (D % 4 || D > 256 * MAXV || D <= 0 || (qs != nullptr && D % 32)) return hipErrorInvalidValue;
   const int rows = B * tokens;
-  if (dt == DT_BF16) {
-    CLIPGPU_ROW_LAUNCH(vision_embed_ln_kernel, __bf16, rows_grid(rows), D, x, cls, pos, lnpre_w, lnpre_b, ln1_w, ln1_b, eps,
-                       (__bf16*)h, qs, rows, tokens, D);
-  } else {
-    CLIPGPU_ROW_LAUNCH(vision_embed_ln_kernel, _Float16, rows_grid(rows), D, x, cls, pos, lnpre_w, lnpre_b, ln1_w, ln1_b, eps,
-                       (_Float16*)h, qs, rows, tokens, D);
-  }
+  dispatch_dx(dt, x16, [&](auto tp_, auto xp_) {
+    CLIPGPU_TX_TYPES;
+    CLIPGPU_ROW_LAUNCH_X(vision_embed_ln_kernel, T, XT, rows_grid(rows), D, (XT*)x, cls, pos, lnpre_w, lnpre_b, ln1_w,
+                         ln1_b, eps, (T*)h, qs, rows, tokens, D);
+  });
   return hipGetLastError();
 }
 
 hipError_t launch_text_embed_ln(DType dt, const int64_t* ids, const float* tok, const float* pos,
-                                const float* ln1_w, const float* ln1_b, float eps, float* x, void* h, int B,
-                                int T, int D, int vocab, hipStream_t s, uint8_t* qs) {
+                                const float* ln1_w, const float* ln1_b, float eps, void* x, int x16, void* h,
+                                int B, int Tctx, int D, int vocab, hipStream_t s, uint8_t* qs) {
   if (D % 4 || D > 256 * MAXV || D <= 0 || (qs != nullptr && D % 32)) return hipErrorInvalidValue;
-  const int rows = B * T;
-  if (dt == DT_BF16) {
-    CLIPGPU_ROW_LAUNCH(text_embed_ln_kernel, __bf16, rows_grid(rows), D, ids, tok, pos, ln1_w, ln1_b, eps, x, (__bf16*)h,
-                       qs, rows, T, D, vocab);
-  } else {
-    CLIPGPU_ROW_LAUNCH(text_embed_ln_kernel, _Float16, rows_grid(rows), D, ids, tok, pos, ln1_w, ln1_b, eps, x, (_Float16*)h,
-                       qs, rows, T, D, vocab);
-  }
+  const int rows = B * Tctx;
+  dispatch_dx(dt, x16, [&](auto tp_, auto xp_) {
+    CLIPGPU_TX_TYPES;
+    CLIPGPU_ROW_LAUNCH_X(text_embed_ln_kernel, T, XT, rows_grid(rows), D, ids, tok, pos, ln1_w, ln1_b, eps, (XT*)x,
+                         (T*)h, qs, rows, Tctx, D, vocab);
+  });
   return hipGetLastError();
 }
 
-hipError_t launch_gather_pooled(const float* x, const void* h16, const int64_t* ids, int tokens, float* xc,
+hipError_t launch_gather_pooled(const void* x, int x16, const void* h16, const int64_t* ids, int tokens, void* xc,
                                 void* hc16, int B, int D, hipStream_t s) {
   if (D % 4 || D <= 0 || B <= 0 || tokens <= 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(gather_pooled_kernel, rows_grid(B), dim3(256), 0, s, x, (const uint16_t*)h16, ids, tokens, xc,
-                     (uint16_t*)hc16, B, D);
+  hipLaunchKernelGGL(gather_pooled_kernel, rows_grid(B), dim3(256), 0, s, (const char*)x, (const uint16_t*)h16, ids,
+                     tokens, (char*)xc, (uint16_t*)hc16, B, D, x16 ? 2 : 4);
   return hipGetLastError();
 }
 
-hipError_t launch_pool_ln(DType dt, const float* x, const int64_t* ids, int tokens,
+hipError_t launch_pool_ln(DType dt, const void* x, int x16, const int64_t* ids, int tokens,
                           const float* w, const float* b, float eps, void* out16, int B, int D, hipStream_t s) {
   if (D % 4 || D > 256 * MAXV || D <= 0) return hipErrorInvalidValue;
-  if (dt == DT_BF16) {
-    CLIPGPU_ROW_LAUNCH(pool_ln_kernel, __bf16, rows_grid(B), D, x, ids, tokens, w, b, eps, (__bf16*)out16, B, D);
-  } else {
-    CLIPGPU_ROW_LAUNCH(pool_ln_kernel, _Float16, rows_grid(B), D, x, ids, tokens, w, b, eps, (_Float16*)out16, B, D);
-  }
+  dispatch_dx(dt, x16, [&](auto tp_, auto xp_) {
+    CLIPGPU_TX_TYPES;
+    CLIPGPU_ROW_LAUNCH_X(pool_ln_kernel, T, XT, rows_grid(B), D, (const XT*)x, ids, tokens, w, b, eps, (T*)out16, B, D);
+  });
   return hipGetLastError();
 }
 

@@ -142,7 +142,7 @@ int clipgpu_test_layernorm(int dtype, int64_t rows, int64_t D, float eps, const 
     up(dx.p, x, rows * D * 4);
     up(dw.p, w, D * 4);
     up(db.p, b, D * 4);
-    TCHECK(launch_ln_rows(dt, dx.as<float>(), dw.as<float>(), db.as<float>(), eps, dO.p, (int)rows, (int)D, nullptr));
+    TCHECK(launch_ln_rows(dt, dx.as<float>(), 0, dw.as<float>(), db.as<float>(), eps, dO.p, (int)rows, (int)D, nullptr));
     TCHECK(hipDeviceSynchronize());
     down16(dt, out, dO.p, rows * D);
   });
@@ -340,7 +340,7 @@ int clipgpu_test_layernorm_mx(int64_t rows, int64_t D, float eps, const float* x
     up(dx.p, x, rows * D * 4);
     up(dw.p, w, D * 4);
     up(db.p, b, D * 4);
-    TCHECK(launch_ln_rows(DT_BF16, dx.as<float>(), dw.as<float>(), db.as<float>(), eps, dq.p, (int)rows, (int)D,
+    TCHECK(launch_ln_rows(DT_BF16, dx.as<float>(), 0, dw.as<float>(), db.as<float>(), eps, dq.p, (int)rows, (int)D,
                           nullptr, ds.as<uint8_t>()));
     TCHECK(hipDeviceSynchronize());
     down(q, dq.p, rows * D);

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define CLIPGPU_ABI_VERSION 3
+#define CLIPGPU_ABI_VERSION 4
 
 enum clipgpu_status {
   CLIPGPU_OK = 0,
@@ -83,6 +83,8 @@ void clipgpu_destroy(clipgpu_engine* e);
 #define CLIPGPU_MX_QKV 1u  /* fp8 engines: the QKV projection runs as an MX-fp8 GEMM */
 #define CLIPGPU_MX_FC 2u   /* c_fc */
 #define CLIPGPU_MX_PROJ 4u /* c_proj (needs CLIPGPU_MX_FC: c_fc's epilogue quantizes the hidden rows) */
+#define CLIPGPU_RESIDUAL_F32 1
+#define CLIPGPU_RESIDUAL_F16 2
 typedef struct clipgpu_options {
   uint32_t struct_size; /* sizeof(clipgpu_options) (set by clipgpu_options_init); an older caller's
                            smaller struct keeps the defaults of the fields it does not have */
@@ -110,6 +112,11 @@ typedef struct clipgpu_options {
                            run every GEMM in bf16; 0 = every layer (default).  Layers 0..31 only (a
                            tower's layers >= 32 run bf16 under a non-zero mask); a bit at or beyond the
                            tower's layer count is refused (CLIPGPU_ERR_INVALID) */
+  /* ---- ABI v4 (round 5) */
+  int32_t residual;     /* storage of the residual stream x: 0 = the default (CLIPGPU_RESIDUAL_F32), 1 = f32,
+                           2 = f16 (half the bytes of x's two read-modify-writes and two LayerNorm reads per
+                           layer; every add into x and every LayerNorm statistic stays f32; bf16 / f16
+                           engines of the CLIP family only, else CLIPGPU_ERR_INVALID) */
 } clipgpu_options;
 /* Fills *opts with the defaults. */
 int clipgpu_options_init(clipgpu_options* opts);

@@ -35,7 +35,7 @@ def test_library_exports_every_declared_symbol():
     missing = [n for n in names if not hasattr(L, n)]
     assert not missing, missing
     assert set(_lib.SYMBOLS) == names  # the ctypes binding covers exactly the headers
-    assert L.clipgpu_abi_version() == 3
+    assert L.clipgpu_abi_version() == 4
 
 
 def test_no_oracle_in_product():
@@ -203,7 +203,7 @@ def test_bench_names_every_gemm_tile():
 
 
 def test_engine_reads_no_environment():
-    """ABI v3: every engine behaviour is a clipgpu_options field; the product sources read no
+    """ABI v3+: every engine behaviour is a clipgpu_options field; the product sources read no
     environment variable (the kernel-level test hooks in testing.hip take CLIPGPU_TEST_TILE only)."""
     csrc = os.path.join(ROOT, "clip-embedder-rs_amd", "csrc")
     for dirpath, _, files in os.walk(csrc):
@@ -254,7 +254,7 @@ def test_options_init_and_validation():
     rc = _lib.lib().clipgpu_create_ex(d.encode(), 0, devs, 1, 0, 8, ctypes.byref(o), ctypes.byref(h))
     assert rc != 0 and b"struct_size" in _lib.lib().clipgpu_last_error()
     # only the published struct sizes (v2: through `communicator`; v3): not one ending inside a field
-    for bad in (Options.graphs.offset + 2, ctypes.sizeof(Options) - 4, 8):
+    for bad in (Options.graphs.offset + 2, ctypes.sizeof(Options) - 2, 8):
         o.struct_size = bad
         rc = _lib.lib().clipgpu_create_ex(d.encode(), 0, devs, 1, 0, 8, ctypes.byref(o), ctypes.byref(h))
         assert rc != 0 and b"struct_size" in _lib.lib().clipgpu_last_error(), bad
@@ -262,6 +262,17 @@ def test_options_init_and_validation():
     for bad in ([32], [40], [0, 33], 1 << 32):
         with pytest.raises(ValueError, match="mx_layers"):
             Engine(d, 0, [0], "fp8", 8, mx_layers=bad)
+    # residual stream storage (ABI v4): f32 / f16, f16 only for bf16 / f16 CLIP-family engines
+    with pytest.raises(ValueError, match="residual"):
+        Engine(d, 0, [0], "bf16", 8, residual="bf16")
+    with pytest.raises(ClipError, match="residual = f16"):
+        Engine(d, 0, [0], "fp8", 8, residual="f16")
+    o3 = Options()
+    _lib.check(_lib.lib().clipgpu_options_init(ctypes.byref(o3)))
+    assert o3.residual == 0
+    o3.residual = 3
+    rc = _lib.lib().clipgpu_create_ex(d.encode(), 0, devs, 1, 0, 8, ctypes.byref(o3), ctypes.byref(h))
+    assert rc != 0 and b"residual" in _lib.lib().clipgpu_last_error()
     tiny_layers = json.load(open(os.path.join(d, "open_clip_config.json")))["model_cfg"]["vision_cfg"]["layers"]
     with pytest.raises(ClipError, match="beyond the tower"):
         Engine(d, 0, [0], "fp8", 8, mx_layers=[tiny_layers])

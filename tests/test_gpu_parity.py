@@ -78,6 +78,34 @@ def test_text_parity(cfg, B, random_eot, dtype):
     check_rows(got, oracle_text(cfg, 1234, ids))
 
 
+@pytest.mark.parametrize("residual", ["f32", "f16"])
+@pytest.mark.parametrize("dtype", ["bf16", "f16"])
+def test_residual_stream_storage_parity(residual, dtype):
+    """clipgpu_options.residual (ABI v4): the residual stream stored in f32 or in f16 (every add and
+    LayerNorm statistic in f32).  Both towers at ViT-B/32 dims against the fp64 oracle at the
+    north-star bar, the lanes / pruning / trimming paths included (a batch over max_batch, host ids
+    with random EOTs), and f16 within 2e-5 of the f32 stream's cosine to the oracle."""
+    v, t = specs(VIT_B_32_CFG)
+    u8 = weights.synth_images_u8(41, 9, v.image_size)
+    px = normalized_pixels(u8, OPENAI_MEAN, OPENAI_STD)
+    ids = weights.synth_token_ids(41, 9, t.context_length, t.vocab_size, t.vocab_size - 2, t.vocab_size - 1,
+                                  random_eot=True)
+    ref_v, ref_t = oracle_vision(VIT_B_32_CFG, 1234, px), oracle_text(VIT_B_32_CFG, 1234, ids)
+    cos = {}
+    for res in ("f32", residual):
+        ve = engine(VIT_B_32_CFG, 0, dtype=dtype, max_batch=8, residual=res)
+        te = engine(VIT_B_32_CFG, 1, dtype=dtype, max_batch=8, residual=res)
+        cos[res] = (check_rows(ve.embed_pixels(px), ref_v).min(), check_rows(te.embed_tokens(ids), ref_t).min())
+        # the device-resident path (graphs, lanes) gives the same rows as the host path
+        import torch
+        d_px = torch.from_numpy(px[:8]).cuda()
+        out = torch.empty((8, 512), device="cuda")
+        ve.embed_pixels_device(d_px.data_ptr(), 8, out.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy(), ve.embed_pixels(px[:8]))
+    assert cos[residual][0] >= cos["f32"][0] - 2e-5 and cos[residual][1] >= cos["f32"][1] - 2e-5, cos
+
+
 def test_vision_u8_path_matches_f32_path():
     v, _ = specs(VIT_B_32_CFG)
     u8 = weights.synth_images_u8(21, 3, v.image_size)
