@@ -379,9 +379,6 @@ def main():
                          "shader clock of each window, and the c_fc launch time per window); 0 skips them")
     ap.add_argument("--residual", default=None, choices=["f32", "f16"],
                     help="the residual stream's storage (clipgpu_options.residual; default: the library's)")
-    ap.add_argument("--lane-offset", type=int, default=-1,
-                    help="A/B runs: hold lane 1 this many trunk op slots behind lane 0 (clipgpu_test_lane_offset; "
-                         "-1 = the library's default)")
     ap.add_argument("--gather", action="store_true",
                     help="N = 1: run the data-parallel path anyway (gloo control plane, the engine's RCCL "
                          "communicator, gathered entry points) -- a one-GPU rehearsal of N > 1")
@@ -412,8 +409,6 @@ def main():
         pins = [int(t) for t in args.tiles.split(",")]
         vopts.update(gemm_tiles=pins, patch_tile=pins[3])
     ve = Engine(mdir, _lib.TOWER_VISION, [local], args.dtype, B_VISION, **vopts)
-    if args.lane_offset >= 0:
-        _lib.check(_lib.lib().clipgpu_test_lane_offset(ve._h, args.lane_offset))
     if dp:
         init_engine_comm(ve)
     px, ids = synth_inputs(rank, dev)
@@ -569,8 +564,6 @@ def main():
         if args.text_tiles:
             topts["gemm_tiles"] = [int(t) for t in args.text_tiles.split(",")]
         te = Engine(mdir, _lib.TOWER_TEXT, [local], args.dtype, B_TEXT, **topts)
-        if args.lane_offset >= 0:
-            _lib.check(_lib.lib().clipgpu_test_lane_offset(te._h, args.lane_offset))
         if dp:
             init_engine_comm(te)
         tout_full = torch.empty((world * B_TEXT, 512), device=dev, dtype=torch.float32)

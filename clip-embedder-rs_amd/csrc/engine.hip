@@ -134,12 +134,6 @@ struct Replica {
   // ncclCommInitRank for one-process-per-GPU deployments (clipgpu_comm_init_rank).
   ncclComm_t comm = nullptr;
   hipEvent_t coll = nullptr;  // recorded behind this replica's last collective (destroy_comms waits for it)
-  // Lane offset (clipgpu_engine::lane_offset): the trunk's op slots of lane 0 record stage_ev[slot];
-  // lane 1's slot k waits for lane 0's slot k + offset.  lane_id: the lane a view runs (run_lanes'
-  // concurrent lanes: 0, 1, ...; -1 otherwise).
-  hipEvent_t* stage_ev = nullptr;
-  int n_stage_ev = 0;
-  int lane_id = -1;
 };
 
 // Replayable forwards: one hipGraphExec per (entry point, input / output buffers, batch,
@@ -213,11 +207,7 @@ struct clipgpu_engine {
   // stays f32.  bf16 / f16 engines of the CLIP family only (fp8 engines' MX residual epilogue and the
   // SigLIP MAP head take the f32 stream).
   bool x16 = false;
-  // Concurrent lanes run identical op chains and, left alone, stay in lockstep: both lanes' LayerNorms and
-  // attentions run side by side and nothing hides them (the round-5 timeline).  lane_offset > 0 holds
-  // lane 1 that many trunk op slots (7 per layer) behind lane 0, so one lane's memory-bound ops run beside
-  // the other's GEMMs.  Speed only: the ops and their operands are unchanged (bit-identical).
-  int lane_offset = 0;
+
   int tuning = 0;  // clipgpu_options.tuning: 1 = timing tuner (+ whole-forward pass), 2 = per-site pass only
   // clipgpu_options.gemm_tiles / patch_tile pins (0 = the table's tile, -1 = the shape heuristic)
   int pin_tiles[4] = {0, 0, 0, 0};
@@ -551,9 +541,6 @@ void alloc_workspace(clipgpu_engine& e, Replica& r) {
     HIP_CHECK(hipEventCreateWithFlags(&r.done[i], hipEventDisableTiming));
     HIP_CHECK(hipEventCreateWithFlags(&r.copied[i], hipEventDisableTiming));
   }
-  r.n_stage_ev = 7 * std::max(1, e.spec.layers);
-  r.stage_ev = new hipEvent_t[r.n_stage_ev];
-  for (int i = 0; i < r.n_stage_ev; ++i) HIP_CHECK(hipEventCreateWithFlags(&r.stage_ev[i], hipEventDisableTiming));
   HIP_CHECK(hipStreamCreateWithFlags(&r.copy, hipStreamNonBlocking));
   HIP_CHECK(hipStreamCreateWithFlags(&r.copy2, hipStreamNonBlocking));
   HIP_CHECK(hipEventCreateWithFlags(&r.fork, hipEventDisableTiming));
@@ -627,7 +614,7 @@ inline void* xrows(const clipgpu_engine& e, void* x, size_t rows) {
 }
 
 // clipgpu_options.residual = 0: the residual stream's default storage
-constexpr int kResidualDefault = CLIPGPU_RESIDUAL_F32;
+constexpr int kResidualDefault = CLIPGPU_RESIDUAL_F16;
 
 int site_epi(int site) { return (site == GS_OUT || site == GS_PROJ) ? EPI_RESID : EPI_STORE16; }
 
@@ -742,17 +729,6 @@ PoolSrc trunk(const clipgpu_engine& e, const Replica& r, int B, int causal, cons
   const TowerSpec& s = e.spec;
   const int D = s.width;
   const bool prune = prune_last(e, B, T);
-  // lane offset (clipgpu_engine::lane_offset): slot k = 7 l + {qkv, attention, out_proj, ln_2, c_fc, c_proj, ln_1}
-  const bool sync0 = e.lane_offset > 0 && r.lane_id == 0 && r.stage_ev != nullptr;
-  const bool sync1 = e.lane_offset > 0 && r.lane_id == 1 && r.stage_ev != nullptr;
-  auto slot_begin = [&](int l, int o) {
-    const int k = 7 * l + o + e.lane_offset;
-    if (sync1 && k < r.n_stage_ev) HIP_CHECK(hipStreamWaitEvent(st, r.stage_ev[k], 0));
-  };
-  auto slot_end = [&](int l, int o) {
-    const int k = 7 * l + o;
-    if (sync0 && k < r.n_stage_ev) HIP_CHECK(hipEventRecord(r.stage_ev[k], st));
-  };
   for (int l = 0; l < s.layers; ++l) {
     const LayerW& L = r.w.layers[l];
     const bool compact = prune && l + 1 == s.layers;
@@ -772,10 +748,7 @@ PoolSrc trunk(const clipgpu_engine& e, const Replica& r, int B, int causal, cons
       g.tile = tuned ? e.tile[site] : TILE_AUTO;
       check(launch_gemm(e.dt, A_ROWS, site_epi(site), site == GS_FC ? s.act : ACT_NONE, g, st), what);
     };
-    slot_begin(l, 0);
     gemm(GS_QKV, PC_QKV, "qkv gemm");
-    slot_end(l, 0);
-    slot_begin(l, 1);
     if (!ABLATED(1)) { ProfScope ps(e, PC_ATTN, st);
       check(launch_attention(e.dt, r.big, r.h, B, T, s.heads, D, causal, st), "attention"); }
     if (compact) {  // pooled rows only from here on (QKV in `big` is dead after attention)
@@ -788,30 +761,19 @@ PoolSrc trunk(const clipgpu_engine& e, const Replica& r, int B, int causal, cons
                                  B, D, st),
             "gather pooled rows");
     }
-    slot_end(l, 1);
-    slot_begin(l, 2);
     gemm(GS_OUT, PC_OUT_PROJ, "out_proj gemm");
-    slot_end(l, 2);
-    slot_begin(l, 3);
     if (!ABLATED(0)) {
       ProfScope ps(e, compact ? PC_TAIL : PC_LN, st);
       check(launch_ln_rows(e.dt, c.x, e.x16, L.ln2_w, L.ln2_b, s.ln_eps, c.h, rows, D, st, ln_q(e, l, GS_FC, c.hs)),
             "ln_2");
     }
-    slot_end(l, 3);
-    slot_begin(l, 4);
     gemm(GS_FC, PC_C_FC, "c_fc gemm");
-    slot_end(l, 4);
-    slot_begin(l, 5);
     gemm(GS_PROJ, PC_C_PROJ, "c_proj gemm");
-    slot_end(l, 5);
-    slot_begin(l, 6);
     if (l + 1 < s.layers && !ABLATED(0)) {
       ProfScope ps(e, PC_LN, st);
       check(launch_ln_rows(e.dt, r.x, e.x16, r.w.layers[l + 1].ln1_w, r.w.layers[l + 1].ln1_b, s.ln_eps, r.h, rows, D, st,
                            ln_q(e, l + 1, GS_QKV, r.hs)), "ln_1");
     }
-    slot_end(l, 6);
     if (compact) return PoolSrc{c.x, 1, nullptr};
   }
   return PoolSrc{xrows(e, r.x, pool_pos), T, ids};
@@ -1129,9 +1091,7 @@ void run_lanes(const clipgpu_engine& e, const Replica& r, int B, hipStream_t st,
     int b0, b1;
     lane_range(B, L, i, b0, b1);
     HIP_CHECK(hipStreamWaitEvent(r.lane[i], r.fork, 0));
-    Replica v = lane_view(e, r, b0);
-    v.lane_id = i;
-    fwd(v, b0, b1 - b0, r.lane[i]);
+    fwd(lane_view(e, r, b0), b0, b1 - b0, r.lane[i]);
     HIP_CHECK(hipEventRecord(r.join[i], r.lane[i]));
   }
   for (int i = 0; i < L; ++i) HIP_CHECK(hipStreamWaitEvent(st, r.join[i], 0));
@@ -1153,10 +1113,11 @@ void run_graph(const clipgpu_engine& e, const Replica& r, const std::vector<uint
   hipStream_t gs = own ? st : r.stream;
   GraphCache& gc = *r.graphs;
   hipGraphExec_t exec = nullptr;
-  std::vector<uint64_t> key = key_in;
-  key.push_back(0x1A9E0000u | (uint64_t)e.lane_offset);  // the lane offset shapes the captured graph
 #ifdef CLIPGPU_ABLATE
+  std::vector<uint64_t> key = key_in;
   key.push_back(0xAB1A7E00u | g_ablate);
+#else
+  const std::vector<uint64_t>& key = key_in;
 #endif
   ++gc.clock;
   for (auto& en : gc.entries)
@@ -1812,11 +1773,6 @@ void destroy_replica(Replica& r) {
     if (r.done2[i]) (void)hipEventDestroy(r.done2[i]);
     if (r.copied2[i]) (void)hipEventDestroy(r.copied2[i]);
   }
-  if (r.stage_ev) {
-    for (int i = 0; i < r.n_stage_ev; ++i) (void)hipEventDestroy(r.stage_ev[i]);
-    delete[] r.stage_ev;
-    r.stage_ev = nullptr;
-  }
   if (r.fork) (void)hipEventDestroy(r.fork);
   if (r.gin) (void)hipEventDestroy(r.gin);
   if (r.gout) (void)hipEventDestroy(r.gout);
@@ -2384,15 +2340,6 @@ int clipgpu_test_force_broadcast(clipgpu_engine* e, int on) {
     if (!e) throw ClipErr(CLIPGPU_ERR_INVALID, "engine is NULL");
     std::lock_guard<std::mutex> lk(e->mu);
     e->force_bcast = on != 0;
-  });
-}
-
-// Lane offset of the concurrent-lane forward in trunk op slots (clipgpu_engine::lane_offset; 0 = none).
-int clipgpu_test_lane_offset(clipgpu_engine* e, int slots) {
-  return guarded([&]() {
-    if (!e || slots < 0 || slots > 64) throw ClipErr(CLIPGPU_ERR_INVALID, "lane offset: 0..64 slots");
-    std::lock_guard<std::mutex> lk(e->mu);
-    e->lane_offset = slots;
   });
 }
 

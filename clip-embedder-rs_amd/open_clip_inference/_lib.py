@@ -79,7 +79,6 @@ _PROTOS = [
     ("clipgpu_test_host_plan", c_int, [c_void_p, c_int, POINTER(c_int), c_int]),
     ("clipgpu_test_force_broadcast", c_int, [c_void_p, c_int]),
     ("clipgpu_test_comm_lazy", c_int, [c_void_p]),
-    ("clipgpu_test_lane_offset", c_int, [c_void_p, c_int]),
     ("clipgpu_test_profile_timeline", c_int, [c_void_p, c_int64, POINTER(c_double), POINTER(c_double), POINTER(c_int),
                                               POINTER(c_int), POINTER(c_int64)]),
     ("clipgpu_test_gather_plan", c_int, [c_int, POINTER(c_int64), POINTER(c_int64), POINTER(c_int)]),

@@ -113,10 +113,10 @@ typedef struct clipgpu_options {
                            tower's layers >= 32 run bf16 under a non-zero mask); a bit at or beyond the
                            tower's layer count is refused (CLIPGPU_ERR_INVALID) */
   /* ---- ABI v4 (round 5) */
-  int32_t residual;     /* storage of the residual stream x: 0 = the default (CLIPGPU_RESIDUAL_F32), 1 = f32,
-                           2 = f16 (half the bytes of x's two read-modify-writes and two LayerNorm reads per
-                           layer; every add into x and every LayerNorm statistic stays f32; bf16 / f16
-                           engines of the CLIP family only, else CLIPGPU_ERR_INVALID) */
+  int32_t residual;     /* storage of the residual stream x: 1 = f32; 2 = f16 (half the bytes of x's two
+                           read-modify-writes and two LayerNorm reads per layer; every add into x and every
+                           LayerNorm statistic stays f32; bf16 / f16 engines of the CLIP family only, else
+                           CLIPGPU_ERR_INVALID); 0 = the default: f16 where it applies, else f32 */
 } clipgpu_options;
 /* Fills *opts with the defaults. */
 int clipgpu_options_init(clipgpu_options* opts);

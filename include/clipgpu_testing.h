@@ -129,9 +129,6 @@ int clipgpu_test_force_broadcast(struct clipgpu_engine* e, int on);
 /* A handle without a communicator takes the multi-device handle's lazy path: a clique over its
  * replicas' distinct devices, created (ncclCommInitAll) by the first gathered call. */
 int clipgpu_test_comm_lazy(struct clipgpu_engine* e);
-/* Concurrent-lane forwards: lane 1 runs `slots` trunk op slots (7 per layer: qkv, attention, out_proj,
- * ln_2, c_fc, c_proj, ln_1) behind lane 0 (event waits; 0 = free-running lanes).  Speed only. */
-int clipgpu_test_lane_offset(struct clipgpu_engine* e, int slots);
 /* The launches recorded by clipgpu_profile_enable as a timeline: up to n_max entries of start / end
  * (ms from the first recorded start), category (clipgpu_profile_category_name) and lane (the device
  * lane stream index, -1 for another stream); *n_out = the number recorded.  Consumes the records as
