@@ -253,9 +253,9 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
     mfma_block(std::false_type{}, a1, b1);
   };
 
-  // x16c: the residual stream (EPI_RESID's out, EPI_PATCH's out) is f16 (GemmParams.x16), else f32
-  auto epilogue = [&](auto x16c, int m0, int n0, int bpar) {
-    typedef typename std::conditional<decltype(x16c)::value, _Float16, float>::type XE;
+  // XE: the residual stream's element type (EPI_RESID16 / EPI_PATCH16: f16, else f32)
+  auto epilogue = [&](int m0, int n0, int bpar) {
+    typedef typename std::conditional<epi_x16(EPI), _Float16, float>::type XE;
     const int G2 = p.G * p.G;
     // EPI_RESID: the residual rows of column block ni+1 are loaded before block ni
     // is stored, so no load waits behind this epilogue's own stores.
@@ -268,10 +268,10 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
         if (m < p.M && n + 4 <= p.N) dst[mi] = ldx4((const XE*)p.out + (long)m * p.ldo + n);
       }
     };
-    if constexpr (EPI == EPI_RESID) load_x(0, xr[0]);
+    if constexpr (epi_resid(EPI)) load_x(0, xr[0]);
 #pragma unroll
     for (int ni = 0; ni < NI; ++ni) {
-      if constexpr (EPI == EPI_RESID) {
+      if constexpr (epi_resid(EPI)) {
         if (ni + 1 < NI) load_x(ni + 1, xr[(ni + 1) & 1]);
       }
       const int n = n0 + wn + ni * 16 + fq * 4;
@@ -312,9 +312,9 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
               if (n + j < p.N) o[j] = to16<T>(apply_act<ACT>(v[j]));
           }
         } else {
-          XE* o;  // (EPI_STORE32: f32 output, x16c false)
+          XE* o;  // (EPI_STORE32: f32 output)
           const float* ps = nullptr;
-          if constexpr (EPI == EPI_PATCH) {
+          if constexpr (epi_patch(EPI)) {
             const int b = m / G2, pp = m - b * G2;
             o = (XE*)p.out + ((long)b * (G2 + p.cls) + p.cls + pp) * p.ldo + n;
             ps = p.pos + (long)(p.cls + pp) * p.N + n;
@@ -323,10 +323,10 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
           }
           if (nfull) {
             float4 w = make_float4(v[0], v[1], v[2], v[3]);
-            if constexpr (EPI == EPI_RESID) {
+            if constexpr (epi_resid(EPI)) {
               const float4 x = xr[ni & 1][mi];
               w.x += x.x; w.y += x.y; w.z += x.z; w.w += x.w;
-            } else if constexpr (EPI == EPI_PATCH) {
+            } else if constexpr (epi_patch(EPI)) {
               const float4 x = *(const float4*)ps;
               w.x += x.x; w.y += x.y; w.z += x.z; w.w += x.w;
             }
@@ -335,8 +335,8 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
             for (int j = 0; j < 4; ++j) {
               if (n + j >= p.N) continue;
               float r = v[j];
-              if constexpr (EPI == EPI_RESID) r += (float)o[j];
-              if constexpr (EPI == EPI_PATCH) r += ps[j];
+              if constexpr (epi_resid(EPI)) r += (float)o[j];
+              if constexpr (epi_patch(EPI)) r += ps[j];
               o[j] = (XE)r;
             }
           }
@@ -396,12 +396,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
     else compute(std::false_type{}, cur1 ? sA1 : sA0, cur1 ? sB1 : sB0);
     GEMM_STAMP(4 + ti * 4);
     vm_wait<0>();  // the next tile's stage 0 lands before the epilogue's stores (see gemm_pipe_kernel)
-    if constexpr (EPI == EPI_RESID || EPI == EPI_PATCH) {
-      if (p.x16) epilogue(std::true_type{}, m0, n0, bias_par);
-      else epilogue(std::false_type{}, m0, n0, bias_par);
-    } else {
-      epilogue(std::false_type{}, m0, n0, bias_par);
-    }
+    epilogue(m0, n0, bias_par);
     // Retire the next tile's stage-0 glds but not this tile's output stores
     // (issued after them; in-order vmcnt): a full tile issues exactly MI*NI
     // epilogue stores per lane, a partial one may issue fewer -> wait for all.
@@ -750,9 +745,9 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
   };
 
   // ---- epilogue: lane owns row wm+mi*16+fr, columns nc .. nc+4*NI-1 ------------
-  // x16c: the residual stream (EPI_RESID's out, EPI_PATCH's out) is f16 (GemmParams.x16), else f32
-  auto epilogue = [&](auto x16c, int m0, int n0, int bpar) {
-    typedef typename std::conditional<decltype(x16c)::value, _Float16, float>::type XE;
+  // XE: the residual stream's element type (EPI_RESID16 / EPI_PATCH16: f16, else f32)
+  auto epilogue = [&](int m0, int n0, int bpar) {
+    typedef typename std::conditional<epi_x16(EPI), _Float16, float>::type XE;
     const int nc = n0 + wn + fq * (4 * NI);
     const bool nfull = nc + 4 * NI <= p.N;
     f32x4 bias[NI];
@@ -767,10 +762,10 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
     }
     // EPI_RESID adds the residual row x[m]; EPI_PATCH writes patch p of image b to token
     // row b*(G2+cls) + cls + p and adds pos[cls + p].
-    constexpr bool ADDX = EPI == EPI_RESID || EPI == EPI_PATCH;
+    constexpr bool ADDX = epi_resid(EPI) || epi_patch(EPI);
     const int G2 = p.G * p.G;
     auto out_row = [&](int m) -> long {
-      if constexpr (EPI == EPI_PATCH) {
+      if constexpr (epi_patch(EPI)) {
         const int b = m / G2;
         return ((long)b * (G2 + p.cls) + p.cls + (m - b * G2)) * p.ldo;
       } else {
@@ -779,7 +774,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
     };
     // the rows added in: the positional embedding (f32) for EPI_PATCH, the residual row (XE) for EPI_RESID
     auto add_src = [&](int m) {
-      if constexpr (EPI == EPI_PATCH) return p.pos + (long)(p.cls + m % G2) * p.N + nc;
+      if constexpr (epi_patch(EPI)) return p.pos + (long)(p.cls + m % G2) * p.N + nc;
       else return (const XE*)p.out + (long)m * p.ldo + nc;
     };
     // The rows added in (residual x / positional embedding) are loaded before the epilogue math:
@@ -860,7 +855,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
               if (nc + ni * 4 + j < p.N) o[ni * 4 + j] = to16<T>(apply_act<ACT>(v[ni][j]));
         }
       } else {
-        XE* o = (XE*)p.out + out_row(m) + nc;  // (EPI_STORE32: f32, x16c false)
+        XE* o = (XE*)p.out + out_row(m) + nc;  // (EPI_STORE32: f32)
         if (nfull) {
 #pragma unroll
           for (int ni = 0; ni < NI; ++ni) {
@@ -885,11 +880,10 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
       }
     }
   };
-  constexpr bool ADDX_EPI = EPI == EPI_RESID || EPI == EPI_PATCH;  // epilogues that touch the residual stream
   // vm ops a full tile's epilogue leaves in flight behind the DMA of the step after it (the same
   // count on both paths: MI NI / 2 16-byte stores of 16-bit values, MI NI of f32, + as many loads)
   constexpr int EPI_VM = EPI == EPI_STORE16 ? (NI % 2 ? MI * NI : MI * NI / 2)
-                                            : ((EPI == EPI_RESID || EPI == EPI_PATCH) ? 2 * MI * NI : MI * NI);
+                                            : ((epi_resid(EPI) || epi_patch(EPI)) ? 2 * MI * NI : MI * NI);
   // 3 stages: retire all but this wave's DMA pieces of the youngest step (+ X more recent vm ops):
   // NP pieces per step on waves < PT % NW (or every wave when the split is even), else NP - 1
   auto vm_wait_step = [&](auto xc) {
@@ -966,12 +960,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
     if constexpr (NS == 3) vm_wait_step(std::integral_constant<int, 0>{});
     else vm_wait<0>();
 #endif
-    if constexpr (ADDX_EPI) {
-      if (p.x16) epilogue(std::true_type{}, m0, n0, ti & 1);
-      else epilogue(std::false_type{}, m0, n0, ti & 1);
-    } else {
-      epilogue(std::false_type{}, m0, n0, ti & 1);
-    }
+    epilogue(m0, n0, ti & 1);
     // partial tiles and half tiles issue fewer vm ops than EPI_VM: drain them
     after_full_epi = m0 + BM <= p.M && n0 + BN <= p.N && (!HM || t < hm_F);
     if (!after_full_epi) vm_wait<0>();
@@ -1124,22 +1113,14 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmParams p) {
     for (int j = 0; j < 4; ++j) o[j] = to16<T>(apply_act<ACT>(v[j]));
     *(typename Vec4<T>::type*)((T*)p.out + (long)m * p.ldo + n) = o;
   } else {
+    typedef typename std::conditional<epi_x16(EPI), _Float16, float>::type XE;  // (EPI_STORE32: f32)
+    XE* o = (XE*)p.out + (long)m * p.ldo + n;
     float4 r = make_float4(v[0], v[1], v[2], v[3]);
-    if constexpr (EPI == EPI_RESID) {
-      if (p.x16) {  // the residual stream in f16
-        _Float16* o = (_Float16*)p.out + (long)m * p.ldo + n;
-        const float4 x = ldx4(o);
-        r.x += x.x; r.y += x.y; r.z += x.z; r.w += x.w;
-        stx4(o, r);
-        return;
-      }
-    }
-    float* o = (float*)p.out + (long)m * p.ldo + n;
-    if constexpr (EPI == EPI_RESID) {
-      const float4 x = *(const float4*)o;
+    if constexpr (epi_resid(EPI)) {
+      const float4 x = ldx4(o);
       r.x += x.x; r.y += x.y; r.z += x.z; r.w += x.w;
     }
-    *(float4*)o = r;
+    stx4(o, r);
   }
 }
 
@@ -1159,7 +1140,7 @@ hipError_t launch_skinny(const GemmParams& p, hipStream_t s) {
 
 template <typename T, int EPI, int ACT>
 hipError_t launch_tile(const GemmParams& p, hipStream_t s) {
-  if constexpr (EPI != EPI_PATCH) {
+  if constexpr (!epi_patch(EPI)) {
     if ((p.tile == TILE_AUTO || p.tile == TILE_SKINNY) && skinny_ok(p)) return launch_skinny<T, EPI, ACT>(p, s);
   }
   if (p.tile == TILE_SKINNY) return hipErrorInvalidValue;
@@ -1193,9 +1174,11 @@ hipError_t launch_typed(int epi, int act, const GemmParams& p, hipStream_t s) {
         case ACT_GELU_TANH: return launch_tile<T, EPI_STORE16, ACT_GELU_TANH>(p, s);
       }
       break;
-    case EPI_RESID: return launch_tile<T, EPI_RESID, ACT_NONE>(p, s);
+    case EPI_RESID:  // the residual stream: f32, or f16 (GemmParams.x16)
+      return p.x16 ? launch_tile<T, EPI_RESID16, ACT_NONE>(p, s) : launch_tile<T, EPI_RESID, ACT_NONE>(p, s);
     case EPI_STORE32: return launch_tile<T, EPI_STORE32, ACT_NONE>(p, s);
-    case EPI_PATCH: return launch_tile<T, EPI_PATCH, ACT_NONE>(p, s);  // rows from launch_patch_rows
+    case EPI_PATCH:  // rows from launch_patch_rows
+      return p.x16 ? launch_tile<T, EPI_PATCH16, ACT_NONE>(p, s) : launch_tile<T, EPI_PATCH, ACT_NONE>(p, s);
   }
   return hipErrorInvalidValue;
 }

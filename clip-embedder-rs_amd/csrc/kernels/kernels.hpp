@@ -22,7 +22,13 @@ enum Epi {
   EPI_STORE32 = 2,  // out32[m][n] = acc + bias[n]
   EPI_PATCH = 3,    // x[b*(G^2+cls) + cls + p][n] = acc + bias[n] + pos[cls + p][n]
   EPI_STOREQ = 4,   // launch_gemm_mx only: out = MX-fp8 of act(acc + bias[n]) (e4m3 + scales)
+  // (internal: the residual-stream epilogues with an f16 stream, GemmParams.x16; launch_gemm picks them)
+  EPI_RESID16 = 5,
+  EPI_PATCH16 = 6,
 };
+constexpr bool epi_resid(int e) { return e == EPI_RESID || e == EPI_RESID16; }
+constexpr bool epi_patch(int e) { return e == EPI_PATCH || e == EPI_PATCH16; }
+constexpr bool epi_x16(int e) { return e == EPI_RESID16 || e == EPI_PATCH16; }
 
 struct GemmParams {
   const void* A; long lda;   // A_ROWS source
