@@ -7,10 +7,12 @@ HBM: ViT-B/32-224 vision tower on 256 normalised f32 images per GPU
 (BASELINE.json configs[1]) -> L2-normalised [256, 512], then (N > 1) the RCCL
 all-gather of the embedding matrix over xGMI (weak scaling).
 Weights are seeded synthetic (no checkpoint can be fetched); arithmetic in bf16
-with f32 accumulation / residual stream / LayerNorm / softmax.
+with f32 accumulation / residual adds / LayerNorm statistics / softmax; the residual
+stream stored in f16 (the library default for bf16 engines; `--residual f32` for f32).
 
 Also reported: texts/s for configs[2] (text tower, batch 1024 x 77 tokens);
-roofline of the dominant kernel (c_fc GEMM) from HIP events on the launch stream;
+roofline of the dominant kernel (the trunk GEMM site with the most time per step) from HIP
+events on the launch stream;
 end-to-end legs through the host-buffer entry points (PCIe included; N = 1);
 CPU baseline = the fp32 torch CPU port of the same graphs (oracle/torch_cpu.py) on a bounded
 sample of the same inputs on rank 0, which also checks the GPU rows (cosine).
@@ -74,7 +76,7 @@ def text_flops(B, T=77, executed=False):
 # GemmTile ids the library builds (csrc/kernels/kernels.hpp kGemmTiles)
 # trunk GEMM sites of the ViT-B/32 vision tower: (N, K), and what the epilogue adds
 SITE_SHAPES = {"qkv": (2304, 768), "out_proj": (768, 768), "c_fc": (3072, 768), "c_proj": (768, 3072)}
-SITE_EPI = {"qkv": "+bias", "out_proj": "+bias, f32 residual", "c_fc": "+QuickGELU", "c_proj": "+bias, f32 residual"}
+SITE_EPI = {"qkv": "+bias", "out_proj": "+bias, {x} residual", "c_fc": "+QuickGELU", "c_proj": "+bias, {x} residual"}
 TILE_NAMES = {0: "heuristic", 1: "128x128", 2: "256x128", 3: "256x256", 13: "192x256w8", 14: "256x256rs",
               15: "160x128rs", 17: "160x128w8rs", 18: "256x256half", 26: "224x192w8"}
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md chip table)
@@ -452,6 +454,9 @@ def main():
     _lib.check(_lib.lib().clipgpu_test_engine_tiles(ve._h, tiles))
     dev_lanes = ctypes.c_int()
     _lib.check(_lib.lib().clipgpu_test_engine_lanes(ve._h, ctypes.byref(dev_lanes)))
+    x_store = ctypes.c_int()
+    _lib.check(_lib.lib().clipgpu_test_engine_residual(ve._h, ctypes.byref(x_store)))
+    x_store = "f16" if x_store.value == 2 else "f32"  # CLIPGPU_RESIDUAL_F16 / _F32
     mx_names = {0: "heuristic", 2: "mx256x128", 3: "mx128x128"}  # fp8 engines: QKV / c_fc / c_proj sites
     fp8 = args.dtype == "fp8"
     gemm_tiles = {site: (mx_names if fp8 and site != "out_proj" else TILE_NAMES).get(t, f"tile{t}")
@@ -656,7 +661,7 @@ def main():
                        "global_batch": world * B_VISION, "seq_len": 50,
                        "parallelism": f"dp{world}, {dev_lanes.value} concurrent sub-batch lane(s)/GPU (committed MI355X tile table)" + (" + the engine's RCCL all-gather (ncclAllGather in the C ABI) of the [B,512] embeddings on every rank" if dp else "")},
             "roofline": {"bound": "mfma",
-                         "kernel": f"{dom} GEMM ({sites[dom]['shape']}, {SITE_EPI[dom]}, tile {sites[dom]['tile']}): the "
+                         "kernel": f"{dom} GEMM ({sites[dom]['shape']}, {SITE_EPI[dom].format(x=x_store)}, tile {sites[dom]['tile']}): the "
                                    f"site with the most GEMM time per step",
                          "rows_per_launch": sites[dom]["rows_per_launch"],
                          "achieved": sites[dom]["tflops"], "peak": peak, "unit": "TFLOP/s",
@@ -679,6 +684,7 @@ def main():
             "whole_forward_mfma_tflops_per_gpu": round(whole_tflops, 1),
             "whole_forward_frac_of_peak": round(whole_tflops / PEAK_BF16_TFLOPS, 4),
             "last_layer_pruned": PRUNE_LAST,
+            "residual_stream": x_store,
             "windows": windows,
             "sclk_mhz": windows["sclk_mhz_median"] if windows else None,
             **({"breakdown_serialized": breakdown} if breakdown is not None else {}),

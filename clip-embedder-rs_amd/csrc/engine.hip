@@ -2398,6 +2398,13 @@ int clipgpu_test_engine_lanes(const clipgpu_engine* e, int* dev_lanes) {
   });
 }
 
+int clipgpu_test_engine_residual(const clipgpu_engine* e, int* residual) {
+  return guarded([&]() {
+    if (!e || !residual) throw ClipErr(CLIPGPU_ERR_INVALID, "NULL argument");
+    *residual = e->x16 ? CLIPGPU_RESIDUAL_F16 : CLIPGPU_RESIDUAL_F32;
+  });
+}
+
 int clipgpu_profile_enable(clipgpu_engine* e, unsigned mask) {
   return guarded([&]() {
     if (!e) throw ClipErr(CLIPGPU_ERR_INVALID, "engine is NULL");

@@ -76,6 +76,7 @@ _PROTOS = [
                                            POINTER(c_double)]),
     ("clipgpu_test_engine_tiles", c_int, [c_void_p, POINTER(c_int)]),
     ("clipgpu_test_engine_lanes", c_int, [c_void_p, POINTER(c_int)]),
+    ("clipgpu_test_engine_residual", c_int, [c_void_p, POINTER(c_int)]),
     ("clipgpu_test_host_plan", c_int, [c_void_p, c_int, POINTER(c_int), c_int]),
     ("clipgpu_test_force_broadcast", c_int, [c_void_p, c_int]),
     ("clipgpu_test_comm_lazy", c_int, [c_void_p]),

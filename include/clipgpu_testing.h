@@ -116,6 +116,8 @@ int clipgpu_test_engine_tiles(const struct clipgpu_engine* e, int tiles[4]);
 /* Concurrent sub-batches the engine's device-side forwards run (the creation-time tuning's pick,
  * or clipgpu_options.lanes). */
 int clipgpu_test_engine_lanes(const struct clipgpu_engine* e, int* dev_lanes);
+/* The residual stream's resolved storage: CLIPGPU_RESIDUAL_F32 or CLIPGPU_RESIDUAL_F16. */
+int clipgpu_test_engine_residual(const struct clipgpu_engine* e, int* residual);
 /* The host-buffer vision path's chunk plan (tools/host_plan_ab.py): n_chunks (1..4) chunks of a
  * max_batch round cut at bounds[0 .. n_chunks - 2]; n_chunks = 0 restores the default
  * (engine.hip host_chunks).  copy_stream = 1: the H2Ds in chunk order on the replica's copy

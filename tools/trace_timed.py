@@ -5,7 +5,8 @@
 
 For a vision-only bench (`--no-text --no-fp8 --no-e2e --no-cpu-baseline`): after the engine's
 creation-time tuning, the trace ends with W warmup steps, the STEPS timed steps, then the c_fc
-profiling pass (1 warmup + P = max(3, STEPS // 2) steps, lanes serialized).  Every step issues the
+profiling pass (1 warmup + P = max(3, STEPS // 2) steps, lanes serialized), then the same P + 1
+steps with the lanes concurrent (the concurrent site profile; skipped when finding the period).  Every step issues the
 same kernel sequence, so the launches per step n is the period of the trace's tail; the timed
 block is the STEPS * n launches before the last (P + 1) * n.  With LANES concurrent lanes the
 profiling pass runs them one after the other, so the tail's period is one lane's forward and a
@@ -44,13 +45,16 @@ def main():
     prof_steps = max(3, steps // 2) + 1
     n = None
     for cand in range(8, 2000):
-        if len(names) >= 3 * cand and names[-cand:] == names[-2 * cand:-cand] == names[-3 * cand:-2 * cand]:
+        # the serialized pass ends where the concurrent pass (prof_steps steps of cand * lanes
+        # launches, its lanes interleaved in start order) begins
+        e = len(names) - prof_steps * cand * lanes
+        if e >= 3 * cand and names[e - cand:e] == names[e - 2 * cand:e - cand] == names[e - 3 * cand:e - 2 * cand]:
             n = cand
             break
     if n is None:
         raise SystemExit("no periodic tail: not a vision-only bench trace?")
     n *= lanes  # launches per step
-    end = len(rows) - prof_steps * n
+    end = len(rows) - 2 * prof_steps * n
     timed = rows[end - steps * n:end]
     out = [f"# {path}: {len(rows)} launches, {n} per step ({lanes} lane(s)); timed block = {steps} steps "
            f"({len(timed)} launches) before the {prof_steps}-step profiling pass",
