@@ -1371,6 +1371,35 @@ void run_host_shard(clipgpu_engine& e, Replica& r, InKind kind, const void* in, 
     hipEvent_t* const done = set ? r.done2 : r.done;
     hipEvent_t* const copied = set ? r.copied2 : r.copied;
     const int R = (int)std::min<int64_t>(MB, b1 - c0);  // rows of this round
+    struct Chunk { int k, n; int64_t rc; char* din; float* dout; hipStream_t st; };
+    Chunk ch[4];
+    int nch = 0;
+    // A chunk's forward and D2H.  A one-round call issues chunk k's forward right after chunk k's
+    // H2D, to start once chunk k has landed (the first half's forward overlaps the second half's
+    // host copy and transfer).  A multi-round call issues the round's forwards after all its H2Ds and
+    // starts every one once the round's last chunk has landed: the lanes then run side by side in
+    // step, as in the device-resident forward, instead of one chunk transfer apart for the whole
+    // call (lanes held apart run slower: DESIGN.md §5 round 5, lane offset).  From the second round
+    // on, a round's input lands (and its host copy runs) during the previous round's forwards.
+    auto issue_forward = [&](const Chunk& c, int gate_k) {
+      if (e.host_copy_stream) HIP_CHECK(hipStreamWaitEvent(c.st, copied[gate_k], 0));
+      const Replica v = lane_view(e, r, part[c.k]);
+      run_graph(e, r,
+                {(uint64_t)(10 + kind), (uint64_t)c.k, (uint64_t)c.n, fbits(mean, 0), fbits(mean, 1),
+                 fbits(mean, 2), fbits(stdv, 0), fbits(stdv, 1), fbits(stdv, 2), (uint64_t)tokens,
+                 (uint64_t)part[c.k], (uint64_t)set},
+                c.st, [&](hipStream_t gs) {
+                  if (kind == IN_IDS)
+                    text_forward(e, v, (const int64_t*)c.din, c.n, c.dout, gs, tokens);
+                  else
+                    vision_forward(e, v, c.din, kind == IN_F32 ? A_IMG_F32 : A_IMG_U8, mean, stdv, c.n, c.dout, gs);
+                });
+      float* dst = direct_out ? out + c.rc * E : pin_out_set[set] + (size_t)part[c.k] * E;
+      HIP_CHECK(hipMemcpyAsync(dst, c.dout, (size_t)c.n * E * 4, hipMemcpyDeviceToHost, c.st));
+      HIP_CHECK(hipEventRecord(done[c.k], c.st));
+      pend[set][c.k].c0 = c.rc;
+      pend[set][c.k].n = c.n;
+    };
     int off = 0;
     for (int k = 0; k < C && off < R; ++k) {
       const int cap = part[k + 1] - part[k];
@@ -1401,7 +1430,6 @@ void run_host_shard(clipgpu_engine& e, Replica& r, InKind kind, const void* in, 
         // test hook: pull the chunk through the host mapping with a copy kernel on the copy stream
         check(launch_pull_copy(mapped, din, (size_t)n * in_row_bytes, r.copy), "pull copy");
         HIP_CHECK(hipEventRecord(copied[k], r.copy));
-        HIP_CHECK(hipStreamWaitEvent(st, copied[k], 0));
       } else if (e.host_copy_stream == 2 && n >= 2) {  // test hook: the chunk's halves on two copy streams
         const size_t h = (size_t)(n / 2) * in_row_bytes, all = (size_t)n * in_row_bytes;
         HIP_CHECK(hipStreamWaitEvent(r.copy2, copied[(k + C - 1) % C], 0));  // chunk order kept
@@ -1410,31 +1438,19 @@ void run_host_shard(clipgpu_engine& e, Replica& r, InKind kind, const void* in, 
         HIP_CHECK(hipEventRecord(copied[k], r.copy2));
         HIP_CHECK(hipStreamWaitEvent(r.copy, copied[k], 0));
         HIP_CHECK(hipEventRecord(copied[k], r.copy));
-        HIP_CHECK(hipStreamWaitEvent(st, copied[k], 0));
       } else if (e.host_copy_stream) {
         HIP_CHECK(hipMemcpyAsync(din, src, (size_t)n * in_row_bytes, hipMemcpyHostToDevice, r.copy));
         HIP_CHECK(hipEventRecord(copied[k], r.copy));
-        HIP_CHECK(hipStreamWaitEvent(st, copied[k], 0));
       } else {
         HIP_CHECK(hipMemcpyAsync(din, src, (size_t)n * in_row_bytes, hipMemcpyHostToDevice, st));
       }
-      const Replica v = lane_view(e, r, part[k]);
-      run_graph(e, r,
-                {(uint64_t)(10 + kind), (uint64_t)k, (uint64_t)n, fbits(mean, 0), fbits(mean, 1), fbits(mean, 2),
-                 fbits(stdv, 0), fbits(stdv, 1), fbits(stdv, 2), (uint64_t)tokens, (uint64_t)part[k], (uint64_t)set},
-                st, [&](hipStream_t gs) {
-                  if (kind == IN_IDS)
-                    text_forward(e, v, (const int64_t*)din, n, dout, gs, tokens);
-                  else
-                    vision_forward(e, v, din, kind == IN_F32 ? A_IMG_F32 : A_IMG_U8, mean, stdv, n, dout, gs);
-                });
-      float* dst = direct_out ? out + rc * E : pin_out_set[set] + (size_t)part[k] * E;
-      HIP_CHECK(hipMemcpyAsync(dst, dout, (size_t)n * E * 4, hipMemcpyDeviceToHost, st));
-      HIP_CHECK(hipEventRecord(done[k], st));
-      pend[set][k].c0 = rc;
-      pend[set][k].n = n;
+      ch[nch] = {k, n, rc, din, dout, st};
+      if (!two_sets) issue_forward(ch[nch], k);
+      ++nch;
       off += n;
     }
+    if (two_sets)
+      for (int i = 0; i < nch; ++i) issue_forward(ch[i], ch[nch - 1].k);
     c0 += R;
   }
   for (int set = 0; set < 2; ++set)
