@@ -76,7 +76,8 @@ def text_flops(B, T=77, executed=False):
 # GemmTile ids the library builds (csrc/kernels/kernels.hpp kGemmTiles)
 # trunk GEMM sites of the ViT-B/32 vision tower: (N, K), and what the epilogue adds
 SITE_SHAPES = {"qkv": (2304, 768), "out_proj": (768, 768), "c_fc": (3072, 768), "c_proj": (768, 3072)}
-SITE_EPI = {"qkv": "+bias", "out_proj": "+bias, {x} residual", "c_fc": "+QuickGELU", "c_proj": "+bias, {x} residual"}
+SITE_EPI = {"qkv": "{ln}+bias", "out_proj": "+bias, {x} residual", "c_fc": "{ln}+QuickGELU",
+            "c_proj": "+bias, {x} residual"}
 TILE_NAMES = {0: "heuristic", 1: "128x128", 2: "256x128", 3: "256x256", 13: "192x256w8", 14: "256x256rs",
               15: "160x128rs", 17: "160x128w8rs", 18: "256x256half", 26: "224x192w8"}
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md chip table)
@@ -379,6 +380,8 @@ def main():
     ap.add_argument("--windows", type=int, default=5,
                     help="N = 1: repeated K-step windows after the timed one (min / median / max images/s, the "
                          "shader clock of each window, and the c_fc launch time per window); 0 skips them")
+    ap.add_argument("--ln-fold", default=None, choices=["on", "off"],
+                    help="ln_1 / ln_2 folded into the QKV / c_fc GEMMs (clipgpu_options.ln_fold; default: the library's)")
     ap.add_argument("--residual", default=None, choices=["f32", "f16"],
                     help="the residual stream's storage (clipgpu_options.residual; default: the library's)")
     ap.add_argument("--gather", action="store_true",
@@ -406,7 +409,8 @@ def main():
     dev = torch.device("cuda", local)
 
     mdir = make_model_dir()
-    vopts = {"lanes": args.lanes, "residual": args.residual}
+    fold = {None: None, "on": True, "off": False}[args.ln_fold]
+    vopts = {"lanes": args.lanes, "residual": args.residual, "ln_fold": fold}
     if args.tiles:
         pins = [int(t) for t in args.tiles.split(",")]
         vopts.update(gemm_tiles=pins, patch_tile=pins[3])
@@ -454,9 +458,10 @@ def main():
     _lib.check(_lib.lib().clipgpu_test_engine_tiles(ve._h, tiles))
     dev_lanes = ctypes.c_int()
     _lib.check(_lib.lib().clipgpu_test_engine_lanes(ve._h, ctypes.byref(dev_lanes)))
-    x_store = ctypes.c_int()
-    _lib.check(_lib.lib().clipgpu_test_engine_residual(ve._h, ctypes.byref(x_store)))
+    x_store, ln_fold = ctypes.c_int(), ctypes.c_int()
+    _lib.check(_lib.lib().clipgpu_test_engine_residual(ve._h, ctypes.byref(x_store), ctypes.byref(ln_fold)))
     x_store = "f16" if x_store.value == 2 else "f32"  # CLIPGPU_RESIDUAL_F16 / _F32
+    ln_fold = bool(ln_fold.value)
     mx_names = {0: "heuristic", 2: "mx256x128", 3: "mx128x128"}  # fp8 engines: QKV / c_fc / c_proj sites
     fp8 = args.dtype == "fp8"
     gemm_tiles = {site: (mx_names if fp8 and site != "out_proj" else TILE_NAMES).get(t, f"tile{t}")
@@ -513,6 +518,7 @@ def main():
                                       "cu_us_per_step": round(ms_cc * 1e3 / psteps * held / cus, 1),
                                       "cu_frac": round(tf_cc / peak * cus / held, 4)}}
     dom = max(sites, key=lambda k: sites[k]["us_per_step"])
+    dom_epi = SITE_EPI[dom].format(x=x_store, ln="LayerNorm folded, " if ln_fold else "")
     fc_rows_per_launch = sites["c_fc"]["rows_per_launch"]
     whole_tflops = vit_flops(B_VISION, executed=True) * args.steps / dt / 1e12 / 1.0
 
@@ -565,7 +571,7 @@ def main():
     text = None
     tout_host = None
     if not args.no_text:
-        topts = {"lanes": args.text_lanes, "residual": args.residual}
+        topts = {"lanes": args.text_lanes, "residual": args.residual, "ln_fold": fold}
         if args.text_tiles:
             topts["gemm_tiles"] = [int(t) for t in args.text_tiles.split(",")]
         te = Engine(mdir, _lib.TOWER_TEXT, [local], args.dtype, B_TEXT, **topts)
@@ -661,7 +667,7 @@ def main():
                        "global_batch": world * B_VISION, "seq_len": 50,
                        "parallelism": f"dp{world}, {dev_lanes.value} concurrent sub-batch lane(s)/GPU (committed MI355X tile table)" + (" + the engine's RCCL all-gather (ncclAllGather in the C ABI) of the [B,512] embeddings on every rank" if dp else "")},
             "roofline": {"bound": "mfma",
-                         "kernel": f"{dom} GEMM ({sites[dom]['shape']}, {SITE_EPI[dom].format(x=x_store)}, tile {sites[dom]['tile']}): the "
+                         "kernel": f"{dom} GEMM ({sites[dom]['shape']}, {dom_epi}, tile {sites[dom]['tile']}): the "
                                    f"site with the most GEMM time per step",
                          "rows_per_launch": sites[dom]["rows_per_launch"],
                          "achieved": sites[dom]["tflops"], "peak": peak, "unit": "TFLOP/s",
@@ -685,6 +691,7 @@ def main():
             "whole_forward_frac_of_peak": round(whole_tflops / PEAK_BF16_TFLOPS, 4),
             "last_layer_pruned": PRUNE_LAST,
             "residual_stream": x_store,
+            "ln_fold": ln_fold,
             "windows": windows,
             "sclk_mhz": windows["sclk_mhz_median"] if windows else None,
             **({"breakdown_serialized": breakdown} if breakdown is not None else {}),

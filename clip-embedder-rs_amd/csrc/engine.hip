@@ -58,6 +58,9 @@ struct MxW {
 
 struct LayerW {
   float *ln1_w, *ln1_b, *bqkv, *bo, *ln2_w, *ln2_b, *b1, *b2;
+  // LayerNorm-folded engines (clipgpu_engine::lnf): wqkv / w1 hold W' = f16(W diag(gamma)), bqkv / b1
+  // hold b + W beta, and these the column sums of W' (EPI_LNF)
+  float *cs_qkv = nullptr, *cs_1 = nullptr;
   void *wqkv, *wo, *w1, *w2;  // 16-bit (fp8 engines: wo only)
   MxW mqkv, m1, m2;           // fp8 engines: QKV, c_fc, c_proj
 };
@@ -207,6 +210,9 @@ struct clipgpu_engine {
   // stays f32.  bf16 / f16 engines of the CLIP family only (fp8 engines' MX residual epilogue and the
   // SigLIP MAP head take the f32 stream).
   bool x16 = false;
+  // ln_1 / ln_2 folded into the QKV / c_fc GEMMs (clipgpu_options.ln_fold; f16 stream only): those
+  // GEMMs read x (f16) with W' = W diag(gamma) (f16) and EPI_LNF; no LayerNorm launches in the trunk.
+  bool lnf = false;
 
   int tuning = 0;  // clipgpu_options.tuning: 1 = timing tuner (+ whole-forward pass), 2 = per-site pass only
   // clipgpu_options.gemm_tiles / patch_tile pins (0 = the table's tile, -1 = the shape heuristic)
@@ -224,6 +230,10 @@ struct clipgpu_engine {
   // default) and whether its H2Ds go on the replica's copy stream (1) or on each chunk's lane stream (0)
   std::vector<int> host_part;
   int host_copy_stream = 1;
+  // test hook (clipgpu_test_host_plan copy_stream bits 4-5): 1 = a multi-round call starts each round's
+  // forwards together once the round's last chunk has landed (lanes in step); 2 = the D2Hs go on the copy
+  // stream (the lane streams run straight into their next forward)
+  int host_flags = 0;
   clipgpu::TowerSpec spec;
   clipgpu::PreprocessCfg pre;
   clipgpu::DType dt = clipgpu::DT_BF16;
@@ -442,24 +452,55 @@ void upload_weights(clipgpu_engine& e, Replica& r, const TensorMap& m) {
     w.pos = f32("positional_embedding");
     pre = "transformer.resblocks.";
   }
+  // LayerNorm fold (clipgpu_engine::lnf) of the GEMM W [R][D] + b behind LayerNorm (gamma, beta):
+  // W' = f16(W diag(gamma)) zero-padded to Rp rows, bias b + W beta (f64 sums, the f32 W), and the
+  // column sums of W' as the kernel sees it (f16-rounded; f64 sums): LN(x) W^T + b =
+  // rstd (x W'^T - mean cs) + b + W beta.
+  auto fold_w = [&](const std::string& wk, const std::string& bk, const std::string& gk, const std::string& bek,
+                    int64_t Rp, void*& wout, float*& bout, float*& csout) {
+    const HostTensor& W = need(m, wk);
+    const HostTensor& b = need(m, bk);
+    const HostTensor& g = need(m, gk);
+    const HostTensor& be = need(m, bek);
+    const int64_t R = W.shape[0], C = W.numel() / W.shape[0];
+    std::vector<float> wf((size_t)(Rp * C), 0.f), cs((size_t)Rp, 0.f), bp((size_t)Rp, 0.f);
+    for (int64_t i = 0; i < R; ++i) {
+      double sb = b.data[(size_t)i], sc = 0.0;
+      for (int64_t k = 0; k < C; ++k) {
+        const float wv = W.data[(size_t)(i * C + k)];
+        const float wg = wv * g.data[(size_t)k];
+        wf[(size_t)(i * C + k)] = wg;
+        sc += (double)(float)(_Float16)wg;  // the device cast's rounding (to nearest even)
+        sb += (double)wv * (double)be.data[(size_t)k];
+      }
+      cs[(size_t)i] = (float)sc;
+      bp[(size_t)i] = (float)sb;
+    }
+    wout = a.take(wf.size() * 2);
+    upload_16(DT_F16, wf.data(), wf.size(), wout, staging_pad(wf.size()), r.stream);
+    bout = a_take_f32(bp);
+    csout = a_take_f32(cs);
+  };
   for (int l = 0; l < s.layers; ++l) {
     const std::string p = pre + std::to_string(l) + ".";
     LayerW L;
     L.ln1_w = f32(p + n_ln1w);
     L.ln1_b = f32(p + n_ln1b);
     L.wqkv = L.w1 = L.w2 = nullptr;
-    if (mx_at(e, l, GS_QKV)) L.mqkv = wmx_pad(p + n_qkvw, 3 * D, D);
+    if (e.lnf) fold_w(p + n_qkvw, p + n_qkvb, p + n_ln1w, p + n_ln1b, 3 * D, L.wqkv, L.bqkv, L.cs_qkv);
+    else if (mx_at(e, l, GS_QKV)) L.mqkv = wmx_pad(p + n_qkvw, 3 * D, D);
     else L.wqkv = w16(p + n_qkvw);
-    if (mx_at(e, l, GS_FC)) L.m1 = wmx_pad(p + n_fc1w, mlp_pad(s), D);
+    if (e.lnf) fold_w(p + n_fc1w, p + n_fc1b, p + n_ln2w, p + n_ln2b, mlp_pad(s), L.w1, L.b1, L.cs_1);
+    else if (mx_at(e, l, GS_FC)) L.m1 = wmx_pad(p + n_fc1w, mlp_pad(s), D);
     else L.w1 = w16_pad(p + n_fc1w, mlp_pad(s), D);
     if (mx_at(e, l, GS_PROJ)) L.m2 = wmx_pad(p + n_fc2w, D, mlp_pad(s));
     else L.w2 = w16_pad(p + n_fc2w, D, mlp_pad(s));
-    L.bqkv = f32(p + n_qkvb);
+    if (!e.lnf) L.bqkv = f32(p + n_qkvb);
     L.wo = w16(p + n_ow);
     L.bo = f32(p + n_ob);
     L.ln2_w = f32(p + n_ln2w);
     L.ln2_b = f32(p + n_ln2b);
-    L.b1 = f32_pad(p + n_fc1b, mlp_pad(s));
+    if (!e.lnf) L.b1 = f32_pad(p + n_fc1b, mlp_pad(s));
     L.b2 = f32(p + n_fc2b);
     w.layers.push_back(L);
   }
@@ -616,7 +657,10 @@ inline void* xrows(const clipgpu_engine& e, void* x, size_t rows) {
 // clipgpu_options.residual = 0: the residual stream's default storage
 constexpr int kResidualDefault = CLIPGPU_RESIDUAL_F16;
 
-int site_epi(int site) { return (site == GS_OUT || site == GS_PROJ) ? EPI_RESID : EPI_STORE16; }
+int site_epi(const clipgpu_engine& e, int site) {
+  if (site == GS_OUT || site == GS_PROJ) return EPI_RESID;
+  return e.lnf ? EPI_LNF : EPI_STORE16;  // QKV / c_fc behind the folded LayerNorm
+}
 
 // Tile order per trunk site (GemmParams.group: row panels per group, 0 = the kernels' 8).  qkv and
 // c_proj walk N first (group 1): their W (3 D x D, D x MLP) is small beside A, so each XCD reads an A
@@ -632,11 +676,17 @@ constexpr int kSiteGroup[4] = {CLIPGPU_SITE_GROUPS ? 1 : 0, 0, 0, CLIPGPU_SITE_G
 GemmParams site_gemm(const clipgpu_engine& e, const Replica& r, const LayerW& L, int site, int rows) {
   const int D = e.spec.width, MLP = mlp_pad(e.spec);
   GemmParams g;
+  // (LayerNorm-folded engines: QKV and c_fc read the residual stream x itself, EPI_LNF)
+  const void* ln_in = e.lnf ? r.x : r.h;
   switch (site) {
-    case GS_QKV: g = rows_gemm(r.h, D, L.wqkv, L.bqkv, r.big, 3 * D, rows, 3 * D, D); break;
+    case GS_QKV: g = rows_gemm(ln_in, D, L.wqkv, L.bqkv, r.big, 3 * D, rows, 3 * D, D); break;
     case GS_OUT: g = rows_gemm(r.h, D, L.wo, L.bo, r.x, D, rows, D, D); break;
-    case GS_FC: g = rows_gemm(r.h, D, L.w1, L.b1, r.big, MLP, rows, MLP, D); break;
+    case GS_FC: g = rows_gemm(ln_in, D, L.w1, L.b1, r.big, MLP, rows, MLP, D); break;
     default: g = rows_gemm(r.big, MLP, L.w2, L.b2, r.x, D, rows, D, MLP); break;
+  }
+  if (e.lnf && (site == GS_QKV || site == GS_FC)) {
+    g.cs = site == GS_QKV ? L.cs_qkv : L.cs_1;
+    g.ln_eps = e.spec.ln_eps;
   }
   g.group = kSiteGroup[site];
   g.x16 = e.x16 ? 1 : 0;
@@ -746,7 +796,7 @@ PoolSrc trunk(const clipgpu_engine& e, const Replica& r, int B, int causal, cons
       }
       GemmParams g = site_gemm(e, c, L, site, rows);
       g.tile = tuned ? e.tile[site] : TILE_AUTO;
-      check(launch_gemm(e.dt, A_ROWS, site_epi(site), site == GS_FC ? s.act : ACT_NONE, g, st), what);
+      check(launch_gemm(e.dt, A_ROWS, site_epi(e, site), site == GS_FC ? s.act : ACT_NONE, g, st), what);
     };
     gemm(GS_QKV, PC_QKV, "qkv gemm");
     if (!ABLATED(1)) { ProfScope ps(e, PC_ATTN, st);
@@ -762,14 +812,14 @@ PoolSrc trunk(const clipgpu_engine& e, const Replica& r, int B, int causal, cons
             "gather pooled rows");
     }
     gemm(GS_OUT, PC_OUT_PROJ, "out_proj gemm");
-    if (!ABLATED(0)) {
+    if (!ABLATED(0) && !e.lnf) {
       ProfScope ps(e, compact ? PC_TAIL : PC_LN, st);
       check(launch_ln_rows(e.dt, c.x, e.x16, L.ln2_w, L.ln2_b, s.ln_eps, c.h, rows, D, st, ln_q(e, l, GS_FC, c.hs)),
             "ln_2");
     }
     gemm(GS_FC, PC_C_FC, "c_fc gemm");
     gemm(GS_PROJ, PC_C_PROJ, "c_proj gemm");
-    if (l + 1 < s.layers && !ABLATED(0)) {
+    if (l + 1 < s.layers && !ABLATED(0) && !e.lnf) {
       ProfScope ps(e, PC_LN, st);
       check(launch_ln_rows(e.dt, r.x, e.x16, r.w.layers[l + 1].ln1_w, r.w.layers[l + 1].ln1_b, s.ln_eps, r.h, rows, D, st,
                            ln_q(e, l + 1, GS_QKV, r.hs)), "ln_1");
@@ -859,6 +909,13 @@ void table_tiles(clipgpu_engine& e) {
     e.tile[GS_OUT] = e.tile[GS_PROJ] = TILE_224x192_W8;
     if (prow >= 2048) e.tile_patch = TILE_224x192_W8;
   }
+  // LayerNorm-folded QKV / c_fc (EPI_LNF): the 256x256 tiles and the 8-wave 160x128 spill with the row
+  // statistics' registers; the 4-wave 160x128 RS tile holds them (221 VGPRs, tools/kernel_regs.py)
+  if (e.lnf && rows >= 2048)
+    for (int site : {GS_QKV, GS_FC})
+      if (e.tile[site] == TILE_256x256_HALF || e.tile[site] == TILE_256x256 || e.tile[site] == TILE_256x256_RS ||
+          e.tile[site] == TILE_160x128_W8_RS)
+        e.tile[site] = TILE_160x128_RS;
 }
 
 // clipgpu_options.gemm_tiles / patch_tile pins over the table's (or the tuner's) choice: a GemmTile
@@ -938,7 +995,7 @@ void autotune_tiles(clipgpu_engine& e, Replica& r) {
       e.tile[site] = table_tile(site, rows, shape[site][0], shape[site][1]);
       continue;
     }
-    e.tile[site] = tune(site_gemm(e, r, L, site, rows), site_epi(site), site == GS_FC ? e.spec.act : ACT_NONE);
+    e.tile[site] = tune(site_gemm(e, r, L, site, rows), site_epi(e, site), site == GS_FC ? e.spec.act : ACT_NONE);
   }
   if (e.spec.tower == TOWER_VISION) {
     const TowerSpec& s = e.spec;
@@ -1018,7 +1075,8 @@ void vision_forward(const clipgpu_engine& e, const Replica& r, const void* pixel
   {
   ProfScope ps(e, PC_STEM, st);
   check(launch_vision_embed_ln(e.dt, r.x, e.x16, r.w.cls, r.w.pos, r.w.lnpre_w, r.w.lnpre_b, r.w.layers[0].ln1_w,
-                               r.w.layers[0].ln1_b, s.ln_eps, r.h, B, s.tokens(), D, st, ln_q(e, 0, GS_QKV, r.hs)),
+                               r.w.layers[0].ln1_b, s.ln_eps, e.lnf ? nullptr : r.h, B, s.tokens(), D, st,
+                               ln_q(e, 0, GS_QKV, r.hs)),
         "embed+ln_pre");
   }
   head(e, r, B, trunk(e, r, B, 0, nullptr, st, s.tokens()), d_out, st);
@@ -1034,7 +1092,8 @@ void text_forward(const clipgpu_engine& e, const Replica& r, const int64_t* d_id
   {
   ProfScope ps(e, PC_STEM, st);
   check(launch_text_embed_ln(e.dt, d_ids, r.w.tok, r.w.pos, r.w.layers[0].ln1_w, r.w.layers[0].ln1_b, s.ln_eps,
-                             r.x, e.x16, r.h, B, T, s.width, s.vocab_size, st, ln_q(e, 0, GS_QKV, r.hs)),
+                             r.x, e.x16, e.lnf ? nullptr : r.h, B, T, s.width, s.vocab_size, st,
+                             ln_q(e, 0, GS_QKV, r.hs)),
         "token embed+ln_1");
   }
   // CLIP: causal, the EOT (argmax id) row pooled; SigLIP2: no mask, the last position pooled
@@ -1352,6 +1411,8 @@ void run_host_shard(clipgpu_engine& e, Replica& r, InKind kind, const void* in, 
   const int C = (int)part.size() - 1;
   const bool two_sets = b1 - b0 > MB;
   if (two_sets) ensure_host_set2(e, r);
+  const bool lockstep = two_sets && (e.host_flags & 1) && e.host_copy_stream;
+  const bool d2h_copy = (e.host_flags & 2) && e.host_copy_stream;
   struct Pending { int64_t c0 = -1; int n = 0; };
   Pending pend[2][4];
   float* const pin_out_set[2] = {r.pin_out, r.pin_out2};
@@ -1374,15 +1435,15 @@ void run_host_shard(clipgpu_engine& e, Replica& r, InKind kind, const void* in, 
     struct Chunk { int k, n; int64_t rc; char* din; float* dout; hipStream_t st; };
     Chunk ch[4];
     int nch = 0;
-    // A chunk's forward and D2H.  A one-round call issues chunk k's forward right after chunk k's
-    // H2D, to start once chunk k has landed (the first half's forward overlaps the second half's
-    // host copy and transfer).  A multi-round call issues the round's forwards after all its H2Ds and
-    // starts every one once the round's last chunk has landed: the lanes then run side by side in
-    // step, as in the device-resident forward, instead of one chunk transfer apart for the whole
-    // call (lanes held apart run slower: DESIGN.md §5 round 5, lane offset).  From the second round
-    // on, a round's input lands (and its host copy runs) during the previous round's forwards.
+    // A chunk's forward and D2H, issued right after the chunk's H2D: it starts once the chunk has
+    // landed, so the first half's forward overlaps the second half's host copy and transfer, and from the
+    // second round of a multi-round call on, a round's input lands during the previous round's forwards.
+    // (Test hook, host_flags bit 0: a multi-round call issues the round's forwards after all its H2Ds,
+    // gated on the last one -- the lanes in step; bit 1: the D2Hs on the copy stream.)
     auto issue_forward = [&](const Chunk& c, int gate_k) {
       if (e.host_copy_stream) HIP_CHECK(hipStreamWaitEvent(c.st, copied[gate_k], 0));
+      // (D2H on the copy stream: the other set's last D2H of these output rows has read them)
+      if (d2h_copy && two_sets) HIP_CHECK(hipStreamWaitEvent(c.st, done_set[set ^ 1][c.k], 0));
       const Replica v = lane_view(e, r, part[c.k]);
       run_graph(e, r,
                 {(uint64_t)(10 + kind), (uint64_t)c.k, (uint64_t)c.n, fbits(mean, 0), fbits(mean, 1),
@@ -1395,8 +1456,15 @@ void run_host_shard(clipgpu_engine& e, Replica& r, InKind kind, const void* in, 
                     vision_forward(e, v, c.din, kind == IN_F32 ? A_IMG_F32 : A_IMG_U8, mean, stdv, c.n, c.dout, gs);
                 });
       float* dst = direct_out ? out + c.rc * E : pin_out_set[set] + (size_t)part[c.k] * E;
-      HIP_CHECK(hipMemcpyAsync(dst, c.dout, (size_t)c.n * E * 4, hipMemcpyDeviceToHost, c.st));
-      HIP_CHECK(hipEventRecord(done[c.k], c.st));
+      if (d2h_copy) {
+        HIP_CHECK(hipEventRecord(done[c.k], c.st));  // the forward's end ...
+        HIP_CHECK(hipStreamWaitEvent(r.copy, done[c.k], 0));
+        HIP_CHECK(hipMemcpyAsync(dst, c.dout, (size_t)c.n * E * 4, hipMemcpyDeviceToHost, r.copy));
+        HIP_CHECK(hipEventRecord(done[c.k], r.copy));  // ... then the D2H's
+      } else {
+        HIP_CHECK(hipMemcpyAsync(dst, c.dout, (size_t)c.n * E * 4, hipMemcpyDeviceToHost, c.st));
+        HIP_CHECK(hipEventRecord(done[c.k], c.st));
+      }
       pend[set][c.k].c0 = c.rc;
       pend[set][c.k].n = c.n;
     };
@@ -1445,11 +1513,11 @@ void run_host_shard(clipgpu_engine& e, Replica& r, InKind kind, const void* in, 
         HIP_CHECK(hipMemcpyAsync(din, src, (size_t)n * in_row_bytes, hipMemcpyHostToDevice, st));
       }
       ch[nch] = {k, n, rc, din, dout, st};
-      if (!two_sets) issue_forward(ch[nch], k);
+      if (!lockstep) issue_forward(ch[nch], k);
       ++nch;
       off += n;
     }
-    if (two_sets)
+    if (lockstep)
       for (int i = 0; i < nch; ++i) issue_forward(ch[i], ch[nch - 1].k);
     c0 += R;
   }
@@ -1859,6 +1927,8 @@ int clipgpu_create_ex(const char* model_dir, int tower, const int* device_ids, i
       throw ClipErr(CLIPGPU_ERR_INVALID, "clipgpu_options.mx_layers needs dtype CLIPGPU_DTYPE_FP8");
     if (opts.residual < 0 || opts.residual > CLIPGPU_RESIDUAL_F16)
       throw ClipErr(CLIPGPU_ERR_INVALID, "clipgpu_options.residual must be 0, 1 (f32) or 2 (f16)");
+    if (opts.ln_fold < -1 || opts.ln_fold > 1)
+      throw ClipErr(CLIPGPU_ERR_INVALID, "clipgpu_options.ln_fold must be -1, 0 or 1");
     if (opts.communicator < 0 || opts.communicator > 1)
       throw ClipErr(CLIPGPU_ERR_INVALID, "clipgpu_options.communicator must be 0 or 1");
     if (!model_dir) throw ClipErr(CLIPGPU_ERR_INVALID, "model_dir is NULL");
@@ -1916,6 +1986,12 @@ int clipgpu_create_ex(const char* model_dir, int tower, const int* device_ids, i
       if (opts.residual == CLIPGPU_RESIDUAL_F16 && !f16_ok)
         throw ClipErr(CLIPGPU_ERR_INVALID, "clipgpu_options.residual = f16: bf16 / f16 engines of the CLIP family only");
       e->x16 = res == CLIPGPU_RESIDUAL_F16 && f16_ok;
+      // the LayerNorm fold (clipgpu_options.ln_fold): the f16 stream, a QuickGELU / GELU MLP
+      const bool fold_ok = e->x16 && (e->spec.act == ACT_QUICK_GELU || e->spec.act == ACT_GELU);
+      if (opts.ln_fold == 1 && !fold_ok)
+        throw ClipErr(CLIPGPU_ERR_INVALID,
+                      "clipgpu_options.ln_fold = 1: needs the f16 residual stream and a QuickGELU / GELU MLP");
+      e->lnf = fold_ok && opts.ln_fold != -1;
     }
     for (int i = 0; i < 4; ++i) e->pin_tiles[i] = opts.gemm_tiles[i];
     e->pin_patch = opts.patch_tile;
@@ -2391,8 +2467,10 @@ int clipgpu_test_host_plan(clipgpu_engine* e, int n_chunks, const int* bounds, i
   return guarded([&]() {
     if (!e) throw ClipErr(CLIPGPU_ERR_INVALID, "engine is NULL");
     std::lock_guard<std::mutex> lk(e->mu);
-    if (copy_stream < 0 || copy_stream > 3) throw ClipErr(CLIPGPU_ERR_INVALID, "copy_stream: 0 .. 3");
-    e->host_copy_stream = copy_stream;
+    if (copy_stream < 0 || (copy_stream & 15) > 3 || copy_stream >= 64)
+      throw ClipErr(CLIPGPU_ERR_INVALID, "copy_stream: 0 .. 3, + 16 (lockstep rounds), + 32 (D2H on the copy stream)");
+    e->host_copy_stream = copy_stream & 15;
+    e->host_flags = copy_stream >> 4;
     e->host_part.clear();
     if (n_chunks == 0) return;
     if (n_chunks < 1 || n_chunks > 4 || !bounds) throw ClipErr(CLIPGPU_ERR_INVALID, "1..4 chunks");
@@ -2414,10 +2492,11 @@ int clipgpu_test_engine_lanes(const clipgpu_engine* e, int* dev_lanes) {
   });
 }
 
-int clipgpu_test_engine_residual(const clipgpu_engine* e, int* residual) {
+int clipgpu_test_engine_residual(const clipgpu_engine* e, int* residual, int* ln_fold) {
   return guarded([&]() {
     if (!e || !residual) throw ClipErr(CLIPGPU_ERR_INVALID, "NULL argument");
     *residual = e->x16 ? CLIPGPU_RESIDUAL_F16 : CLIPGPU_RESIDUAL_F32;
+    if (ln_fold) *ln_fold = e->lnf ? 1 : 0;
   });
 }
 

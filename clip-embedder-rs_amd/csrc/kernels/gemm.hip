@@ -109,13 +109,17 @@ __device__ __forceinline__ T to16(float v) { return (T)v; }
 template <typename T, int BM, int BN, int WGM, int WGN, int EPI, int ACT>
 __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p) {
   typedef typename Vec8<T>::type V8;
-  typedef typename Vec4<T>::type V4;
+  constexpr bool LNF = epi_lnf(EPI);
+  static_assert(!LNF || std::is_same<T, _Float16>::value, "LayerNorm fold: f16 operands");
+  typedef typename std::conditional<EPI == EPI_LNF_BF, __bf16, T>::type OT;  // 16-bit output type
+  typedef typename Vec4<OT>::type V4;
   constexpr int NW = WGM * WGN;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
   constexpr int A_INSTR = BM / 8 / NW, B_INSTR = BN / 8 / NW;  // 1 KiB glds per wave-instruction
   constexpr int TM = BM / WGM, TN = BN / WGN, MI = TM / 16, NI = TN / 16;
   static_assert(A_INSTR >= 1 && B_INSTR >= 1 && MI >= 1 && NI >= 1, "bad tile");
-  constexpr int BIAS_BYTES = 2 * 1024;  // 2 x 256 f32 (tile-parity double buffer)
+  // 2 x 256 f32 (tile-parity double buffer) of bias (+ EPI_LNF: of column sums, 2 KiB further on)
+  constexpr int BIAS_BYTES = (LNF ? 2 : 1) * 2 * 1024;
   static_assert(BN <= 256, "bias slice is one 1 KiB DMA");
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + BIAS_BYTES];
 
@@ -202,6 +206,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
     if (p.bias != nullptr && wave == 0) {
       const int n = min(n0 + lane * 4, ((p.N - 1) / 4) * 4);  // clamped in-bounds 16 B (N % 4 == 0 checked)
       glds16(p.bias + n, smem + 2 * STAGE + par * 1024);
+      if constexpr (LNF) glds16(p.cs + n, smem + 2 * STAGE + 2048 + par * 1024);
     }
   };
 
@@ -220,6 +225,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
   // C[m = wm + mi*16 + fr][n = wn + ni*16 + fq*4 + j], i.e. each lane owns 4
   // consecutive output columns of one row -> 8 / 16-byte epilogue stores.
   f32x4 acc[NI][MI];
+  float st_s[MI], st_q[MI];  // EPI_LNF: the lane's running row sums / sums of squares (lnf_acc)
   const uint32_t lds0 = lds_addr(smem);
   auto mfma_block = [&](auto zero, const V8(&a)[MI], const V8(&b)[NI]) {
 #pragma unroll
@@ -245,12 +251,17 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
 #pragma unroll
       for (int ni = 0; ni < NI; ++ni)
         acc[ni][mi] = mfma_16x16x32(b0[ni], a0[mi], decltype(zero)::value ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[ni][mi]);
+      if constexpr (LNF) lnf_acc<decltype(zero)::value>(st_s[mi], st_q[mi], a0[mi]);  // chunk 2 kt
       __builtin_amdgcn_sched_barrier(0);
       ds_read_b128<(int)mi * 2048>(a1[mi], aB + offA[1]);
     });
     static_for<NI>([&](auto ni) { ds_read_b128<(int)ni * 2048>(b1[ni], bB + offB[1]); });
     lgkm_wait_all(a1, b1);
     mfma_block(std::false_type{}, a1, b1);
+    if constexpr (LNF) {
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi) lnf_acc<false>(st_s[mi], st_q[mi], a1[mi]);  // chunk 2 kt + 1
+    }
   };
 
   // XE: the residual stream's element type (EPI_RESID16 / EPI_PATCH16: f16, else f32)
@@ -269,6 +280,11 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
       }
     };
     if constexpr (epi_resid(EPI)) load_x(0, xr[0]);
+    if constexpr (LNF) {  // the rows' mean / rstd (every lane: cross-lane combine)
+      const float inv_k = 1.0f / (float)p.K;
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi) lnf_finish(st_s[mi], st_q[mi], inv_k, p.ln_eps);
+    }
 #pragma unroll
     for (int ni = 0; ni < NI; ++ni) {
       if constexpr (epi_resid(EPI)) {
@@ -276,13 +292,19 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
       }
       const int n = n0 + wn + ni * 16 + fq * 4;
       const bool nfull = n + 4 <= p.N;
-      float bv[4] = {0.f, 0.f, 0.f, 0.f};
+      float bv[4] = {0.f, 0.f, 0.f, 0.f}, cv[4] = {0.f, 0.f, 0.f, 0.f};
       if (p.bias != nullptr) {
-        f32x4 b4;
+        f32x4 b4, c4;
         ds_read_b128<0>(b4, lds0 + 2 * STAGE + bpar * 1024 + (wn + ni * 16 + fq * 4) * 4);
+        if constexpr (LNF) ds_read_b128<2048>(c4, lds0 + 2 * STAGE + bpar * 1024 + (wn + ni * 16 + fq * 4) * 4);
         asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(b4)::"memory");
+        if constexpr (LNF) asm volatile("" : "+v"(c4));
 #pragma unroll
         for (int j = 0; j < 4; ++j) bv[j] = b4[j];
+        if constexpr (LNF) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) cv[j] = c4[j];
+        }
       }
 #pragma unroll
       for (int mi = 0; mi < MI; ++mi) {
@@ -290,7 +312,8 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
         if (m >= p.M) continue;
         float v[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = acc[ni][mi][j] + bv[j];
+        for (int j = 0; j < 4; ++j)
+          v[j] = LNF ? lnf_out(acc[ni][mi][j], st_s[mi], st_q[mi], cv[j], bv[j]) : acc[ni][mi][j] + bv[j];
 #ifdef CLIPGPU_GEMM_STAMPS
         if (p.diag & 1) {  // timing experiment: same arithmetic, no store
           float s = 0.f;
@@ -300,16 +323,16 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
           continue;
         }
 #endif
-        if constexpr (EPI == EPI_STORE16) {
-          T* o = (T*)p.out + (long)m * p.ldo + n;
+        if constexpr (epi_st16(EPI)) {
+          OT* o = (OT*)p.out + (long)m * p.ldo + n;
           if (nfull) {
             V4 w;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) w[j] = to16<T>(apply_act<ACT>(v[j]));
+            for (int j = 0; j < 4; ++j) w[j] = to16<OT>(apply_act<ACT>(v[j]));
             *(V4*)o = w;
           } else {
             for (int j = 0; j < 4; ++j)
-              if (n + j < p.N) o[j] = to16<T>(apply_act<ACT>(v[j]));
+              if (n + j < p.N) o[j] = to16<OT>(apply_act<ACT>(v[j]));
           }
         } else {
           XE* o;  // (EPI_STORE32: f32 output)
@@ -467,6 +490,10 @@ template <typename T, int BM, int BN, int WGM, int WGN, int EPI, int ACT, int NS
 __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_per_eu)) void gemm_pipe_kernel(
     GemmParams p) {
   typedef typename Vec8<T>::type V8;
+  constexpr bool LNF = epi_lnf(EPI);
+  static_assert(!LNF || std::is_same<T, _Float16>::value, "LayerNorm fold: f16 operands");
+  typedef typename std::conditional<EPI == EPI_LNF_BF, __bf16, T>::type OT;  // 16-bit output type
+  constexpr int EXTRA = LNF ? 4096 : 2048;  // LDS: bias slots (+ the LNF column-sum slots)
   constexpr int NW = WGM * WGN;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
   constexpr int PW = BN / 8, PA = BM / 8, PT = PW + PA;
@@ -484,7 +511,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
   static_assert(BM % 8 == 0 && BN % 8 == 0 && MI >= 1 && BN <= 256 && PT >= NW, "bad tile");
   static_assert(NI == 2 || NI == 3 || NI == 4 || NI == 6 || NI == 8, "column permutation: NI in {2,3,4,6,8}");
   static_assert(NS == 2 || NS == 3, "2 or 3 LDS stages");
-  __shared__ __attribute__((aligned(16))) char smem[NS * STAGE + 2048];
+  __shared__ __attribute__((aligned(16))) char smem[NS * STAGE + EXTRA];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -497,7 +524,9 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
   const char* const Ab = (const char*)p.A;
   const char* const Wb = (const char*)p.W;
   const float* const bias_p = p.bias;
+  const float* const cs_p = p.cs;  // EPI_LNF
   asm volatile("" ::"s"(lda_i), "s"(ldw_i), "s"(nb), "s"(Ab), "s"(Wb), "s"(bias_p));
+  if constexpr (LNF) asm volatile("" ::"s"(cs_p));
   const int nTn = (p.N + BN - 1) / BN;
   const int grp = p.group > 0 ? p.group : CLIPGPU_TILE_GROUP;
   asm volatile("" ::"s"(grp));
@@ -609,6 +638,10 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
       const int n = min(d_n0 + lane * 4, ((p.N - 1) / 4) * 4);
       GEMM_POISON(smem + NS * STAGE + (d_ti & 1) * 1024);
       glds16(bias_p + n, smem + NS * STAGE + (d_ti & 1) * 1024);
+      if constexpr (LNF) {  // and its column sums (issued before the step's pieces, like the bias)
+        GEMM_POISON(smem + NS * STAGE + 2048 + (d_ti & 1) * 1024);
+        glds16(cs_p + n, smem + NS * STAGE + 2048 + (d_ti & 1) * 1024);
+      }
     }
   };
   auto dma_advance = [&]() {
@@ -663,6 +696,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
   };
   const uint32_t lds0 = lds_addr(smem);
   f32x4 acc[NI][MI];
+  float st_s[MI], st_q[MI];  // EPI_LNF: the lane's running row sums / sums of squares (lnf_acc)
   V8 a0[MI], b0[NI], a1[MI], b1[NI];  // fragments of one phase
 
   auto rd_b = [&](auto kc, V8(&b)[NI], uint32_t buf, int kk) {
@@ -699,6 +733,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
 #pragma unroll
       for (int ni = 0; ni < NI; ++ni)
         acc[ni][g] = mfma_16x16x32(b[ni], a[g], Z ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[ni][g]);
+      if constexpr (LNF) lnf_acc<Z>(st_s[g], st_q[g], a[g]);  // (phase 0 = chunk 2 kt, phase 1 = 2 kt + 1)
     }
   };
   auto phase0 = [&](auto zero, uint32_t buf) {
@@ -750,15 +785,25 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
     typedef typename std::conditional<epi_x16(EPI), _Float16, float>::type XE;
     const int nc = n0 + wn + fq * (4 * NI);
     const bool nfull = nc + 4 * NI <= p.N;
-    f32x4 bias[NI];
+    f32x4 bias[NI], csv[NI];
 #pragma unroll
     for (int ni = 0; ni < NI; ++ni) bias[ni] = f32x4{0.f, 0.f, 0.f, 0.f};
     if (bias_p != nullptr) {
       const uint32_t ba = lds0 + NS * STAGE + bpar * 1024 + (wn + fq * (4 * NI)) * 4;
       static_for<NI>([&](auto ni) { ds_read_b128<(int)ni * 16>(bias[ni], ba); });
+      if constexpr (LNF) static_for<NI>([&](auto ni) { ds_read_b128<2048 + (int)ni * 16>(csv[ni], ba); });
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
       for (int ni = 0; ni < NI; ++ni) asm volatile("" : "+v"(bias[ni]));
+      if constexpr (LNF) {
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni) asm volatile("" : "+v"(csv[ni]));
+      }
+    }
+    if constexpr (LNF) {  // the rows' mean / rstd (every lane: cross-lane combine)
+      const float inv_k = 1.0f / (float)p.K;
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi) lnf_finish(st_s[mi], st_q[mi], inv_k, p.ln_eps);
     }
     // EPI_RESID adds the residual row x[m]; EPI_PATCH writes patch p of image b to token
     // row b*(G2+cls) + cls + p and adds pos[cls + p].
@@ -815,7 +860,9 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
 #pragma unroll
       for (int ni = 0; ni < NI; ++ni)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[ni][j] = acc[ni][mi][j] + bias[ni][j];
+        for (int j = 0; j < 4; ++j)
+          v[ni][j] = LNF ? lnf_out(acc[ni][mi][j], st_s[mi], st_q[mi], csv[ni][j], bias[ni][j])
+                         : acc[ni][mi][j] + bias[ni][j];
 #ifdef CLIPGPU_GEMM_STAMPS
       if (p.diag & 1) {
         float s = 0.f;
@@ -827,24 +874,24 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
         continue;
       }
 #endif
-      if constexpr (EPI == EPI_STORE16) {
-        T* o = (T*)p.out + (long)m * p.ldo + nc;
+      if constexpr (epi_st16(EPI)) {
+        OT* o = (OT*)p.out + (long)m * p.ldo + nc;
         if (nfull) {
           if constexpr (NI % 2 == 0) {
 #pragma unroll
             for (int h = 0; h < NI / 2; ++h) {
-              V8 w;
+              typename Vec8<OT>::type w;
 #pragma unroll
-              for (int e = 0; e < 8; ++e) w[e] = to16<T>(apply_act<ACT>(v[2 * h + e / 4][e % 4]));
-              *(V8*)(o + h * 8) = w;
+              for (int e = 0; e < 8; ++e) w[e] = to16<OT>(apply_act<ACT>(v[2 * h + e / 4][e % 4]));
+              *(typename Vec8<OT>::type*)(o + h * 8) = w;
             }
           } else {  // odd NI: the lane's 4 NI columns start 8-byte aligned only -> 8-byte stores
 #pragma unroll
             for (int ni = 0; ni < NI; ++ni) {
-              typename Vec4<T>::type w;
+              typename Vec4<OT>::type w;
 #pragma unroll
-              for (int j = 0; j < 4; ++j) w[j] = to16<T>(apply_act<ACT>(v[ni][j]));
-              *(typename Vec4<T>::type*)(o + ni * 4) = w;
+              for (int j = 0; j < 4; ++j) w[j] = to16<OT>(apply_act<ACT>(v[ni][j]));
+              *(typename Vec4<OT>::type*)(o + ni * 4) = w;
             }
           }
         } else {
@@ -852,7 +899,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
           for (int ni = 0; ni < NI; ++ni)
 #pragma unroll
             for (int j = 0; j < 4; ++j)
-              if (nc + ni * 4 + j < p.N) o[ni * 4 + j] = to16<T>(apply_act<ACT>(v[ni][j]));
+              if (nc + ni * 4 + j < p.N) o[ni * 4 + j] = to16<OT>(apply_act<ACT>(v[ni][j]));
         }
       } else {
         XE* o = (XE*)p.out + out_row(m) + nc;  // (EPI_STORE32: f32)
@@ -882,7 +929,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
   };
   // vm ops a full tile's epilogue leaves in flight behind the DMA of the step after it (the same
   // count on both paths: MI NI / 2 16-byte stores of 16-bit values, MI NI of f32, + as many loads)
-  constexpr int EPI_VM = EPI == EPI_STORE16 ? (NI % 2 ? MI * NI : MI * NI / 2)
+  constexpr int EPI_VM = epi_st16(EPI) ? (NI % 2 ? MI * NI : MI * NI / 2)
                                             : ((epi_resid(EPI) || epi_patch(EPI)) ? 2 * MI * NI : MI * NI);
   // 3 stages: retire all but this wave's DMA pieces of the youngest step (+ X more recent vm ops):
   // NP pieces per step on waves < PT % NW (or every wave when the split is even), else NP - 1
@@ -1044,7 +1091,7 @@ template <typename T, int EPI, int ACT>
 hipError_t launch_pipe_224(const GemmParams& p, hipStream_t s) {
   const int grid = grid_224(p.M, p.N);
   if (p.K / BK >= 3) gemm_launch(gemm_pipe_kernel<T, 224, 192, 2, 4, EPI, ACT, 3, 1, 1, 0>, grid, 512, s, p);
-  else gemm_launch(gemm_pipe_kernel<T, 224, 192, 2, 4, EPI, ACT, 2, 1, 1, 0>, grid, 512, s, p);
+  else if constexpr (!epi_lnf(EPI)) gemm_launch(gemm_pipe_kernel<T, 224, 192, 2, 4, EPI, ACT, 2, 1, 1, 0>, grid, 512, s, p);
   return hipGetLastError();
 }
 
@@ -1064,6 +1111,9 @@ constexpr int SKINNY_U = 8;
 template <typename T, int EPI, int ACT>
 __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmParams p) {
   typedef typename Vec8<T>::type V8;
+  constexpr bool LNF = epi_lnf(EPI);
+  static_assert(!LNF || std::is_same<T, _Float16>::value, "LayerNorm fold: f16 operands");
+  typedef typename std::conditional<EPI == EPI_LNF_BF, __bf16, T>::type OT;  // 16-bit output type
   constexpr int U = SKINNY_U;
   const int lane = threadIdx.x & 63;
   const int wid = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -1088,10 +1138,15 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmParams p) {
   load(w0, a0, 0);
   if (U < nc) load(w1, a1, U);
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  float st_s = 0.f, st_q = 0.f;  // EPI_LNF: the lane's running row sum / sum of squares (lnf_acc)
   for (int c0 = 0; c0 < nc; c0 += U) {
     if (c0 + 2 * U < nc) load(w2, a2, c0 + 2 * U);
 #pragma unroll
     for (int u = 0; u < U; ++u) acc = mfma_16x16x32(w0[u], a0[u], acc);
+    if constexpr (LNF) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) lnf_acc_dyn(c0 + u == 0, st_s, st_q, a0[u]);  // chunks in K order
+    }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       w0[u] = w1[u];
@@ -1100,18 +1155,20 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmParams p) {
       a1[u] = a2[u];
     }
   }
+  if constexpr (LNF) lnf_finish(st_s, st_q, 1.0f / (float)p.K, p.ln_eps);  // (every lane)
   if (m >= p.M) return;
   const int n = tn * 16 + fq * 4;
-  f32x4 bias = {0.f, 0.f, 0.f, 0.f};
+  f32x4 bias = {0.f, 0.f, 0.f, 0.f}, csv = {0.f, 0.f, 0.f, 0.f};
   if (p.bias != nullptr) bias = *(const f32x4*)(p.bias + n);
+  if constexpr (LNF) csv = *(const f32x4*)(p.cs + n);
   float v[4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) v[j] = acc[j] + bias[j];
-  if constexpr (EPI == EPI_STORE16) {
-    typename Vec4<T>::type o;
+  for (int j = 0; j < 4; ++j) v[j] = LNF ? lnf_out(acc[j], st_s, st_q, csv[j], bias[j]) : acc[j] + bias[j];
+  if constexpr (epi_st16(EPI)) {
+    typename Vec4<OT>::type o;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) o[j] = to16<T>(apply_act<ACT>(v[j]));
-    *(typename Vec4<T>::type*)((T*)p.out + (long)m * p.ldo + n) = o;
+    for (int j = 0; j < 4; ++j) o[j] = to16<OT>(apply_act<ACT>(v[j]));
+    *(typename Vec4<OT>::type*)((OT*)p.out + (long)m * p.ldo + n) = o;
   } else {
     typedef typename std::conditional<epi_x16(EPI), _Float16, float>::type XE;  // (EPI_STORE32: f32)
     XE* o = (XE*)p.out + (long)m * p.ldo + n;
@@ -1144,20 +1201,38 @@ hipError_t launch_tile(const GemmParams& p, hipStream_t s) {
     if ((p.tile == TILE_AUTO || p.tile == TILE_SKINNY) && skinny_ok(p)) return launch_skinny<T, EPI, ACT>(p, s);
   }
   if (p.tile == TILE_SKINNY) return hipErrorInvalidValue;
-  const int tile = p.tile == TILE_AUTO ? pick_gemm_tile(p.M, p.N, p.K) : p.tile;
+  // (EPI_LNF: the 4-wave 160x128 RS tile, which holds the row statistics without spilling)
+  const int tile = p.tile != TILE_AUTO ? p.tile
+                   : (epi_lnf(EPI) && p.M >= 2048 ? TILE_160x128_RS : pick_gemm_tile(p.M, p.N, p.K));
   // software-pipelined kernel: K >= 128, 16-byte-aligned 16-bit output rows (diag bit 1: legacy, stamp builds)
-  const bool pipe = p.K >= 2 * BK && !(p.diag & 2) && (EPI != EPI_STORE16 || p.ldo % 8 == 0);
+  const bool pipe = p.K >= 2 * BK && !(p.diag & 2) && (!epi_st16(EPI) || p.ldo % 8 == 0);
   if (pipe) {
-    switch (tile) {
-      case TILE_256x128: return launch_pipe<T, 256, 128, 4, 2, EPI, ACT>(p, s);
-      case TILE_256x256: return launch_pipe<T, 256, 256, 2, 4, EPI, ACT>(p, s);
-      case TILE_192x256_W8: return launch_pipe<T, 192, 256, 2, 4, EPI, ACT, 1>(p, s);
-      case TILE_256x256_RS: return launch_pipe<T, 256, 256, 2, 4, EPI, ACT, 3, 1>(p, s);
-      case TILE_160x128_RS: return launch_pipe<T, 160, 128, 2, 2, EPI, ACT, 3, 1>(p, s);
-      case TILE_160x128_W8_RS: return launch_pipe<T, 160, 128, 2, 4, EPI, ACT, 2, 1>(p, s);
-      case TILE_256x256_HALF: return launch_pipe_half<T, EPI, ACT>(p, s);
-      case TILE_224x192_W8: return launch_pipe_224<T, EPI, ACT>(p, s);
-      default: break;
+    if constexpr (epi_lnf(EPI)) {
+      // EPI_LNF: the tiles whose row statistics fit beside their accumulators and fragments; the
+      // 256x256 tiles (3, 14, 18), the 8-wave 160x128 (17) and the two-stage 224x192 would spill
+      // (tools/kernel_regs.py) and run the 4-wave 160x128 RS tile instead (the same bits: every
+      // kernel accumulates a row's statistics in the same order)
+      switch (tile) {
+        case TILE_256x128: return launch_pipe<T, 256, 128, 4, 2, EPI, ACT>(p, s);
+        case TILE_192x256_W8: return launch_pipe<T, 192, 256, 2, 4, EPI, ACT, 1>(p, s);
+        case TILE_224x192_W8:
+          if (p.K / BK >= 3) return launch_pipe_224<T, EPI, ACT>(p, s);
+          return launch_pipe<T, 160, 128, 2, 2, EPI, ACT, 3, 1>(p, s);
+        case TILE_128x128: break;
+        default: return launch_pipe<T, 160, 128, 2, 2, EPI, ACT, 3, 1>(p, s);
+      }
+    } else {
+      switch (tile) {
+        case TILE_256x128: return launch_pipe<T, 256, 128, 4, 2, EPI, ACT>(p, s);
+        case TILE_256x256: return launch_pipe<T, 256, 256, 2, 4, EPI, ACT>(p, s);
+        case TILE_192x256_W8: return launch_pipe<T, 192, 256, 2, 4, EPI, ACT, 1>(p, s);
+        case TILE_256x256_RS: return launch_pipe<T, 256, 256, 2, 4, EPI, ACT, 3, 1>(p, s);
+        case TILE_160x128_RS: return launch_pipe<T, 160, 128, 2, 2, EPI, ACT, 3, 1>(p, s);
+        case TILE_160x128_W8_RS: return launch_pipe<T, 160, 128, 2, 4, EPI, ACT, 2, 1>(p, s);
+        case TILE_256x256_HALF: return launch_pipe_half<T, EPI, ACT>(p, s);
+        case TILE_224x192_W8: return launch_pipe_224<T, EPI, ACT>(p, s);
+        default: break;
+      }
     }
   }
   return launch_cfg<T, 128, 128, 2, 2, EPI, ACT>(p, s);
@@ -1179,6 +1254,24 @@ hipError_t launch_typed(int epi, int act, const GemmParams& p, hipStream_t s) {
     case EPI_STORE32: return launch_tile<T, EPI_STORE32, ACT_NONE>(p, s);
     case EPI_PATCH:  // rows from launch_patch_rows
       return p.x16 ? launch_tile<T, EPI_PATCH16, ACT_NONE>(p, s) : launch_tile<T, EPI_PATCH, ACT_NONE>(p, s);
+    case EPI_LNF:
+    case EPI_LNF_BF:  // f16 operands only (launch_gemm); the CLIP trunk's activations
+      if constexpr (std::is_same<T, _Float16>::value) {
+        if (epi == EPI_LNF) {
+          switch (act) {
+            case ACT_NONE: return launch_tile<T, EPI_LNF, ACT_NONE>(p, s);
+            case ACT_QUICK_GELU: return launch_tile<T, EPI_LNF, ACT_QUICK_GELU>(p, s);
+            case ACT_GELU: return launch_tile<T, EPI_LNF, ACT_GELU>(p, s);
+          }
+        } else {
+          switch (act) {
+            case ACT_NONE: return launch_tile<T, EPI_LNF_BF, ACT_NONE>(p, s);
+            case ACT_QUICK_GELU: return launch_tile<T, EPI_LNF_BF, ACT_QUICK_GELU>(p, s);
+            case ACT_GELU: return launch_tile<T, EPI_LNF_BF, ACT_GELU>(p, s);
+          }
+        }
+      }
+      break;
   }
   return hipErrorInvalidValue;
 }
@@ -1254,8 +1347,16 @@ long gemm_chunk_rows(long lda, int G) {
   return rows;
 }
 
+// EPI_LNF: f16 operands, output in dt (EPI_LNF_BF for bf16); bias and column sums required.
+hipError_t launch_dt(DType dt, int epi, int act, const GemmParams& p, hipStream_t s) {
+  if (epi == EPI_LNF) return launch_typed<_Float16>(dt == DT_BF16 ? EPI_LNF_BF : EPI_LNF, act, p, s);
+  return dt == DT_BF16 ? launch_typed<__bf16>(epi, act, p, s) : launch_typed<_Float16>(epi, act, p, s);
+}
+
 hipError_t launch_gemm(DType dt, int asrc, int epi, int act, const GemmParams& p, hipStream_t s) {
   if (p.K % BK != 0 || p.M <= 0 || p.N <= 0) return hipErrorInvalidValue;
+  if (epi == EPI_LNF && (p.bias == nullptr || p.cs == nullptr || p.N % 4 != 0)) return hipErrorInvalidValue;
+  if (epi == EPI_LNF_BF) return hipErrorInvalidValue;  // internal code
   if (p.bias != nullptr && p.N % 4 != 0) return hipErrorInvalidValue;  // 16-byte bias DMA
   // 32-bit staging offsets: W must fit whole; A is chunked by rows
   if ((long)p.N * p.ldw * 2 >= (1L << 31) || p.lda <= 0) return hipErrorInvalidValue;
@@ -1264,19 +1365,19 @@ hipError_t launch_gemm(DType dt, int asrc, int epi, int act, const GemmParams& p
     const int G = epi == EPI_PATCH ? p.G : 0;
     const long chunk = gemm_chunk_rows(p.lda, G);
     if (chunk <= 0) return hipErrorInvalidValue;
-    const long osz = epi == EPI_STORE16 ? 2 : 4;
+    const long osz = epi_st16(epi) ? 2 : 4;
     for (long m0 = 0; m0 < p.M; m0 += chunk) {
       GemmParams q = p;
       q.M = (int)std::min<long>(chunk, p.M - m0);
       q.A = (const char*)p.A + m0 * p.lda * 2;
       const long orow = G > 0 ? m0 / ((long)G * G) * ((long)G * G + p.cls) : m0;  // EPI_PATCH: token rows
       q.out = (char*)p.out + orow * p.ldo * osz;
-      const hipError_t err = dt == DT_BF16 ? launch_typed<__bf16>(epi, act, q, s) : launch_typed<_Float16>(epi, act, q, s);
+      const hipError_t err = launch_dt(dt, epi, act, q, s);
       if (err != hipSuccess) return err;
     }
     return hipSuccess;
   }
-  return dt == DT_BF16 ? launch_typed<__bf16>(epi, act, p, s) : launch_typed<_Float16>(epi, act, p, s);
+  return launch_dt(dt, epi, act, p, s);
 }
 
 #ifdef CLIPGPU_GEMM_STAMPS

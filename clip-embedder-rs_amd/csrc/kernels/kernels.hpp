@@ -25,10 +25,19 @@ enum Epi {
   // (internal: the residual-stream epilogues with an f16 stream, GemmParams.x16; launch_gemm picks them)
   EPI_RESID16 = 5,
   EPI_PATCH16 = 6,
+  // LayerNorm folded into the GEMM (A = the f16 residual stream x itself, W' = W diag(gamma) in f16):
+  //   out16[m][n] = act(rstd_m (acc - mean_m cs[n]) + bias[n]),  cs[n] = sum_k W'[n][k]
+  //   (GemmParams.cs), bias = b + W beta, mean_m / rstd_m from sum / sum of squares of row m of A
+  //   accumulated from the MFMA A fragments in K order (kernels/gemm.hip "LayerNorm fold").
+  //   launch_gemm takes EPI_LNF with dt = the output type; the operands are f16.
+  EPI_LNF = 7,
+  EPI_LNF_BF = 8,  // (internal: EPI_LNF with a bf16 output)
 };
 constexpr bool epi_resid(int e) { return e == EPI_RESID || e == EPI_RESID16; }
 constexpr bool epi_patch(int e) { return e == EPI_PATCH || e == EPI_PATCH16; }
 constexpr bool epi_x16(int e) { return e == EPI_RESID16 || e == EPI_PATCH16; }
+constexpr bool epi_lnf(int e) { return e == EPI_LNF || e == EPI_LNF_BF; }
+constexpr bool epi_st16(int e) { return e == EPI_STORE16 || epi_lnf(e); }  // 16-bit activation outputs
 
 struct GemmParams {
   const void* A; long lda;   // A_ROWS source
@@ -44,6 +53,8 @@ struct GemmParams {
   int group;                 // tile order: row panels per group (gemm_util.hpp tile_coords); 0 = 8
   int prio;                  // 8-wave gemm_pipe tiles: 1 = the younger half of the block at s_setprio 1
   int x16;                   // EPI_RESID / EPI_PATCH: the residual stream `out` is f16 (else f32); the adds are f32
+  const float* cs;           // EPI_LNF: [N] column sums of W' (f32)
+  float ln_eps;              // EPI_LNF: the LayerNorm epsilon
 };
 
 // Tile configurations of the MFMA GEMM.  Ids are stable across rounds; the ones not listed were
@@ -108,13 +119,13 @@ hipError_t launch_ln_rows(DType dt, const void* x, int x16, const float* w, cons
 // qs != nullptr (these LN launchers): the output is MX-fp8, out16 = e4m3 bytes [rows][D],
 // qs = scales [rows][D/32] (gemm_mx.hip's A operand); D % 32 == 0.
 
-// Vision stem tail: CLS row = cls + pos[0]; x = ln_pre(x) (in place); h = ln_1(x).
+// Vision stem tail: CLS row = cls + pos[0]; x = ln_pre(x) (in place); h = ln_1(x) (h == nullptr: x only).
 hipError_t launch_vision_embed_ln(DType dt, void* x, int x16, const float* cls, const float* pos,
                                   const float* lnpre_w, const float* lnpre_b,
                                   const float* ln1_w, const float* ln1_b, float eps,
                                   void* h, int B, int tokens, int D, hipStream_t s, uint8_t* qs = nullptr);
 
-// Text stem: x = tok[ids] + pos; h = ln_1(x).
+// Text stem: x = tok[ids] + pos; h = ln_1(x) (h == nullptr: x only).
 hipError_t launch_text_embed_ln(DType dt, const int64_t* ids, const float* tok, const float* pos,
                                 const float* ln1_w, const float* ln1_b, float eps, void* x, int x16,
                                 void* h, int B, int T, int D, int vocab, hipStream_t s, uint8_t* qs = nullptr);

@@ -216,11 +216,14 @@ __global__ __launch_bounds__(256) void vision_embed_ln_kernel(XT* __restrict__ x
   }
   load_row(lnpre_w, D4, lane, g0);
   load_row(lnpre_b, D4, lane, b0);
-  load_row(ln1_w, D4, lane, g1);
-  load_row(ln1_b, D4, lane, b1);
+  if (h != nullptr) {
+    load_row(ln1_w, D4, lane, g1);
+    load_row(ln1_b, D4, lane, b1);
+  }
   layer_norm_regs(r, y, g0, b0, eps, D, lane);
   round_rowx<XT>(y);  // ln_1 of the residual row as stored
   store_rowx(x + (long)row * D, y, D4, lane);
+  if (h == nullptr) return;  // (LayerNorm folded into the QKV GEMM: x only)
   layer_norm_regs(y, z, g1, b1, eps, D, lane);
   store_ln_out(h, qs, row, D, z, lane);
 }
@@ -239,11 +242,14 @@ __global__ __launch_bounds__(256) void text_embed_ln_kernel(const int64_t* __res
   Row<NV> e, p, y, g, bb;
   load_row(tok + id * D, D4, lane, e);
   load_row(pos + (long)(row % Tctx) * D, D4, lane, p);
-  load_row(ln1_w, D4, lane, g);
-  load_row(ln1_b, D4, lane, bb);
+  if (h != nullptr) {
+    load_row(ln1_w, D4, lane, g);
+    load_row(ln1_b, D4, lane, bb);
+  }
   add_row(e, p);
   round_rowx<XT>(e);  // ln_1 of the residual row as stored
   store_rowx(x + (long)row * D, e, D4, lane);
+  if (h == nullptr) return;  // (LayerNorm folded into the QKV GEMM: x only)
   layer_norm_regs(e, y, g, bb, eps, D, lane);
   store_ln_out(h, qs, row, D, y, lane);
 }

@@ -121,6 +121,27 @@ int clipgpu_test_gemm(int dtype, int mode, int act, int64_t M, int64_t N, int64_
   });
 }
 
+int clipgpu_test_gemm_lnf(int dtype, int act, int64_t M, int64_t N, int64_t K, const float* x, const float* wf,
+                          const float* cs, const float* bias, float eps, int tile, float* out) {
+  return guarded([&]() {
+    const DType dt = dt_of(dtype);
+    if (M <= 0 || N <= 0 || K <= 0 || K % 64 || N % 4) throw ClipErr(CLIPGPU_ERR_INVALID, "bad GEMM shape");
+    if (tile != 0 && tile != TILE_SKINNY && !gemm_tile_built(tile)) throw ClipErr(CLIPGPU_ERR_INVALID, "bad tile");
+    DevBuf dA(M * K * 2), dW(N * K * 2), dB(N * 4), dC(N * 4), dO(M * N * 2);
+    up16(DT_F16, dA.p, x, M * K);
+    up16(DT_F16, dW.p, wf, N * K);
+    up(dB.p, bias, N * 4);
+    up(dC.p, cs, N * 4);
+    GemmParams g{};
+    g.tile = tile;
+    g.A = dA.p; g.lda = K; g.W = dW.p; g.ldw = K; g.bias = dB.as<float>(); g.cs = dC.as<float>(); g.ln_eps = eps;
+    g.out = dO.p; g.ldo = N; g.M = (int)M; g.N = (int)N; g.K = (int)K;
+    TCHECK(launch_gemm(dt, A_ROWS, EPI_LNF, act, g, nullptr));
+    TCHECK(hipDeviceSynchronize());
+    down16(dt, out, dO.p, M * N);
+  });
+}
+
 int clipgpu_test_attention(int dtype, int64_t B, int64_t N, int64_t H, int64_t HD, int causal, const float* qkv,
                            float* out) {
   return guarded([&]() {

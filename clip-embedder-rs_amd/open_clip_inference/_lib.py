@@ -67,6 +67,8 @@ _PROTOS = [
     ("clipgpu_synth_tensor", c_int, [c_uint64, c_char_p, c_double, c_double, c_void_p, c_int64]),
     # include/clipgpu_testing.h
     ("clipgpu_test_gemm", c_int, [c_int, c_int, c_int, c_int64, c_int64, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    ("clipgpu_test_gemm_lnf", c_int, [c_int, c_int, c_int64, c_int64, c_int64, c_void_p, c_void_p, c_void_p,
+                               c_void_p, c_float, c_int, c_void_p]),
     ("clipgpu_test_attention", c_int, [c_int, c_int64, c_int64, c_int64, c_int64, c_int, c_void_p, c_void_p]),
     ("clipgpu_test_layernorm", c_int, [c_int, c_int64, c_int64, c_float, c_void_p, c_void_p, c_void_p, c_void_p]),
     ("clipgpu_test_gemm_grid", c_int, [c_int, c_int64, c_int64, c_int64, POINTER(c_int)]),
@@ -76,7 +78,7 @@ _PROTOS = [
                                            POINTER(c_double)]),
     ("clipgpu_test_engine_tiles", c_int, [c_void_p, POINTER(c_int)]),
     ("clipgpu_test_engine_lanes", c_int, [c_void_p, POINTER(c_int)]),
-    ("clipgpu_test_engine_residual", c_int, [c_void_p, POINTER(c_int)]),
+    ("clipgpu_test_engine_residual", c_int, [c_void_p, POINTER(c_int), POINTER(c_int)]),
     ("clipgpu_test_host_plan", c_int, [c_void_p, c_int, POINTER(c_int), c_int]),
     ("clipgpu_test_force_broadcast", c_int, [c_void_p, c_int]),
     ("clipgpu_test_comm_lazy", c_int, [c_void_p]),

@@ -20,7 +20,7 @@ class Options(ctypes.Structure):
                 ("tuning", ctypes.c_int32), ("communicator", ctypes.c_int32),
                 ("graphs", ctypes.c_int32), ("prune_last", ctypes.c_int32), ("trim_text", ctypes.c_int32),
                 ("gemm_tiles", ctypes.c_int32 * 4), ("patch_tile", ctypes.c_int32), ("mx_layers", ctypes.c_uint32),
-                ("residual", ctypes.c_int32)]
+                ("residual", ctypes.c_int32), ("ln_fold", ctypes.c_int32)]
 
 
 def _tristate(v) -> int:
@@ -50,7 +50,7 @@ class Engine:
                  dtype: str = "bf16", max_batch: int = 256, mx_sites=None, lanes: int = 0, tuning=False,
                  communicator: bool = False, graphs: Optional[bool] = None, prune_last: Optional[bool] = None,
                  trim_text: Optional[bool] = None, gemm_tiles: Optional[Sequence[int]] = None, patch_tile: int = 0,
-                 mx_layers=None, residual: Optional[str] = None):
+                 mx_layers=None, residual: Optional[str] = None, ln_fold: Optional[bool] = None):
         """mx_sites: fp8 engines' MX split ("qkv,fc,proj" by default); lanes: concurrent sub-batch lanes
         (0 = the tile table's); tuning: time the GEMM tiles at creation instead of the committed table
         (True / 1: per site + whole forwards, 2: per site only); communicator: create a multi-device
@@ -59,7 +59,8 @@ class Engine:
         GemmTile ids (0 = the table's, -1 = the shape heuristic), patch_tile likewise; mx_layers: fp8
         engines' layers that run their MX sites in MX-fp8 (a bit mask or a list of layer indices;
         None = every layer); residual: the residual stream's storage, "f32" or "f16" (None = the
-        library's default)."""
+        library's default); ln_fold: ln_1 / ln_2 folded into the QKV / c_fc GEMMs (None = where it
+        applies, True = required, False = LayerNorm kernels)."""
         self.model_dir = model_dir
         self.tower = tower
         self.devices = list(devices) if devices else [0]
@@ -68,7 +69,8 @@ class Engine:
         self.opts = {"mx_sites": mx_sites, "lanes": int(lanes), "tuning": tuning, "communicator": bool(communicator),
                      "graphs": graphs, "prune_last": prune_last, "trim_text": trim_text,
                      "gemm_tiles": list(gemm_tiles) if gemm_tiles else None, "patch_tile": int(patch_tile),
-                     "mx_layers": mx_layers, "residual": residual}  # duplicate() rebuilds with the same
+                     "mx_layers": mx_layers, "residual": residual,
+                     "ln_fold": ln_fold}  # duplicate() rebuilds with the same
         dt = {"bf16": _lib.DTYPE_BF16, "f16": _lib.DTYPE_F16, "fp16": _lib.DTYPE_F16, "fp8": _lib.DTYPE_FP8}[dtype]
         devs = (c_int * len(self.devices))(*self.devices)
         opts = Options()
@@ -100,6 +102,7 @@ class Engine:
         if residual not in (None, "f32", "f16"):
             raise ValueError('residual: "f32" or "f16"')
         opts.residual = {None: 0, "f32": 1, "f16": 2}[residual]
+        opts.ln_fold = _tristate(ln_fold)
         h = c_void_p()
         check(lib().clipgpu_create_ex(model_dir.encode(), tower, devs, len(self.devices), dt, self.max_batch,
                                       ctypes.byref(opts), ctypes.byref(h)))

@@ -21,6 +21,11 @@ extern "C" {
  * kGemmTiles; 0 auto, 100 skinny) forces the tile (test hooks only: the engine reads no environment). */
 int clipgpu_test_gemm(int dtype, int mode, int act, int64_t M, int64_t N, int64_t K, const float* A,
                       const float* W, const float* bias, const float* resid, float* out);
+/* The LayerNorm-folded GEMM (EPI_LNF): out[m][n] = act(rstd_m (x W'^T - mean_m cs)[m][n] + bias[n]) with
+ * x [M][K] and wf [N][K] rounded to f16 on upload, mean / rstd of each row of x (eps), the output in
+ * dtype (bf16 / f16), widened to f32.  tile: a built GemmTile, 0 = the launcher's choice, 100 = skinny. */
+int clipgpu_test_gemm_lnf(int dtype, int act, int64_t M, int64_t N, int64_t K, const float* x, const float* wf,
+                          const float* cs, const float* bias, float eps, int tile, float* out);
 
 /* qkv: [B*N][3*D] f32 (rounded to 16-bit on upload), D = H * HD (HD in {64, 72, 80}); out: [B*N][D]. */
 int clipgpu_test_attention(int dtype, int64_t B, int64_t N, int64_t H, int64_t HD, int causal, const float* qkv,
@@ -116,14 +121,17 @@ int clipgpu_test_engine_tiles(const struct clipgpu_engine* e, int tiles[4]);
 /* Concurrent sub-batches the engine's device-side forwards run (the creation-time tuning's pick,
  * or clipgpu_options.lanes). */
 int clipgpu_test_engine_lanes(const struct clipgpu_engine* e, int* dev_lanes);
-/* The residual stream's resolved storage: CLIPGPU_RESIDUAL_F32 or CLIPGPU_RESIDUAL_F16. */
-int clipgpu_test_engine_residual(const struct clipgpu_engine* e, int* residual);
+/* The residual stream's resolved storage (CLIPGPU_RESIDUAL_F32 / _F16) and whether ln_1 / ln_2 are
+ * folded into the QKV / c_fc GEMMs (*ln_fold = 1; clipgpu_options.ln_fold; ln_fold may be NULL). */
+int clipgpu_test_engine_residual(const struct clipgpu_engine* e, int* residual, int* ln_fold);
 /* The host-buffer vision path's chunk plan (tools/host_plan_ab.py): n_chunks (1..4) chunks of a
  * max_batch round cut at bounds[0 .. n_chunks - 2]; n_chunks = 0 restores the default
  * (engine.hip host_chunks).  copy_stream = 1: the H2Ds in chunk order on the replica's copy
  * stream (default); 0: each on its chunk's lane stream; 2: each chunk's two halves on two copy
  * streams at once; 3: registered inputs pulled through their host mapping by a copy kernel on
- * the copy stream (others as 1).  Speed only, never the bits. */
+ * the copy stream (others as 1).  + 16: a multi-round call starts each round's forwards together,
+ * once the round's last chunk has landed; + 32: the D2Hs on the copy stream.  Speed only, never the
+ * bits. */
 int clipgpu_test_host_plan(struct clipgpu_engine* e, int n_chunks, const int* bounds, int copy_stream);
 /* Gathered calls of this handle take the ragged branch (one ncclBroadcast per block) even when
  * every block has the same size (on != 0), so a one-rank or equal-shard run exercises it. */

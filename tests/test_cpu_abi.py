@@ -273,6 +273,16 @@ def test_options_init_and_validation():
     o3.residual = 3
     rc = _lib.lib().clipgpu_create_ex(d.encode(), 0, devs, 1, 0, 8, ctypes.byref(o3), ctypes.byref(h))
     assert rc != 0 and b"residual" in _lib.lib().clipgpu_last_error()
+    # LayerNorm fold (ABI v4): -1 / 0 / 1; on only with the f16 stream and a QuickGELU / GELU MLP
+    assert o3.ln_fold == 0
+    o3.residual = 0
+    o3.ln_fold = 2
+    rc = _lib.lib().clipgpu_create_ex(d.encode(), 0, devs, 1, 0, 8, ctypes.byref(o3), ctypes.byref(h))
+    assert rc != 0 and b"ln_fold" in _lib.lib().clipgpu_last_error()
+    with pytest.raises(ClipError, match="ln_fold = 1"):
+        Engine(d, 0, [0], "bf16", 8, residual="f32", ln_fold=True)
+    with pytest.raises(ClipError, match="ln_fold = 1"):
+        Engine(d, 0, [0], "fp8", 8, ln_fold=True)
     tiny_layers = json.load(open(os.path.join(d, "open_clip_config.json")))["model_cfg"]["vision_cfg"]["layers"]
     with pytest.raises(ClipError, match="beyond the tower"):
         Engine(d, 0, [0], "fp8", 8, mx_layers=[tiny_layers])

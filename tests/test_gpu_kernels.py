@@ -237,6 +237,71 @@ def test_gemm_persistent_multi_tile(mode, tile):
         assert np.abs(out - ref).max() < 1e-4
 
 
+def run_lnf(dtype, act, x, wf, cs, bias, eps, tile, lib=None):
+    """clipgpu_test_gemm_lnf (EPI_LNF): x / wf rounded to f16 on upload, output widened to f32."""
+    M, K = x.shape
+    N = wf.shape[0]
+    out = np.empty((M, N), np.float32)
+    args = [np.ascontiguousarray(a, np.float32) for a in (x, wf, cs, bias)]
+    if lib is None:
+        L = _lib()
+        L.check(L.lib().clipgpu_test_gemm_lnf(dtype, act, M, N, K, *[a.ctypes.data for a in args], eps, tile,
+                                              out.ctypes.data))
+    else:
+        import ctypes
+        f = lib.clipgpu_test_gemm_lnf
+        f.argtypes = [ctypes.c_int, ctypes.c_int] + [ctypes.c_int64] * 3 + [ctypes.c_void_p] * 4 + \
+            [ctypes.c_float, ctypes.c_int, ctypes.c_void_p]
+        f.restype = ctypes.c_int
+        rc = f(dtype, act, M, N, K, *[a.ctypes.data for a in args], eps, tile, out.ctypes.data)
+        assert rc == 0, lib.clipgpu_last_error()
+    return out
+
+
+def lnf_case(M, N, K, seed):
+    """A residual-stream-like x (f16: per-row offsets, a few large channels), a Linear behind a
+    LayerNorm (gamma, beta), and its fold: W' = f16(W diag(gamma)), cs = row sums of W', bias b + W beta."""
+    rng = np.random.default_rng(seed)
+    x = rng.standard_normal((M, K)) * rng.uniform(0.5, 4.0, (M, 1)) + rng.standard_normal((M, 1))
+    x[:, rng.choice(K, 3, replace=False)] *= 40.0  # the stream's massive channels
+    x = x.astype(np.float16).astype(np.float64)
+    w = rng.standard_normal((N, K)) / np.sqrt(K)
+    gamma = 1.0 + 0.2 * rng.standard_normal(K)
+    beta = 0.1 * rng.standard_normal(K)
+    b = 0.1 * rng.standard_normal(N)
+    wf = (w.astype(np.float32) * gamma.astype(np.float32)).astype(np.float16).astype(np.float64)
+    cs = wf.sum(1)
+    bp = b + w.astype(np.float32).astype(np.float64) @ beta.astype(np.float32).astype(np.float64)
+    return x, w, gamma, beta, b, wf, cs, bp
+
+
+@pytest.mark.parametrize("M,N,K,act", [(77, 2304, 768, 0), (250, 3072, 768, 1), (3000, 2304, 768, 0),
+                                       (6400, 3072, 768, 1), (12801, 1536, 512, 0), (1000, 2048, 512, 2)])
+def test_layernorm_folded_gemm(M, N, K, act):
+    """EPI_LNF (ln_1 / ln_2 folded into QKV / c_fc): every tile -- and the skinny kernel at M <= 256 --
+    gives the same bits (the row statistics are accumulated from the MFMA A fragments in the same
+    K order everywhere), and the result matches LayerNorm-then-Linear in fp64 within the bf16
+    output rounding plus the f16 rounding of W diag(gamma) (|err| <= 2^-7 |ref| + 0.01 rms(ref))."""
+    x, w, gamma, beta, b, wf, cs, bp = lnf_case(M, N, K, M + N + act)
+    eps = 1e-5
+    tiles = [0] + BUILT_TILES + ([100] if M <= 256 else [])
+    outs = [run_lnf(BF16, act, x, wf, cs, bp, eps, t) for t in tiles]
+    for t, o in zip(tiles[1:], outs[1:]):
+        assert np.array_equal(o, outs[0]), t
+    mu = x.mean(1, keepdims=True)
+    var = ((x - mu) ** 2).mean(1, keepdims=True)
+    ref = ref_act(act, ((x - mu) / np.sqrt(var + eps) * gamma + beta) @ w.T + b)
+    err = np.abs(outs[0] - ref)
+    assert np.all(err <= 2 ** -7 * np.abs(ref) + 0.01 * np.sqrt(np.mean(ref ** 2))), float(err.max())
+    # f16 output (f16 engines): the same sums, rounded to f16
+    o16 = run_lnf(F16, act, x, wf, cs, bp, eps, 0)
+    assert np.all(np.abs(o16 - ref) <= 2 ** -9 * np.abs(ref) + 0.01 * np.sqrt(np.mean(ref ** 2)))
+    if M == 6400:  # race check: the column-sum DMA beside the bias DMA, every pipelined tile
+        P = _poison_lib()
+        for t in BUILT_TILES[1:]:
+            assert np.array_equal(run_lnf(BF16, act, x, wf, cs, bp, eps, t, lib=P), outs[0]), t
+
+
 def ref_attention(qkv, B, N, H, causal, HD=64):
     D = H * HD
     x = qkv.reshape(B, N, 3, H, HD).astype(np.float64)

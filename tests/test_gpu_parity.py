@@ -78,13 +78,15 @@ def test_text_parity(cfg, B, random_eot, dtype):
     check_rows(got, oracle_text(cfg, 1234, ids))
 
 
-@pytest.mark.parametrize("residual", ["f32", "f16"])
+@pytest.mark.parametrize("residual,fold", [("f32", None), ("f16", False), ("f16", None)],
+                         ids=["f32", "f16-ln-kernels", "f16-ln-folded"])
 @pytest.mark.parametrize("dtype", ["bf16", "f16"])
-def test_residual_stream_storage_parity(residual, dtype):
-    """clipgpu_options.residual (ABI v4): the residual stream stored in f32 or in f16 (every add and
-    LayerNorm statistic in f32).  Both towers at ViT-B/32 dims against the fp64 oracle at the
+def test_residual_stream_storage_parity(residual, fold, dtype):
+    """clipgpu_options.residual / ln_fold (ABI v4): the residual stream stored in f32 or in f16 (every
+    add and LayerNorm statistic in f32), with the LayerNorm kernels or with ln_1 / ln_2 folded into the
+    QKV / c_fc GEMMs (the f16 default).  Both towers at ViT-B/32 dims against the fp64 oracle at the
     north-star bar, the lanes / pruning / trimming paths included (a batch over max_batch, host ids
-    with random EOTs), and f16 within 2e-5 of the f32 stream's cosine to the oracle."""
+    with random EOTs), and within 2e-5 of the f32 stream's cosine to the oracle."""
     v, t = specs(VIT_B_32_CFG)
     u8 = weights.synth_images_u8(41, 9, v.image_size)
     px = normalized_pixels(u8, OPENAI_MEAN, OPENAI_STD)
@@ -93,8 +95,9 @@ def test_residual_stream_storage_parity(residual, dtype):
     ref_v, ref_t = oracle_vision(VIT_B_32_CFG, 1234, px), oracle_text(VIT_B_32_CFG, 1234, ids)
     cos = {}
     for res in ("f32", residual):
-        ve = engine(VIT_B_32_CFG, 0, dtype=dtype, max_batch=8, residual=res)
-        te = engine(VIT_B_32_CFG, 1, dtype=dtype, max_batch=8, residual=res)
+        fo = fold if res == residual else None
+        ve = engine(VIT_B_32_CFG, 0, dtype=dtype, max_batch=8, residual=res, ln_fold=fo)
+        te = engine(VIT_B_32_CFG, 1, dtype=dtype, max_batch=8, residual=res, ln_fold=fo)
         cos[res] = (check_rows(ve.embed_pixels(px), ref_v).min(), check_rows(te.embed_tokens(ids), ref_t).min())
         # the device-resident path (graphs, lanes) gives the same rows as the host path
         import torch

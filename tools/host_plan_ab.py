@@ -3,7 +3,9 @@
 max_batch 256 (the bench's), u8 [256,224,224,3] host input; per plan (clipgpu_test_host_plan:
 chunk bounds, H2D on the copy stream or on the lane streams) the ms per clipgpu_embed_u8 call,
 pageable (pinned staging) and caller-registered (clipgpu_host_register), interleaved rounds,
-medians; beside the device-resident forward.  Prints one JSON line per plan.  Runs on the GPU box."""
+medians; beside the device-resident forward.  HP_BATCHES = n: calls of n x 256 images (the
+multi-round path; times per 256-image batch).  copy_stream + 16 / + 32: the multi-round flags of
+clipgpu_test_host_plan.  Prints one JSON line per plan.  Runs on the GPU box."""
 import ctypes
 import json
 import os
@@ -31,10 +33,14 @@ def main():
     B = 256
     rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 3
     calls = int(sys.argv[2]) if len(sys.argv) > 2 else 8
+    nb = int(os.environ.get("HP_BATCHES", "1"))  # batches of 256 per call (multi-round calls: > 1)
     e = Engine(make_model_dir(VIT_B_32_CFG, 1234), 0, [0], "bf16", B)
     g = np.random.default_rng(5)
     x = np.ascontiguousarray(g.integers(0, 256, (B, 224, 224, 3), dtype=np.uint8))
     out = np.empty((B, 512), np.float32)
+    if nb > 1:
+        x = np.ascontiguousarray(np.concatenate([x] * nb))
+        out = np.empty((nb * B, 512), np.float32)
     L = _lib.lib()
     # device-resident reference (the bench's value path)
     d_in = torch.from_numpy(x).cuda()
@@ -69,12 +75,12 @@ def main():
                     if reg:
                         host_unregister(x)
                         host_unregister(out)
-                res.setdefault((tuple(bounds), cs, reg), []).append(ms)
+                res.setdefault((tuple(bounds), cs, reg), []).append(ms / nb)
         print(json.dumps({"round": r}), flush=True)
     for (bounds, cs, reg), v in res.items():
         med = statistics.median(v)
         print(json.dumps({"bounds": list(bounds) or "default", "copy_stream": cs, "registered": reg,
-                          "ms_per_call": round(med, 3), "all": [round(t, 3) for t in v],
+                          "batches_per_call": nb, "ms_per_batch": round(med, 3), "all": [round(t, 3) for t in v],
                           "vs_device": round(dev_ms / med, 3)}), flush=True)
 
 
