@@ -91,6 +91,7 @@ struct Replica {
   char* work = nullptr;   // activations
   DevWeights w;
   void* x = nullptr;      // [rows][D] residual stream: f32, or f16 (clipgpu_engine::x16)
+  float* xs = nullptr;    // [rows + 256][2] (mean, rstd) of x's rows (LayerNorm-folded engines: ln_stats)
   void* h = nullptr;      // [rows][D] 16-bit (LN output / attention output); fp8 engines: LN output as e4m3
   uint8_t* hs = nullptr;   // fp8 engines: [rows][D/32] scales of the LN output in h
   uint8_t* bigs = nullptr; // fp8 engines: [rows][MLP/32] scales of the c_fc output (e4m3 in big)
@@ -559,7 +560,8 @@ void alloc_workspace(clipgpu_engine& e, Replica& r) {
   const size_t E = s.embed_dim;
   const size_t MLP = (size_t)mlp_pad(s);
   const size_t sizes[] = {rows * D * 4, rows * D * 2, rows * wide * 2, B * D * 2, B * E * 4, B * E * 4,
-                          B * e.in_bytes_per_row, e.mx ? rows * D / 32 : 0, e.mx ? rows * MLP / 32 : 0};
+                          B * e.in_bytes_per_row, e.mx ? rows * D / 32 : 0, e.mx ? rows * MLP / 32 : 0,
+                          (rows + 256) * 8};
   size_t total = 0;
   for (size_t z : sizes) total += align256(z);
   HIP_CHECK(hipMalloc(&r.work, total));
@@ -574,6 +576,7 @@ void alloc_workspace(clipgpu_engine& e, Replica& r) {
   r.in = a.take(sizes[6]);
   r.hs = e.mx ? (uint8_t*)a.take(sizes[7]) : nullptr;
   r.bigs = e.mx ? (uint8_t*)a.take(sizes[8]) : nullptr;
+  r.xs = (float*)a.take(sizes[9]);
   for (int i = 0; i < e.lanes; ++i) {
     HIP_CHECK(hipStreamCreateWithFlags(&r.lane[i], hipStreamNonBlocking));
     HIP_CHECK(hipEventCreateWithFlags(&r.join[i], hipEventDisableTiming));
@@ -686,7 +689,7 @@ GemmParams site_gemm(const clipgpu_engine& e, const Replica& r, const LayerW& L,
   }
   if (e.lnf && (site == GS_QKV || site == GS_FC)) {
     g.cs = site == GS_QKV ? L.cs_qkv : L.cs_1;
-    g.ln_eps = e.spec.ln_eps;
+    g.rowstats = r.xs;
   }
   g.group = kSiteGroup[site];
   g.x16 = e.x16 ? 1 : 0;
@@ -764,10 +767,13 @@ inline size_t prune_off_x(const TowerSpec& s, int B) { return align256((size_t)B
 inline size_t prune_off_h(const TowerSpec& s, int B) {
   return prune_off_x(s, B) + align256((size_t)B * s.width * 4);
 }
+inline size_t prune_off_xs(const TowerSpec& s, int B) {  // the compact rows' statistics (ln_fold)
+  return prune_off_h(s, B) + align256((size_t)B * s.width * 2);
+}
 inline bool prune_last(const clipgpu_engine& e, int B, int T) {
   const TowerSpec& s = e.spec;
   return e.prune && s.family != FAMILY_SIGLIP && s.layers > 0 &&
-         prune_off_h(s, B) + (size_t)B * s.width * 2 <= (size_t)B * T * big_wide(s) * 2;
+         prune_off_xs(s, B) + ((size_t)B + 256) * 8 <= (size_t)B * T * big_wide(s) * 2;
 }
 
 // The transformer trunk shared by both towers: L x [LN1 -> QKV -> MHA -> out+res ->
@@ -804,6 +810,7 @@ PoolSrc trunk(const clipgpu_engine& e, const Replica& r, int B, int causal, cons
     if (compact) {  // pooled rows only from here on (QKV in `big` is dead after attention)
       c.x = (char*)r.big + prune_off_x(s, B);
       c.h = (char*)r.big + prune_off_h(s, B);
+      c.xs = (float*)((char*)r.big + prune_off_xs(s, B));
       rows = B;
       ProfScope ps(e, PC_TAIL, st);
       // ids == nullptr: position pool_pos of every sequence (CLS 0, SigLIP2 text T - 1)
@@ -812,17 +819,24 @@ PoolSrc trunk(const clipgpu_engine& e, const Replica& r, int B, int causal, cons
             "gather pooled rows");
     }
     gemm(GS_OUT, PC_OUT_PROJ, "out_proj gemm");
-    if (!ABLATED(0) && !e.lnf) {
+    if (!ABLATED(0)) {
       ProfScope ps(e, compact ? PC_TAIL : PC_LN, st);
-      check(launch_ln_rows(e.dt, c.x, e.x16, L.ln2_w, L.ln2_b, s.ln_eps, c.h, rows, D, st, ln_q(e, l, GS_FC, c.hs)),
-            "ln_2");
+      if (e.lnf)  // (folded into c_fc: its rows' statistics only)
+        check(launch_ln_stats(c.x, 1, s.ln_eps, c.xs, rows, D, st), "ln_2 statistics");
+      else
+        check(launch_ln_rows(e.dt, c.x, e.x16, L.ln2_w, L.ln2_b, s.ln_eps, c.h, rows, D, st, ln_q(e, l, GS_FC, c.hs)),
+              "ln_2");
     }
     gemm(GS_FC, PC_C_FC, "c_fc gemm");
     gemm(GS_PROJ, PC_C_PROJ, "c_proj gemm");
-    if (l + 1 < s.layers && !ABLATED(0) && !e.lnf) {
+    if (l + 1 < s.layers && !ABLATED(0)) {
       ProfScope ps(e, PC_LN, st);
-      check(launch_ln_rows(e.dt, r.x, e.x16, r.w.layers[l + 1].ln1_w, r.w.layers[l + 1].ln1_b, s.ln_eps, r.h, rows, D, st,
-                           ln_q(e, l + 1, GS_QKV, r.hs)), "ln_1");
+      if (e.lnf)  // (folded into the next QKV: its rows' statistics only)
+        check(launch_ln_stats(r.x, 1, s.ln_eps, r.xs, rows, D, st), "ln_1 statistics");
+      else
+        check(launch_ln_rows(e.dt, r.x, e.x16, r.w.layers[l + 1].ln1_w, r.w.layers[l + 1].ln1_b, s.ln_eps, r.h, rows,
+                             D, st, ln_q(e, l + 1, GS_QKV, r.hs)),
+              "ln_1");
     }
     if (compact) return PoolSrc{c.x, 1, nullptr};
   }
@@ -909,13 +923,6 @@ void table_tiles(clipgpu_engine& e) {
     e.tile[GS_OUT] = e.tile[GS_PROJ] = TILE_224x192_W8;
     if (prow >= 2048) e.tile_patch = TILE_224x192_W8;
   }
-  // LayerNorm-folded QKV / c_fc (EPI_LNF): the 256x256 tiles and the 8-wave 160x128 spill with the row
-  // statistics' registers; the 4-wave 160x128 RS tile holds them (221 VGPRs, tools/kernel_regs.py)
-  if (e.lnf && rows >= 2048)
-    for (int site : {GS_QKV, GS_FC})
-      if (e.tile[site] == TILE_256x256_HALF || e.tile[site] == TILE_256x256 || e.tile[site] == TILE_256x256_RS ||
-          e.tile[site] == TILE_160x128_W8_RS)
-        e.tile[site] = TILE_160x128_RS;
 }
 
 // clipgpu_options.gemm_tiles / patch_tile pins over the table's (or the tuner's) choice: a GemmTile
@@ -1076,7 +1083,7 @@ void vision_forward(const clipgpu_engine& e, const Replica& r, const void* pixel
   ProfScope ps(e, PC_STEM, st);
   check(launch_vision_embed_ln(e.dt, r.x, e.x16, r.w.cls, r.w.pos, r.w.lnpre_w, r.w.lnpre_b, r.w.layers[0].ln1_w,
                                r.w.layers[0].ln1_b, s.ln_eps, e.lnf ? nullptr : r.h, B, s.tokens(), D, st,
-                               ln_q(e, 0, GS_QKV, r.hs)),
+                               ln_q(e, 0, GS_QKV, r.hs), r.xs),
         "embed+ln_pre");
   }
   head(e, r, B, trunk(e, r, B, 0, nullptr, st, s.tokens()), d_out, st);
@@ -1093,7 +1100,7 @@ void text_forward(const clipgpu_engine& e, const Replica& r, const int64_t* d_id
   ProfScope ps(e, PC_STEM, st);
   check(launch_text_embed_ln(e.dt, d_ids, r.w.tok, r.w.pos, r.w.layers[0].ln1_w, r.w.layers[0].ln1_b, s.ln_eps,
                              r.x, e.x16, e.lnf ? nullptr : r.h, B, T, s.width, s.vocab_size, st,
-                             ln_q(e, 0, GS_QKV, r.hs)),
+                             ln_q(e, 0, GS_QKV, r.hs), r.xs),
         "token embed+ln_1");
   }
   // CLIP: causal, the EOT (argmax id) row pooled; SigLIP2: no mask, the last position pooled
@@ -1109,6 +1116,7 @@ Replica lane_view(const clipgpu_engine& e, const Replica& r, int b0) {
   const size_t wide = big_wide(s);
   Replica v = r;
   v.x = (char*)r.x + rows * D * xbytes(e);
+  v.xs = r.xs + rows * 2;
   v.h = (char*)r.h + rows * D * 2;
   v.big = (char*)r.big + rows * wide * 2;
   if (r.hs) v.hs = r.hs + rows * D / 32;

@@ -148,43 +148,8 @@ __device__ __forceinline__ float group16_sum(float v) { return row16_sum(v); }
 __device__ __forceinline__ float group16_max(float v) { return row16_max(v); }
 
 // ---- LayerNorm fold (EPI_LNF, kernels/gemm.hip) ---------------------------------------------
-// A lane's running sum and sum of squares of the A-operand elements it feeds the MFMAs: its 8 f16
-// elements of one row per 32-k chunk (lane (fr, fq): k = 32 c + 8 fq .. + 7), chunk by chunk in K
-// order.  Every GEMM kernel gives a lane the same chunks in the same order, so a row's statistics
-// are bit-identical whichever kernel, tile or launch computes it.  Z: the row's first chunk.
-typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
-template <bool Z>
-__device__ __forceinline__ void lnf_acc(float& s, float& q, const f16x8& a) {
-  const f16x2 one = {(_Float16)1.0f, (_Float16)1.0f};
-  float s_ = Z ? 0.f : s, q_ = Z ? 0.f : q;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const f16x2 p2 = {a[2 * j], a[2 * j + 1]};
-    s_ = __builtin_amdgcn_fdot2(p2, one, s_, false);  // v_dot2_f32_f16: exact products, f32 sum
-    q_ = __builtin_amdgcn_fdot2(p2, p2, q_, false);
-  }
-  s = s_;
-  q = q_;
-}
-__device__ __forceinline__ void lnf_acc_dyn(bool z, float& s, float& q, const f16x8& a) {
-  if (z) lnf_acc<true>(s, q, a);
-  else lnf_acc<false>(s, q, a);
-}
-// (bf16 instantiations of the kernels never call these; the overload keeps them compiling)
-template <bool Z>
-__device__ __forceinline__ void lnf_acc(float&, float&, const bf16x8&) {}
-__device__ __forceinline__ void lnf_acc_dyn(bool, float&, float&, const bf16x8&) {}
-// Row statistics from the four lanes of a row (fq = 0..3; lanes ^ 16 and ^ 32 combined in a fixed
-// order, so all four hold the same bits): in place, s -> mean, q -> rstd = 1 / sqrt(var + eps),
-// var = E[x^2] - mean^2 clamped at 0.  Every lane of the wave must execute it (cross-lane swaps).
-__device__ __forceinline__ void lnf_finish(float& s, float& q, float inv_k, float eps) {
-  const float S = xsum32(xsum16(s)), Q = xsum32(xsum16(q));
-  const float mean = S * inv_k;
-  const float var = fmaxf(fmaf(-mean, mean, Q * inv_k), 0.f);
-  s = mean;
-  q = __builtin_amdgcn_rsqf(var + eps);
-}
-// The folded LayerNorm + bias of one output: rstd (acc - mean cs) + bias
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+// The folded LayerNorm + bias of one output from its row's (mean, rstd): rstd (acc - mean cs) + bias
 __device__ __forceinline__ float lnf_out(float acc, float mean, float rstd, float cs, float bias) {
   return fmaf(fmaf(-mean, cs, acc), rstd, bias);
 }

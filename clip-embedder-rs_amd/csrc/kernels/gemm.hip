@@ -118,8 +118,10 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
   constexpr int A_INSTR = BM / 8 / NW, B_INSTR = BN / 8 / NW;  // 1 KiB glds per wave-instruction
   constexpr int TM = BM / WGM, TN = BN / WGN, MI = TM / 16, NI = TN / 16;
   static_assert(A_INSTR >= 1 && B_INSTR >= 1 && MI >= 1 && NI >= 1, "bad tile");
-  // 2 x 256 f32 (tile-parity double buffer) of bias (+ EPI_LNF: of column sums, 2 KiB further on)
-  constexpr int BIAS_BYTES = (LNF ? 2 : 1) * 2 * 1024;
+  // 2 x 256 f32 (tile-parity double buffer) of bias (+ EPI_LNF: of column sums, 2 KiB further on, and
+  // of the tile's row statistics, 2 x SROWP after those)
+  constexpr int SROWP = LNF ? (BM * 8 + 1023) / 1024 * 1024 : 0;
+  constexpr int BIAS_BYTES = LNF ? 4096 + 2 * SROWP : 2048;
   static_assert(BN <= 256, "bias slice is one 1 KiB DMA");
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + BIAS_BYTES];
 
@@ -202,11 +204,16 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
   // The tile's bias slice bias[n0 .. n0+255] goes to LDS by one 1 KiB DMA
   // (wave 0, with the tile's first K-step), so the epilogue needs no global load
   // (which, issued after the next tile's DMA, would wait for it: vmcnt is in order).
-  auto stage_bias = [&](int n0, int par) {
+  auto stage_bias = [&](int m0s, int n0, int par) {
     if (p.bias != nullptr && wave == 0) {
       const int n = min(n0 + lane * 4, ((p.N - 1) / 4) * 4);  // clamped in-bounds 16 B (N % 4 == 0 checked)
       glds16(p.bias + n, smem + 2 * STAGE + par * 1024);
-      if constexpr (LNF) glds16(p.cs + n, smem + 2 * STAGE + 2048 + par * 1024);
+      if constexpr (LNF) {
+        glds16(p.cs + n, smem + 2 * STAGE + 2048 + par * 1024);
+#pragma unroll
+        for (int i = 0; i < SROWP / 1024; ++i)
+          glds16(p.rowstats + (size_t)m0s * 2 + i * 256 + lane * 4, smem + 2 * STAGE + 4096 + par * SROWP + i * 1024);
+      }
     }
   };
 
@@ -225,7 +232,6 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
   // C[m = wm + mi*16 + fr][n = wn + ni*16 + fq*4 + j], i.e. each lane owns 4
   // consecutive output columns of one row -> 8 / 16-byte epilogue stores.
   f32x4 acc[NI][MI];
-  float st_s[MI], st_q[MI];  // EPI_LNF: the lane's running row sums / sums of squares (lnf_acc)
   const uint32_t lds0 = lds_addr(smem);
   auto mfma_block = [&](auto zero, const V8(&a)[MI], const V8(&b)[NI]) {
 #pragma unroll
@@ -251,17 +257,12 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
 #pragma unroll
       for (int ni = 0; ni < NI; ++ni)
         acc[ni][mi] = mfma_16x16x32(b0[ni], a0[mi], decltype(zero)::value ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[ni][mi]);
-      if constexpr (LNF) lnf_acc<decltype(zero)::value>(st_s[mi], st_q[mi], a0[mi]);  // chunk 2 kt
       __builtin_amdgcn_sched_barrier(0);
       ds_read_b128<(int)mi * 2048>(a1[mi], aB + offA[1]);
     });
     static_for<NI>([&](auto ni) { ds_read_b128<(int)ni * 2048>(b1[ni], bB + offB[1]); });
     lgkm_wait_all(a1, b1);
     mfma_block(std::false_type{}, a1, b1);
-    if constexpr (LNF) {
-#pragma unroll
-      for (int mi = 0; mi < MI; ++mi) lnf_acc<false>(st_s[mi], st_q[mi], a1[mi]);  // chunk 2 kt + 1
-    }
   };
 
   // XE: the residual stream's element type (EPI_RESID16 / EPI_PATCH16: f16, else f32)
@@ -280,10 +281,13 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
       }
     };
     if constexpr (epi_resid(EPI)) load_x(0, xr[0]);
-    if constexpr (LNF) {  // the rows' mean / rstd (every lane: cross-lane combine)
-      const float inv_k = 1.0f / (float)p.K;
+    f32x2 rst[MI];  // EPI_LNF: (mean, rstd) of the lane's rows
+    if constexpr (LNF) {
+      const uint32_t sa = lds0 + 2 * STAGE + 4096 + bpar * SROWP + (wm + fr) * 8;
+      static_for<MI>([&](auto mi) { ds_read_b64<(int)mi * 128>(rst[mi], sa); });
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-      for (int mi = 0; mi < MI; ++mi) lnf_finish(st_s[mi], st_q[mi], inv_k, p.ln_eps);
+      for (int mi = 0; mi < MI; ++mi) asm volatile("" : "+v"(rst[mi]));
     }
 #pragma unroll
     for (int ni = 0; ni < NI; ++ni) {
@@ -313,7 +317,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
         float v[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          v[j] = LNF ? lnf_out(acc[ni][mi][j], st_s[mi], st_q[mi], cv[j], bv[j]) : acc[ni][mi][j] + bv[j];
+          v[j] = LNF ? lnf_out(acc[ni][mi][j], rst[mi][0], rst[mi][1], cv[j], bv[j]) : acc[ni][mi][j] + bv[j];
 #ifdef CLIPGPU_GEMM_STAMPS
         if (p.diag & 1) {  // timing experiment: same arithmetic, no store
           float s = 0.f;
@@ -376,7 +380,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
   tile_coords(t_first, nTm, nTn, BM, BN, m0, n0, grp);
   set_tile(m0, n0);
   stage(0, sA0, sB0);
-  stage_bias(n0, 0);
+  stage_bias(m0, n0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
@@ -413,7 +417,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
       tile_coords(tn, nTm, nTn, BM, BN, nm0, nn0, grp);
       set_tile(nm0, nn0);
       stage(0, cur1 ? sA0 : sA1, cur1 ? sB0 : sB1);
-      stage_bias(nn0, bias_par ^ 1);
+      stage_bias(nm0, nn0, bias_par ^ 1);
     }
     if (nk == 1) compute(std::true_type{}, cur1 ? sA1 : sA0, cur1 ? sB1 : sB0);
     else compute(std::false_type{}, cur1 ? sA1 : sA0, cur1 ? sB1 : sB0);
@@ -493,7 +497,9 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
   constexpr bool LNF = epi_lnf(EPI);
   static_assert(!LNF || std::is_same<T, _Float16>::value, "LayerNorm fold: f16 operands");
   typedef typename std::conditional<EPI == EPI_LNF_BF, __bf16, T>::type OT;  // 16-bit output type
-  constexpr int EXTRA = LNF ? 4096 : 2048;  // LDS: bias slots (+ the LNF column-sum slots)
+  // LDS beyond the stages: bias slots; EPI_LNF: + column-sum slots + the tile's row statistics (2 x SROWP)
+  constexpr int SROWP = LNF ? (BM * 8 + 1023) / 1024 * 1024 : 0;
+  constexpr int EXTRA = LNF ? 4096 + 2 * SROWP : 2048;
   constexpr int NW = WGM * WGN;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
   constexpr int PW = BN / 8, PA = BM / 8, PT = PW + PA;
@@ -524,9 +530,10 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
   const char* const Ab = (const char*)p.A;
   const char* const Wb = (const char*)p.W;
   const float* const bias_p = p.bias;
-  const float* const cs_p = p.cs;  // EPI_LNF
+  const float* const cs_p = p.cs;        // EPI_LNF
+  const float* const rs_p = p.rowstats;  // EPI_LNF
   asm volatile("" ::"s"(lda_i), "s"(ldw_i), "s"(nb), "s"(Ab), "s"(Wb), "s"(bias_p));
-  if constexpr (LNF) asm volatile("" ::"s"(cs_p));
+  if constexpr (LNF) asm volatile("" ::"s"(cs_p), "s"(rs_p));
   const int nTn = (p.N + BN - 1) / BN;
   const int grp = p.group > 0 ? p.group : CLIPGPU_TILE_GROUP;
   asm volatile("" ::"s"(grp));
@@ -613,12 +620,13 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
       }
     }
   };
-  int d_g = 0, d_kt = 0, d_t = t_first, d_n0 = 0, d_ti = 0;
+  int d_g = 0, d_kt = 0, d_t = t_first, d_n0 = 0, d_m0 = 0, d_ti = 0;
   {
     int m0, n0;
     unit_coords(d_t, m0, n0);
     set_tile(m0, n0);
     d_n0 = n0;
+    d_m0 = m0;
   }
   auto dma_piece = [&](auto ic) {
     constexpr int i = decltype(ic)::value;
@@ -638,9 +646,15 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
       const int n = min(d_n0 + lane * 4, ((p.N - 1) / 4) * 4);
       GEMM_POISON(smem + NS * STAGE + (d_ti & 1) * 1024);
       glds16(bias_p + n, smem + NS * STAGE + (d_ti & 1) * 1024);
-      if constexpr (LNF) {  // and its column sums (issued before the step's pieces, like the bias)
+      if constexpr (LNF) {  // its column sums and row statistics (before the step's pieces, like the bias)
         GEMM_POISON(smem + NS * STAGE + 2048 + (d_ti & 1) * 1024);
         glds16(cs_p + n, smem + NS * STAGE + 2048 + (d_ti & 1) * 1024);
+        char* const sst = smem + NS * STAGE + 4096 + (d_ti & 1) * SROWP;
+#pragma unroll
+        for (int i = 0; i < SROWP / 1024; ++i) {
+          GEMM_POISON(sst + i * 1024);
+          glds16(rs_p + (size_t)d_m0 * 2 + i * 256 + lane * 4, sst + i * 1024);
+        }
       }
     }
   };
@@ -655,6 +669,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
         unit_coords(d_t, m0, n0);
         set_tile(m0, n0);
         d_n0 = n0;
+        d_m0 = m0;
       }
     }
   };
@@ -696,7 +711,6 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
   };
   const uint32_t lds0 = lds_addr(smem);
   f32x4 acc[NI][MI];
-  float st_s[MI], st_q[MI];  // EPI_LNF: the lane's running row sums / sums of squares (lnf_acc)
   V8 a0[MI], b0[NI], a1[MI], b1[NI];  // fragments of one phase
 
   auto rd_b = [&](auto kc, V8(&b)[NI], uint32_t buf, int kk) {
@@ -733,7 +747,6 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
 #pragma unroll
       for (int ni = 0; ni < NI; ++ni)
         acc[ni][g] = mfma_16x16x32(b[ni], a[g], Z ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[ni][g]);
-      if constexpr (LNF) lnf_acc<Z>(st_s[g], st_q[g], a[g]);  // (phase 0 = chunk 2 kt, phase 1 = 2 kt + 1)
     }
   };
   auto phase0 = [&](auto zero, uint32_t buf) {
@@ -786,24 +799,31 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
     const int nc = n0 + wn + fq * (4 * NI);
     const bool nfull = nc + 4 * NI <= p.N;
     f32x4 bias[NI], csv[NI];
+    // EPI_LNF: (mean, rstd) of the lane's rows, read up front -- or, on the 256-row tiles (whose
+    // epilogue would spill with them), per row block inside the loop below
+    constexpr bool RST_ALL = MI * NI < 32;
+    f32x2 rst[RST_ALL ? MI : 1];
+    const uint32_t rst_a = lds0 + NS * STAGE + 4096 + bpar * SROWP + (wm_cur + fr) * 8;
 #pragma unroll
     for (int ni = 0; ni < NI; ++ni) bias[ni] = f32x4{0.f, 0.f, 0.f, 0.f};
     if (bias_p != nullptr) {
       const uint32_t ba = lds0 + NS * STAGE + bpar * 1024 + (wn + fq * (4 * NI)) * 4;
       static_for<NI>([&](auto ni) { ds_read_b128<(int)ni * 16>(bias[ni], ba); });
-      if constexpr (LNF) static_for<NI>([&](auto ni) { ds_read_b128<2048 + (int)ni * 16>(csv[ni], ba); });
+      if constexpr (LNF) {
+        static_for<NI>([&](auto ni) { ds_read_b128<2048 + (int)ni * 16>(csv[ni], ba); });
+        if constexpr (RST_ALL) static_for<MI>([&](auto mi) { ds_read_b64<(int)mi * 128>(rst[mi], rst_a); });
+      }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
       for (int ni = 0; ni < NI; ++ni) asm volatile("" : "+v"(bias[ni]));
       if constexpr (LNF) {
 #pragma unroll
         for (int ni = 0; ni < NI; ++ni) asm volatile("" : "+v"(csv[ni]));
-      }
-    }
-    if constexpr (LNF) {  // the rows' mean / rstd (every lane: cross-lane combine)
-      const float inv_k = 1.0f / (float)p.K;
+        if constexpr (RST_ALL) {
 #pragma unroll
-      for (int mi = 0; mi < MI; ++mi) lnf_finish(st_s[mi], st_q[mi], inv_k, p.ln_eps);
+          for (int mi = 0; mi < MI; ++mi) asm volatile("" : "+v"(rst[mi]));
+        }
+      }
     }
     // EPI_RESID adds the residual row x[m]; EPI_PATCH writes patch p of image b to token
     // row b*(G2+cls) + cls + p and adds pos[cls + p].
@@ -856,12 +876,20 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
       }
       const int m = m0 + wm_cur + mi * 16 + fr;
       if (m >= p.M || (HM && mi >= mi_lim)) continue;
+      f32x2 rs = {0.f, 0.f};
+      if constexpr (LNF) {
+        if constexpr (RST_ALL) {
+          rs = rst[mi];
+        } else {
+          asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(rs) : "v"(rst_a + (uint32_t)mi * 128) : "memory");
+        }
+      }
       float v[NI][4];
 #pragma unroll
       for (int ni = 0; ni < NI; ++ni)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          v[ni][j] = LNF ? lnf_out(acc[ni][mi][j], st_s[mi], st_q[mi], csv[ni][j], bias[ni][j])
+          v[ni][j] = LNF ? lnf_out(acc[ni][mi][j], rs[0], rs[1], csv[ni][j], bias[ni][j])
                          : acc[ni][mi][j] + bias[ni][j];
 #ifdef CLIPGPU_GEMM_STAMPS
       if (p.diag & 1) {
@@ -1091,7 +1119,7 @@ template <typename T, int EPI, int ACT>
 hipError_t launch_pipe_224(const GemmParams& p, hipStream_t s) {
   const int grid = grid_224(p.M, p.N);
   if (p.K / BK >= 3) gemm_launch(gemm_pipe_kernel<T, 224, 192, 2, 4, EPI, ACT, 3, 1, 1, 0>, grid, 512, s, p);
-  else if constexpr (!epi_lnf(EPI)) gemm_launch(gemm_pipe_kernel<T, 224, 192, 2, 4, EPI, ACT, 2, 1, 1, 0>, grid, 512, s, p);
+  else gemm_launch(gemm_pipe_kernel<T, 224, 192, 2, 4, EPI, ACT, 2, 1, 1, 0>, grid, 512, s, p);
   return hipGetLastError();
 }
 
@@ -1138,15 +1166,11 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmParams p) {
   load(w0, a0, 0);
   if (U < nc) load(w1, a1, U);
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  float st_s = 0.f, st_q = 0.f;  // EPI_LNF: the lane's running row sum / sum of squares (lnf_acc)
   for (int c0 = 0; c0 < nc; c0 += U) {
     if (c0 + 2 * U < nc) load(w2, a2, c0 + 2 * U);
 #pragma unroll
     for (int u = 0; u < U; ++u) acc = mfma_16x16x32(w0[u], a0[u], acc);
-    if constexpr (LNF) {
-#pragma unroll
-      for (int u = 0; u < U; ++u) lnf_acc_dyn(c0 + u == 0, st_s, st_q, a0[u]);  // chunks in K order
-    }
+
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       w0[u] = w1[u];
@@ -1155,15 +1179,18 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmParams p) {
       a1[u] = a2[u];
     }
   }
-  if constexpr (LNF) lnf_finish(st_s, st_q, 1.0f / (float)p.K, p.ln_eps);  // (every lane)
   if (m >= p.M) return;
   const int n = tn * 16 + fq * 4;
   f32x4 bias = {0.f, 0.f, 0.f, 0.f}, csv = {0.f, 0.f, 0.f, 0.f};
+  f32x2 rst = {0.f, 0.f};
   if (p.bias != nullptr) bias = *(const f32x4*)(p.bias + n);
-  if constexpr (LNF) csv = *(const f32x4*)(p.cs + n);
+  if constexpr (LNF) {
+    csv = *(const f32x4*)(p.cs + n);
+    rst = *(const f32x2*)(p.rowstats + (long)m * 2);
+  }
   float v[4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) v[j] = LNF ? lnf_out(acc[j], st_s, st_q, csv[j], bias[j]) : acc[j] + bias[j];
+  for (int j = 0; j < 4; ++j) v[j] = LNF ? lnf_out(acc[j], rst[0], rst[1], csv[j], bias[j]) : acc[j] + bias[j];
   if constexpr (epi_st16(EPI)) {
     typename Vec4<OT>::type o;
 #pragma unroll
@@ -1201,25 +1228,23 @@ hipError_t launch_tile(const GemmParams& p, hipStream_t s) {
     if ((p.tile == TILE_AUTO || p.tile == TILE_SKINNY) && skinny_ok(p)) return launch_skinny<T, EPI, ACT>(p, s);
   }
   if (p.tile == TILE_SKINNY) return hipErrorInvalidValue;
-  // (EPI_LNF: the 4-wave 160x128 RS tile, which holds the row statistics without spilling)
-  const int tile = p.tile != TILE_AUTO ? p.tile
-                   : (epi_lnf(EPI) && p.M >= 2048 ? TILE_160x128_RS : pick_gemm_tile(p.M, p.N, p.K));
+  const int tile = p.tile == TILE_AUTO ? pick_gemm_tile(p.M, p.N, p.K) : p.tile;
   // software-pipelined kernel: K >= 128, 16-byte-aligned 16-bit output rows (diag bit 1: legacy, stamp builds)
   const bool pipe = p.K >= 2 * BK && !(p.diag & 2) && (!epi_st16(EPI) || p.ldo % 8 == 0);
   if (pipe) {
     if constexpr (epi_lnf(EPI)) {
-      // EPI_LNF: the tiles whose row statistics fit beside their accumulators and fragments; the
-      // 256x256 tiles (3, 14, 18), the 8-wave 160x128 (17) and the two-stage 224x192 would spill
-      // (tools/kernel_regs.py) and run the 4-wave 160x128 RS tile instead (the same bits: every
-      // kernel accumulates a row's statistics in the same order)
+      // EPI_LNF: the 224x192 tile's three stages leave no LDS for the row statistics; it runs the
+      // 4-wave 160x128 RS tile instead (the same bits: every tile computes the same sums)
       switch (tile) {
         case TILE_256x128: return launch_pipe<T, 256, 128, 4, 2, EPI, ACT>(p, s);
+        case TILE_256x256: return launch_pipe<T, 256, 256, 2, 4, EPI, ACT>(p, s);
         case TILE_192x256_W8: return launch_pipe<T, 192, 256, 2, 4, EPI, ACT, 1>(p, s);
-        case TILE_224x192_W8:
-          if (p.K / BK >= 3) return launch_pipe_224<T, EPI, ACT>(p, s);
-          return launch_pipe<T, 160, 128, 2, 2, EPI, ACT, 3, 1>(p, s);
-        case TILE_128x128: break;
-        default: return launch_pipe<T, 160, 128, 2, 2, EPI, ACT, 3, 1>(p, s);
+        case TILE_256x256_RS: return launch_pipe<T, 256, 256, 2, 4, EPI, ACT, 3, 1>(p, s);
+        case TILE_160x128_RS: return launch_pipe<T, 160, 128, 2, 2, EPI, ACT, 3, 1>(p, s);
+        case TILE_160x128_W8_RS: return launch_pipe<T, 160, 128, 2, 4, EPI, ACT, 2, 1>(p, s);
+        case TILE_256x256_HALF: return launch_pipe_half<T, EPI, ACT>(p, s);
+        case TILE_224x192_W8: return launch_pipe<T, 160, 128, 2, 2, EPI, ACT, 3, 1>(p, s);
+        default: break;
       }
     } else {
       switch (tile) {
@@ -1355,7 +1380,8 @@ hipError_t launch_dt(DType dt, int epi, int act, const GemmParams& p, hipStream_
 
 hipError_t launch_gemm(DType dt, int asrc, int epi, int act, const GemmParams& p, hipStream_t s) {
   if (p.K % BK != 0 || p.M <= 0 || p.N <= 0) return hipErrorInvalidValue;
-  if (epi == EPI_LNF && (p.bias == nullptr || p.cs == nullptr || p.N % 4 != 0)) return hipErrorInvalidValue;
+  if (epi == EPI_LNF && (p.bias == nullptr || p.cs == nullptr || p.rowstats == nullptr || p.N % 4 != 0))
+    return hipErrorInvalidValue;
   if (epi == EPI_LNF_BF) return hipErrorInvalidValue;  // internal code
   if (p.bias != nullptr && p.N % 4 != 0) return hipErrorInvalidValue;  // 16-byte bias DMA
   // 32-bit staging offsets: W must fit whole; A is chunked by rows

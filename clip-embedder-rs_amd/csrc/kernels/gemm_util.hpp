@@ -46,6 +46,11 @@ __device__ __forceinline__ void ds_read_b128(V& r, uint32_t addr) {
   asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF));
 }
 
+template <int OFF, typename V>
+__device__ __forceinline__ void ds_read_b64(V& r, uint32_t addr) {
+  asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF));
+}
+
 // s_waitcnt lgkmcnt(0) that names every fragment register as read-write, so no
 // consumer of them can be scheduled above it (cdna_hip_programming.md §5.7 form ii).
 template <typename V, int MI, int NI>

@@ -27,8 +27,7 @@ enum Epi {
   EPI_PATCH16 = 6,
   // LayerNorm folded into the GEMM (A = the f16 residual stream x itself, W' = W diag(gamma) in f16):
   //   out16[m][n] = act(rstd_m (acc - mean_m cs[n]) + bias[n]),  cs[n] = sum_k W'[n][k]
-  //   (GemmParams.cs), bias = b + W beta, mean_m / rstd_m from sum / sum of squares of row m of A
-  //   accumulated from the MFMA A fragments in K order (kernels/gemm.hip "LayerNorm fold").
+  //   (GemmParams.cs), bias = b + W beta, (mean_m, rstd_m) = GemmParams.rowstats[m] (launch_ln_stats).
   //   launch_gemm takes EPI_LNF with dt = the output type; the operands are f16.
   EPI_LNF = 7,
   EPI_LNF_BF = 8,  // (internal: EPI_LNF with a bf16 output)
@@ -54,7 +53,7 @@ struct GemmParams {
   int prio;                  // 8-wave gemm_pipe tiles: 1 = the younger half of the block at s_setprio 1
   int x16;                   // EPI_RESID / EPI_PATCH: the residual stream `out` is f16 (else f32); the adds are f32
   const float* cs;           // EPI_LNF: [N] column sums of W' (f32)
-  float ln_eps;              // EPI_LNF: the LayerNorm epsilon
+  const float* rowstats;     // EPI_LNF: [M + 256][2] (mean, rstd) of A's rows (rows >= M are read, unused)
 };
 
 // Tile configurations of the MFMA GEMM.  Ids are stable across rounds; the ones not listed were
@@ -113,22 +112,28 @@ hipError_t launch_attention(DType dt, const void* qkv, void* out, int B, int N, 
 
 // The residual stream x (launchers taking `x, x16`): f32 rows, or f16 rows when x16 != 0
 // (clipgpu_options.residual); every add into it and every statistic of it is computed in f32.
+// stats[r] = (mean, 1 / sqrt(var + eps)) of x[r] for r < rows, as launch_ln_rows computes them
+// (the EPI_LNF GEMMs' GemmParams.rowstats).
+hipError_t launch_ln_stats(const void* x, int x16, float eps, float* stats, int rows, int D, hipStream_t s);
 // out16[r] = LN(x[r]) for r < rows.
 hipError_t launch_ln_rows(DType dt, const void* x, int x16, const float* w, const float* b, float eps,
                           void* out16, int rows, int D, hipStream_t s, uint8_t* qs = nullptr);
 // qs != nullptr (these LN launchers): the output is MX-fp8, out16 = e4m3 bytes [rows][D],
 // qs = scales [rows][D/32] (gemm_mx.hip's A operand); D % 32 == 0.
 
-// Vision stem tail: CLS row = cls + pos[0]; x = ln_pre(x) (in place); h = ln_1(x) (h == nullptr: x only).
+// Vision stem tail: CLS row = cls + pos[0]; x = ln_pre(x) (in place); h = ln_1(x) -- or, h == nullptr,
+// stats = ln_1's row statistics (launch_ln_stats; the LayerNorm-folded QKV GEMM).
 hipError_t launch_vision_embed_ln(DType dt, void* x, int x16, const float* cls, const float* pos,
                                   const float* lnpre_w, const float* lnpre_b,
                                   const float* ln1_w, const float* ln1_b, float eps,
-                                  void* h, int B, int tokens, int D, hipStream_t s, uint8_t* qs = nullptr);
+                                  void* h, int B, int tokens, int D, hipStream_t s, uint8_t* qs = nullptr,
+                                  float* stats = nullptr);
 
-// Text stem: x = tok[ids] + pos; h = ln_1(x) (h == nullptr: x only).
+// Text stem: x = tok[ids] + pos; h = ln_1(x) -- or, h == nullptr, stats as launch_vision_embed_ln.
 hipError_t launch_text_embed_ln(DType dt, const int64_t* ids, const float* tok, const float* pos,
                                 const float* ln1_w, const float* ln1_b, float eps, void* x, int x16,
-                                void* h, int B, int T, int D, int vocab, hipStream_t s, uint8_t* qs = nullptr);
+                                void* h, int B, int T, int D, int vocab, hipStream_t s, uint8_t* qs = nullptr,
+                                float* stats = nullptr);
 
 // Pool one row per sequence (CLS: ids == nullptr; else first argmax of ids) and LN it.
 hipError_t launch_pool_ln(DType dt, const void* x, int x16, const int64_t* ids, int tokens,

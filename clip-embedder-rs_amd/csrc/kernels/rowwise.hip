@@ -54,10 +54,10 @@ __device__ __forceinline__ void load_row(const _Float16* src, int D4, int lane, 
   }
 }
 
-// torch LayerNorm, two-pass mean / biased variance in f32; g, b preloaded rows.
+// torch LayerNorm statistics: two-pass mean / biased variance in f32, rstd = 1 / sqrt(var + eps).
 template <int NV>
-__device__ __forceinline__ void layer_norm_regs(const Row<NV>& in, Row<NV>& out, const Row<NV>& g, const Row<NV>& b,
-                                                float eps, int D, int lane) {
+__device__ __forceinline__ void ln_stats_regs(const Row<NV>& in, float eps, int D, int lane, float& mean_out,
+                                              float& rstd_out) {
   const int D4 = D >> 2;
   float s = 0.f;
 #pragma unroll
@@ -72,7 +72,16 @@ __device__ __forceinline__ void layer_norm_regs(const Row<NV>& in, Row<NV>& out,
     }
   }
   const float var = wave_sum(q) / (float)D;
-  const float rstd = 1.0f / sqrtf(var + eps);
+  mean_out = mean;
+  rstd_out = 1.0f / sqrtf(var + eps);
+}
+
+// torch LayerNorm (ln_stats_regs, then the affine map); g, b preloaded rows.
+template <int NV>
+__device__ __forceinline__ void layer_norm_regs(const Row<NV>& in, Row<NV>& out, const Row<NV>& g, const Row<NV>& b,
+                                                float eps, int D, int lane) {
+  float mean, rstd;
+  ln_stats_regs(in, eps, D, lane, mean, rstd);
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     out.v[i].x = (in.v[i].x - mean) * rstd * g.v[i].x + b.v[i].x;
@@ -195,12 +204,37 @@ __global__ __launch_bounds__(256) void ln_rows_kernel(const XT* __restrict__ x, 
   }
 }
 
+// Row statistics only (the LayerNorm-folded GEMMs' GemmParams.rowstats): one wave per row as
+// ln_rows_kernel, stats[row] = (mean, rstd) by the same arithmetic.  (T unused: the launch macro's.)
+template <typename T, int NV, typename XT>
+__global__ __launch_bounds__(256) void ln_stats_kernel(const XT* __restrict__ x, float eps, float* __restrict__ stats,
+                                                       int rows, int D) {
+  const int stride = gridDim.x * 4, lane = threadIdx.x & 63;
+  int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int D4 = D >> 2;
+  Row<NV> r;
+  load_row(x + (long)row * D, D4, lane, r);
+  for (;;) {
+    const int next = row + stride;
+    Row<NV> nr;
+    if (next < rows) load_row(x + (long)next * D, D4, lane, nr);
+    float mean, rstd;
+    ln_stats_regs(r, eps, D, lane, mean, rstd);
+    if (lane == 0) *(float2*)(stats + 2L * row) = make_float2(mean, rstd);
+    if (next >= rows) break;
+    row = next;
+    r = nr;
+  }
+}
+
 template <typename T, int NV, typename XT>
 __global__ __launch_bounds__(256) void vision_embed_ln_kernel(XT* __restrict__ x, const float* cls,
                                                               const float* pos, const float* lnpre_w,
                                                               const float* lnpre_b, const float* ln1_w,
                                                               const float* ln1_b, float eps, T* __restrict__ h,
-                                                              uint8_t* __restrict__ qs, int rows, int tokens, int D) {
+                                                              uint8_t* __restrict__ qs, int rows, int tokens, int D,
+                                                              float* __restrict__ stats) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= rows) return;
   const int D4 = D >> 2;
@@ -223,7 +257,12 @@ __global__ __launch_bounds__(256) void vision_embed_ln_kernel(XT* __restrict__ x
   layer_norm_regs(r, y, g0, b0, eps, D, lane);
   round_rowx<XT>(y);  // ln_1 of the residual row as stored
   store_rowx(x + (long)row * D, y, D4, lane);
-  if (h == nullptr) return;  // (LayerNorm folded into the QKV GEMM: x only)
+  if (h == nullptr) {  // LayerNorm folded into the QKV GEMM: ln_1's statistics only
+    float mean, rstd;
+    ln_stats_regs(y, eps, D, lane, mean, rstd);
+    if (lane == 0) *(float2*)(stats + 2L * row) = make_float2(mean, rstd);
+    return;
+  }
   layer_norm_regs(y, z, g1, b1, eps, D, lane);
   store_ln_out(h, qs, row, D, z, lane);
 }
@@ -233,7 +272,7 @@ __global__ __launch_bounds__(256) void text_embed_ln_kernel(const int64_t* __res
                                                             const float* pos, const float* ln1_w,
                                                             const float* ln1_b, float eps, XT* __restrict__ x,
                                                             T* __restrict__ h, uint8_t* __restrict__ qs, int rows,
-                                                            int Tctx, int D, int vocab) {
+                                                            int Tctx, int D, int vocab, float* __restrict__ stats) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= rows) return;
   const int D4 = D >> 2;
@@ -249,7 +288,12 @@ __global__ __launch_bounds__(256) void text_embed_ln_kernel(const int64_t* __res
   add_row(e, p);
   round_rowx<XT>(e);  // ln_1 of the residual row as stored
   store_rowx(x + (long)row * D, e, D4, lane);
-  if (h == nullptr) return;  // (LayerNorm folded into the QKV GEMM: x only)
+  if (h == nullptr) {  // LayerNorm folded into the QKV GEMM: ln_1's statistics only
+    float mean, rstd;
+    ln_stats_regs(e, eps, D, lane, mean, rstd);
+    if (lane == 0) *(float2*)(stats + 2L * row) = make_float2(mean, rstd);
+    return;
+  }
   layer_norm_regs(e, y, g, bb, eps, D, lane);
   store_ln_out(h, qs, row, D, y, lane);
 }
@@ -382,28 +426,42 @@ hipError_t launch_ln_rows(DType dt, const void* x, int x16, const float* w, cons
   return hipGetLastError();
 }
 
+hipError_t launch_ln_stats(const void* x, int x16, float eps, float* stats, int rows, int D, hipStream_t s) {
+  if (D % 4 || D > 256 * MAXV || D <= 0 || rows <= 0 || stats == nullptr) return hipErrorInvalidValue;
+  dim3 grid = rows_grid(rows);
+  const int cap = device_cus() * 8;
+  if ((int)grid.x > cap) grid.x = cap;
+  dispatch_dx(DT_BF16, x16, [&](auto tp_, auto xp_) {
+    CLIPGPU_TX_TYPES;
+    CLIPGPU_ROW_LAUNCH_X(ln_stats_kernel, T, XT, grid, D, (const XT*)x, eps, stats, rows, D);
+  });
+  return hipGetLastError();
+}
+
 hipError_t launch_vision_embed_ln(DType dt, void* x, int x16, const float* cls, const float* pos, const float* lnpre_w,
                                   const float* lnpre_b, const float* ln1_w, const float* ln1_b, float eps,
-                                  void* h, int B, int tokens, int D, hipStream_t s, uint8_t* qs) {
+                                  void* h, int B, int tokens, int D, hipStream_t s, uint8_t* qs, float* stats) {
+  if (h == nullptr && stats == nullptr) return hipErrorInvalidValue;
   if (D % 4 || D > 256 * MAXV || D <= 0 || (qs != nullptr && D % 32)) return hipErrorInvalidValue;
   const int rows = B * tokens;
   dispatch_dx(dt, x16, [&](auto tp_, auto xp_) {
     CLIPGPU_TX_TYPES;
     CLIPGPU_ROW_LAUNCH_X(vision_embed_ln_kernel, T, XT, rows_grid(rows), D, (XT*)x, cls, pos, lnpre_w, lnpre_b, ln1_w,
-                         ln1_b, eps, (T*)h, qs, rows, tokens, D);
+                         ln1_b, eps, (T*)h, qs, rows, tokens, D, stats);
   });
   return hipGetLastError();
 }
 
 hipError_t launch_text_embed_ln(DType dt, const int64_t* ids, const float* tok, const float* pos,
                                 const float* ln1_w, const float* ln1_b, float eps, void* x, int x16, void* h,
-                                int B, int Tctx, int D, int vocab, hipStream_t s, uint8_t* qs) {
+                                int B, int Tctx, int D, int vocab, hipStream_t s, uint8_t* qs, float* stats) {
+  if (h == nullptr && stats == nullptr) return hipErrorInvalidValue;
   if (D % 4 || D > 256 * MAXV || D <= 0 || (qs != nullptr && D % 32)) return hipErrorInvalidValue;
   const int rows = B * Tctx;
   dispatch_dx(dt, x16, [&](auto tp_, auto xp_) {
     CLIPGPU_TX_TYPES;
     CLIPGPU_ROW_LAUNCH_X(text_embed_ln_kernel, T, XT, rows_grid(rows), D, ids, tok, pos, ln1_w, ln1_b, eps, (XT*)x,
-                         (T*)h, qs, rows, Tctx, D, vocab);
+                         (T*)h, qs, rows, Tctx, D, vocab, stats);
   });
   return hipGetLastError();
 }

@@ -127,14 +127,16 @@ int clipgpu_test_gemm_lnf(int dtype, int act, int64_t M, int64_t N, int64_t K, c
     const DType dt = dt_of(dtype);
     if (M <= 0 || N <= 0 || K <= 0 || K % 64 || N % 4) throw ClipErr(CLIPGPU_ERR_INVALID, "bad GEMM shape");
     if (tile != 0 && tile != TILE_SKINNY && !gemm_tile_built(tile)) throw ClipErr(CLIPGPU_ERR_INVALID, "bad tile");
-    DevBuf dA(M * K * 2), dW(N * K * 2), dB(N * 4), dC(N * 4), dO(M * N * 2);
+    DevBuf dA(M * K * 2), dW(N * K * 2), dB(N * 4), dC(N * 4), dO(M * N * 2), dS((M + 256) * 8);
     up16(DT_F16, dA.p, x, M * K);
     up16(DT_F16, dW.p, wf, N * K);
     up(dB.p, bias, N * 4);
     up(dC.p, cs, N * 4);
+    TCHECK(launch_ln_stats(dA.p, 1, eps, dS.as<float>(), (int)M, (int)K, nullptr));  // the rows' (mean, rstd)
     GemmParams g{};
     g.tile = tile;
-    g.A = dA.p; g.lda = K; g.W = dW.p; g.ldw = K; g.bias = dB.as<float>(); g.cs = dC.as<float>(); g.ln_eps = eps;
+    g.A = dA.p; g.lda = K; g.W = dW.p; g.ldw = K; g.bias = dB.as<float>(); g.cs = dC.as<float>();
+    g.rowstats = dS.as<float>();
     g.out = dO.p; g.ldo = N; g.M = (int)M; g.N = (int)N; g.K = (int)K;
     TCHECK(launch_gemm(dt, A_ROWS, EPI_LNF, act, g, nullptr));
     TCHECK(hipDeviceSynchronize());

@@ -22,8 +22,9 @@ extern "C" {
 int clipgpu_test_gemm(int dtype, int mode, int act, int64_t M, int64_t N, int64_t K, const float* A,
                       const float* W, const float* bias, const float* resid, float* out);
 /* The LayerNorm-folded GEMM (EPI_LNF): out[m][n] = act(rstd_m (x W'^T - mean_m cs)[m][n] + bias[n]) with
- * x [M][K] and wf [N][K] rounded to f16 on upload, mean / rstd of each row of x (eps), the output in
- * dtype (bf16 / f16), widened to f32.  tile: a built GemmTile, 0 = the launcher's choice, 100 = skinny. */
+ * x [M][K] and wf [N][K] rounded to f16 on upload, mean / rstd of each row of x (eps; launch_ln_stats,
+ * K <= 1280), the output in dtype (bf16 / f16), widened to f32.  tile: a built GemmTile, 0 = the
+ * launcher's choice, 100 = skinny. */
 int clipgpu_test_gemm_lnf(int dtype, int act, int64_t M, int64_t N, int64_t K, const float* x, const float* wf,
                           const float* cs, const float* bias, float eps, int tile, float* out);
 
