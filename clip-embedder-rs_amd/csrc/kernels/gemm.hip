@@ -268,6 +268,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
   // XE: the residual stream's element type (EPI_RESID16 / EPI_PATCH16: f16, else f32)
   auto epilogue = [&](int m0, int n0, int bpar) {
     typedef typename std::conditional<epi_x16(EPI), _Float16, float>::type XE;
+    xdl_srcc_guard();
     const int G2 = p.G * p.G;
     // EPI_RESID: the residual rows of column block ni+1 are loaded before block ni
     // is stored, so no load waits behind this epilogue's own stores.
@@ -796,6 +797,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
   // XE: the residual stream's element type (EPI_RESID16 / EPI_PATCH16: f16, else f32)
   auto epilogue = [&](int m0, int n0, int bpar) {
     typedef typename std::conditional<epi_x16(EPI), _Float16, float>::type XE;
+    xdl_srcc_guard();
     const int nc = n0 + wn + fq * (4 * NI);
     const bool nfull = nc + 4 * NI <= p.N;
     f32x4 bias[NI], csv[NI];
