@@ -187,6 +187,9 @@ __device__ __forceinline__ float fast_erf(float x) {
 
 template <int ACT>
 __device__ __forceinline__ float apply_act(float x) {
+#ifdef CLIPGPU_TEST_NO_ACT  // timing-experiment variant only (make variant): the activation skipped
+  return x;
+#endif
   if constexpr (ACT == ACT_QUICK_GELU) {
     return sigmoid_mul_exp2(x, x * -2.4554669596f);  // -1.702 * log2(e) (|rel err| 2^-24 of the product)
   } else if constexpr (ACT == ACT_GELU) {
