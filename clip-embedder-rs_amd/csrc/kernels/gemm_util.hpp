@@ -46,17 +46,6 @@ __device__ __forceinline__ void ds_read_b128(V& r, uint32_t addr) {
   asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF));
 }
 
-// Before an epilogue's inline-asm LDS reads: the tile's last MFMAs may still be in flight and may not yet
-// have read their SrcC accumulators, whose registers the compiler can hand to those reads' results once
-// the MFMA is issued -- and it does not pad inline asm against that write-after-read (a bt-kernel EPI_LNF
-// epilogue lost accumulator values this way).  32 wait states cover the XDL SrcC read window; the
-// scheduling barrier keeps the MFMAs above the padding.
-__device__ __forceinline__ void xdl_srcc_guard() {
-  __builtin_amdgcn_sched_barrier(0);
-  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
-  __builtin_amdgcn_sched_barrier(0);
-}
-
 template <int OFF, typename V>
 __device__ __forceinline__ void ds_read_b64(V& r, uint32_t addr) {
   asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF));
