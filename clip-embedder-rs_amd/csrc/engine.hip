@@ -717,6 +717,7 @@ MxGemmParams site_gemm_mx(const clipgpu_engine& e, const Replica& r, const Layer
     g.A = (const uint8_t*)r.big; g.lda = MLP; g.As = r.bigs; g.ldas = MLP / 32;
     g.W = L.m2.q; g.ldw = MLP; g.Ws = L.m2.s; g.ldws = MLP / 32;
     g.bias = L.b2; g.out = r.x; g.ldo = D; g.N = D; g.K = MLP;
+    g.x16 = e.x16 ? 1 : 0;
     return g;
   }
   g.A = (const uint8_t*)r.h; g.lda = D; g.As = r.hs; g.ldas = D / 32;
@@ -1990,15 +1991,16 @@ int clipgpu_create_ex(const char* model_dir, int tower, const int* device_ids, i
     e->trim = opts.trim_text != -1;
     {  // the residual stream's storage (clipgpu_options.residual; kResidualDefault when 0)
       const int res = opts.residual ? opts.residual : kResidualDefault;
-      const bool f16_ok = !e->mx && e->spec.family != FAMILY_SIGLIP;
+      const bool f16_ok = e->spec.family != FAMILY_SIGLIP;
       if (opts.residual == CLIPGPU_RESIDUAL_F16 && !f16_ok)
-        throw ClipErr(CLIPGPU_ERR_INVALID, "clipgpu_options.residual = f16: bf16 / f16 engines of the CLIP family only");
+        throw ClipErr(CLIPGPU_ERR_INVALID, "clipgpu_options.residual = f16: CLIP-family engines only");
       e->x16 = res == CLIPGPU_RESIDUAL_F16 && f16_ok;
       // the LayerNorm fold (clipgpu_options.ln_fold): the f16 stream, a QuickGELU / GELU MLP
-      const bool fold_ok = e->x16 && (e->spec.act == ACT_QUICK_GELU || e->spec.act == ACT_GELU);
+      const bool fold_ok = e->x16 && !e->mx && (e->spec.act == ACT_QUICK_GELU || e->spec.act == ACT_GELU);
       if (opts.ln_fold == 1 && !fold_ok)
         throw ClipErr(CLIPGPU_ERR_INVALID,
-                      "clipgpu_options.ln_fold = 1: needs the f16 residual stream and a QuickGELU / GELU MLP");
+                      "clipgpu_options.ln_fold = 1: needs a bf16 / f16 engine, the f16 residual stream and a "
+                      "QuickGELU / GELU MLP");
       e->lnf = fold_ok && opts.ln_fold != -1;
     }
     for (int i = 0; i < 4; ++i) e->pin_tiles[i] = opts.gemm_tiles[i];

@@ -30,6 +30,7 @@
 // each 32-row group, so register r of lane half h is output column 16 h + r: 16
 // consecutive columns per lane (64-byte f32 / 32-byte 16-bit / 16-byte fp8 stores).
 #include <algorithm>
+#include <type_traits>
 #include <utility>
 
 #include "common.hpp"
@@ -347,15 +348,17 @@ void gemm_mx_kernel(MxGemmParams p) {
           *(uint4*)((uint8_t*)p.out + (long)m * p.ldo + nc) = w;
           if (h == 0) p.outs[(long)m * p.ldos + (nc >> 5)] = (uint8_t)(e + 127);
         } else {
-          float* o = (float*)p.out + (long)m * p.ldo + nc;
+          // (EPI_RESID16: the residual stream in f16)
+          typedef typename std::conditional<EPI == EPI_RESID16, _Float16, float>::type XE;
+          XE* o = (XE*)p.out + (long)m * p.ldo + nc;
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             float4 w = make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
-            if constexpr (EPI == EPI_RESID) {
-              const float4 x = *(const float4*)(o + 4 * q);
+            if constexpr (epi_resid(EPI)) {
+              const float4 x = ldx4(o + 4 * q);
               w.x += x.x; w.y += x.y; w.z += x.z; w.w += x.w;
             }
-            *(float4*)(o + 4 * q) = w;
+            stx4(o + 4 * q, w);
           }
         }
       }
@@ -364,7 +367,7 @@ void gemm_mx_kernel(MxGemmParams p) {
   // vm ops a full tile's epilogue leaves in flight behind the DMA of the step after it
   constexpr int EPI_VM = EPI == EPI_STORE16 ? 2 * MI * NI
                          : EPI == EPI_STOREQ ? 2 * MI * NI
-                         : EPI == EPI_RESID  ? 8 * MI * NI
+                         : epi_resid(EPI)    ? 8 * MI * NI
                                              : 4 * MI * NI;
 
   // ---- prologue: steps 0 and 1 in flight, step 0 landed, its kk0 fragments read ----
@@ -443,7 +446,9 @@ hipError_t launch_mx_typed(int epi, int act, const MxGemmParams& p, hipStream_t 
   switch (epi) {
     case EPI_STORE16: return launch_mx_act<T, EPI_STORE16>(act, p, s);
     case EPI_STOREQ: return launch_mx_act<T, EPI_STOREQ>(act, p, s);
-    case EPI_RESID: return act == ACT_NONE ? launch_mx_tile<T, EPI_RESID, ACT_NONE>(p, s) : hipErrorInvalidValue;
+    case EPI_RESID:  // the residual stream: f32, or f16 (MxGemmParams.x16)
+      if (act != ACT_NONE) return hipErrorInvalidValue;
+      return p.x16 ? launch_mx_tile<T, EPI_RESID16, ACT_NONE>(p, s) : launch_mx_tile<T, EPI_RESID, ACT_NONE>(p, s);
     case EPI_STORE32: return act == ACT_NONE ? launch_mx_tile<T, EPI_STORE32, ACT_NONE>(p, s) : hipErrorInvalidValue;
   }
   return hipErrorInvalidValue;
@@ -499,7 +504,7 @@ hipError_t launch_gemm_mx(DType dt, int epi, int act, const MxGemmParams& p, hip
     // tiles, bit-invisible (per-row scales, per-row MFMA chains)
     long chunk = ((1L << 31) - 1) / p.lda;
     chunk -= chunk % 256;
-    const long osz = epi == EPI_STORE16 ? 2 : (epi == EPI_STOREQ ? 1 : 4);
+    const long osz = epi == EPI_STORE16 || (epi == EPI_RESID && p.x16) ? 2 : (epi == EPI_STOREQ ? 1 : 4);
     for (long m0 = 0; m0 < p.M; m0 += chunk) {
       MxGemmParams q = p;
       q.M = (int)std::min<long>(chunk, p.M - m0);

@@ -193,6 +193,7 @@ struct MxGemmParams {
   uint8_t* outs; long ldos;  // EPI_STOREQ: the output's scales [M][N/32]
   int M, N, K;
   int tile;                // MxTile
+  int x16;                 // EPI_RESID: the residual stream `out` is f16 (else f32); the adds are f32
 };
 enum MxTile {
   MX_TILE_AUTO = 0,

@@ -11,7 +11,7 @@ import numpy as np
 import pytest
 
 from oracle import weights
-from oracle.model_spec import TINY_CFG, VIT_B_32_CFG, text_spec_from_cfg, vision_spec_from_cfg
+from oracle.model_spec import TINY_CFG, TINY_SIGLIP_CFG, VIT_B_32_CFG, text_spec_from_cfg, vision_spec_from_cfg
 from tests.helpers import make_model_dir
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -262,11 +262,11 @@ def test_options_init_and_validation():
     for bad in ([32], [40], [0, 33], 1 << 32):
         with pytest.raises(ValueError, match="mx_layers"):
             Engine(d, 0, [0], "fp8", 8, mx_layers=bad)
-    # residual stream storage (ABI v4): f32 / f16, f16 only for bf16 / f16 CLIP-family engines
+    # residual stream storage (ABI v4): f32 / f16, f16 only for CLIP-family engines (not SigLIP)
     with pytest.raises(ValueError, match="residual"):
         Engine(d, 0, [0], "bf16", 8, residual="bf16")
     with pytest.raises(ClipError, match="residual = f16"):
-        Engine(d, 0, [0], "fp8", 8, residual="f16")
+        Engine(make_model_dir(TINY_SIGLIP_CFG, 3), 0, [0], "bf16", 8, residual="f16")
     o3 = Options()
     _lib.check(_lib.lib().clipgpu_options_init(ctypes.byref(o3)))
     assert o3.residual == 0
