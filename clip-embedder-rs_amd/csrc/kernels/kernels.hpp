@@ -201,7 +201,8 @@ enum MxTile {
                         // 128x128-per-wave form spills past 512 with the loop-carried fragment copies)
   MX_TILE_256x128 = 2,  // 8 waves (4x2, 64x64 each), 99 KiB LDS, 1 block / CU
   MX_TILE_128x128 = 3,  // 4 waves (64x64 each), 68 KiB LDS, 2 blocks / CU
-  MX_TILE_LAST = MX_TILE_128x128,
+  MX_TILE_128x256 = 4,  // 4 waves (2x2 of 64x128), one wave per SIMD (512 registers), 1 block / CU
+  MX_TILE_LAST = MX_TILE_128x256,
 };
 // epi: EPI_STORE16 (act), EPI_RESID, EPI_STORE32, EPI_STOREQ (act); N % 32 == 0.
 hipError_t launch_gemm_mx(DType dt, int epi, int act, const MxGemmParams& p, hipStream_t s);

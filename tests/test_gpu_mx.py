@@ -99,7 +99,7 @@ def run_gemm_mx(mode, act, aq, as_, wq, ws, bias=None, resid=None):
     return out, outq, outs
 
 
-@pytest.fixture(params=[0, 2, 3], ids=["auto", "mx256x128", "mx128x128"])
+@pytest.fixture(params=[0, 2, 3, 4], ids=["auto", "mx256x128", "mx128x128", "mx128x256"])
 def mx_tile(request, monkeypatch):
     monkeypatch.setenv("CLIPGPU_TEST_TILE", str(request.param))
     return request.param
@@ -156,6 +156,24 @@ def test_gemm_mx_quantized_out(act, mx_tile):
     deq = mx_ref.dequantize(q, s)
     half = np.ldexp(1.0, s.astype(np.int64) - 127 + 4).repeat(32, -1)
     assert np.all(np.abs(deq - ref) <= half * 1.01)
+
+
+@pytest.mark.parametrize("mode,act", [(2, 0), (1, 0), (0, 1), (3, 1)])
+def test_mx_tiles_are_bit_exact(mode, act, monkeypatch):
+    """Every MX tile (incl. the one-wave-per-SIMD 128x256 with 64x128 per wave) computes each output
+    with the same MFMA chain in the same K order: identical bits across tiles, tails included."""
+    rng = np.random.default_rng(31 + mode)
+    M, N, K = 3001, 1312, 768
+    aq, as_, wq, ws = _mx_operands(rng, M, N, K)
+    bias = rng.standard_normal(N).astype(np.float32)
+    resid = rng.standard_normal((M, N)).astype(np.float32) if mode == 1 else None
+    outs = []
+    for t in ("3", "2", "4"):
+        monkeypatch.setenv("CLIPGPU_TEST_TILE", t)
+        outs.append(run_gemm_mx(mode, act, aq, as_, wq, ws, bias, resid))
+    for o in outs[1:]:
+        for a, b in zip(o, outs[0]):
+            assert np.array_equal(a, b)
 
 
 def test_gemm_mx_rejects_bad_shapes():
