@@ -199,12 +199,14 @@ def cpu_baseline(px_host, ids_host, gpu_vision, gpu_text, fp8_vision=None, targe
     return res
 
 
-def load_traffic(site, rows_per_launch, tiles):
+def load_traffic(site, rows_per_launch, tiles, form):
     """HBM bytes per launch of the roofline kernel: NOT measured in this run -- read from the
     committed PMC summary (separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench,
     gfx950 FETCH_SIZE x2 correction, tools/pmc_traffic.py); its `source` names the run it came from.
     Only used when it was measured for this site at this run's rows per launch AND with this run's
-    GEMM tiles (the record's `tiles`); otherwise null, with the reason in traffic_source."""
+    GEMM tiles (the record's `tiles`) and epilogue form (`form`: "f16 residual" / "f32 residual" for
+    out_proj / c_proj, "LayerNorm folded" or "" for c_fc, matched against the record's `kernel` text);
+    otherwise null, with the reason in traffic_source."""
     p = os.path.join(ROOT, "profiles", "pmc_c_fc.json")
     if os.path.exists(p):
         with open(p) as f:
@@ -219,6 +221,10 @@ def load_traffic(site, rows_per_launch, tiles):
         if rec.get("tiles") != tiles:
             return None, (f"profiles/pmc_c_fc.json's record at {int(rows_per_launch)} rows was taken with tiles "
                           f"{rec.get('tiles')}, this run uses {tiles}: not applicable")
+        k = rec.get("kernel", "")
+        if (form and form not in k) or (not form and "LayerNorm folded" in k):
+            return None, (f"profiles/pmc_c_fc.json's {site} record ({k}) is not this run's epilogue form "
+                          f"({form or 'no LayerNorm fold'}): not applicable")
         return rec.get("hbm_bytes_per_launch"), "profiles/pmc_c_fc.json: " + rec.get("source", "rocprofv3 PMC passes")
     return None, None
 
@@ -646,8 +652,9 @@ def main():
         torch.cuda.synchronize()
         cpu = cpu_baseline(px.cpu().numpy(), ids.cpu().numpy(), out.cpu().numpy(), tout_host, fout_host)
 
-    traffic, traffic_src = (load_traffic(dom, sites[dom]["rows_per_launch"], ",".join(str(t) for t in tiles)) if not fp8
-                            else (None, None))
+    form = ("LayerNorm folded" if ln_fold else "") if dom == "c_fc" else f"{x_store} residual"
+    traffic, traffic_src = (load_traffic(dom, sites[dom]["rows_per_launch"], ",".join(str(t) for t in tiles), form)
+                            if not fp8 else (None, None))
     if rank == 0:
         line = {
             "metric": "images/sec embedding, ViT-B/32-224 vision tower, batch 256 per GPU",

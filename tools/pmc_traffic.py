@@ -32,11 +32,16 @@ import statistics
 import sys
 
 KERNELS = {
-    "c_fc": re.compile(r"gemm_(bt|pipe)_kernelIDF16bLi\d+ELi\d+ELi\d+ELi\d+ELi0ELi1E(?:Li\d+E)*EEv"),
-    "resid": re.compile(r"gemm_(bt|pipe)_kernelIDF16bLi\d+ELi\d+ELi\d+ELi\d+ELi1ELi0E(?:Li\d+E)*EEv"),
+    # c_fc: EPI_STORE16 (bf16 operands) or, LayerNorm-folded, EPI_LNF_BF = 8 (f16 operands); QuickGELU
+    "c_fc": re.compile(r"gemm_(bt|pipe)_kernelIDF16(?:b|_)Li\d+ELi\d+ELi\d+ELi\d+ELi(?:0|8)ELi1E(?:Li\d+E)*EEv"),
+    # out_proj / c_proj: EPI_RESID = 1 (f32 stream) or EPI_RESID16 = 5 (f16 stream)
+    "resid": re.compile(r"gemm_(bt|pipe)_kernelIDF16bLi\d+ELi\d+ELi\d+ELi\d+ELi(?:1|5)ELi0E(?:Li\d+E)*EEv"),
 }
 D, MLP = 768, 3072  # ViT-B/32 vision
 SHAPES = {"c_fc": (MLP, D), "c_proj": (D, MLP), "out_proj": (D, D)}  # (N, K)
+
+
+NAMES = set()  # the matched kernel names (the epilogue forms the compulsory bytes follow)
 
 
 def dispatches(d, counter, pattern):
@@ -46,6 +51,7 @@ def dispatches(d, counter, pattern):
             for row in csv.DictReader(fh):
                 if row["Counter_Name"] == counter and pattern.search(row["Kernel_Name"]):
                     out.append((int(row["Dispatch_Id"]), float(row["Counter_Value"])))
+                    NAMES.add(pattern.search(row["Kernel_Name"]).group(0))
     out.sort()
     return [v for _, v in out]
 
@@ -76,9 +82,15 @@ def main():
     read_b, write_b = 2.0 * f_kb * 1024.0, w_kb * 1024.0
     N, K = SHAPES[site]
     if site == "c_fc":
-        compulsory, what = 2 * (M * K + N * K + M * N) + 4 * N, "+QuickGELU"
+        lnf = any("ELi8ELi1E" in n for n in NAMES)
+        if lnf:  # + the column sums (f32) and the rows' (mean, rstd)
+            compulsory, what = 2 * (M * K + N * K + M * N) + 8 * N + 8 * M, "LayerNorm folded, +QuickGELU"
+        else:
+            compulsory, what = 2 * (M * K + N * K + M * N) + 4 * N, "+QuickGELU"
     else:
-        compulsory, what = 2 * (M * K + N * K) + 4 * N + 2 * 4 * M * N, "+bias, f32 residual read and write"
+        xb = 2 if any("ELi5ELi0E" in n for n in NAMES) else 4
+        compulsory = 2 * (M * K + N * K) + 4 * N + 2 * xb * M * N
+        what = f"+bias, {'f16' if xb == 2 else 'f32'} residual read and write"
     res = {
         "kernel": f"{site} GEMM ({M}x{N}x{K}, bf16, {what})", "site": site, "rows_per_launch": M,
         "fetch_size_kb_median": f_kb, "write_size_kb_median": w_kb,
