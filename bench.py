@@ -468,7 +468,7 @@ def main():
     _lib.check(_lib.lib().clipgpu_test_engine_residual(ve._h, ctypes.byref(x_store), ctypes.byref(ln_fold)))
     x_store = "f16" if x_store.value == 2 else "f32"  # CLIPGPU_RESIDUAL_F16 / _F32
     ln_fold = bool(ln_fold.value)
-    mx_names = {0: "heuristic", 2: "mx256x128", 3: "mx128x128", 4: "mx128x256"}  # fp8 engines' MX sites
+    mx_names = {0: "heuristic", 2: "mx256x128", 3: "mx128x128"}  # fp8 engines: QKV / c_fc / c_proj sites
     fp8 = args.dtype == "fp8"
     gemm_tiles = {site: (mx_names if fp8 and site != "out_proj" else TILE_NAMES).get(t, f"tile{t}")
                   for site, t in zip(["qkv", "out_proj", "c_fc", "c_proj"], tiles)}

@@ -981,7 +981,7 @@ void autotune_tiles(clipgpu_engine& e, Replica& r) {
       MxGemmParams g = site_gemm_mx(e, r, L, site, rows);
       const int epi = site_epi_mx(e, 0, site), act = site == GS_FC ? e.spec.act : ACT_NONE;
       float best = 1e30f;
-      for (int t : {MX_TILE_256x128, MX_TILE_128x128, MX_TILE_128x256}) {
+      for (int t : {MX_TILE_256x128, MX_TILE_128x128}) {
         g.tile = t;
         check(launch_gemm_mx(e.dt, epi, act, g, r.stream), "autotune mx gemm");
         HIP_CHECK(hipEventRecord(a, r.stream));

@@ -62,9 +62,8 @@ __device__ __forceinline__ f32x16 mfma_mx(const v4i (&w)[2], const v4i (&a)[2], 
   return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(wv, av, c, 0, 0, OPS, sw, OPS, sa);
 }
 
-// OCC: blocks per CU the kernel is built for (1: one wave per SIMD, 512 registers -- the 64x128 wave tile)
-template <typename T, int BM, int BN, int WGM, int WGN, int EPI, int ACT, int OCC = 2>
-__global__ __launch_bounds__(WGM* WGN * 64, OCC)
+template <typename T, int BM, int BN, int WGM, int WGN, int EPI, int ACT>
+__global__ __launch_bounds__(WGM* WGN * 64, 2)
 void gemm_mx_kernel(MxGemmParams p) {
   typedef typename Vec8<T>::type V8;
   constexpr int NW = WGM * WGN;
@@ -404,14 +403,14 @@ void gemm_mx_kernel(MxGemmParams p) {
   }
 }
 
-template <typename T, int BM, int BN, int WGM, int WGN, int EPI, int ACT, int OCC = 2>
+template <typename T, int BM, int BN, int WGM, int WGN, int EPI, int ACT>
 hipError_t launch_mx_cfg(const MxGemmParams& p, hipStream_t s) {
   const int ntiles = ((p.N + BN - 1) / BN) * ((p.M + BM - 1) / BM);
   const int lds = 2 * ((BM + BN) * KB + (BM + BN) * 4) + 2048;
-  const int per_cu = (WGM * WGN == 8 || OCC == 1) ? 1 : std::min(2, (160 * 1024) / lds);
+  const int per_cu = WGM * WGN == 8 ? 1 : std::min(2, (160 * 1024) / lds);
   const int resident = device_cus() * per_cu;
   const int grid = ntiles <= resident ? ntiles : resident;
-  gemm_launch(gemm_mx_kernel<T, BM, BN, WGM, WGN, EPI, ACT, OCC>, grid, WGM * WGN * 64, s, p);
+  gemm_launch(gemm_mx_kernel<T, BM, BN, WGM, WGN, EPI, ACT>, grid, WGM * WGN * 64, s, p);
   return hipGetLastError();
 }
 
@@ -427,7 +426,6 @@ template <typename T, int EPI, int ACT>
 hipError_t launch_mx_tile(const MxGemmParams& p, hipStream_t s) {
   switch (p.tile == MX_TILE_AUTO ? pick_mx_tile(p.M, p.N) : p.tile) {
     case MX_TILE_256x128: return launch_mx_cfg<T, 256, 128, 4, 2, EPI, ACT>(p, s);
-    case MX_TILE_128x256: return launch_mx_cfg<T, 128, 256, 2, 2, EPI, ACT, 1>(p, s);
     default: return launch_mx_cfg<T, 128, 128, 2, 2, EPI, ACT>(p, s);
   }
 }

@@ -201,8 +201,9 @@ enum MxTile {
                         // 128x128-per-wave form spills past 512 with the loop-carried fragment copies)
   MX_TILE_256x128 = 2,  // 8 waves (4x2, 64x64 each), 99 KiB LDS, 1 block / CU
   MX_TILE_128x128 = 3,  // 4 waves (64x64 each), 68 KiB LDS, 2 blocks / CU
-  MX_TILE_128x256 = 4,  // 4 waves (2x2 of 64x128), one wave per SIMD (512 registers), 1 block / CU
-  MX_TILE_LAST = MX_TILE_128x256,
+  // (round 5: a 4-wave 128x256 with 64x128 per wave at one wave per SIMD -- 387 VGPRs, no spills --
+  // measured 0.75-1.0x of this tile at every trunk shape, profiles/r05_mx_sweep.jsonl: not kept)
+  MX_TILE_LAST = MX_TILE_128x128,
 };
 // epi: EPI_STORE16 (act), EPI_RESID, EPI_STORE32, EPI_STOREQ (act); N % 32 == 0.
 hipError_t launch_gemm_mx(DType dt, int epi, int act, const MxGemmParams& p, hipStream_t s);

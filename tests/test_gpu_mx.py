@@ -99,7 +99,7 @@ def run_gemm_mx(mode, act, aq, as_, wq, ws, bias=None, resid=None):
     return out, outq, outs
 
 
-@pytest.fixture(params=[0, 2, 3, 4], ids=["auto", "mx256x128", "mx128x128", "mx128x256"])
+@pytest.fixture(params=[0, 2, 3], ids=["auto", "mx256x128", "mx128x128"])
 def mx_tile(request, monkeypatch):
     monkeypatch.setenv("CLIPGPU_TEST_TILE", str(request.param))
     return request.param
@@ -160,15 +160,15 @@ def test_gemm_mx_quantized_out(act, mx_tile):
 
 @pytest.mark.parametrize("mode,act", [(2, 0), (1, 0), (0, 1), (3, 1)])
 def test_mx_tiles_are_bit_exact(mode, act, monkeypatch):
-    """Every MX tile (incl. the one-wave-per-SIMD 128x256 with 64x128 per wave) computes each output
-    with the same MFMA chain in the same K order: identical bits across tiles, tails included."""
+    """Both MX tiles compute each output with the same MFMA chain in the same K order: identical bits
+    across tiles, M / N tails included."""
     rng = np.random.default_rng(31 + mode)
     M, N, K = 3001, 1312, 768
     aq, as_, wq, ws = _mx_operands(rng, M, N, K)
     bias = rng.standard_normal(N).astype(np.float32)
     resid = rng.standard_normal((M, N)).astype(np.float32) if mode == 1 else None
     outs = []
-    for t in ("3", "2", "4"):
+    for t in ("3", "2"):
         monkeypatch.setenv("CLIPGPU_TEST_TILE", t)
         outs.append(run_gemm_mx(mode, act, aq, as_, wq, ws, bias, resid))
     for o in outs[1:]:
