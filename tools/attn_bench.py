@@ -14,6 +14,10 @@ from open_clip_inference import _lib  # noqa: E402
 CASES = [("h14_vision", 32, 730, 16, 80, 0), ("so400m_vision", 64, 576, 16, 72, 0), ("h14_text", 32, 77, 16, 64, 1),
          ("b32_vision", 128, 50, 12, 64, 0), ("b32_text", 512, 77, 8, 64, 1),
          ("b32_vision_1lane", 256, 50, 12, 64, 0), ("b32_text_1lane", 1024, 77, 8, 64, 1)]
+if os.environ.get("ATTN_LAYOUT_PROBE"):  # the same workgroups and bytes with one head per row: each
+    # workgroup's rows then sit 3 x 128 B apart instead of 3 x 768 x 2 B (the head-major-layout question)
+    CASES = [("b32_vision", 128, 50, 12, 64, 0), ("b32_vision_h1", 1536, 50, 1, 64, 0),
+             ("b32_text", 512, 77, 8, 64, 1), ("b32_text_h1", 4096, 77, 1, 64, 1)] * 2
 
 L = _lib.lib()
 us = ctypes.c_double()
