@@ -140,3 +140,30 @@ def test_torch_cpu_port_matches_oracle(cfg_name):
           if v.family == "clip" else np.ones(1))  # SigLIP vision: the MAP head is not ported
     ct = clip_ref.cosine_rows(torch_cpu.TextCPU(Pt, t)(ids), clip_ref.encode_text(Pt, t, ids))
     assert cv.min() > 0.999999 and ct.min() > 0.999999, (cv, ct)
+
+
+def test_layernorm_fold_identity():
+    """The algebra behind the engine's LayerNorm fold (EPI_LNF): for a Linear
+    W, b behind LayerNorm (gamma, beta), LN(x) W^T + b = rstd (x W'^T - mean cs) + (b + W beta) with
+    W' = W diag(gamma), cs = W' 1, mean / rstd of each row of x.  Checked in fp64 on the oracle's
+    own LayerNorm (`clip_ref.layer_norm`) and on residual-stream-like rows (per-row offsets, a few
+    massive channels), then with W' rounded to f16 and x in f16 as the GPU computes it: the
+    difference stays far inside the bf16 output rounding."""
+    rng = np.random.default_rng(3)
+    M, K, N = 64, 768, 256
+    x = rng.standard_normal((M, K)) * rng.uniform(0.5, 4.0, (M, 1)) + rng.standard_normal((M, 1))
+    x[:, [7, 300, 511]] *= 40.0
+    w = rng.standard_normal((N, K)) / np.sqrt(K)
+    g, beta, b = 1 + 0.2 * rng.standard_normal(K), 0.1 * rng.standard_normal(K), 0.1 * rng.standard_normal(N)
+    ref = clip_ref.layer_norm(x, g, beta, 1e-5) @ w.T + b
+    mean = x.mean(1, keepdims=True)
+    rstd = 1.0 / np.sqrt(((x - mean) ** 2).mean(1, keepdims=True) + 1e-5)
+    wf = w * g
+    fold = rstd * (x @ wf.T - mean * wf.sum(1)) + (b + w @ beta)
+    assert np.abs(fold - ref).max() <= 1e-9 * np.abs(ref).max()
+    # the GPU's operand rounding: x (the stream) and W' in f16
+    x16, wf16 = x.astype(np.float16).astype(np.float64), wf.astype(np.float16).astype(np.float64)
+    mean16 = x16.mean(1, keepdims=True)
+    rstd16 = 1.0 / np.sqrt(((x16 - mean16) ** 2).mean(1, keepdims=True) + 1e-5)
+    gpu = rstd16 * (x16 @ wf16.T - mean16 * wf16.sum(1)) + (b + w @ beta)
+    assert np.abs(gpu - ref).max() <= 2.0 ** -9 * np.sqrt((ref ** 2).mean()) * 4
