@@ -1354,8 +1354,11 @@ int gemm_grid(int tile, int M, int N, int K) {
 // instead of 64); among those, the column tile that wastes the least of the
 // last wave of blocks over the 256 CUs (one 8-wave block per CU).
 int pick_gemm_tile(int M, int N, int K) {
-  (void)K;
-  if (M < 2048) return TILE_128x128;
+  // Small M: the 4-wave 160x128 pipelined tile (round 5; the bt kernel only where the pipelined
+  // kernel cannot run: K < 128).  The bt kernel's LayerNorm-fold build returned run-to-run wrong
+  // outputs, and one flaky small-batch mismatch in a STORE16 / RESID16
+  // engine suite run is not excluded to share its cause; the pipelined tiles give the same bits.
+  if (M < 2048) return K >= 128 ? TILE_160x128_RS : TILE_128x128;
   const int cus = 256;
   auto eff = [&](int bm, int bn) {
     const long tiles = (long)((M + bm - 1) / bm) * ((N + bn - 1) / bn);
