@@ -291,7 +291,7 @@ def test_rccl_communicator_and_gathered_entry_points(monkeypatch):
         torch.cuda.synchronize()
         got = out.cpu().numpy()
         ref = e.embed_pixels(x) if tower == 0 else e.embed_tokens(x)
-        assert np.array_equal(got, ref)
+        np.testing.assert_array_equal(got, ref, err_msg=f"tower {tower}")
         # the ragged branch (one ncclBroadcast per non-empty block, rank offsets) forced on the
         # equal one-rank block: the same bits
         _lib.check(_lib.lib().clipgpu_test_force_broadcast(e.handle, 1))
@@ -388,7 +388,7 @@ def test_one_device_clique_runs_the_multi_device_comm_path():
         side = torch.cuda.Stream()
         gather([d_in.data_ptr()], [B], [out.data_ptr()], [side.cuda_stream])  # the lazy clique is built here
         side.synchronize()
-        assert np.array_equal(out.cpu().numpy(), ref)
+        np.testing.assert_array_equal(out.cpu().numpy(), ref, err_msg=f"tower {tower} lazy {lazy}")
         # destroy with the collective still queued: behind ~50 ms of spinning on the caller's stream
         out2 = torch.full((B, 512), float("nan"), device="cuda")
         null_array = tower == 1

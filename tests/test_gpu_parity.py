@@ -105,7 +105,7 @@ def test_residual_stream_storage_parity(residual, fold, dtype):
         out = torch.empty((8, 512), device="cuda")
         ve.embed_pixels_device(d_px.data_ptr(), 8, out.data_ptr(), torch.cuda.current_stream().cuda_stream)
         torch.cuda.synchronize()
-        assert np.array_equal(out.cpu().numpy(), ve.embed_pixels(px[:8]))
+        np.testing.assert_array_equal(out.cpu().numpy(), ve.embed_pixels(px[:8]))
     assert cos[residual][0] >= cos["f32"][0] - 2e-5 and cos[residual][1] >= cos["f32"][1] - 2e-5, cos
 
 
