@@ -233,7 +233,8 @@ struct clipgpu_engine {
   int host_copy_stream = 1;
   // test hook (clipgpu_test_host_plan copy_stream bits 4-5): 1 = a multi-round call starts each round's
   // forwards together once the round's last chunk has landed (lanes in step); 2 = the D2Hs go on the copy
-  // stream (the lane streams run straight into their next forward)
+  // stream (the lane streams run straight into their next forward); 4 = a multi-round call joins the lanes
+  // every round (each chunk's forward also waits for the other chunks' previous-round forwards)
   int host_flags = 0;
   clipgpu::TowerSpec spec;
   clipgpu::PreprocessCfg pre;
@@ -1422,6 +1423,7 @@ void run_host_shard(clipgpu_engine& e, Replica& r, InKind kind, const void* in, 
   if (two_sets) ensure_host_set2(e, r);
   const bool lockstep = two_sets && (e.host_flags & 1) && e.host_copy_stream;
   const bool d2h_copy = (e.host_flags & 2) && e.host_copy_stream;
+  const bool join = two_sets && (e.host_flags & 4);
   struct Pending { int64_t c0 = -1; int n = 0; };
   Pending pend[2][4];
   float* const pin_out_set[2] = {r.pin_out, r.pin_out2};
@@ -1453,6 +1455,10 @@ void run_host_shard(clipgpu_engine& e, Replica& r, InKind kind, const void* in, 
       if (e.host_copy_stream) HIP_CHECK(hipStreamWaitEvent(c.st, copied[gate_k], 0));
       // (D2H on the copy stream: the other set's last D2H of these output rows has read them)
       if (d2h_copy && two_sets) HIP_CHECK(hipStreamWaitEvent(c.st, done_set[set ^ 1][c.k], 0));
+      // (joined rounds: the other lanes' previous-round forwards have ended, as after the device path's join)
+      if (join)
+        for (int j = 0; j < C; ++j)
+          if (j != c.k && pend[set ^ 1][j].c0 >= 0) HIP_CHECK(hipStreamWaitEvent(c.st, done_set[set ^ 1][j], 0));
       const Replica v = lane_view(e, r, part[c.k]);
       run_graph(e, r,
                 {(uint64_t)(10 + kind), (uint64_t)c.k, (uint64_t)c.n, fbits(mean, 0), fbits(mean, 1),
@@ -2477,8 +2483,9 @@ int clipgpu_test_host_plan(clipgpu_engine* e, int n_chunks, const int* bounds, i
   return guarded([&]() {
     if (!e) throw ClipErr(CLIPGPU_ERR_INVALID, "engine is NULL");
     std::lock_guard<std::mutex> lk(e->mu);
-    if (copy_stream < 0 || (copy_stream & 15) > 3 || copy_stream >= 64)
-      throw ClipErr(CLIPGPU_ERR_INVALID, "copy_stream: 0 .. 3, + 16 (lockstep rounds), + 32 (D2H on the copy stream)");
+    if (copy_stream < 0 || (copy_stream & 15) > 3 || copy_stream >= 128)
+      throw ClipErr(CLIPGPU_ERR_INVALID,
+                    "copy_stream: 0 .. 3, + 16 (lockstep rounds), + 32 (D2H on the copy stream), + 64 (joined rounds)");
     e->host_copy_stream = copy_stream & 15;
     e->host_flags = copy_stream >> 4;
     e->host_part.clear();

@@ -131,8 +131,9 @@ int clipgpu_test_engine_residual(const struct clipgpu_engine* e, int* residual, 
  * stream (default); 0: each on its chunk's lane stream; 2: each chunk's two halves on two copy
  * streams at once; 3: registered inputs pulled through their host mapping by a copy kernel on
  * the copy stream (others as 1).  + 16: a multi-round call starts each round's forwards together,
- * once the round's last chunk has landed; + 32: the D2Hs on the copy stream.  Speed only, never the
- * bits. */
+ * once the round's last chunk has landed; + 32: the D2Hs on the copy stream; + 64: a multi-round call
+ * joins the lanes every round (a chunk's forward also waits for the other chunks' previous-round
+ * forwards).  Speed only, never the bits. */
 int clipgpu_test_host_plan(struct clipgpu_engine* e, int n_chunks, const int* bounds, int copy_stream);
 /* Gathered calls of this handle take the ragged branch (one ncclBroadcast per block) even when
  * every block has the same size (on != 0), so a one-rank or equal-shard run exercises it. */

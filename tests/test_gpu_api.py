@@ -310,8 +310,11 @@ def test_multi_round_host_calls_alternate_buffer_sets_bit_exactly():
     (engine.hip run_host_shard: round i + 1's H2D under round i's forward).  Every
     round must equal the same rows embedded by a call of their own, bit for bit: u8 and f32 pixels
     and token ids, pageable and caller-registered buffers, a ragged last round, and a second
-    multi-round call (graph replay on both sets)."""
+    multi-round call (graph replay on both sets) -- under the default schedule and the host-plan
+    hook's multi-round schedules (+16 lanes in step, +32 D2H on the copy stream, +64 joined rounds)."""
+    import ctypes
     from oracle.model_spec import VIT_B_32_CFG
+    from open_clip_inference import _lib
     from open_clip_inference.engine import Engine, host_register, host_unregister
     from tests.helpers import normalized_pixels
     d = make_model_dir(VIT_B_32_CFG, seed=1234)
@@ -327,9 +330,12 @@ def test_multi_round_host_calls_alternate_buffer_sets_bit_exactly():
     calls = {"u8": (ve, lambda e, x, out=None: e.embed_u8(x, OPENAI_MEAN, OPENAI_STD, out=out), u8),
              "f32": (ve, lambda e, x, out=None: e.embed_pixels(x, out=out), px),
              "ids": (te, lambda e, x, out=None: e.embed_tokens(x, out=out), ids)}
+    no_bounds = (ctypes.c_int * 4)()
     for name, (e, fn, x) in calls.items():
         ref = np.concatenate([fn(e, x[i:i + MB]) for i in range(0, B, MB)])
-        for registered in (False, True):
+        for registered, flags in ((False, 1), (True, 1), (False, 1 + 16), (True, 1 + 32), (False, 1 + 64),
+                                  (True, 1 + 64)):
+            _lib.check(_lib.lib().clipgpu_test_host_plan(e.handle, 0, no_bounds, flags))
             xin = np.ascontiguousarray(x)
             out = np.full((B, 512), np.nan, np.float32)
             if registered:
@@ -339,7 +345,7 @@ def test_multi_round_host_calls_alternate_buffer_sets_bit_exactly():
                 for _ in range(2):
                     out.fill(np.nan)
                     fn(e, xin, out=out)
-                    assert np.array_equal(out, ref), (name, registered)
+                    assert np.array_equal(out, ref), (name, registered, flags)
             finally:
                 if registered:
                     host_unregister(xin)
