@@ -234,7 +234,9 @@ struct clipgpu_engine {
   // test hook (clipgpu_test_host_plan copy_stream bits 4-5): 1 = a multi-round call starts each round's
   // forwards together once the round's last chunk has landed (lanes in step); 2 = the D2Hs go on the copy
   // stream (the lane streams run straight into their next forward); 4 = a multi-round call joins the lanes
-  // every round (each chunk's forward also waits for the other chunks' previous-round forwards)
+  // every round (each chunk's forward also waits for the other chunks' previous-round forwards); 8 = a
+  // multi-round vision call runs each round as the device path does (one fork / join graph over the
+  // lanes once the round's input has landed, one D2H)
   int host_flags = 0;
   clipgpu::TowerSpec spec;
   clipgpu::PreprocessCfg pre;
@@ -1424,6 +1426,7 @@ void run_host_shard(clipgpu_engine& e, Replica& r, InKind kind, const void* in, 
   const bool lockstep = two_sets && (e.host_flags & 1) && e.host_copy_stream;
   const bool d2h_copy = (e.host_flags & 2) && e.host_copy_stream;
   const bool join = two_sets && (e.host_flags & 4);
+  const bool fused = two_sets && (e.host_flags & 8) && e.host_copy_stream && kind != IN_IDS;
   struct Pending { int64_t c0 = -1; int n = 0; };
   Pending pend[2][4];
   float* const pin_out_set[2] = {r.pin_out, r.pin_out2};
@@ -1528,12 +1531,30 @@ void run_host_shard(clipgpu_engine& e, Replica& r, InKind kind, const void* in, 
         HIP_CHECK(hipMemcpyAsync(din, src, (size_t)n * in_row_bytes, hipMemcpyHostToDevice, st));
       }
       ch[nch] = {k, n, rc, din, dout, st};
-      if (!lockstep) issue_forward(ch[nch], k);
+      if (!lockstep && !fused) issue_forward(ch[nch], k);
       ++nch;
       off += n;
     }
-    if (lockstep)
+    if (lockstep && !fused)
       for (int i = 0; i < nch; ++i) issue_forward(ch[i], ch[nch - 1].k);
+    if (fused && nch > 0) {  // (test hook, host_flags bit 3) the round as one device-path forward
+      hipStream_t st = r.stream;
+      HIP_CHECK(hipStreamWaitEvent(st, copied[ch[nch - 1].k], 0));
+      // the previous round (its D2H) is done before this round's graph reuses the workspace
+      for (int j = 0; j < C; ++j)
+        if (pend[set ^ 1][j].c0 >= 0) HIP_CHECK(hipStreamWaitEvent(st, done_set[set ^ 1][j], 0));
+      run_graph(e, r,
+                {(uint64_t)(30 + kind), (uint64_t)R, fbits(mean, 0), fbits(mean, 1), fbits(mean, 2), fbits(stdv, 0),
+                 fbits(stdv, 1), fbits(stdv, 2), (uint64_t)set},
+                st, [&](hipStream_t gs) {
+                  vision_forward_lanes(e, r, in_base, kind == IN_F32 ? A_IMG_F32 : A_IMG_U8, mean, stdv, R, r.out, gs);
+                });
+      float* dst = direct_out ? out + c0 * E : pin_out_set[set];
+      HIP_CHECK(hipMemcpyAsync(dst, r.out, (size_t)R * E * 4, hipMemcpyDeviceToHost, st));
+      HIP_CHECK(hipEventRecord(done[0], st));
+      pend[set][0].c0 = c0;
+      pend[set][0].n = R;
+    }
     c0 += R;
   }
   for (int set = 0; set < 2; ++set)
@@ -2483,9 +2504,10 @@ int clipgpu_test_host_plan(clipgpu_engine* e, int n_chunks, const int* bounds, i
   return guarded([&]() {
     if (!e) throw ClipErr(CLIPGPU_ERR_INVALID, "engine is NULL");
     std::lock_guard<std::mutex> lk(e->mu);
-    if (copy_stream < 0 || (copy_stream & 15) > 3 || copy_stream >= 128)
+    if (copy_stream < 0 || (copy_stream & 15) > 3 || copy_stream >= 256)
       throw ClipErr(CLIPGPU_ERR_INVALID,
-                    "copy_stream: 0 .. 3, + 16 (lockstep rounds), + 32 (D2H on the copy stream), + 64 (joined rounds)");
+                    "copy_stream: 0 .. 3, + 16 (lockstep rounds), + 32 (D2H on the copy stream), + 64 (joined rounds), "
+                    "+ 128 (device-path rounds)");
     e->host_copy_stream = copy_stream & 15;
     e->host_flags = copy_stream >> 4;
     e->host_part.clear();

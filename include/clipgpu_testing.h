@@ -133,7 +133,9 @@ int clipgpu_test_engine_residual(const struct clipgpu_engine* e, int* residual, 
  * the copy stream (others as 1).  + 16: a multi-round call starts each round's forwards together,
  * once the round's last chunk has landed; + 32: the D2Hs on the copy stream; + 64: a multi-round call
  * joins the lanes every round (a chunk's forward also waits for the other chunks' previous-round
- * forwards).  Speed only, never the bits. */
+ * forwards); + 128: a multi-round vision call runs each round as the device path does (one
+ * fork / join forward over the lanes once the round's input has landed, one D2H).  Speed only,
+ * never the bits. */
 int clipgpu_test_host_plan(struct clipgpu_engine* e, int n_chunks, const int* bounds, int copy_stream);
 /* Gathered calls of this handle take the ragged branch (one ncclBroadcast per block) even when
  * every block has the same size (on != 0), so a one-rank or equal-shard run exercises it. */
