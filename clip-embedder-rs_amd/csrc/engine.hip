@@ -116,6 +116,7 @@ struct Replica {
   void* in2 = nullptr;
   void* pin_in2 = nullptr;
   float* pin_out2 = nullptr;
+  float* out2 = nullptr;  // (host_flags bit 4: set 1's device output rows)
   hipEvent_t done2[4] = {nullptr, nullptr, nullptr, nullptr};
   hipEvent_t copied2[4] = {nullptr, nullptr, nullptr, nullptr};
   // Decoded-image path (clipgpu_embed_images_rgb8): per slot, pinned staging and a device
@@ -236,7 +237,9 @@ struct clipgpu_engine {
   // stream (the lane streams run straight into their next forward); 4 = a multi-round call joins the lanes
   // every round (each chunk's forward also waits for the other chunks' previous-round forwards); 8 = a
   // multi-round vision call runs each round as the device path does (one fork / join graph over the
-  // lanes once the round's input has landed, one D2H)
+  // lanes once the round's input has landed, one D2H); 16 = a multi-round call writes each set's
+  // embeddings to its own device rows and copies them back on the second copy stream, so a lane's
+  // next forward does not queue behind its D2H
   int host_flags = 0;
   clipgpu::TowerSpec spec;
   clipgpu::PreprocessCfg pre;
@@ -1393,6 +1396,7 @@ void ensure_host_set2(const clipgpu_engine& e, Replica& r) {
   HIP_CHECK(hipMalloc(&r.in2, B * e.in_bytes_per_row));
   HIP_CHECK(hipHostMalloc(&r.pin_in2, B * e.in_bytes_per_row, hipHostMallocDefault));
   HIP_CHECK(hipHostMalloc((void**)&r.pin_out2, B * (size_t)e.spec.embed_dim * 4, hipHostMallocDefault));
+  HIP_CHECK(hipMalloc((void**)&r.out2, B * (size_t)e.spec.embed_dim * 4));
   for (int i = 0; i < 4; ++i) {
     HIP_CHECK(hipEventCreateWithFlags(&r.done2[i], hipEventDisableTiming));
     HIP_CHECK(hipEventCreateWithFlags(&r.copied2[i], hipEventDisableTiming));
@@ -1427,6 +1431,7 @@ void run_host_shard(clipgpu_engine& e, Replica& r, InKind kind, const void* in, 
   const bool d2h_copy = (e.host_flags & 2) && e.host_copy_stream;
   const bool join = two_sets && (e.host_flags & 4);
   const bool fused = two_sets && (e.host_flags & 8) && e.host_copy_stream && kind != IN_IDS;
+  const bool d2h_side = two_sets && (e.host_flags & 16) && !fused && !d2h_copy && e.host_copy_stream != 2;
   struct Pending { int64_t c0 = -1; int n = 0; };
   Pending pend[2][4];
   float* const pin_out_set[2] = {r.pin_out, r.pin_out2};
@@ -1474,7 +1479,12 @@ void run_host_shard(clipgpu_engine& e, Replica& r, InKind kind, const void* in, 
                     vision_forward(e, v, c.din, kind == IN_F32 ? A_IMG_F32 : A_IMG_U8, mean, stdv, c.n, c.dout, gs);
                 });
       float* dst = direct_out ? out + c.rc * E : pin_out_set[set] + (size_t)part[c.k] * E;
-      if (d2h_copy) {
+      if (d2h_side) {  // the forward's end, then the D2H on the second copy stream
+        HIP_CHECK(hipEventRecord(done[c.k], c.st));
+        HIP_CHECK(hipStreamWaitEvent(r.copy2, done[c.k], 0));
+        HIP_CHECK(hipMemcpyAsync(dst, c.dout, (size_t)c.n * E * 4, hipMemcpyDeviceToHost, r.copy2));
+        HIP_CHECK(hipEventRecord(done[c.k], r.copy2));
+      } else if (d2h_copy) {
         HIP_CHECK(hipEventRecord(done[c.k], c.st));  // the forward's end ...
         HIP_CHECK(hipStreamWaitEvent(r.copy, done[c.k], 0));
         HIP_CHECK(hipMemcpyAsync(dst, c.dout, (size_t)c.n * E * 4, hipMemcpyDeviceToHost, r.copy));
@@ -1499,7 +1509,7 @@ void run_host_shard(clipgpu_engine& e, Replica& r, InKind kind, const void* in, 
       drain(set, k);  // this set's round before last: its D2H (so also its H2D and forward) done
       hipStream_t st = r.lane[k % L] ? r.lane[k % L] : r.stream;
       char* din = in_base + (size_t)part[k] * in_row_bytes;
-      float* dout = r.out + (size_t)part[k] * E;
+      float* dout = (set && d2h_side ? r.out2 : r.out) + (size_t)part[k] * E;
       const char* src = (const char*)in + rc * in_row_bytes;
       if (!direct_in) {
         char* pin = pin_in_base + (size_t)part[k] * in_row_bytes;
@@ -1882,6 +1892,7 @@ void destroy_replica(Replica& r) {
   if (r.in2) (void)hipFree(r.in2);
   if (r.pin_in2) (void)hipHostFree(r.pin_in2);
   if (r.pin_out2) (void)hipHostFree(r.pin_out2);
+  if (r.out2) (void)hipFree(r.out2);
   if (r.stream) (void)hipStreamDestroy(r.stream);
   if (r.copy) (void)hipStreamDestroy(r.copy);
   if (r.copy2) (void)hipStreamDestroy(r.copy2);
@@ -2504,10 +2515,10 @@ int clipgpu_test_host_plan(clipgpu_engine* e, int n_chunks, const int* bounds, i
   return guarded([&]() {
     if (!e) throw ClipErr(CLIPGPU_ERR_INVALID, "engine is NULL");
     std::lock_guard<std::mutex> lk(e->mu);
-    if (copy_stream < 0 || (copy_stream & 15) > 3 || copy_stream >= 256)
+    if (copy_stream < 0 || (copy_stream & 15) > 3 || copy_stream >= 512)
       throw ClipErr(CLIPGPU_ERR_INVALID,
                     "copy_stream: 0 .. 3, + 16 (lockstep rounds), + 32 (D2H on the copy stream), + 64 (joined rounds), "
-                    "+ 128 (device-path rounds)");
+                    "+ 128 (device-path rounds), + 256 (per-set outputs, D2H on the second copy stream)");
     e->host_copy_stream = copy_stream & 15;
     e->host_flags = copy_stream >> 4;
     e->host_part.clear();

@@ -134,8 +134,10 @@ int clipgpu_test_engine_residual(const struct clipgpu_engine* e, int* residual, 
  * once the round's last chunk has landed; + 32: the D2Hs on the copy stream; + 64: a multi-round call
  * joins the lanes every round (a chunk's forward also waits for the other chunks' previous-round
  * forwards); + 128: a multi-round vision call runs each round as the device path does (one
- * fork / join forward over the lanes once the round's input has landed, one D2H).  Speed only,
- * never the bits. */
+ * fork / join forward over the lanes once the round's input has landed, one D2H); + 256: a
+ * multi-round call writes each buffer set's embeddings to its own device rows and copies them back
+ * on a second copy stream (a lane's next forward does not queue behind its D2H).  Speed only, never
+ * the bits. */
 int clipgpu_test_host_plan(struct clipgpu_engine* e, int n_chunks, const int* bounds, int copy_stream);
 /* Gathered calls of this handle take the ragged branch (one ncclBroadcast per block) even when
  * every block has the same size (on != 0), so a one-rank or equal-shard run exercises it. */
