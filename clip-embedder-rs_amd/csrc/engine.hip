@@ -116,7 +116,7 @@ struct Replica {
   void* in2 = nullptr;
   void* pin_in2 = nullptr;
   float* pin_out2 = nullptr;
-  float* out2 = nullptr;  // (host_flags bit 4: set 1's device output rows)
+  float* out2 = nullptr;  // set 1's device embedding rows
   hipEvent_t done2[4] = {nullptr, nullptr, nullptr, nullptr};
   hipEvent_t copied2[4] = {nullptr, nullptr, nullptr, nullptr};
   // Decoded-image path (clipgpu_embed_images_rgb8): per slot, pinned staging and a device
@@ -237,9 +237,8 @@ struct clipgpu_engine {
   // stream (the lane streams run straight into their next forward); 4 = a multi-round call joins the lanes
   // every round (each chunk's forward also waits for the other chunks' previous-round forwards); 8 = a
   // multi-round vision call runs each round as the device path does (one fork / join graph over the
-  // lanes once the round's input has landed, one D2H); 16 = a multi-round call writes each set's
-  // embeddings to its own device rows and copies them back on the second copy stream, so a lane's
-  // next forward does not queue behind its D2H
+  // lanes once the round's input has landed, one D2H); 16 = a multi-round call's D2Hs on the lane
+  // streams, behind each forward (the round-4 schedule; see run_host_shard)
   int host_flags = 0;
   clipgpu::TowerSpec spec;
   clipgpu::PreprocessCfg pre;
@@ -1415,8 +1414,9 @@ void ensure_host_set2(const clipgpu_engine& e, Replica& r) {
 // A range of more than max_batch rows alternates its rounds between two buffer sets (device input
 // rows, pinned staging, events): round i's host copy and H2D are issued while round i - 1's forward
 // runs, and a set is reused two rounds later, after its round's D2H event -- so every round but the
-// first starts its forward with its input already on the device.  Each round
-// runs the same forward on the same rows as a call of its own: the outputs are bit-identical.
+// first starts its forward with its input already on the device.  Each set also
+// has its own device embedding rows, copied back on the second copy stream (d2h_side below).  Each
+// round runs the same forward on the same rows as a call of its own: the outputs are bit-identical.
 void run_host_shard(clipgpu_engine& e, Replica& r, InKind kind, const void* in, size_t in_row_bytes, int64_t b0,
                     int64_t b1, const float* mean, const float* stdv, float* out, int tokens = 0) {
   HIP_CHECK(hipSetDevice(r.device));
@@ -1431,7 +1431,12 @@ void run_host_shard(clipgpu_engine& e, Replica& r, InKind kind, const void* in, 
   const bool d2h_copy = (e.host_flags & 2) && e.host_copy_stream;
   const bool join = two_sets && (e.host_flags & 4);
   const bool fused = two_sets && (e.host_flags & 8) && e.host_copy_stream && kind != IN_IDS;
-  const bool d2h_side = two_sets && (e.host_flags & 16) && !fused && !d2h_copy && e.host_copy_stream != 2;
+  // Multi-round calls: each set writes its embeddings to its own device rows (r.out / r.out2), and their
+  // D2H runs on the second copy stream once the forward has ended, so a lane's next forward starts right
+  // behind its last one instead of queueing behind a D2H and its event.  4 x 256 u8 images, registered:
+  // 0.913 -> 0.927 of the device-resident rate, 8 x 256: 0.929 -> 0.946 (profiles/r05_host_plan_side.jsonl).
+  // A set's rows are rewritten two rounds later, after drain() has seen their D2H event.
+  const bool d2h_side = two_sets && !(e.host_flags & 16) && !fused && !d2h_copy && e.host_copy_stream != 2;
   struct Pending { int64_t c0 = -1; int n = 0; };
   Pending pend[2][4];
   float* const pin_out_set[2] = {r.pin_out, r.pin_out2};
@@ -1471,7 +1476,7 @@ void run_host_shard(clipgpu_engine& e, Replica& r, InKind kind, const void* in, 
       run_graph(e, r,
                 {(uint64_t)(10 + kind), (uint64_t)c.k, (uint64_t)c.n, fbits(mean, 0), fbits(mean, 1),
                  fbits(mean, 2), fbits(stdv, 0), fbits(stdv, 1), fbits(stdv, 2), (uint64_t)tokens,
-                 (uint64_t)part[c.k], (uint64_t)set},
+                 (uint64_t)part[c.k], (uint64_t)set, (uint64_t)(uintptr_t)c.dout},
                 c.st, [&](hipStream_t gs) {
                   if (kind == IN_IDS)
                     text_forward(e, v, (const int64_t*)c.din, c.n, c.dout, gs, tokens);
@@ -2518,7 +2523,7 @@ int clipgpu_test_host_plan(clipgpu_engine* e, int n_chunks, const int* bounds, i
     if (copy_stream < 0 || (copy_stream & 15) > 3 || copy_stream >= 512)
       throw ClipErr(CLIPGPU_ERR_INVALID,
                     "copy_stream: 0 .. 3, + 16 (lockstep rounds), + 32 (D2H on the copy stream), + 64 (joined rounds), "
-                    "+ 128 (device-path rounds), + 256 (per-set outputs, D2H on the second copy stream)");
+                    "+ 128 (device-path rounds), + 256 (D2H on the lane streams)");
     e->host_copy_stream = copy_stream & 15;
     e->host_flags = copy_stream >> 4;
     e->host_part.clear();

@@ -135,9 +135,9 @@ int clipgpu_test_engine_residual(const struct clipgpu_engine* e, int* residual, 
  * joins the lanes every round (a chunk's forward also waits for the other chunks' previous-round
  * forwards); + 128: a multi-round vision call runs each round as the device path does (one
  * fork / join forward over the lanes once the round's input has landed, one D2H); + 256: a
- * multi-round call writes each buffer set's embeddings to its own device rows and copies them back
- * on a second copy stream (a lane's next forward does not queue behind its D2H).  Speed only, never
- * the bits. */
+ * multi-round call's D2Hs on the lane streams behind each forward (the round-4 schedule; the default
+ * writes each buffer set's embeddings to its own device rows and copies them back on a second copy
+ * stream).  Speed only, never the bits. */
 int clipgpu_test_host_plan(struct clipgpu_engine* e, int n_chunks, const int* bounds, int copy_stream);
 /* Gathered calls of this handle take the ragged branch (one ncclBroadcast per block) even when
  * every block has the same size (on != 0), so a one-rank or equal-shard run exercises it. */

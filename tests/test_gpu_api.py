@@ -312,7 +312,7 @@ def test_multi_round_host_calls_alternate_buffer_sets_bit_exactly():
     and token ids, pageable and caller-registered buffers, a ragged last round, and a second
     multi-round call (graph replay on both sets) -- under the default schedule and the host-plan
     hook's multi-round schedules (+16 lanes in step, +32 D2H on the copy stream, +64 joined rounds, +128
-    device-path rounds, +256 per-set outputs with the D2H on a second copy stream)."""
+    device-path rounds, +256 the D2Hs on the lane streams)."""
     import ctypes
     from oracle.model_spec import VIT_B_32_CFG
     from open_clip_inference import _lib
