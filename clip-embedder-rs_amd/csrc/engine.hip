@@ -238,8 +238,7 @@ struct clipgpu_engine {
   // every round (each chunk's forward also waits for the other chunks' previous-round forwards); 8 = a
   // multi-round vision call runs each round as the device path does (one fork / join graph over the
   // lanes once the round's input has landed, one D2H); 16 = a multi-round call's D2Hs on the lane
-  // streams, behind each forward (the round-4 schedule; see run_host_shard); 32 = a multi-round vision
-  // call's first round is a whole max_batch round (default: half of one)
+  // streams, behind each forward (the round-4 schedule; see run_host_shard)
   int host_flags = 0;
   clipgpu::TowerSpec spec;
   clipgpu::PreprocessCfg pre;
@@ -1438,11 +1437,6 @@ void run_host_shard(clipgpu_engine& e, Replica& r, InKind kind, const void* in, 
   // 0.913 -> 0.927 of the device-resident rate, 8 x 256: 0.929 -> 0.946 (profiles/r05_host_plan_side.jsonl).
   // A set's rows are rewritten two rounds later, after drain() has seen their D2H event.
   const bool d2h_side = two_sets && !(e.host_flags & 16) && !fused && !d2h_copy && e.host_copy_stream != 2;
-  // A vision call of at least two max_batch rounds starts with a half round: the lanes wait for half
-  // the input bytes before their first forwards (a 256-image u8 round is 38.5 MB, ~1 ms of H2D), and
-  // the next round's H2D runs under it.  Every row still gets the same bits (rows are independent).
-  const bool half_first = two_sets && kind != IN_IDS && b1 - b0 >= 2 * (int64_t)MB && MB >= 2 &&
-                          !(e.host_flags & 32) && !fused;
   struct Pending { int64_t c0 = -1; int n = 0; };
   Pending pend[2][4];
   float* const pin_out_set[2] = {r.pin_out, r.pin_out2};
@@ -1461,7 +1455,7 @@ void run_host_shard(clipgpu_engine& e, Replica& r, InKind kind, const void* in, 
     char* const pin_in_base = (char*)(set ? r.pin_in2 : r.pin_in);
     hipEvent_t* const done = set ? r.done2 : r.done;
     hipEvent_t* const copied = set ? r.copied2 : r.copied;
-    const int R = (int)std::min<int64_t>(round == 0 && half_first ? MB / 2 : MB, b1 - c0);  // rows of this round
+    const int R = (int)std::min<int64_t>(MB, b1 - c0);  // rows of this round
     struct Chunk { int k, n; int64_t rc; char* din; float* dout; hipStream_t st; };
     Chunk ch[4];
     int nch = 0;
@@ -2526,10 +2520,10 @@ int clipgpu_test_host_plan(clipgpu_engine* e, int n_chunks, const int* bounds, i
   return guarded([&]() {
     if (!e) throw ClipErr(CLIPGPU_ERR_INVALID, "engine is NULL");
     std::lock_guard<std::mutex> lk(e->mu);
-    if (copy_stream < 0 || (copy_stream & 15) > 3 || copy_stream >= 1024)
+    if (copy_stream < 0 || (copy_stream & 15) > 3 || copy_stream >= 512)
       throw ClipErr(CLIPGPU_ERR_INVALID,
                     "copy_stream: 0 .. 3, + 16 (lockstep rounds), + 32 (D2H on the copy stream), + 64 (joined rounds), "
-                    "+ 128 (device-path rounds), + 256 (D2H on the lane streams), + 512 (whole first round)");
+                    "+ 128 (device-path rounds), + 256 (D2H on the lane streams)");
     e->host_copy_stream = copy_stream & 15;
     e->host_flags = copy_stream >> 4;
     e->host_part.clear();

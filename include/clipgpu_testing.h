@@ -137,8 +137,7 @@ int clipgpu_test_engine_residual(const struct clipgpu_engine* e, int* residual, 
  * fork / join forward over the lanes once the round's input has landed, one D2H); + 256: a
  * multi-round call's D2Hs on the lane streams behind each forward (the round-4 schedule; the default
  * writes each buffer set's embeddings to its own device rows and copies them back on a second copy
- * stream); + 512: a multi-round vision call's first round is a whole max_batch round (the default
- * starts with half of one).  Speed only, never the bits. */
+ * stream).  Speed only, never the bits. */
 int clipgpu_test_host_plan(struct clipgpu_engine* e, int n_chunks, const int* bounds, int copy_stream);
 /* Gathered calls of this handle take the ragged branch (one ncclBroadcast per block) even when
  * every block has the same size (on != 0), so a one-rank or equal-shard run exercises it. */
