@@ -17,12 +17,18 @@ end-to-end legs through the host-buffer entry points (PCIe included; N = 1);
 CPU baseline = the fp32 torch CPU port of the same graphs (oracle/torch_cpu.py) on a bounded
 sample of the same inputs on rank 0, which also checks the GPU rows (cosine).
 
-Launch: python bench.py [--gpus 1 --steps K --warmup W]   (N > 1: torch.distributed.run)
+Launch: python bench.py [--gpus N --steps K --warmup W].  N > 1: one rank per GPU.  Started without a
+torch.distributed launcher (no WORLD_SIZE in the environment), bench.py starts the N ranks itself --
+`python -m torch.distributed.run --nproc-per-node N` as a child process, before anything touches the GPU
+-- and exits with its status; rank 0 prints the JSON line.  Under a launcher, WORLD_SIZE must equal
+--gpus (a mismatch exits with status 2), so `n_gpus` is always --gpus.
 """
 import argparse
 import ctypes
 import json
 import os
+import socket
+import subprocess
 import sys
 import tempfile
 import time
@@ -78,8 +84,8 @@ def text_flops(B, T=77, executed=False):
 SITE_SHAPES = {"qkv": (2304, 768), "out_proj": (768, 768), "c_fc": (3072, 768), "c_proj": (768, 3072)}
 SITE_EPI = {"qkv": "{ln}+bias", "out_proj": "+bias, {x} residual", "c_fc": "{ln}+QuickGELU",
             "c_proj": "+bias, {x} residual"}
-TILE_NAMES = {0: "heuristic", 1: "128x128", 2: "256x128", 3: "256x256", 13: "192x256w8", 14: "256x256rs",
-              15: "160x128rs", 17: "160x128w8rs", 18: "256x256half", 26: "224x192w8"}
+TILE_NAMES = {0: "heuristic", 2: "256x128", 3: "256x256", 13: "192x256w8", 14: "256x256rs",
+              15: "160x128rs", 17: "160x128w8rs", 18: "256x256half", 26: "224x192w8", 100: "skinny", 101: "general"}
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md chip table)
 B_VISION = 256
 B_TEXT = 1024
@@ -313,9 +319,15 @@ def host_leg(engine, kind, host, steps, registered=False):
     staging; `registered` pins the caller's input and output arrays first (clipgpu_host_register:
     direct DMA).  Either way the engine moves the batch in even per-lane chunks (engine.hip
     host_chunks), each chunk's forward starting once its H2D has landed."""
-    from open_clip_inference.engine import host_register, host_unregister
-    host = np.ascontiguousarray(host)
-    out = np.empty((len(host), engine.embed_dim), np.float32)
+    from open_clip_inference.engine import host_buffer, host_register, host_unregister
+    if registered:  # page-owning arrays (registration pins whole pages)
+        buf = host_buffer(host.shape, host.dtype)
+        buf[...] = host
+        host = buf
+        out = host_buffer((len(host), engine.embed_dim), np.float32)
+    else:
+        host = np.ascontiguousarray(host)
+        out = np.empty((len(host), engine.embed_dim), np.float32)
     call = {"u8": lambda: engine.embed_u8(host, CFG["preprocess_cfg"]["mean"], CFG["preprocess_cfg"]["std"], out=out),
             "f32": lambda: engine.embed_pixels(host, out=out),
             "tokens": lambda: engine.embed_tokens(host, out=out)}[kind]
@@ -366,6 +378,57 @@ def images_leg(engine, images, steps, host_preprocess=False):
                      f": {len(images)} decoded {w}x{h} RGB8 images per call"}
 
 
+def free_port():
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    return port
+
+
+def launch_ranks(n, argv):
+    """--gpus N > 1 without a launcher: N rank processes through torch.distributed.run (a child process:
+    this process has not touched the GPU and never execs), one per GPU, rendezvous on 127.0.0.1.  Their
+    output passes through; returns the launcher's exit status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    return subprocess.call(cmd, env=env)
+
+
+def resolve_world(gpus, env):
+    """(world, rank, local rank) of this process, or an int exit status for main() to return: launch
+    the ranks (no WORLD_SIZE and gpus > 1) or refuse a WORLD_SIZE that is not --gpus."""
+    if gpus < 1:
+        print(f"bench.py: --gpus {gpus} < 1", file=sys.stderr)
+        return 2
+    if "WORLD_SIZE" not in env:
+        if gpus > 1:
+            return ("launch", gpus)
+        return 1, 0, 0
+    world = int(env["WORLD_SIZE"])
+    if world != gpus:
+        print(f"bench.py: --gpus {gpus} but WORLD_SIZE={world} (the launcher started {world} ranks): refusing "
+              f"to report n_gpus={world} for a {gpus}-GPU request", file=sys.stderr)
+        return 2
+    return world, int(env.get("RANK", "0")), int(env.get("LOCAL_RANK", "0"))
+
+
+def plumbing_check(world, rank):
+    """--plumbing-check: the N > 1 rank plumbing without a GPU call (tests/test_cpu_bench_launcher.py):
+    the gloo control plane the bench uses, a barrier and a gather of (rank, local rank, world) from
+    every rank; rank 0 prints them as one JSON line."""
+    dist.init_process_group("gloo")
+    me = torch.tensor([rank, int(os.environ.get("LOCAL_RANK", "0")), world], dtype=torch.int64)
+    got = [torch.zeros(3, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(got, me)
+    dist.barrier()
+    if rank == 0:
+        print(json.dumps({"plumbing": [g.tolist() for g in got], "n_gpus": world}), flush=True)
+    dist.destroy_process_group()
+    return 0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -393,11 +456,17 @@ def main():
     ap.add_argument("--gather", action="store_true",
                     help="N = 1: run the data-parallel path anyway (gloo control plane, the engine's RCCL "
                          "communicator, gathered entry points) -- a one-GPU rehearsal of N > 1")
+    ap.add_argument("--plumbing-check", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    w = resolve_world(args.gpus, os.environ)
+    if isinstance(w, int):
+        return w
+    if w[0] == "launch":
+        return launch_ranks(w[1], sys.argv[1:])
+    world, rank, local = w
+    if args.plumbing_check:
+        return plumbing_check(world, rank) if world > 1 else 0
     # dp: the data-parallel path (every N > 1 run; --gather rehearses it at N = 1 on one GPU)
     dp = world > 1 or args.gather
     if world > 1:
@@ -405,12 +474,7 @@ def main():
         # collective is the engine's own RCCL communicator (clipgpu_comm_init_rank)
         dist.init_process_group("gloo")
     elif dp:
-        import socket
-        sk = socket.socket()
-        sk.bind(("127.0.0.1", 0))
-        port = sk.getsockname()[1]
-        sk.close()
-        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{free_port()}", rank=0, world_size=1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
@@ -711,7 +775,8 @@ def main():
     ve.close()
     if dp:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -27,6 +27,7 @@
 #include "../../include/clipgpu.h"
 #include "../../include/clipgpu_testing.h"
 #include "host/api_util.hpp"
+#include "host/copy_pool.hpp"
 #include "host/json.hpp"
 #include "host/model.hpp"
 #include "host/resize_plan.hpp"
@@ -108,7 +109,7 @@ struct Replica {
   hipStream_t lane[4] = {nullptr, nullptr, nullptr, nullptr};
   hipEvent_t fork = nullptr, join[4] = {nullptr, nullptr, nullptr, nullptr};
   hipEvent_t done[4] = {nullptr, nullptr, nullptr, nullptr};  // host path: chunk slot's D2H finished
-  hipStream_t copy = nullptr, copy2 = nullptr;  // host path: every H2D, in chunk order (copy2: test hook)
+  hipStream_t copy = nullptr, copy2 = nullptr;  // host path: every H2D, in chunk order; copy2: multi-round D2Hs
   hipEvent_t copied[4] = {nullptr, nullptr, nullptr, nullptr};  // host path: chunk slot's H2D finished
   // Host path, second buffer set (run_host_shard): a call of more than max_batch rows alternates
   // rounds between two sets of input / output staging, so round i + 1's host copy and H2D run under
@@ -229,17 +230,10 @@ struct clipgpu_engine {
   std::vector<int> comm_devs;
   bool force_bcast = false;  // test hook: gathered calls take the ragged (broadcast) branch
   // test hook (clipgpu_test_host_plan): the host path's chunk partition of max_batch (empty = host_chunks'
-  // default) and whether its H2Ds go on the replica's copy stream (1) or on each chunk's lane stream (0)
+  // default)
   std::vector<int> host_part;
-  int host_copy_stream = 1;
-  // test hook (clipgpu_test_host_plan copy_stream bits 4-5): 1 = a multi-round call starts each round's
-  // forwards together once the round's last chunk has landed (lanes in step); 2 = the D2Hs go on the copy
-  // stream (the lane streams run straight into their next forward); 4 = a multi-round call joins the lanes
-  // every round (each chunk's forward also waits for the other chunks' previous-round forwards); 8 = a
-  // multi-round vision call runs each round as the device path does (one fork / join graph over the
-  // lanes once the round's input has landed, one D2H); 16 = a multi-round call's D2Hs on the lane
-  // streams, behind each forward (the round-4 schedule; see run_host_shard)
-  int host_flags = 0;
+  // test hook (clipgpu_test_rgb8_resize_always): S x S decoded images also take the resize path
+  bool rgb8_resize_always = false;
   clipgpu::TowerSpec spec;
   clipgpu::PreprocessCfg pre;
   clipgpu::DType dt = clipgpu::DT_BF16;
@@ -1336,26 +1330,16 @@ void tune_forward(clipgpu_engine& e, Replica& r) {
 
 enum InKind { IN_F32 = 0, IN_U8 = 1, IN_IDS = 2 };
 
-// Host -> pinned staging copy, split over a few threads when large (one thread moves
-// ~10 GB/s; a 128-image f32 sub-chunk is 77 MB).
-void par_memcpy(void* dst, const void* src, size_t n) {
-  const size_t kMin = 4u << 20;
-  const int nt = (int)std::min<size_t>(8, std::max<size_t>(1, n / kMin));
-  if (nt == 1) {
-    std::memcpy(dst, src, n);
-    return;
-  }
-  std::vector<std::thread> th;
-  const size_t per = (n + nt - 1) / nt;
-  for (int t = 0; t < nt; ++t) {
-    const size_t o = (size_t)t * per;
-    if (o >= n) break;
-    th.emplace_back([=]() { std::memcpy((char*)dst + o, (const char*)src + o, std::min(per, n - o)); });
-  }
-  for (auto& t : th) t.join();
-}
+// Row source of a host entry point: a contiguous array (row i at in + i * row_bytes), or one pointer per
+// row (`rows`: the decoded-image entry point's S x S images, which already are the u8 NHWC rows).
+struct HostRows {
+  const char* in = nullptr;
+  const void* const* rows = nullptr;
+  size_t row_bytes = 0;
+};
 
 // Caller-registered host ranges (clipgpu_host_register): process-wide, hipHostRegister'ed.
+constexpr size_t kHostPage = 4096;
 struct HostRanges {
   std::mutex mu;
   std::vector<std::pair<uintptr_t, size_t>> r;  // (base, bytes)
@@ -1409,34 +1393,32 @@ void ensure_host_set2(const clipgpu_engine& e, Replica& r) {
 // event.  The H2Ds go in chunk order on the replica's copy stream (the first chunk gets the whole
 // link); chunk k's forward runs on lane stream k % lanes once its copy event has fired, so the
 // transfer of chunk k + 1 overlaps the forward of chunk k, and forwards of different lanes
-// overlap each other.  Inputs are staged through pinned memory (par_memcpy) or DMA'd straight
-// from a caller-registered range (clipgpu_host_register); outputs likewise.
+// overlap each other.  Inputs are DMA'd straight from a caller-registered range
+// (clipgpu_host_register) or staged through pinned memory by the copy pool in pieces of whole rows
+// (kStagePiece), each piece's H2D issued as soon as it is packed, so a chunk's transfer runs under the
+// packing of its later pieces; outputs are written straight into a registered range, or staged.
 // A range of more than max_batch rows alternates its rounds between two buffer sets (device input
 // rows, pinned staging, events): round i's host copy and H2D are issued while round i - 1's forward
 // runs, and a set is reused two rounds later, after its round's D2H event -- so every round but the
 // first starts its forward with its input already on the device.  Each set also
-// has its own device embedding rows, copied back on the second copy stream (d2h_side below).  Each
-// round runs the same forward on the same rows as a call of its own: the outputs are bit-identical.
-void run_host_shard(clipgpu_engine& e, Replica& r, InKind kind, const void* in, size_t in_row_bytes, int64_t b0,
-                    int64_t b1, const float* mean, const float* stdv, float* out, int tokens = 0) {
+// has its own device embedding rows, copied back on the second copy stream once the forward has ended,
+// so a lane's next forward starts right behind its last one.  Each round runs the same forward on the
+// same rows as a call of its own: the outputs are bit-identical.
+// (Round 6 removed the schedules measured and not kept -- lockstep, joined and device-path rounds, D2H
+// on the copy or lane streams, split and pulled H2Ds; DESIGN.md §6 keeps their numbers.)
+constexpr size_t kStagePiece = 4u << 20;
+
+void run_host_shard(clipgpu_engine& e, Replica& r, InKind kind, const HostRows& src, int64_t b0, int64_t b1,
+                    const float* mean, const float* stdv, float* out, int tokens = 0) {
   HIP_CHECK(hipSetDevice(r.device));
   const int E = e.spec.embed_dim, L = e.lanes, MB = e.max_batch;
-  const bool direct_in = host_registered((const char*)in + b0 * in_row_bytes, (size_t)(b1 - b0) * in_row_bytes);
+  const size_t rb = src.row_bytes;
+  const bool direct_in = src.rows == nullptr && host_registered(src.in + b0 * rb, (size_t)(b1 - b0) * rb);
   const bool direct_out = host_registered(out + b0 * E, (size_t)(b1 - b0) * E * 4);
   const std::vector<int> part = host_chunks(e, kind);
   const int C = (int)part.size() - 1;
   const bool two_sets = b1 - b0 > MB;
   if (two_sets) ensure_host_set2(e, r);
-  const bool lockstep = two_sets && (e.host_flags & 1) && e.host_copy_stream;
-  const bool d2h_copy = (e.host_flags & 2) && e.host_copy_stream;
-  const bool join = two_sets && (e.host_flags & 4);
-  const bool fused = two_sets && (e.host_flags & 8) && e.host_copy_stream && kind != IN_IDS;
-  // Multi-round calls: each set writes its embeddings to its own device rows (r.out / r.out2), and their
-  // D2H runs on the second copy stream once the forward has ended, so a lane's next forward starts right
-  // behind its last one instead of queueing behind a D2H and its event.  4 x 256 u8 images, registered:
-  // 0.913 -> 0.927 of the device-resident rate, 8 x 256: 0.929 -> 0.946 (profiles/r05_host_plan_side.jsonl).
-  // A set's rows are rewritten two rounds later, after drain() has seen their D2H event.
-  const bool d2h_side = two_sets && !(e.host_flags & 16) && !fused && !d2h_copy && e.host_copy_stream != 2;
   struct Pending { int64_t c0 = -1; int n = 0; };
   Pending pend[2][4];
   float* const pin_out_set[2] = {r.pin_out, r.pin_out2};
@@ -1448,6 +1430,7 @@ void run_host_shard(clipgpu_engine& e, Replica& r, InKind kind, const void* in, 
       std::memcpy(out + pend[set][k].c0 * E, pin_out_set[set] + (size_t)part[k] * E, (size_t)pend[set][k].n * E * 4);
     pend[set][k].c0 = -1;
   };
+  const int rows_per_piece = (int)std::max<size_t>(1, kStagePiece / rb);
   int round = 0;
   for (int64_t c0 = b0; c0 < b1; ++round) {
     const int set = two_sets ? (round & 1) : 0;
@@ -1456,51 +1439,6 @@ void run_host_shard(clipgpu_engine& e, Replica& r, InKind kind, const void* in, 
     hipEvent_t* const done = set ? r.done2 : r.done;
     hipEvent_t* const copied = set ? r.copied2 : r.copied;
     const int R = (int)std::min<int64_t>(MB, b1 - c0);  // rows of this round
-    struct Chunk { int k, n; int64_t rc; char* din; float* dout; hipStream_t st; };
-    Chunk ch[4];
-    int nch = 0;
-    // A chunk's forward and D2H, issued right after the chunk's H2D: it starts once the chunk has
-    // landed, so the first half's forward overlaps the second half's host copy and transfer, and from the
-    // second round of a multi-round call on, a round's input lands during the previous round's forwards.
-    // (Test hook, host_flags bit 0: a multi-round call issues the round's forwards after all its H2Ds,
-    // gated on the last one -- the lanes in step; bit 1: the D2Hs on the copy stream.)
-    auto issue_forward = [&](const Chunk& c, int gate_k) {
-      if (e.host_copy_stream) HIP_CHECK(hipStreamWaitEvent(c.st, copied[gate_k], 0));
-      // (D2H on the copy stream: the other set's last D2H of these output rows has read them)
-      if (d2h_copy && two_sets) HIP_CHECK(hipStreamWaitEvent(c.st, done_set[set ^ 1][c.k], 0));
-      // (joined rounds: the other lanes' previous-round forwards have ended, as after the device path's join)
-      if (join)
-        for (int j = 0; j < C; ++j)
-          if (j != c.k && pend[set ^ 1][j].c0 >= 0) HIP_CHECK(hipStreamWaitEvent(c.st, done_set[set ^ 1][j], 0));
-      const Replica v = lane_view(e, r, part[c.k]);
-      run_graph(e, r,
-                {(uint64_t)(10 + kind), (uint64_t)c.k, (uint64_t)c.n, fbits(mean, 0), fbits(mean, 1),
-                 fbits(mean, 2), fbits(stdv, 0), fbits(stdv, 1), fbits(stdv, 2), (uint64_t)tokens,
-                 (uint64_t)part[c.k], (uint64_t)set, (uint64_t)(uintptr_t)c.dout},
-                c.st, [&](hipStream_t gs) {
-                  if (kind == IN_IDS)
-                    text_forward(e, v, (const int64_t*)c.din, c.n, c.dout, gs, tokens);
-                  else
-                    vision_forward(e, v, c.din, kind == IN_F32 ? A_IMG_F32 : A_IMG_U8, mean, stdv, c.n, c.dout, gs);
-                });
-      float* dst = direct_out ? out + c.rc * E : pin_out_set[set] + (size_t)part[c.k] * E;
-      if (d2h_side) {  // the forward's end, then the D2H on the second copy stream
-        HIP_CHECK(hipEventRecord(done[c.k], c.st));
-        HIP_CHECK(hipStreamWaitEvent(r.copy2, done[c.k], 0));
-        HIP_CHECK(hipMemcpyAsync(dst, c.dout, (size_t)c.n * E * 4, hipMemcpyDeviceToHost, r.copy2));
-        HIP_CHECK(hipEventRecord(done[c.k], r.copy2));
-      } else if (d2h_copy) {
-        HIP_CHECK(hipEventRecord(done[c.k], c.st));  // the forward's end ...
-        HIP_CHECK(hipStreamWaitEvent(r.copy, done[c.k], 0));
-        HIP_CHECK(hipMemcpyAsync(dst, c.dout, (size_t)c.n * E * 4, hipMemcpyDeviceToHost, r.copy));
-        HIP_CHECK(hipEventRecord(done[c.k], r.copy));  // ... then the D2H's
-      } else {
-        HIP_CHECK(hipMemcpyAsync(dst, c.dout, (size_t)c.n * E * 4, hipMemcpyDeviceToHost, c.st));
-        HIP_CHECK(hipEventRecord(done[c.k], c.st));
-      }
-      pend[set][c.k].c0 = c.rc;
-      pend[set][c.k].n = c.n;
-    };
     int off = 0;
     for (int k = 0; k < C && off < R; ++k) {
       const int cap = part[k + 1] - part[k];
@@ -1513,62 +1451,46 @@ void run_host_shard(clipgpu_engine& e, Replica& r, InKind kind, const void* in, 
       const int64_t rc = c0 + off;
       drain(set, k);  // this set's round before last: its D2H (so also its H2D and forward) done
       hipStream_t st = r.lane[k % L] ? r.lane[k % L] : r.stream;
-      char* din = in_base + (size_t)part[k] * in_row_bytes;
-      float* dout = (set && d2h_side ? r.out2 : r.out) + (size_t)part[k] * E;
-      const char* src = (const char*)in + rc * in_row_bytes;
-      if (!direct_in) {
-        char* pin = pin_in_base + (size_t)part[k] * in_row_bytes;
-        par_memcpy(pin, src, (size_t)n * in_row_bytes);
-        src = pin;
-      }
-      const void* mapped = nullptr;
-      if (e.host_copy_stream == 3 && direct_in &&
-          hipHostGetDevicePointer((void**)&mapped, (void*)src, 0) != hipSuccess) {
-        (void)hipGetLastError();
-        mapped = nullptr;
-      }
-      if (mapped != nullptr && (((uintptr_t)src | (uintptr_t)din | ((size_t)n * in_row_bytes)) & 15) == 0) {
-        // test hook: pull the chunk through the host mapping with a copy kernel on the copy stream
-        check(launch_pull_copy(mapped, din, (size_t)n * in_row_bytes, r.copy), "pull copy");
-        HIP_CHECK(hipEventRecord(copied[k], r.copy));
-      } else if (e.host_copy_stream == 2 && n >= 2) {  // test hook: the chunk's halves on two copy streams
-        const size_t h = (size_t)(n / 2) * in_row_bytes, all = (size_t)n * in_row_bytes;
-        HIP_CHECK(hipStreamWaitEvent(r.copy2, copied[(k + C - 1) % C], 0));  // chunk order kept
-        HIP_CHECK(hipMemcpyAsync(din, src, h, hipMemcpyHostToDevice, r.copy));
-        HIP_CHECK(hipMemcpyAsync(din + h, src + h, all - h, hipMemcpyHostToDevice, r.copy2));
-        HIP_CHECK(hipEventRecord(copied[k], r.copy2));
-        HIP_CHECK(hipStreamWaitEvent(r.copy, copied[k], 0));
-        HIP_CHECK(hipEventRecord(copied[k], r.copy));
-      } else if (e.host_copy_stream) {
-        HIP_CHECK(hipMemcpyAsync(din, src, (size_t)n * in_row_bytes, hipMemcpyHostToDevice, r.copy));
-        HIP_CHECK(hipEventRecord(copied[k], r.copy));
+      char* din = in_base + (size_t)part[k] * rb;
+      float* dout = (set ? r.out2 : r.out) + (size_t)part[k] * E;
+      if (direct_in) {
+        HIP_CHECK(hipMemcpyAsync(din, src.in + rc * rb, (size_t)n * rb, hipMemcpyHostToDevice, r.copy));
       } else {
-        HIP_CHECK(hipMemcpyAsync(din, src, (size_t)n * in_row_bytes, hipMemcpyHostToDevice, st));
+        char* pin = pin_in_base + (size_t)part[k] * rb;
+        for (int p0 = 0; p0 < n; p0 += rows_per_piece) {
+          const int pn = std::min(rows_per_piece, n - p0);
+          char* pp = pin + (size_t)p0 * rb;
+          if (src.rows) pool_gather(pp, src.rows + rc + p0, rb, pn);
+          else pool_memcpy(pp, src.in + (rc + p0) * rb, (size_t)pn * rb);
+          HIP_CHECK(hipMemcpyAsync(din + (size_t)p0 * rb, pp, (size_t)pn * rb, hipMemcpyHostToDevice, r.copy));
+        }
       }
-      ch[nch] = {k, n, rc, din, dout, st};
-      if (!lockstep && !fused) issue_forward(ch[nch], k);
-      ++nch;
-      off += n;
-    }
-    if (lockstep && !fused)
-      for (int i = 0; i < nch; ++i) issue_forward(ch[i], ch[nch - 1].k);
-    if (fused && nch > 0) {  // (test hook, host_flags bit 3) the round as one device-path forward
-      hipStream_t st = r.stream;
-      HIP_CHECK(hipStreamWaitEvent(st, copied[ch[nch - 1].k], 0));
-      // the previous round (its D2H) is done before this round's graph reuses the workspace
-      for (int j = 0; j < C; ++j)
-        if (pend[set ^ 1][j].c0 >= 0) HIP_CHECK(hipStreamWaitEvent(st, done_set[set ^ 1][j], 0));
+      HIP_CHECK(hipEventRecord(copied[k], r.copy));
+      HIP_CHECK(hipStreamWaitEvent(st, copied[k], 0));
+      const Replica v = lane_view(e, r, part[k]);
       run_graph(e, r,
-                {(uint64_t)(30 + kind), (uint64_t)R, fbits(mean, 0), fbits(mean, 1), fbits(mean, 2), fbits(stdv, 0),
-                 fbits(stdv, 1), fbits(stdv, 2), (uint64_t)set},
+                {(uint64_t)(10 + kind), (uint64_t)k, (uint64_t)n, fbits(mean, 0), fbits(mean, 1), fbits(mean, 2),
+                 fbits(stdv, 0), fbits(stdv, 1), fbits(stdv, 2), (uint64_t)tokens, (uint64_t)part[k], (uint64_t)set,
+                 (uint64_t)(uintptr_t)dout},
                 st, [&](hipStream_t gs) {
-                  vision_forward_lanes(e, r, in_base, kind == IN_F32 ? A_IMG_F32 : A_IMG_U8, mean, stdv, R, r.out, gs);
+                  if (kind == IN_IDS)
+                    text_forward(e, v, (const int64_t*)din, n, dout, gs, tokens);
+                  else
+                    vision_forward(e, v, din, kind == IN_F32 ? A_IMG_F32 : A_IMG_U8, mean, stdv, n, dout, gs);
                 });
-      float* dst = direct_out ? out + c0 * E : pin_out_set[set];
-      HIP_CHECK(hipMemcpyAsync(dst, r.out, (size_t)R * E * 4, hipMemcpyDeviceToHost, st));
-      HIP_CHECK(hipEventRecord(done[0], st));
-      pend[set][0].c0 = c0;
-      pend[set][0].n = R;
+      float* dst = direct_out ? out + rc * E : pin_out_set[set] + (size_t)part[k] * E;
+      if (two_sets) {  // the forward's end, then the D2H on the second copy stream
+        HIP_CHECK(hipEventRecord(done[k], st));
+        HIP_CHECK(hipStreamWaitEvent(r.copy2, done[k], 0));
+        HIP_CHECK(hipMemcpyAsync(dst, dout, (size_t)n * E * 4, hipMemcpyDeviceToHost, r.copy2));
+        HIP_CHECK(hipEventRecord(done[k], r.copy2));
+      } else {
+        HIP_CHECK(hipMemcpyAsync(dst, dout, (size_t)n * E * 4, hipMemcpyDeviceToHost, st));
+        HIP_CHECK(hipEventRecord(done[k], st));
+      }
+      pend[set][k].c0 = rc;
+      pend[set][k].n = n;
+      off += n;
     }
     c0 += R;
   }
@@ -1576,11 +1498,11 @@ void run_host_shard(clipgpu_engine& e, Replica& r, InKind kind, const void* in, 
     for (int k = 0; k < C; ++k) drain(set, k);
 }
 
-void run_host(clipgpu_engine& e, InKind kind, const void* in, size_t in_row_bytes, int64_t B, const float* mean,
-              const float* stdv, float* out, int tokens = 0) {
+void run_host(clipgpu_engine& e, InKind kind, const HostRows& src, int64_t B, const float* mean, const float* stdv,
+              float* out, int tokens = 0) {
   const int G = (int)e.reps.size();
   if (G == 1) {
-    run_host_shard(e, e.reps[0], kind, in, in_row_bytes, 0, B, mean, stdv, out, tokens);
+    run_host_shard(e, e.reps[0], kind, src, 0, B, mean, stdv, out, tokens);
     return;
   }
   // Contiguous row blocks, rank order == input order.
@@ -1592,7 +1514,7 @@ void run_host(clipgpu_engine& e, InKind kind, const void* in, size_t in_row_byte
     if (b0 == b1) continue;
     th.emplace_back([&, g, b0, b1]() {
       try {
-        run_host_shard(e, e.reps[g], kind, in, in_row_bytes, b0, b1, mean, stdv, out, tokens);
+        run_host_shard(e, e.reps[g], kind, src, b0, b1, mean, stdv, out, tokens);
       } catch (const ClipErr& ex) {
         codes[g] = ex.code;
         errs[g] = ex.what();
@@ -1678,6 +1600,11 @@ void grow_device(P*& p, size_t& cap, size_t need) {
   cap = need;
 }
 
+// Chunks alternate over the lane slots; per chunk: the resize plans' tables and the source images are
+// packed into the slot's pinned staging by the copy pool, in pieces of whole images (kStagePiece) whose
+// H2Ds go on the copy stream as soon as each is packed (round 6; round 5 spawned std::threads per chunk
+// and ran the H2D on the lane stream), then on the lane: the resize kernels into the slot's u8 rows and
+// the u8 forward.  The packing of chunk j + 1 runs while chunk j transfers and computes.
 void run_images_shard(clipgpu_engine& e, Replica& r, const uint8_t* const* images, const int* W, const int* H,
                       int64_t b0, int64_t b1, float* out) {
   HIP_CHECK(hipSetDevice(r.device));
@@ -1703,37 +1630,39 @@ void run_images_shard(clipgpu_engine& e, Replica& r, const uint8_t* const* image
       ++n;
     }
     const int k = j % L;
-    drain(k);
+    drain(k);  // slot k's previous chunk (its H2D, resize, forward and D2H) is done
     hipStream_t st = r.lane[k] ? r.lane[k] : r.stream;
     const ResizeBatch b = plan_resize_batch(S, e.pre.interpolation, e.pre.resize_mode, W, H, c0, n);
     const size_t desc_bytes = align16(b.d.size() * sizeof(ResizeImage));
     const size_t ints_bytes = align16(b.ints.size() * sizeof(int));
-    const size_t total = desc_bytes + ints_bytes + b.raw_bytes;
+    const size_t head = desc_bytes + ints_bytes, total = head + b.raw_bytes;
     Replica::ImageSlot& sl = r.islot[k];
     grow_pinned(sl.pin, sl.pin_cap, total);
     grow_device(sl.dev, sl.dev_cap, total);
     grow_device(sl.tmp, sl.tmp_cap, std::max<size_t>(b.tmp_bytes, 16));
     std::memcpy(sl.pin, b.d.data(), b.d.size() * sizeof(ResizeImage));
     std::memcpy(sl.pin + desc_bytes, b.ints.data(), b.ints.size() * sizeof(int));
-    {  // pack the source images into pinned staging: images split over up to 8 copy threads
-      char* const raw_pin = sl.pin + desc_bytes + ints_bytes;
-      auto copy_range = [&](int i0, int i1) {
-        for (int i = i0; i < i1; ++i)
-          std::memcpy(raw_pin + b.raw_off[i], images[c0 + i], (size_t)W[c0 + i] * H[c0 + i] * 3);
-      };
-      const int nt = (int)std::min<size_t>({8, (size_t)n, std::max<size_t>(1, b.raw_bytes / (4u << 20))});
-      if (nt <= 1) {
-        if (n == 1) par_memcpy(raw_pin, images[c0], (size_t)W[c0] * H[c0] * 3);
-        else copy_range(0, n);
+    HIP_CHECK(hipMemcpyAsync(sl.dev, sl.pin, head, hipMemcpyHostToDevice, r.copy));
+    char* const raw_pin = sl.pin + head;
+    for (int i0 = 0; i0 < n;) {  // pieces of whole images
+      int i1 = i0 + 1;
+      while (i1 < n && b.raw_off[i1] - b.raw_off[i0] < kStagePiece) ++i1;
+      const size_t p0 = b.raw_off[i0], p1 = i1 < n ? b.raw_off[i1] : b.raw_bytes;
+      if (i1 - i0 == 1) {
+        pool_memcpy(raw_pin + p0, images[c0 + i0], (size_t)W[c0 + i0] * H[c0 + i0] * 3);
       } else {
-        std::vector<std::thread> th;
-        for (int t = 0; t < nt; ++t) th.emplace_back(copy_range, n * t / nt, n * (t + 1) / nt);
-        for (auto& t : th) t.join();
+        CopyPool::instance().run(i1 - i0, [&](int t) {
+          const int i = i0 + t;
+          std::memcpy(raw_pin + b.raw_off[i], images[c0 + i], (size_t)W[c0 + i] * H[c0 + i] * 3);
+        });
       }
+      HIP_CHECK(hipMemcpyAsync(sl.dev + head + p0, raw_pin + p0, p1 - p0, hipMemcpyHostToDevice, r.copy));
+      i0 = i1;
     }
-    HIP_CHECK(hipMemcpyAsync(sl.dev, sl.pin, total, hipMemcpyHostToDevice, st));
+    HIP_CHECK(hipEventRecord(r.copied[k], r.copy));
+    HIP_CHECK(hipStreamWaitEvent(st, r.copied[k], 0));
     uint8_t* din = (uint8_t*)r.in + (size_t)k * rows * e.in_bytes_per_row;  // u8 [n][S][S][3]
-    check(launch_resize((const uint8_t*)sl.dev + desc_bytes + ints_bytes, sl.tmp, (const int*)(sl.dev + desc_bytes),
+    check(launch_resize((const uint8_t*)sl.dev + head, sl.tmp, (const int*)(sl.dev + desc_bytes),
                         (const ResizeImage*)sl.dev, n, b.max_th, S, din, st), "resize");
     float* dout = r.out + (size_t)k * rows * E;
     const Replica v = lane_view(e, r, k * rows);
@@ -2148,7 +2077,7 @@ int clipgpu_embed_pixels(clipgpu_engine* e, const float* nchw, int64_t B, int64_
     if (S != e->spec.image_size)
       throw ClipErr(CLIPGPU_ERR_INVALID, "Shape error: expected image size " + std::to_string(e->spec.image_size));
     std::lock_guard<std::mutex> lk(e->mu);
-    run_host(*e, IN_F32, nchw, (size_t)3 * S * S * 4, B, nullptr, nullptr, out);
+    run_host(*e, IN_F32, HostRows{(const char*)nchw, nullptr, (size_t)3 * S * S * 4}, B, nullptr, nullptr, out);
   });
 }
 
@@ -2161,7 +2090,7 @@ int clipgpu_embed_u8(clipgpu_engine* e, const uint8_t* nhwc, int64_t B, int64_t 
     if (S != e->spec.image_size)
       throw ClipErr(CLIPGPU_ERR_INVALID, "Shape error: expected image size " + std::to_string(e->spec.image_size));
     std::lock_guard<std::mutex> lk(e->mu);
-    run_host(*e, IN_U8, nhwc, (size_t)3 * S * S, B, mean, stdv, out);
+    run_host(*e, IN_U8, HostRows{(const char*)nhwc, nullptr, (size_t)3 * S * S}, B, mean, stdv, out);
   });
 }
 
@@ -2174,6 +2103,16 @@ int clipgpu_host_register(void* ptr, size_t bytes) {
     for (const auto& rg : h.r)
       if (a < rg.first + rg.second && rg.first < a + bytes)
         throw ClipErr(CLIPGPU_ERR_INVALID, "host range overlaps a registered one");
+    // hipHostRegister pins whole pages: two ranges that share a page would pin it twice, and unregistering
+    // one would unpin it under the other (and leave the runtime's page mapping stale for whatever the
+    // allocator puts there next).  Such a range is refused; page-owning buffers (engine.py host_buffer)
+    // never share one.
+    const uintptr_t pg = (uintptr_t)kHostPage;
+    for (const auto& rg : h.r)
+      if (a / pg <= (rg.first + rg.second - 1) / pg && rg.first / pg <= (a + bytes - 1) / pg)
+        throw ClipErr(CLIPGPU_ERR_INVALID,
+                      "host range shares a memory page with a registered one (registration pins whole pages): "
+                      "register page-aligned buffers");
     HIP_CHECK(hipHostRegister(ptr, bytes, hipHostRegisterMapped | hipHostRegisterPortable));  // every device
     h.r.emplace_back(a, bytes);
   });
@@ -2236,7 +2175,7 @@ int clipgpu_embed_tokens(clipgpu_engine* e, const int64_t* ids, const int64_t* m
       src = trimmed.data();
     }
     std::lock_guard<std::mutex> lk(e->mu);
-    run_host(*e, IN_IDS, src, (size_t)Tc * 8, B, nullptr, nullptr, out, (int)Tc);
+    run_host(*e, IN_IDS, HostRows{(const char*)src, nullptr, (size_t)Tc * 8}, B, nullptr, nullptr, out, (int)Tc);
   });
 }
 
@@ -2282,6 +2221,22 @@ int clipgpu_embed_images_rgb8(clipgpu_engine* e, const uint8_t* const* images, c
       if (widths[i] <= 0 || heights[i] <= 0) throw ClipErr(CLIPGPU_ERR_INVALID, "Resize error: empty image");
     }
     std::lock_guard<std::mutex> lk(e->mu);
+    // A batch of S x S images needs no resize (the plan is the identity: a unit tap per output, exact) --
+    // the images are the u8 NHWC rows, and the batch takes the u8 host path (copy pool staging in pieces,
+    // copy-stream H2Ds, alternating buffer sets), bit-identical to the resize path
+    // (test_embed_images_rgb8_identity_batches_take_the_u8_path).
+    const int S = e->spec.image_size;
+    bool identity = true;
+    for (int64_t i = 0; i < n && identity; ++i) identity = widths[i] == S && heights[i] == S;
+    if (identity) {
+      const ResizePlan p = make_resize_plan(S, S, S, e->pre.interpolation, e->pre.resize_mode);
+      identity = !p.need_h && !p.need_v;
+    }
+    if (identity && !e->rgb8_resize_always) {
+      run_host(*e, IN_U8, HostRows{nullptr, (const void* const*)images, (size_t)3 * S * S}, n, e->pre.mean,
+               e->pre.stdv, out);
+      return;
+    }
     run_sharded(*e, n, [&](Replica& r, int64_t b0, int64_t b1) {
       run_images_shard(*e, r, images, widths, heights, b0, b1, out);
     });
@@ -2520,12 +2475,9 @@ int clipgpu_test_host_plan(clipgpu_engine* e, int n_chunks, const int* bounds, i
   return guarded([&]() {
     if (!e) throw ClipErr(CLIPGPU_ERR_INVALID, "engine is NULL");
     std::lock_guard<std::mutex> lk(e->mu);
-    if (copy_stream < 0 || (copy_stream & 15) > 3 || copy_stream >= 512)
-      throw ClipErr(CLIPGPU_ERR_INVALID,
-                    "copy_stream: 0 .. 3, + 16 (lockstep rounds), + 32 (D2H on the copy stream), + 64 (joined rounds), "
-                    "+ 128 (device-path rounds), + 256 (D2H on the lane streams)");
-    e->host_copy_stream = copy_stream & 15;
-    e->host_flags = copy_stream >> 4;
+    // (copy_stream: the schedule variants of rounds 3-5 were removed in round 6; 0 and 1 both mean the one
+    // schedule run_host_shard has)
+    if (copy_stream != 0 && copy_stream != 1) throw ClipErr(CLIPGPU_ERR_INVALID, "copy_stream: 0 or 1");
     e->host_part.clear();
     if (n_chunks == 0) return;
     if (n_chunks < 1 || n_chunks > 4 || !bounds) throw ClipErr(CLIPGPU_ERR_INVALID, "1..4 chunks");
@@ -2537,6 +2489,14 @@ int clipgpu_test_host_plan(clipgpu_engine* e, int n_chunks, const int* bounds, i
     }
     part.push_back(e->max_batch);
     e->host_part = part;
+  });
+}
+
+int clipgpu_test_rgb8_resize_always(clipgpu_engine* e, int on) {
+  return guarded([&]() {
+    if (!e) throw ClipErr(CLIPGPU_ERR_INVALID, "engine is NULL");
+    std::lock_guard<std::mutex> lk(e->mu);
+    e->rgb8_resize_always = on != 0;
   });
 }
 

@@ -10,22 +10,23 @@
 // The patch-embedding conv runs as a row GEMM over the patch rows staged by
 // launch_patch_rows (patch.hip), with the EPI_PATCH epilogue.
 //
-// One kernel template, three tile shapes (GemmTile):
-//   128x128  4 waves (2x2, 64x64 per wave), 64 KiB LDS, 2 blocks / CU
-//   256x128  8 waves (4x2, 64x64 per wave), 96 KiB LDS
-//   256x256  8 waves (2x4, 128x64 per wave), 128 KiB LDS
+// Two kernels (GemmTile, kernels.hpp):
+//   gemm_pipe_kernel    software-pipelined persistent tiles (K >= 128): 160x128, 256x128, 256x256,
+//                       192x256, 224x192 (4 or 8 waves), LDS-DMA staged, 2 or 3 LDS stages
+//   gemm_skinny_kernel  one wave per 16x16 output block, operands streamed from L2: M <= 256
+//                       (the pruned last layer, the heads), and in its general form every shape
+//                       the pipelined kernel does not take (K = 64, unaligned 16-bit rows)
 // Each wave issues v_mfma_f32_16x16x32_{bf16,f16} (f32 accumulate).  Operand
 // tiles (BK = 64) are staged global->LDS by global_load_lds_dwordx4 into a
 // lane-linear image with the XOR swizzle applied on the SOURCE address and on
-// the ds_read_b128 address (cdna_hip_programming.md §5.4 rule 21),
-// double-buffered: the next K-tile's loads are issued before the current one's
-// MFMAs, one vmcnt(0) + barrier per K-step.  Block ids are remapped
-// XCD-aware, then grouped 8 row-panels at a time for L2 reuse.  Persistent:
-// the grid is the resident block count and each block walks its tiles, the
-// next tile's first K-slice staged under the current tile's last K-step.  MFMA
-// operands are swapped so each lane owns 4 consecutive output columns (8 / 16 B
+// the ds_read_b128 address (cdna_hip_programming.md §5.4 rule 21).  Block ids are
+// remapped XCD-aware, then grouped row-panels at a time for L2 reuse.  Persistent:
+// the grid is the resident block count and each block walks its tiles.  MFMA
+// operands are swapped so each lane owns consecutive output columns (16-byte
 // epilogue stores).  M and N tails: clamped source rows + masked stores; K must
-// be a multiple of 64.
+// be a multiple of 64.  Every kernel and tile runs the same MFMA chain per output
+// element in the same K order with the same epilogue float ops, so the tile choice
+// never changes the bits.
 #include <algorithm>
 #include <cstdlib>
 #include <type_traits>
@@ -106,339 +107,6 @@ constexpr int BK = 64;
 template <typename T>
 __device__ __forceinline__ T to16(float v) { return (T)v; }
 
-template <typename T, int BM, int BN, int WGM, int WGN, int EPI, int ACT>
-__global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p) {
-  typedef typename Vec8<T>::type V8;
-  constexpr bool LNF = epi_lnf(EPI);
-  static_assert(!LNF || std::is_same<T, _Float16>::value, "LayerNorm fold: f16 operands");
-  typedef typename std::conditional<EPI == EPI_LNF_BF, __bf16, T>::type OT;  // 16-bit output type
-  typedef typename Vec4<OT>::type V4;
-  constexpr int NW = WGM * WGN;
-  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
-  constexpr int A_INSTR = BM / 8 / NW, B_INSTR = BN / 8 / NW;  // 1 KiB glds per wave-instruction
-  constexpr int TM = BM / WGM, TN = BN / WGN, MI = TM / 16, NI = TN / 16;
-  static_assert(A_INSTR >= 1 && B_INSTR >= 1 && MI >= 1 && NI >= 1, "bad tile");
-  // 2 x 256 f32 (tile-parity double buffer) of bias (+ EPI_LNF: of column sums, 2 KiB further on, and
-  // of the tile's row statistics, 2 x SROWP after those)
-  constexpr int SROWP = LNF ? (BM * 8 + 1023) / 1024 * 1024 : 0;
-  constexpr int BIAS_BYTES = LNF ? 4096 + 2 * SROWP : 2048;
-  static_assert(BN <= 256, "bias slice is one 1 KiB DMA");
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + BIAS_BYTES];
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int nTn = (p.N + BN - 1) / BN;
-  const int grp = p.group > 0 ? p.group : CLIPGPU_TILE_GROUP;
-  const int nTm = (p.M + BM - 1) / BM;
-  const int ntiles = nTn * nTm;
-  const int nk = p.K / BK;
-
-  // Persistent schedule: the grid is <= the resident block count.  With a grid
-  // that is a multiple of 8, XCD x (blocks b = x mod 8) walks a contiguous range
-  // of tiles; otherwise every block owns one tile (grid == ntiles).
-  const int nb = gridDim.x;
-  int t_first, t_stride, t_end;
-  if (nb % 8 == 0 && nb < ntiles) {
-    const int x = blockIdx.x & 7, nbx = nb >> 3;
-    const int q = ntiles >> 3, r = ntiles & 7;
-    const int start = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
-    t_first = start + (blockIdx.x >> 3);
-    t_stride = nbx;
-    t_end = start + q + (x < r ? 1 : 0);
-  } else {
-    t_first = xcd_remap(blockIdx.x, nb);
-    t_stride = ntiles;  // single tile
-    t_end = t_first + 1;
-  }
-  if (t_first >= t_end) return;
-
-  char* const sA0 = smem;
-  char* const sB0 = smem + A_BYTES;
-  char* const sA1 = smem + STAGE;
-  char* const sB1 = smem + STAGE + A_BYTES;
-
-  // ---- per-tile staging sources ----------------------------------------------
-  // glds: wave w, instruction i writes rows (w*INSTR + i)*8 .. +7 (1 KiB); lane
-  // l lands at row +(l>>3), slot (l&7), which holds global chunk slot ^ f(row).
-  // Per-lane 32-bit BYTE offsets from the (wave-uniform) kernel-argument base
-  // pointers: the DMA then uses the SGPR-base + VGPR-offset form with these
-  // persistent registers as the offset -- no per-issue address temporaries, whose
-  // reuse by the asm ds_read destinations made hipcc drain vmcnt(0) (host
-  // checks that every operand fits in 2^31 bytes).
-  uint32_t woff[B_INSTR];
-  uint32_t aoff[A_INSTR];
-  const char* const Wb = (const char*)p.W;
-  const char* const Ab = (const char*)p.A;
-  auto set_tile = [&](int m0, int n0) {
-#pragma unroll
-    for (int i = 0; i < B_INSTR; ++i) {
-      const int r = (wave * B_INSTR + i) * 8 + (lane >> 3);
-      const int c = (lane & 7) ^ ((r >> 1) & 7);
-      woff[i] = (uint32_t)(min(n0 + r, p.N - 1) * (int)p.ldw + c * 8) * 2u;
-    }
-#pragma unroll
-    for (int i = 0; i < A_INSTR; ++i) {
-      const int r = (wave * A_INSTR + i) * 8 + (lane >> 3);
-      const int c = (lane & 7) ^ ((r >> 1) & 7);
-      aoff[i] = (uint32_t)(min(m0 + r, p.M - 1) * (int)p.lda + c * 8) * 2u;
-    }
-  };
-
-  auto stage_w = [&](int kt, char* sB) {
-    const char* const base = Wb + (size_t)kt * (BK * 2);
-#pragma unroll
-    for (int i = 0; i < B_INSTR; ++i) glds16(base + woff[i], sB + (wave * B_INSTR + i) * 1024);
-  };
-  auto stage_a_rows = [&](int kt, char* sA) {
-    const char* const base = Ab + (size_t)kt * (BK * 2);
-#pragma unroll
-    for (int i = 0; i < A_INSTR; ++i) glds16(base + aoff[i], sA + (wave * A_INSTR + i) * 1024);
-  };
-
-  // Issue the loads of K-step kt of the current tile into buffer (sA, sB).
-  auto stage = [&](int kt, char* sA, char* sB) {
-    stage_w(kt, sB);
-    stage_a_rows(kt, sA);
-  };
-  // The tile's bias slice bias[n0 .. n0+255] goes to LDS by one 1 KiB DMA
-  // (wave 0, with the tile's first K-step), so the epilogue needs no global load
-  // (which, issued after the next tile's DMA, would wait for it: vmcnt is in order).
-  auto stage_bias = [&](int m0s, int n0, int par) {
-    if (p.bias != nullptr && wave == 0) {
-      const int n = min(n0 + lane * 4, ((p.N - 1) / 4) * 4);  // clamped in-bounds 16 B (N % 4 == 0 checked)
-      glds16(p.bias + n, smem + 2 * STAGE + par * 1024);
-      if constexpr (LNF) {
-        glds16(p.cs + n, smem + 2 * STAGE + 2048 + par * 1024);
-#pragma unroll
-        for (int i = 0; i < SROWP / 1024; ++i)
-          glds16(p.rowstats + (size_t)m0s * 2 + i * 256 + lane * 4, smem + 2 * STAGE + 4096 + par * SROWP + i * 1024);
-      }
-    }
-  };
-
-  // ---- fragment addressing -------------------------------------------------
-  const int wm = (wave / WGN) * TM, wn = (wave % WGN) * TN;
-  const int fr = lane & 15, fq = lane >> 4;
-  int offA[2], offB[2];
-#pragma unroll
-  for (int kk = 0; kk < 2; ++kk) {
-    const int sw = ((kk * 4 + fq) ^ (fr >> 1)) << 4;  // rows are 16-aligned + fr
-    offA[kk] = (wm + fr) * 128 + sw;
-    offB[kk] = (wn + fr) * 128 + sw;
-  }
-
-  // Operands swapped (W rows as the MFMA "A" operand): acc[ni][mi][j] =
-  // C[m = wm + mi*16 + fr][n = wn + ni*16 + fq*4 + j], i.e. each lane owns 4
-  // consecutive output columns of one row -> 8 / 16-byte epilogue stores.
-  f32x4 acc[NI][MI];
-  const uint32_t lds0 = lds_addr(smem);
-  auto mfma_block = [&](auto zero, const V8(&a)[MI], const V8(&b)[NI]) {
-#pragma unroll
-    for (int ni = 0; ni < NI; ++ni)
-#pragma unroll
-      for (int mi = 0; mi < MI; ++mi)
-        acc[ni][mi] = mfma_16x16x32(b[ni], a[mi], decltype(zero)::value ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[ni][mi]);
-  };
-  // zero: the first K-step of a tile starts the MFMA chain from C = 0 (no
-  // accumulator re-zeroing between tiles).
-  auto compute = [&](auto zero, const char* sA, const char* sB) {
-    // Fragment reads in inline asm (invisible to hipcc's waitcnt pass, which
-    // would otherwise drain vmcnt(0) -- including the previous tile's epilogue
-    // stores -- in front of them); the kk = 1 reads fly under the kk = 0 MFMAs.
-    const uint32_t aB = lds0 + (uint32_t)(sA - smem), bB = lds0 + (uint32_t)(sB - smem);
-    V8 a0[MI], b0[NI], a1[MI], b1[NI];
-    static_for<NI>([&](auto ni) { ds_read_b128<(int)ni * 2048>(b0[ni], bB + offB[0]); });
-    static_for<MI>([&](auto mi) { ds_read_b128<(int)mi * 2048>(a0[mi], aB + offA[0]); });
-    lgkm_wait_all(a0, b0);
-    // kk = 0 MFMAs row block by row block; a1[mi] is read into the registers
-    // a0[mi] just released, b1 after the last kk = 0 MFMA (48 fragment VGPRs, not 96).
-    static_for<MI>([&](auto mi) {
-#pragma unroll
-      for (int ni = 0; ni < NI; ++ni)
-        acc[ni][mi] = mfma_16x16x32(b0[ni], a0[mi], decltype(zero)::value ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[ni][mi]);
-      __builtin_amdgcn_sched_barrier(0);
-      ds_read_b128<(int)mi * 2048>(a1[mi], aB + offA[1]);
-    });
-    static_for<NI>([&](auto ni) { ds_read_b128<(int)ni * 2048>(b1[ni], bB + offB[1]); });
-    lgkm_wait_all(a1, b1);
-    mfma_block(std::false_type{}, a1, b1);
-  };
-
-  // XE: the residual stream's element type (EPI_RESID16 / EPI_PATCH16: f16, else f32)
-  auto epilogue = [&](int m0, int n0, int bpar) {
-    typedef typename std::conditional<epi_x16(EPI), _Float16, float>::type XE;
-    const int G2 = p.G * p.G;
-    // EPI_RESID: the residual rows of column block ni+1 are loaded before block ni
-    // is stored, so no load waits behind this epilogue's own stores.
-    float4 xr[2][MI];
-    auto load_x = [&](int ni, float4 (&dst)[MI]) {
-      const int n = n0 + wn + ni * 16 + fq * 4;
-#pragma unroll
-      for (int mi = 0; mi < MI; ++mi) {
-        const int m = m0 + wm + mi * 16 + fr;
-        if (m < p.M && n + 4 <= p.N) dst[mi] = ldx4((const XE*)p.out + (long)m * p.ldo + n);
-      }
-    };
-    if constexpr (epi_resid(EPI)) load_x(0, xr[0]);
-    f32x2 rst[MI];  // EPI_LNF: (mean, rstd) of the lane's rows
-    if constexpr (LNF) {
-      const uint32_t sa = lds0 + 2 * STAGE + 4096 + bpar * SROWP + (wm + fr) * 8;
-      static_for<MI>([&](auto mi) { ds_read_b64<(int)mi * 128>(rst[mi], sa); });
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-      for (int mi = 0; mi < MI; ++mi) asm volatile("" : "+v"(rst[mi]));
-    }
-#pragma unroll
-    for (int ni = 0; ni < NI; ++ni) {
-      if constexpr (epi_resid(EPI)) {
-        if (ni + 1 < NI) load_x(ni + 1, xr[(ni + 1) & 1]);
-      }
-      const int n = n0 + wn + ni * 16 + fq * 4;
-      const bool nfull = n + 4 <= p.N;
-      float bv[4] = {0.f, 0.f, 0.f, 0.f}, cv[4] = {0.f, 0.f, 0.f, 0.f};
-      if (p.bias != nullptr) {
-        f32x4 b4, c4;
-        ds_read_b128<0>(b4, lds0 + 2 * STAGE + bpar * 1024 + (wn + ni * 16 + fq * 4) * 4);
-        if constexpr (LNF) ds_read_b128<2048>(c4, lds0 + 2 * STAGE + bpar * 1024 + (wn + ni * 16 + fq * 4) * 4);
-        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(b4)::"memory");
-        if constexpr (LNF) asm volatile("" : "+v"(c4));
-#pragma unroll
-        for (int j = 0; j < 4; ++j) bv[j] = b4[j];
-        if constexpr (LNF) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) cv[j] = c4[j];
-        }
-      }
-#pragma unroll
-      for (int mi = 0; mi < MI; ++mi) {
-        const int m = m0 + wm + mi * 16 + fr;
-        if (m >= p.M) continue;
-        float v[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          v[j] = LNF ? lnf_out(acc[ni][mi][j], rst[mi][0], rst[mi][1], cv[j], bv[j]) : acc[ni][mi][j] + bv[j];
-#ifdef CLIPGPU_GEMM_STAMPS
-        if (p.diag & 1) {  // timing experiment: same arithmetic, no store
-          float s = 0.f;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) s += EPI == EPI_STORE16 ? (float)to16<T>(apply_act<ACT>(v[j])) : v[j];
-          if (s == 12345.678f) ((float*)p.out)[0] = s;
-          continue;
-        }
-#endif
-        if constexpr (epi_st16(EPI)) {
-          OT* o = (OT*)p.out + (long)m * p.ldo + n;
-          if (nfull) {
-            V4 w;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) w[j] = to16<OT>(apply_act<ACT>(v[j]));
-            *(V4*)o = w;
-          } else {
-            for (int j = 0; j < 4; ++j)
-              if (n + j < p.N) o[j] = to16<OT>(apply_act<ACT>(v[j]));
-          }
-        } else {
-          XE* o;  // (EPI_STORE32: f32 output)
-          const float* ps = nullptr;
-          if constexpr (epi_patch(EPI)) {
-            const int b = m / G2, pp = m - b * G2;
-            o = (XE*)p.out + ((long)b * (G2 + p.cls) + p.cls + pp) * p.ldo + n;
-            ps = p.pos + (long)(p.cls + pp) * p.N + n;
-          } else {
-            o = (XE*)p.out + (long)m * p.ldo + n;
-          }
-          if (nfull) {
-            float4 w = make_float4(v[0], v[1], v[2], v[3]);
-            if constexpr (epi_resid(EPI)) {
-              const float4 x = xr[ni & 1][mi];
-              w.x += x.x; w.y += x.y; w.z += x.z; w.w += x.w;
-            } else if constexpr (epi_patch(EPI)) {
-              const float4 x = *(const float4*)ps;
-              w.x += x.x; w.y += x.y; w.z += x.z; w.w += x.w;
-            }
-            stx4(o, w);
-          } else {
-            for (int j = 0; j < 4; ++j) {
-              if (n + j >= p.N) continue;
-              float r = v[j];
-              if constexpr (epi_resid(EPI)) r += (float)o[j];
-              if constexpr (epi_patch(EPI)) r += ps[j];
-              o[j] = (XE)r;
-            }
-          }
-        }
-      }
-    }
-  };
-
-  // ---- persistent tile loop: 2-stage K pipeline, next tile's first K-step
-  //      prefetched under the current tile's last K-step and epilogue ----------
-  int m0, n0;
-  GEMM_STAMP_REAL(62);
-  GEMM_STAMP(0);
-  tile_coords(t_first, nTm, nTn, BM, BN, m0, n0, grp);
-  set_tile(m0, n0);
-  stage(0, sA0, sB0);
-  stage_bias(m0, n0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
-  // Step barrier: wait only for this K-step's glds and use a raw s_barrier (a
-  // __syncthreads() fence would also drain the epilogue stores).
-  auto step_sync = [&]() {
-    vm_wait<0>();  // only this K-step's glds are outstanding here
-    __builtin_amdgcn_s_barrier();
-  };
-
-  int parity = 0;    // buffer holding K-step 0 of the current tile
-  int bias_par = 0;  // LDS bias buffer of the current tile
-  GEMM_STAMP(1);
-  int ti = 0;  // (stamps) tile index of this block
-  for (int t = t_first; t < t_end; t += t_stride, ++ti) {
-    GEMM_STAMP(2 + ti * 4);
-    for (int kt = 0; kt + 1 < nk; ++kt) {
-      const bool cur1 = (kt & 1) ^ parity;
-      char* const sAn = cur1 ? sA0 : sA1;
-      char* const sBn = cur1 ? sB0 : sB1;
-      stage(kt + 1, sAn, sBn);
-      if (kt == 0) compute(std::true_type{}, cur1 ? sA1 : sA0, cur1 ? sB1 : sB0);
-      else compute(std::false_type{}, cur1 ? sA1 : sA0, cur1 ? sB1 : sB0);
-      step_sync();
-      if (ti == 0 && 34 + kt < 61) GEMM_STAMP(34 + kt);  // (slots 61-63: HW_ID, realtime)
-    }
-    GEMM_STAMP(3 + ti * 4);
-    // last K-step: prefetch the next tile's first K-step under it and the epilogue
-    const bool cur1 = ((nk - 1) & 1) ^ parity;
-    const int tn = t + t_stride;
-    const bool has_next = tn < t_end;
-    int nm0 = m0, nn0 = n0;
-    if (has_next) {
-      tile_coords(tn, nTm, nTn, BM, BN, nm0, nn0, grp);
-      set_tile(nm0, nn0);
-      stage(0, cur1 ? sA0 : sA1, cur1 ? sB0 : sB1);
-      stage_bias(nm0, nn0, bias_par ^ 1);
-    }
-    if (nk == 1) compute(std::true_type{}, cur1 ? sA1 : sA0, cur1 ? sB1 : sB0);
-    else compute(std::false_type{}, cur1 ? sA1 : sA0, cur1 ? sB1 : sB0);
-    GEMM_STAMP(4 + ti * 4);
-    vm_wait<0>();  // the next tile's stage 0 lands before the epilogue's stores (see gemm_pipe_kernel)
-    epilogue(m0, n0, bias_par);
-    // Retire the next tile's stage-0 glds but not this tile's output stores
-    // (issued after them; in-order vmcnt): a full tile issues exactly MI*NI
-    // epilogue stores per lane, a partial one may issue fewer -> wait for all.
-    if (m0 + BM <= p.M && n0 + BN <= p.N) vm_wait<MI * NI>();
-    else vm_wait<0>();
-    __builtin_amdgcn_s_barrier();
-    GEMM_STAMP(5 + ti * 4);
-    parity ^= (nk & 1);
-    bias_par ^= 1;
-    m0 = nm0;
-    n0 = nn0;
-  }
-  GEMM_STAMP_REAL(63);
-}
-
 // ---------------------------------------------------------------------------
 // Software-pipelined GEMM for row-major A (the trunk GEMMs; K >= 128).
 //
@@ -452,8 +120,8 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
 //           holds g's fragments in registers before the barrier).
 // No fragment-read latency is exposed after a barrier and each DMA has a whole
 // K-step to land.  With >= 32 MFMAs per phase the DMA pieces are spread between
-// MFMA groups; the 128x128 tile (16 per phase, two blocks per CU) issues them
-// up front so the other block's MFMAs cover the issue cost.  The DMA cursor
+// MFMA groups; tiles with 16 per phase issue them up front so the other
+// block's MFMAs cover the issue cost.  The DMA cursor
 // runs on across the tiles of the persistent schedule.
 //
 // Output layout: the W (MFMA "A") fragment of column block ni, row i reads W
@@ -464,8 +132,8 @@ __global__ __launch_bounds__(WGM* WGN * 64, 2) void gemm_bt_kernel(GemmParams p)
 // sw(r) = (r & 2) | (bit (2 + log2 NI) of r) << 2, conflict-free for these
 // reads and independent of ni, so every fragment offset is an immediate.
 //
-// Configs: 128x128 (4 waves, 64x64 each, 2 blocks/CU), 256x128 (8 waves,
-// 4x2 of 64x64), 256x256 (8 waves, 128x64).  (A 4-wave 256x256 with 128x128 per wave
+// Configs: 160x128 (4 waves of 80x64, or 8 of 80x32), 256x128 (8 waves,
+// 4x2 of 64x64), 256x256 (8 waves, 128x64), 192x256, 224x192.  (A 4-wave 256x256 with 128x128 per wave
 // needs 256 accumulator AGPRs plus > 256 VGPRs and spills: not built.)
 // ---------------------------------------------------------------------------
 // NS: LDS stages.  2 = the schedule above.  3 (K-long GEMMs that fit in one round of blocks,
@@ -1053,12 +721,6 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
 
 // Persistent grids (the launchers below and gemm_grid use these, so the bench's per-site block counts
 // are the launches' own).
-inline int cfg_grid(int BM, int BN, int NW, int M, int N) {
-  const int ntiles = ((N + BN - 1) / BN) * ((M + BM - 1) / BM);
-  // resident blocks: one 8-wave block (96-128 KiB LDS) or two 4-wave blocks (64 KiB) per CU
-  const int resident = device_cus() * (NW == 4 ? 2 : 1);
-  return ntiles <= resident ? ntiles : resident;
-}
 // OCC: resident blocks per CU the tile's registers allow (4-wave tiles: up to 3 by LDS; 8-wave
 // tiles: 1, or 2 when built for 4 waves per SIMD).  2 LDS stages.
 constexpr int pipe_kocc(int NW, int OCC) { return NW == 8 ? (OCC >= 2 ? 2 : 1) : 2; }  // launch bounds' OCC
@@ -1084,13 +746,6 @@ inline bool half_round_applies(int M, int N) {
   return ok;
 }
 inline int grid_224(int M, int N) { return std::min(((N + 191) / 192) * ((M + 223) / 224), device_cus()); }
-
-template <typename T, int BM, int BN, int WGM, int WGN, int EPI, int ACT>
-hipError_t launch_cfg(const GemmParams& p, hipStream_t s) {
-  const int grid = cfg_grid(BM, BN, WGM * WGN, p.M, p.N);
-  gemm_launch(gemm_bt_kernel<T, BM, BN, WGM, WGN, EPI, ACT>, grid, WGM * WGN * 64, s, p);
-  return hipGetLastError();
-}
 
 template <typename T, int BM, int BN, int WGM, int WGN, int EPI, int ACT, int OCC = 3, int RS = 0>
 hipError_t launch_pipe(const GemmParams& p, hipStream_t s) {
@@ -1133,25 +788,33 @@ hipError_t launch_pipe_224(const GemmParams& p, hipStream_t s) {
 // and the K order of the MFMA chain are those of the tiled kernels, and the epilogue does the
 // same float ops, so every output element is bit-identical to theirs
 // (test_skinny_gemm_is_bit_exact, test_last_layer_pruning_is_bit_exact).
+//
+// GEN = 1 (U = 2) is the general form for the shapes the pipelined kernel does not take -- K = 64
+// (one K-step), 16-bit outputs whose row pitch is not a multiple of 8 elements -- at any M, with N
+// tails (clamped W rows, masked stores) and element stores where a row is not 4-aligned.  Round 6
+// removed the 128x128 "bt" kernel that used to take these shapes: its run-to-run wrong outputs
+// (one accumulator register of one lane quarter) were never root-caused, and this
+// form gives the pipelined tiles' bits by construction (test_general_gemm_is_bit_exact).
 constexpr int SKINNY_MAX_M = 256;
 constexpr int SKINNY_U = 8;
 
-template <typename T, int EPI, int ACT>
+template <typename T, int EPI, int ACT, int U = SKINNY_U, int GEN = 0>
 __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmParams p) {
   typedef typename Vec8<T>::type V8;
   constexpr bool LNF = epi_lnf(EPI);
   static_assert(!LNF || std::is_same<T, _Float16>::value, "LayerNorm fold: f16 operands");
+  static_assert(!epi_patch(EPI), "the patch GEMM always has K >= 128 (pipelined tiles)");
   typedef typename std::conditional<EPI == EPI_LNF_BF, __bf16, T>::type OT;  // 16-bit output type
-  constexpr int U = SKINNY_U;
   const int lane = threadIdx.x & 63;
-  const int wid = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int nTn = p.N >> 4;
-  const int tm = wid / nTn, tn = wid - tm * nTn;  // a block's 4 waves share the A rows
+  const long wid = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int nTn = GEN ? (p.N + 15) >> 4 : p.N >> 4;
+  const long tm = wid / nTn;
+  const int tn = (int)(wid - tm * nTn);  // a block's 4 waves share the A rows
   if (tm * 16 >= p.M) return;
   const int fr = lane & 15, fq = lane >> 4;
-  const int m = tm * 16 + fr;
+  const int m = (int)tm * 16 + fr;
   const T* a = (const T*)p.A + (long)min(m, p.M - 1) * p.lda + fq * 8;
-  const T* w = (const T*)p.W + (long)(tn * 16 + fr) * p.ldw + fq * 8;
+  const T* w = (const T*)p.W + (long)(GEN ? min(tn * 16 + fr, p.N - 1) : tn * 16 + fr) * p.ldw + fq * 8;
   const int nc = p.K >> 5;
   // three register batches of U k-chunks: the loads of batch i+2 are issued before the
   // MFMAs of batch i, so two batches of L2 / HBM latency are covered
@@ -1181,30 +844,55 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmParams p) {
   }
   if (m >= p.M) return;
   const int n = tn * 16 + fq * 4;
+  if (GEN && n >= p.N) return;
+  // GEN: whole, 4-aligned column groups take the vector loads / stores below (N % 4 == 0 and
+  // ldo % 4 == 0); the rest go element by element
+  const bool vec = !GEN || (n + 4 <= p.N && p.ldo % 4 == 0);
   f32x4 bias = {0.f, 0.f, 0.f, 0.f}, csv = {0.f, 0.f, 0.f, 0.f};
   f32x2 rst = {0.f, 0.f};
-  if (p.bias != nullptr) bias = *(const f32x4*)(p.bias + n);
+  if (p.bias != nullptr) {
+    if (!GEN || n + 4 <= p.N) bias = *(const f32x4*)(p.bias + n);
+    else
+      for (int j = 0; j < 4; ++j) bias[j] = n + j < p.N ? p.bias[n + j] : 0.f;
+  }
   if constexpr (LNF) {
-    csv = *(const f32x4*)(p.cs + n);
+    if (!GEN || n + 4 <= p.N) csv = *(const f32x4*)(p.cs + n);
+    else
+      for (int j = 0; j < 4; ++j) csv[j] = n + j < p.N ? p.cs[n + j] : 0.f;
     rst = *(const f32x2*)(p.rowstats + (long)m * 2);
   }
   float v[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) v[j] = LNF ? lnf_out(acc[j], rst[0], rst[1], csv[j], bias[j]) : acc[j] + bias[j];
   if constexpr (epi_st16(EPI)) {
-    typename Vec4<OT>::type o;
+    OT* o = (OT*)p.out + (long)m * p.ldo + n;
+    if (vec) {
+      typename Vec4<OT>::type ov;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) o[j] = to16<OT>(apply_act<ACT>(v[j]));
-    *(typename Vec4<OT>::type*)((OT*)p.out + (long)m * p.ldo + n) = o;
+      for (int j = 0; j < 4; ++j) ov[j] = to16<OT>(apply_act<ACT>(v[j]));
+      *(typename Vec4<OT>::type*)o = ov;
+    } else {
+      for (int j = 0; j < 4; ++j)
+        if (n + j < p.N) o[j] = to16<OT>(apply_act<ACT>(v[j]));
+    }
   } else {
     typedef typename std::conditional<epi_x16(EPI), _Float16, float>::type XE;  // (EPI_STORE32: f32)
     XE* o = (XE*)p.out + (long)m * p.ldo + n;
-    float4 r = make_float4(v[0], v[1], v[2], v[3]);
-    if constexpr (epi_resid(EPI)) {
-      const float4 x = ldx4(o);
-      r.x += x.x; r.y += x.y; r.z += x.z; r.w += x.w;
+    if (vec) {
+      float4 r = make_float4(v[0], v[1], v[2], v[3]);
+      if constexpr (epi_resid(EPI)) {
+        const float4 x = ldx4(o);
+        r.x += x.x; r.y += x.y; r.z += x.z; r.w += x.w;
+      }
+      stx4(o, r);
+    } else {
+      for (int j = 0; j < 4; ++j) {
+        if (n + j >= p.N) continue;
+        float r = v[j];
+        if constexpr (epi_resid(EPI)) r += (float)o[j];
+        o[j] = (XE)r;
+      }
     }
-    stx4(o, r);
   }
 }
 
@@ -1212,13 +900,17 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(GemmParams p) {
 // 16-byte aligned rows, no split-K.
 inline bool skinny_ok(const GemmParams& p) {
   return p.M > 0 && p.M <= SKINNY_MAX_M && p.N % 16 == 0 && p.K % (32 * SKINNY_U) == 0 && p.lda % 8 == 0 &&
-         p.ldw % 8 == 0 && p.ldo % 4 == 0 && !(p.diag & 2);
+         p.ldw % 8 == 0 && p.ldo % 4 == 0;
 }
+// The general form: K % 64 == 0 (launch_gemm checks), 16-byte aligned operand rows.
+inline bool general_ok(const GemmParams& p) { return p.lda % 8 == 0 && p.ldw % 8 == 0; }
+inline long skinny_waves(int M, int N) { return (long)((M + 15) / 16) * ((N + 15) / 16); }
 
-template <typename T, int EPI, int ACT>
+template <typename T, int EPI, int ACT, int U = SKINNY_U, int GEN = 0>
 hipError_t launch_skinny(const GemmParams& p, hipStream_t s) {
-  const long waves = (long)((p.M + 15) / 16) * (p.N / 16);
-  gemm_launch(gemm_skinny_kernel<T, EPI, ACT>, (int)((waves + 3) / 4), 256, s, p);
+  const long blocks = (skinny_waves(p.M, p.N) + 3) / 4;
+  if (blocks > 0x7fffffffL) return hipErrorInvalidValue;
+  gemm_launch(gemm_skinny_kernel<T, EPI, ACT, U, GEN>, (int)blocks, 256, s, p);
   return hipGetLastError();
 }
 
@@ -1228,46 +920,47 @@ hipError_t launch_tile(const GemmParams& p, hipStream_t s) {
     if ((p.tile == TILE_AUTO || p.tile == TILE_SKINNY) && skinny_ok(p)) return launch_skinny<T, EPI, ACT>(p, s);
   }
   if (p.tile == TILE_SKINNY) return hipErrorInvalidValue;
-  int tile = p.tile == TILE_AUTO ? pick_gemm_tile(p.M, p.N, p.K) : p.tile;
-  // EPI_LNF never runs the bt kernel: its LNF build returned a few wrong 16-row output columns per
-  // launch, differing run to run (tools/lnf_diag.py), while every pipelined
-  // tile agrees with every other bit for bit.  Small-M fold GEMMs take the 4-wave 160x128 RS tile
-  // (the same sums: tile choice never changes the bits).
-  if constexpr (epi_lnf(EPI)) {
-    if (tile == TILE_128x128) tile = TILE_160x128_RS;
-  }
-  // software-pipelined kernel: K >= 128, 16-byte-aligned 16-bit output rows (diag bit 1: legacy, stamp builds)
-  const bool pipe = p.K >= 2 * BK && !(p.diag & 2) && (!epi_st16(EPI) || p.ldo % 8 == 0);
-  if (pipe) {
-    if constexpr (epi_lnf(EPI)) {
-      // EPI_LNF: the 224x192 tile's three stages leave no LDS for the row statistics; it runs the
-      // 4-wave 160x128 RS tile instead (the same bits: every tile computes the same sums)
-      switch (tile) {
-        case TILE_256x128: return launch_pipe<T, 256, 128, 4, 2, EPI, ACT>(p, s);
-        case TILE_256x256: return launch_pipe<T, 256, 256, 2, 4, EPI, ACT>(p, s);
-        case TILE_192x256_W8: return launch_pipe<T, 192, 256, 2, 4, EPI, ACT, 1>(p, s);
-        case TILE_256x256_RS: return launch_pipe<T, 256, 256, 2, 4, EPI, ACT, 3, 1>(p, s);
-        case TILE_160x128_RS: return launch_pipe<T, 160, 128, 2, 2, EPI, ACT, 3, 1>(p, s);
-        case TILE_160x128_W8_RS: return launch_pipe<T, 160, 128, 2, 4, EPI, ACT, 2, 1>(p, s);
-        case TILE_256x256_HALF: return launch_pipe_half<T, EPI, ACT>(p, s);
-        case TILE_224x192_W8: return launch_pipe<T, 160, 128, 2, 2, EPI, ACT, 3, 1>(p, s);
-        default: break;
-      }
+  const int tile = p.tile == TILE_AUTO ? pick_gemm_tile(p.M, p.N, p.K) : p.tile;
+  if (tile != TILE_GENERAL && !gemm_tile_built(tile)) return hipErrorInvalidValue;
+  // software-pipelined kernel: K >= 128, 16-byte-aligned 16-bit output rows
+  const bool pipe = tile != TILE_GENERAL && p.K >= 2 * BK && (!epi_st16(EPI) || p.ldo % 8 == 0);
+  if (!pipe) {
+    // the general one-wave-per-16x16 form (any M; K = 64, unaligned 16-bit rows): the same bits
+    if constexpr (epi_patch(EPI)) {
+      return hipErrorInvalidValue;
     } else {
-      switch (tile) {
-        case TILE_256x128: return launch_pipe<T, 256, 128, 4, 2, EPI, ACT>(p, s);
-        case TILE_256x256: return launch_pipe<T, 256, 256, 2, 4, EPI, ACT>(p, s);
-        case TILE_192x256_W8: return launch_pipe<T, 192, 256, 2, 4, EPI, ACT, 1>(p, s);
-        case TILE_256x256_RS: return launch_pipe<T, 256, 256, 2, 4, EPI, ACT, 3, 1>(p, s);
-        case TILE_160x128_RS: return launch_pipe<T, 160, 128, 2, 2, EPI, ACT, 3, 1>(p, s);
-        case TILE_160x128_W8_RS: return launch_pipe<T, 160, 128, 2, 4, EPI, ACT, 2, 1>(p, s);
-        case TILE_256x256_HALF: return launch_pipe_half<T, EPI, ACT>(p, s);
-        case TILE_224x192_W8: return launch_pipe_224<T, EPI, ACT>(p, s);
-        default: break;
-      }
+      if (!general_ok(p)) return hipErrorInvalidValue;
+      return launch_skinny<T, EPI, ACT, 2, 1>(p, s);
     }
   }
-  return launch_cfg<T, 128, 128, 2, 2, EPI, ACT>(p, s);
+  if constexpr (epi_lnf(EPI)) {
+    // EPI_LNF: the 224x192 tile's three stages leave no LDS for the row statistics; it runs the
+    // 4-wave 160x128 RS tile instead (the same bits: every tile computes the same sums)
+    switch (tile) {
+      case TILE_256x128: return launch_pipe<T, 256, 128, 4, 2, EPI, ACT>(p, s);
+      case TILE_256x256: return launch_pipe<T, 256, 256, 2, 4, EPI, ACT>(p, s);
+      case TILE_192x256_W8: return launch_pipe<T, 192, 256, 2, 4, EPI, ACT, 1>(p, s);
+      case TILE_256x256_RS: return launch_pipe<T, 256, 256, 2, 4, EPI, ACT, 3, 1>(p, s);
+      case TILE_160x128_RS: return launch_pipe<T, 160, 128, 2, 2, EPI, ACT, 3, 1>(p, s);
+      case TILE_160x128_W8_RS: return launch_pipe<T, 160, 128, 2, 4, EPI, ACT, 2, 1>(p, s);
+      case TILE_256x256_HALF: return launch_pipe_half<T, EPI, ACT>(p, s);
+      case TILE_224x192_W8: return launch_pipe<T, 160, 128, 2, 2, EPI, ACT, 3, 1>(p, s);
+      default: break;
+    }
+  } else {
+    switch (tile) {
+      case TILE_256x128: return launch_pipe<T, 256, 128, 4, 2, EPI, ACT>(p, s);
+      case TILE_256x256: return launch_pipe<T, 256, 256, 2, 4, EPI, ACT>(p, s);
+      case TILE_192x256_W8: return launch_pipe<T, 192, 256, 2, 4, EPI, ACT, 1>(p, s);
+      case TILE_256x256_RS: return launch_pipe<T, 256, 256, 2, 4, EPI, ACT, 3, 1>(p, s);
+      case TILE_160x128_RS: return launch_pipe<T, 160, 128, 2, 2, EPI, ACT, 3, 1>(p, s);
+      case TILE_160x128_W8_RS: return launch_pipe<T, 160, 128, 2, 4, EPI, ACT, 2, 1>(p, s);
+      case TILE_256x256_HALF: return launch_pipe_half<T, EPI, ACT>(p, s);
+      case TILE_224x192_W8: return launch_pipe_224<T, EPI, ACT>(p, s);
+      default: break;
+    }
+  }
+  return hipErrorInvalidValue;
 }
 
 template <typename T>
@@ -1332,9 +1025,9 @@ int gemm_grid(int tile, int M, int N, int K) {
   p.K = K;
   p.lda = p.ldw = K;
   p.ldo = N;
-  if ((tile == TILE_AUTO || tile == TILE_SKINNY) && skinny_ok(p)) return (int)((((M + 15) / 16) * (N / 16) + 3) / 4);
+  if ((tile == TILE_AUTO || tile == TILE_SKINNY) && skinny_ok(p)) return (int)((skinny_waves(M, N) + 3) / 4);
   if (tile == TILE_AUTO) tile = pick_gemm_tile(M, N, K);
-  if (K >= 2 * BK) {
+  if (K >= 2 * BK && tile != TILE_GENERAL) {
     switch (tile) {
       case TILE_256x128: return pipe_grid(256, 128, 8, 3, M, N);
       case TILE_256x256: return pipe_grid(256, 256, 8, 3, M, N);
@@ -1347,18 +1040,16 @@ int gemm_grid(int tile, int M, int N, int K) {
       default: break;
     }
   }
-  return cfg_grid(128, 128, 4, M, N);
+  return (int)std::min<long>((skinny_waves(M, N) + 3) / 4, 0x7fffffffL);  // the general form
 }
 
 // Tile choice: large-M GEMMs use the 256-row tiles (128 FLOP per staged byte
 // instead of 64); among those, the column tile that wastes the least of the
 // last wave of blocks over the 256 CUs (one 8-wave block per CU).
 int pick_gemm_tile(int M, int N, int K) {
-  // Small M: the 4-wave 160x128 pipelined tile (round 5; the bt kernel only where the pipelined
-  // kernel cannot run: K < 128).  The bt kernel's LayerNorm-fold build returned run-to-run wrong
-  // outputs, and one flaky small-batch mismatch in a STORE16 / RESID16
-  // engine suite run is not excluded to share its cause; the pipelined tiles give the same bits.
-  if (M < 2048) return K >= 128 ? TILE_160x128_RS : TILE_128x128;
+  // Small M: the 4-wave 160x128 pipelined tile (launch_tile sends K < 128 to the general form).
+  (void)K;
+  if (M < 2048) return TILE_160x128_RS;
   const int cus = 256;
   auto eff = [&](int bm, int bn) {
     const long tiles = (long)((M + bm - 1) / bm) * ((N + bn - 1) / bn);
@@ -1375,8 +1066,13 @@ int pick_gemm_tile(int M, int N, int K) {
 // rows * lda * 2 bytes under 2^31.  Larger M runs as consecutive row chunks (launch_gemm below);
 // every output row is the same MFMA chain whichever launch computes it, so the chunking is
 // bit-invisible (test_gemm_row_chunks_are_bit_exact, the SO400M max_batch 1024 test).
+// Test hook (clipgpu_test_gemm_chunk_rows): a smaller row cap for the chunked path, so the tests run it
+// at small batches (0 = off).
+long g_gemm_chunk_cap = 0;
+
 long gemm_chunk_rows(long lda, int G) {
   long rows = ((1L << 31) - 1) / (2 * lda);
+  if (g_gemm_chunk_cap > 0) rows = std::min(rows, g_gemm_chunk_cap);
   rows -= rows % 256;                           // whole 256-row tiles
   if (G > 0) rows -= rows % ((long)G * G);      // EPI_PATCH: whole images
   return rows;
@@ -1397,15 +1093,17 @@ hipError_t launch_gemm(DType dt, int asrc, int epi, int act, const GemmParams& p
   // 32-bit staging offsets: W must fit whole; A is chunked by rows
   if ((long)p.N * p.ldw * 2 >= (1L << 31) || p.lda <= 0) return hipErrorInvalidValue;
   if (asrc != A_ROWS) return hipErrorInvalidValue;  // pixels go through launch_patch_rows first
-  if ((long)p.M * p.lda * 2 >= (1L << 31)) {
+  if ((long)p.M * p.lda * 2 >= (1L << 31) || (g_gemm_chunk_cap > 0 && p.M > g_gemm_chunk_cap)) {
     const int G = epi == EPI_PATCH ? p.G : 0;
     const long chunk = gemm_chunk_rows(p.lda, G);
     if (chunk <= 0) return hipErrorInvalidValue;
-    const long osz = epi_st16(epi) ? 2 : 4;
+    // output element size: 16-bit activations, the f16 residual stream (x16), else f32
+    const long osz = (epi_st16(epi) || ((epi == EPI_RESID || epi == EPI_PATCH) && p.x16)) ? 2 : 4;
     for (long m0 = 0; m0 < p.M; m0 += chunk) {
       GemmParams q = p;
       q.M = (int)std::min<long>(chunk, p.M - m0);
       q.A = (const char*)p.A + m0 * p.lda * 2;
+      if (epi == EPI_LNF) q.rowstats = p.rowstats + 2 * m0;  // (mean, rstd) of the chunk's rows
       const long orow = G > 0 ? m0 / ((long)G * G) * ((long)G * G + p.cls) : m0;  // EPI_PATCH: token rows
       q.out = (char*)p.out + orow * p.ldo * osz;
       const hipError_t err = launch_dt(dt, epi, act, q, s);

@@ -48,7 +48,7 @@ struct GemmParams {
   int cls;                   // EPI_PATCH: 1 = token 0 of each image is a class token (rows / pos shifted by one)
   const float* pos;          // EPI_PATCH positional embedding [G^2+cls][N]
   int tile;                  // GemmTile (0 = pick by shape)
-  int diag;                  // stamp build only: bit 0 = skip epilogue stores (timing experiments)
+  int diag;                  // stamp build only: bit 0 = skip epilogue stores, bit 2 = no operand DMA, bit 3 = no step barrier
   int group;                 // tile order: row panels per group (gemm_util.hpp tile_coords); 0 = 8
   int prio;                  // 8-wave gemm_pipe tiles: 1 = the younger half of the block at s_setprio 1
   int x16;                   // EPI_RESID / EPI_PATCH: the residual stream `out` is f16 (else f32); the adds are f32
@@ -62,14 +62,15 @@ struct GemmParams {
 // 21-25 (32x32x16 MFMA), 27 (spread-DMA 224x192).
 enum GemmTile {
   TILE_AUTO = 0,
-  TILE_128x128 = 1,       // gemm_bt_kernel: 4 waves, 64 KiB LDS, 2 blocks / CU (M < 2048, K < 128)
+  // (1: the 128x128 "bt" kernel, removed in round 6 -- run-to-run wrong outputs; its
+  // shapes, K < 128 and unaligned 16-bit rows, run the skinny kernel's general form)
   TILE_256x128 = 2,       // gemm_pipe_kernel: 8 waves (4x2, 64x64 each), 96 KiB LDS (shape heuristic)
   TILE_256x256 = 3,       // gemm_pipe_kernel: 8 waves (2x4, 128x64 each), 128 KiB LDS (shape heuristic)
   TILE_192x256_W8 = 13,   // 2x4 waves of 96x64, 114 KiB LDS, 1 block / CU (the table's ViT-H/14 c_proj)
   // the spread fragment-read schedule (gemm_pipe_kernel RS = 1: a phase's reads for the next phase go
   // out over its first MI - 2 MFMA groups); bit-identical to the others, speed only
   TILE_256x256_RS = 14,
-  TILE_160x128_RS = 15,     // 4 waves of 80x64, 74 KiB LDS, 2 blocks / CU (the table's large-text c_proj)
+  TILE_160x128_RS = 15,     // 4 waves of 80x64, 74 KiB LDS, 2 blocks / CU (small M; the table's large-text c_proj)
   TILE_160x128_W8_RS = 17,  // 2x4 waves of 80x32, 74 KiB LDS, 2 blocks / CU (the table's N = width sites)
   TILE_256x256_HALF = 18,   // 256x256 RS with the partial last round as half tiles (HM = 1; the table's
                             // qkv / c_fc)
@@ -77,9 +78,10 @@ enum GemmTile {
   // GEMMs at 12800 rows are 232 tiles, one round
   TILE_224x192_W8 = 26,
   TILE_SKINNY = 100,      // gemm_skinny_kernel: one wave per 16x16 block, M <= 256 (TILE_AUTO's pick there)
+  TILE_GENERAL = 101,     // gemm_skinny_kernel's general form, any M / N (the pick where no pipelined tile runs)
 };
 // The GemmTile ids the library builds (pins, tests and the timing tuner take only these).
-constexpr int kGemmTiles[] = {TILE_128x128, TILE_256x128, TILE_256x256, TILE_192x256_W8, TILE_256x256_RS,
+constexpr int kGemmTiles[] = {TILE_256x128, TILE_256x256, TILE_192x256_W8, TILE_256x256_RS,
                               TILE_160x128_RS, TILE_160x128_W8_RS, TILE_256x256_HALF, TILE_224x192_W8};
 inline bool gemm_tile_built(int t) {
   for (int k : kGemmTiles)
@@ -87,6 +89,9 @@ inline bool gemm_tile_built(int t) {
   return false;
 }
 int pick_gemm_tile(int M, int N, int K);
+// Test hook: cap on the rows of one launch of launch_gemm's row-chunked path (0 = only the 2^31-byte
+// operand limit chunks).  Chunking is bit-invisible (test_chunked_gemm_launches_are_bit_exact).
+extern long g_gemm_chunk_cap;
 int gemm_grid(int tile, int M, int N, int K);  // blocks of one launch (the persistent grid)
 int device_cus();  // CUs of the current device (cached)
 

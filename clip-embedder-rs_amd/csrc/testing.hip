@@ -44,7 +44,7 @@ DType dt_of(int dtype) {
 int tile_override() {
   const char* e = getenv("CLIPGPU_TEST_TILE");
   const int t = e ? atoi(e) : 0;
-  if (t != 0 && t != TILE_SKINNY && !gemm_tile_built(t))
+  if (t != 0 && t != TILE_SKINNY && t != TILE_GENERAL && !gemm_tile_built(t))
     throw ClipErr(CLIPGPU_ERR_INVALID, "CLIPGPU_TEST_TILE: " + std::to_string(t) + " is not a built GEMM tile");
   return t;
 }
@@ -113,11 +113,25 @@ int clipgpu_test_gemm(int dtype, int mode, int act, int64_t M, int64_t N, int64_
       if (resid) up(dO.p, resid, M * N * 4);
     } else if (mode == 2) {
       epi = EPI_STORE32;
+    } else if (mode == 3) {  // the f16 residual stream (GemmParams.x16)
+      epi = EPI_RESID;
+      g.x16 = 1;
+      if (resid) up16(DT_F16, dO.p, resid, M * N);
+    } else if (mode != 0) {
+      throw ClipErr(CLIPGPU_ERR_INVALID, "bad mode");
     }
     TCHECK(launch_gemm(dt, A_ROWS, epi, mode == 0 ? act : 0, g, nullptr));
     TCHECK(hipDeviceSynchronize());
     if (mode == 0) down16(dt, out, dO.p, M * N);
+    else if (mode == 3) down16(DT_F16, out, dO.p, M * N);
     else down(out, dO.p, M * N * 4);
+  });
+}
+
+int clipgpu_test_gemm_chunk_rows(int64_t rows) {
+  return guarded([&]() {
+    if (rows < 0) throw ClipErr(CLIPGPU_ERR_INVALID, "rows < 0");
+    g_gemm_chunk_cap = (long)rows;
   });
 }
 
@@ -126,7 +140,8 @@ int clipgpu_test_gemm_lnf(int dtype, int act, int64_t M, int64_t N, int64_t K, c
   return guarded([&]() {
     const DType dt = dt_of(dtype);
     if (M <= 0 || N <= 0 || K <= 0 || K % 64 || N % 4) throw ClipErr(CLIPGPU_ERR_INVALID, "bad GEMM shape");
-    if (tile != 0 && tile != TILE_SKINNY && !gemm_tile_built(tile)) throw ClipErr(CLIPGPU_ERR_INVALID, "bad tile");
+    if (tile != 0 && tile != TILE_SKINNY && tile != TILE_GENERAL && !gemm_tile_built(tile))
+      throw ClipErr(CLIPGPU_ERR_INVALID, "bad tile");
     DevBuf dA(M * K * 2), dW(N * K * 2), dB(N * 4), dC(N * 4), dO(M * N * 2), dS((M + 256) * 8);
     up16(DT_F16, dA.p, x, M * K);
     up16(DT_F16, dW.p, wf, N * K);

@@ -67,6 +67,7 @@ _PROTOS = [
     ("clipgpu_synth_tensor", c_int, [c_uint64, c_char_p, c_double, c_double, c_void_p, c_int64]),
     # include/clipgpu_testing.h
     ("clipgpu_test_gemm", c_int, [c_int, c_int, c_int, c_int64, c_int64, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    ("clipgpu_test_gemm_chunk_rows", c_int, [c_int64]),
     ("clipgpu_test_gemm_lnf", c_int, [c_int, c_int, c_int64, c_int64, c_int64, c_void_p, c_void_p, c_void_p,
                                c_void_p, c_float, c_int, c_void_p]),
     ("clipgpu_test_attention", c_int, [c_int, c_int64, c_int64, c_int64, c_int64, c_int, c_void_p, c_void_p]),
@@ -81,6 +82,7 @@ _PROTOS = [
     ("clipgpu_test_engine_residual", c_int, [c_void_p, POINTER(c_int), POINTER(c_int)]),
     ("clipgpu_test_host_plan", c_int, [c_void_p, c_int, POINTER(c_int), c_int]),
     ("clipgpu_test_force_broadcast", c_int, [c_void_p, c_int]),
+    ("clipgpu_test_rgb8_resize_always", c_int, [c_void_p, c_int]),
     ("clipgpu_test_comm_lazy", c_int, [c_void_p]),
     ("clipgpu_test_profile_timeline", c_int, [c_void_p, c_int64, POINTER(c_double), POINTER(c_double), POINTER(c_int),
                                               POINTER(c_int), POINTER(c_int64)]),

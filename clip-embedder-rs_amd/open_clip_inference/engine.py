@@ -265,9 +265,22 @@ def profile_read(engine: "Engine", category: str):
     return ms.value, n.value
 
 
+def host_buffer(shape, dtype) -> np.ndarray:
+    """An empty C-contiguous host array that owns whole memory pages (page-aligned start, no other
+    allocation on its last page): what host_register needs, since registration pins whole pages and two
+    registered ranges may not share one (clipgpu_host_register)."""
+    dtype = np.dtype(dtype)
+    n = int(np.prod(shape, dtype=np.int64)) * dtype.itemsize
+    page = 4096
+    raw = np.empty(((n + page - 1) // page + 1) * page, np.uint8)
+    off = (-raw.ctypes.data) % page
+    return raw[off:off + n].view(dtype).reshape(shape)
+
+
 def host_register(arr: np.ndarray) -> None:
     """Registers a C-contiguous host array for direct DMA by the host-buffer entry points
-    (clipgpu_host_register).  Keep `arr` alive until host_unregister(arr)."""
+    (clipgpu_host_register).  Keep `arr` alive until host_unregister(arr).  A range that shares a memory
+    page with a registered one is refused: allocate registered arrays with host_buffer."""
     if not arr.flags["C_CONTIGUOUS"]:
         raise ValueError("host_register needs a C-contiguous array")
     check(lib().clipgpu_host_register(arr.ctypes.data, arr.nbytes))

@@ -16,9 +16,11 @@ extern "C" {
 #endif
 
 /* out[M][N] = act(A[M][K] . W[N][K]^T + bias[N]) (act: 0 none, 1 quick_gelu, 2 gelu, 3 gelu_tanh).
- * mode 0: 16-bit output (returned as f32); mode 1: residual (out = resid + ...); mode 2: f32 output.
+ * mode 0: 16-bit output (returned as f32); mode 1: residual (out = resid + ...); mode 2: f32 output;
+ * mode 3: residual on an f16 stream (resid rounded to f16 on upload, the f16 result widened to f32).
  * bias and resid may be NULL.  CLIPGPU_TEST_TILE = a GemmTile id the library builds (kernels.hpp
- * kGemmTiles; 0 auto, 100 skinny) forces the tile (test hooks only: the engine reads no environment). */
+ * kGemmTiles; 0 auto, 100 skinny, 101 the skinny kernel's general form) forces the tile; shapes the pipelined tiles do not take (K = 64,
+ * 16-bit rows not a multiple of 8 elements) run the skinny kernel's general form whatever the tile (test hooks only: the engine reads no environment). */
 int clipgpu_test_gemm(int dtype, int mode, int act, int64_t M, int64_t N, int64_t K, const float* A,
                       const float* W, const float* bias, const float* resid, float* out);
 /* The LayerNorm-folded GEMM (EPI_LNF): out[m][n] = act(rstd_m (x W'^T - mean_m cs)[m][n] + bias[n]) with
@@ -27,6 +29,11 @@ int clipgpu_test_gemm(int dtype, int mode, int act, int64_t M, int64_t N, int64_
  * launcher's choice, 100 = skinny. */
 int clipgpu_test_gemm_lnf(int dtype, int act, int64_t M, int64_t N, int64_t K, const float* x, const float* wf,
                           const float* cs, const float* bias, float eps, int tile, float* out);
+
+/* Cap the rows of one GEMM launch of launch_gemm's row-chunked path (0 = off: only the 2^31-byte operand
+ * limit chunks), process-wide, for every GEMM launched (or graph captured) afterwards: the chunked path
+ * of large batches runs at test sizes.  Chunking is bit-invisible. */
+int clipgpu_test_gemm_chunk_rows(int64_t rows);
 
 /* qkv: [B*N][3*D] f32 (rounded to 16-bit on upload), D = H * HD (HD in {64, 72, 80}); out: [B*N][D]. */
 int clipgpu_test_attention(int dtype, int64_t B, int64_t N, int64_t H, int64_t HD, int causal, const float* qkv,
@@ -127,18 +134,13 @@ int clipgpu_test_engine_lanes(const struct clipgpu_engine* e, int* dev_lanes);
 int clipgpu_test_engine_residual(const struct clipgpu_engine* e, int* residual, int* ln_fold);
 /* The host-buffer vision path's chunk plan (tools/host_plan_ab.py): n_chunks (1..4) chunks of a
  * max_batch round cut at bounds[0 .. n_chunks - 2]; n_chunks = 0 restores the default
- * (engine.hip host_chunks).  copy_stream = 1: the H2Ds in chunk order on the replica's copy
- * stream (default); 0: each on its chunk's lane stream; 2: each chunk's two halves on two copy
- * streams at once; 3: registered inputs pulled through their host mapping by a copy kernel on
- * the copy stream (others as 1).  + 16: a multi-round call starts each round's forwards together,
- * once the round's last chunk has landed; + 32: the D2Hs on the copy stream; + 64: a multi-round call
- * joins the lanes every round (a chunk's forward also waits for the other chunks' previous-round
- * forwards); + 128: a multi-round vision call runs each round as the device path does (one
- * fork / join forward over the lanes once the round's input has landed, one D2H); + 256: a
- * multi-round call's D2Hs on the lane streams behind each forward (the round-4 schedule; the default
- * writes each buffer set's embeddings to its own device rows and copies them back on a second copy
- * stream).  Speed only, never the bits. */
+ * (engine.hip host_chunks).  copy_stream must be 0 or 1 (round 6 removed the schedule variants it
+ * used to select; DESIGN.md §6 keeps their measurements).  Speed only, never the bits. */
 int clipgpu_test_host_plan(struct clipgpu_engine* e, int n_chunks, const int* bounds, int copy_stream);
+/* on != 0: clipgpu_embed_images_rgb8 sends batches of image_size x image_size images through the GPU
+ * resize path too (by default they take the u8 host path: their resize plan is the identity).  The
+ * test of the identity route compares the two. */
+int clipgpu_test_rgb8_resize_always(struct clipgpu_engine* e, int on);
 /* Gathered calls of this handle take the ragged branch (one ncclBroadcast per block) even when
  * every block has the same size (on != 0), so a one-rank or equal-shard run exercises it. */
 int clipgpu_test_force_broadcast(struct clipgpu_engine* e, int on);

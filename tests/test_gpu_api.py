@@ -208,6 +208,36 @@ def test_embed_images_rgb8_matches_host_preprocess(model):
     assert np.array_equal(multi.session.embed_images_rgb8(ims), gpu)
 
 
+def test_embed_images_rgb8_identity_batches_take_the_u8_path():
+    """A batch of image_size x image_size decoded images needs no resize (its plan is the identity), so
+    clipgpu_embed_images_rgb8 sends it down the u8 host path (copy-pool staging, copy-stream H2Ds, two
+    buffer sets past max_batch) instead of the resize kernels.  Bit-identical to the resize path
+    (clipgpu_test_rgb8_resize_always) and to embed_u8 on the stacked images: one round, several rounds
+    with a ragged last one, and a two-replica handle."""
+    from oracle.model_spec import VIT_B_32_CFG
+    from open_clip_inference import _lib
+    from open_clip_inference.engine import Engine
+    d = make_model_dir(VIT_B_32_CFG, seed=1234)
+    v = vision_spec_from_cfg(VIT_B_32_CFG["model_cfg"])
+    u8 = weights.synth_images_u8(83, 45, v.image_size)
+    ims = [u8[i] for i in range(len(u8))]
+    e = Engine(d, 0, [0], "bf16", 16)
+    for n in (1, 16, 45):
+        fast = e.embed_images_rgb8(ims[:n])
+        _lib.check(_lib.lib().clipgpu_test_rgb8_resize_always(e.handle, 1))
+        slow = e.embed_images_rgb8(ims[:n])
+        _lib.check(_lib.lib().clipgpu_test_rgb8_resize_always(e.handle, 0))
+        assert np.array_equal(fast, slow), n
+        assert np.array_equal(fast, e.embed_u8(u8[:n], OPENAI_MEAN, OPENAI_STD)), n
+    multi = Engine(d, 0, [0, 0], "bf16", 8)
+    assert np.array_equal(multi.embed_images_rgb8(ims), e.embed_images_rgb8(ims))
+    # a batch mixing sizes takes the resize path for every image: the S x S rows do not change
+    mixed = ims[:3] + [np.ascontiguousarray(u8[3][:200])]
+    assert np.array_equal(e.embed_images_rgb8(mixed)[:3], e.embed_images_rgb8(ims[:3]))
+    e.close()
+    multi.close()
+
+
 @pytest.mark.parametrize("ni,nt,E", [(1, 3, 64), (300, 1000, 512), (1000, 1, 768), (65, 129, 1152), (7, 5000, 1024)])
 @pytest.mark.parametrize("act,axis", [("softmax", 1), ("softmax", 0), ("sigmoid", 1), ("logits", 1)])
 def test_similarity_kernel_vs_facade_math(ni, nt, E, act, axis):
@@ -310,9 +340,8 @@ def test_multi_round_host_calls_alternate_buffer_sets_bit_exactly():
     (engine.hip run_host_shard: round i + 1's H2D under round i's forward).  Every
     round must equal the same rows embedded by a call of their own, bit for bit: u8 and f32 pixels
     and token ids, pageable and caller-registered buffers, a ragged last round, and a second
-    multi-round call (graph replay on both sets) -- under the default schedule and the host-plan
-    hook's multi-round schedules (+16 lanes in step, +32 D2H on the copy stream, +64 joined rounds, +128
-    device-path rounds, +256 the D2Hs on the lane streams)."""
+    multi-round call (graph replay on both sets).  The staging copies run on the persistent copy pool
+    in pieces, each piece's H2D issued as soon as it is packed."""
     import ctypes
     from oracle.model_spec import VIT_B_32_CFG
     from open_clip_inference import _lib
@@ -334,12 +363,12 @@ def test_multi_round_host_calls_alternate_buffer_sets_bit_exactly():
     no_bounds = (ctypes.c_int * 4)()
     for name, (e, fn, x) in calls.items():
         ref = np.concatenate([fn(e, x[i:i + MB]) for i in range(0, B, MB)])
-        for registered, flags in ((False, 1), (True, 1), (False, 1 + 16), (True, 1 + 32), (False, 1 + 64),
-                                  (True, 1 + 64), (False, 1 + 128), (True, 1 + 128), (False, 1 + 256),
-                                  (True, 1 + 256)):
+        for registered, flags in ((False, 1), (True, 1)):
             _lib.check(_lib.lib().clipgpu_test_host_plan(e.handle, 0, no_bounds, flags))
-            xin = np.ascontiguousarray(x)
-            out = np.full((B, 512), np.nan, np.float32)
+            from open_clip_inference.engine import host_buffer
+            xin = host_buffer(x.shape, x.dtype)
+            xin[...] = x
+            out = host_buffer((B, 512), np.float32)
             if registered:
                 host_register(xin)
                 host_register(out)

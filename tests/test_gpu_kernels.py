@@ -49,11 +49,11 @@ def run_gemm(dtype, mode, act, A, W, bias=None, resid=None):
 
 
 # every GEMM tile the library builds (kernels.hpp kGemmTiles; test_cpu_abi checks this list against it)
-BUILT_TILES = [1, 2, 3, 13, 14, 15, 17, 18, 26]
+BUILT_TILES = [2, 3, 13, 14, 15, 17, 18, 26]
 
 
 @pytest.fixture(params=BUILT_TILES,
-                ids=["t128x128", "pipe256x128", "pipe256x256", "w8_192x256", "rs_256x256", "rs_160x128",
+                ids=["pipe256x128", "pipe256x256", "w8_192x256", "rs_256x256", "rs_160x128",
                      "rs_w8_160x128", "half_256x256", "w8_224x192"])
 def tile(request, monkeypatch):
     """Every GEMM tile configuration (GemmTile) through the same numerics checks."""
@@ -207,13 +207,52 @@ def test_skinny_gemm_is_bit_exact(mode, act, M, N, K, monkeypatch):
     bias = rng.standard_normal(N).astype(np.float32)
     resid = rng.standard_normal((M, N)).astype(np.float32) if mode == 1 else None
     outs = []
-    for t in ["100", "1", "14"]:
+    for t in ["100", "15", "14", "101"]:
         monkeypatch.setenv("CLIPGPU_TEST_TILE", t)
         outs.append(run_gemm(BF16, mode, act, A, W, bias, resid))
-    assert np.array_equal(outs[0], outs[1]) and np.array_equal(outs[0], outs[2])
+    assert all(np.array_equal(outs[0], o) for o in outs[1:])
     if mode == 2:
         ref = A.astype(np.float64) @ W.T.astype(np.float64) + bias
         assert np.all(np.abs(outs[0] - ref) <= 3e-5 * (np.abs(A) @ np.abs(W).T) + 1e-6)
+
+
+@pytest.mark.parametrize("M", [800, 3000])
+@pytest.mark.parametrize("mode,act", [(0, 1), (1, 0), (2, 0), (3, 0)])
+def test_general_gemm_is_bit_exact(M, mode, act, monkeypatch):
+    """The skinny kernel's general form (TILE_GENERAL 101: any M, N tails, element stores) -- what
+    runs the shapes the pipelined tiles do not take since round 6 removed the 128x128 bt kernel --
+    gives the pipelined tiles' bits at M = 800 and 3000 for every epilogue: the 16-bit store with an
+    activation, the f32 and the f16 residual stream (modes 1 / 3) and the f32 store.  Then the shapes
+    only it takes: K = 64 at any M, and a 16-bit output row of 100 elements (not a multiple of 8),
+    within the f32-accumulation bound of fp64, with N tails."""
+    rng = np.random.default_rng(M + mode)
+    N, K = 520, 384
+    A = round16(rng.standard_normal((M, K)), BF16)
+    W = round16(rng.standard_normal((N, K)) / np.sqrt(K), BF16)
+    bias = rng.standard_normal(N).astype(np.float32)
+    resid = (rng.standard_normal((M, N)) * 30).astype(np.float32) if mode in (1, 3) else None
+    outs = {}
+    for t in ["101", "15", "14", "26"]:
+        monkeypatch.setenv("CLIPGPU_TEST_TILE", t)
+        outs[t] = run_gemm(BF16, mode, act, A, W, bias, resid)
+    for t in ("15", "14", "26"):
+        assert np.array_equal(outs[t], outs["101"]), t
+    monkeypatch.setenv("CLIPGPU_TEST_TILE", "0")
+    for n, k in [(136, 64), (100, 256), (100, 64), (40, 64)]:
+        A2, W2 = A[:, :k], round16(rng.standard_normal((n, k)) / np.sqrt(k), BF16)
+        b2 = bias[:n]
+        r2 = None if resid is None else np.ascontiguousarray(resid[:, :n])
+        got = run_gemm(BF16, mode, act, A2, W2, b2, r2)
+        ref = A2.astype(np.float64) @ W2.T.astype(np.float64) + b2
+        if mode == 0:
+            ref = ref_act(act, ref)
+            assert np.all(np.abs(got - ref) <= 1.01 * 2 ** -8 * np.abs(ref) + 1e-4), (n, k)
+        elif mode == 2:
+            assert np.all(np.abs(got - ref) <= 3e-5 * (np.abs(A2) @ np.abs(W2).T) + 1e-6), (n, k)
+        else:
+            r16 = r2 if mode == 1 else r2.astype(np.float16).astype(np.float64)
+            tol = 1e-4 if mode == 1 else 2 ** -11 * np.abs(ref + r16) + 1e-3
+            assert np.all(np.abs(got - (ref + r16)) <= tol), (n, k)
 
 
 @pytest.mark.parametrize("mode", [0, 1])

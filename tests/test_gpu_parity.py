@@ -5,6 +5,7 @@ Tolerance (north_star): cosine(GPU, oracle) >= 0.9999 per embedding row, and the
 GPU rows are unit-norm to 1e-5.  Weights are the seeded synthetic set (identical
 bits on both sides, tests/test_cpu_host.py::test_synth_matches_oracle).
 """
+import ctypes
 from ctypes import c_int
 
 import numpy as np
@@ -18,7 +19,7 @@ from tests.helpers import COS_TOL, make_model_dir, normalized_pixels, specs
 
 pytestmark = pytest.mark.gpu
 
-BUILT_TILES = [1, 2, 3, 13, 14, 15, 17, 18, 26]  # kernels.hpp kGemmTiles (test_cpu_abi checks the list)
+BUILT_TILES = [2, 3, 13, 14, 15, 17, 18, 26]  # kernels.hpp kGemmTiles (test_cpu_abi checks the list)
 
 _CACHE = {}
 
@@ -252,13 +253,16 @@ def test_registered_host_buffers_are_bit_exact(tower, kind, mb):
         data = weights.synth_token_ids(61, B, t.context_length, t.vocab_size, t.vocab_size - 2,
                                        t.vocab_size - 1, random_eot=True)
         run = lambda x, out: e.embed_tokens(x, out=out)
-    data = np.ascontiguousarray(data)
+    from open_clip_inference.engine import host_buffer
+    buf = host_buffer(data.shape, data.dtype)
+    buf[...] = data
+    data = buf
     want = {n: run(data[:n], None) for n in (1, 5, 37, 60)}
     key = ("host_want", tower, kind)
     if key in _CACHE:  # the other max_batch's partition gave the same bytes
         assert all(np.array_equal(want[n], _CACHE[key][n]) for n in want)
     _CACHE[key] = want
-    out = np.zeros((B, 512), np.float32)
+    out = host_buffer((B, 512), np.float32)
     for reg_in, reg_out in [(1, 0), (0, 1), (1, 1)]:
         if reg_in:
             host_register(data)
@@ -281,6 +285,16 @@ def test_registered_host_buffers_are_bit_exact(tower, kind, mb):
             host_register(data[1:])
     finally:
         host_unregister(data)
+    # a range on a registered range's page that does not overlap it is refused too (registration pins
+    # whole pages): 100 bytes registered, then 64 bytes 200 bytes further on the same page
+    small = host_buffer((100,), np.uint8)
+    host_register(small)
+    try:
+        same_page = np.frombuffer((ctypes.c_uint8 * 64).from_address(small.ctypes.data + 200), np.uint8)
+        with pytest.raises(ClipError, match="shares a memory page"):
+            host_register(same_page)
+    finally:
+        host_unregister(small)
 
 
 def test_native_library_is_loaded():
@@ -321,6 +335,40 @@ def test_gemm_tile_choice_is_bit_exact(tower):
 
 
 @pytest.mark.parametrize("tower", [0, 1])
+def test_chunked_gemm_launches_are_bit_exact(tower):
+    """launch_gemm's row-chunked path (operands past 2^31 bytes: a ViT-L / H engine at max_batch ~1024)
+    on a CLIP-family engine with the f16 residual stream and the LayerNorm fold (the defaults): with the
+    chunk cap lowered to 256 rows (clipgpu_test_gemm_chunk_rows) every trunk GEMM, the patch GEMM
+    included, runs as several launches; the embeddings are bit-equal to the unchunked engine's.  (ADVICE
+    r5: the chunks used to address the f16 stream at f32 strides and reuse chunk 0's row statistics.)"""
+    from open_clip_inference import _lib
+    v, t = specs(VIT_B_32_CFG)
+    if tower == 0:
+        data = normalized_pixels(weights.synth_images_u8(57, 16, v.image_size), OPENAI_MEAN, OPENAI_STD)
+    else:
+        data = weights.synth_token_ids(57, 16, t.context_length, t.vocab_size, t.vocab_size - 2,
+                                       t.vocab_size - 1, random_eot=True)
+    run = (lambda e: e.embed_pixels(data)) if tower == 0 else (lambda e: e.embed_tokens(data))
+    _lib.check(_lib.lib().clipgpu_test_gemm_chunk_rows(256))
+    try:
+        chunked = run(engine(VIT_B_32_CFG, tower, max_batch=16))
+    finally:
+        _lib.check(_lib.lib().clipgpu_test_gemm_chunk_rows(0))
+    whole = run(engine(VIT_B_32_CFG, tower, max_batch=16))
+    np.testing.assert_array_equal(chunked, whole)
+    check_rows(whole[:3], oracle_vision(VIT_B_32_CFG, 1234, data[:3]) if tower == 0
+               else oracle_text(VIT_B_32_CFG, 1234, data[:3]))
+
+
+def test_removed_bt_tile_pin_is_refused():
+    """Tile 1 (the 128x128 bt kernel, removed in round 6: run-to-run wrong outputs) is no
+    longer a built tile: a pin of it fails at creation instead of running a kernel that is gone."""
+    from open_clip_inference.error import ClipError
+    with pytest.raises(ClipError):
+        engine(TINY_CFG, 0, max_batch=4, gemm_tiles=[1, 1, 1, 1])
+
+
+@pytest.mark.parametrize("tower", [0, 1])
 def test_concurrent_lanes_are_bit_exact(tower):
     """Splitting a batch over concurrent lanes (sub-batches on their own streams)
     is invisible in the output: rows never interact outside attention."""
@@ -332,7 +380,7 @@ def test_concurrent_lanes_are_bit_exact(tower):
                                        t.vocab_size - 1, random_eot=True)
     outs = []
     for lanes in [1, 2, 3, 4]:
-        e = engine(VIT_B_32_CFG, tower, max_batch=37, gemm_tiles=[1, 1, 1, 1], lanes=lanes)
+        e = engine(VIT_B_32_CFG, tower, max_batch=37, gemm_tiles=[15, 15, 15, 15], lanes=lanes)
         outs.append(e.embed_pixels(data) if tower == 0 else e.embed_tokens(data))
     for o in outs[1:]:
         assert np.array_equal(o, outs[0])
