@@ -26,6 +26,7 @@
 
 #include "../../include/clipgpu.h"
 #include "../../include/clipgpu_testing.h"
+#include "bounce.hpp"
 #include "host/api_util.hpp"
 #include "host/copy_pool.hpp"
 #include "host/json.hpp"
@@ -320,11 +321,11 @@ size_t weight_bytes(const TowerSpec& s, const TensorMap& m) {
 }
 
 void upload_f32(const HostTensor& t, float* dst) {
-  HIP_CHECK(hipMemcpy(dst, t.data.data(), t.data.size() * 4, hipMemcpyHostToDevice));
+  HIP_CHECK(copy_h2d(dst, t.data.data(), t.data.size() * 4));
 }
 
 void upload_16(DType dt, const float* src, size_t n, void* dst, float* staging, hipStream_t s) {
-  HIP_CHECK(hipMemcpy(staging, src, n * 4, hipMemcpyHostToDevice));
+  HIP_CHECK(copy_h2d(staging, src, n * 4));
   HIP_CHECK(launch_cast_f32(dt, staging, dst, (long)n, s));
   HIP_CHECK(hipStreamSynchronize(s));
 }
@@ -387,7 +388,7 @@ void upload_weights(clipgpu_engine& e, Replica& r, const TensorMap& m) {
       src = pad.data();
     }
     float* stg = staging_pad((size_t)(Rp * Cp));
-    HIP_CHECK(hipMemcpy(stg, src, (size_t)(Rp * Cp) * 4, hipMemcpyHostToDevice));
+    HIP_CHECK(copy_h2d(stg, src, (size_t)(Rp * Cp) * 4));
     MxW w;
     w.q = (uint8_t*)a.take((size_t)(Rp * Cp));
     w.s = (uint8_t*)a.take((size_t)(Rp * Cp / 32));
@@ -400,12 +401,12 @@ void upload_weights(clipgpu_engine& e, Replica& r, const TensorMap& m) {
     std::vector<float> pad((size_t)n, 0.f);
     std::memcpy(pad.data(), t.data.data(), t.data.size() * 4);
     float* p = (float*)a.take(pad.size() * 4);
-    HIP_CHECK(hipMemcpy(p, pad.data(), pad.size() * 4, hipMemcpyHostToDevice));
+    HIP_CHECK(copy_h2d(p, pad.data(), pad.size() * 4));
     return p;
   };
   auto a_take_f32 = [&](const std::vector<float>& v) {
     float* p = (float*)a.take(v.size() * 4);
-    HIP_CHECK(hipMemcpy(p, v.data(), v.size() * 4, hipMemcpyHostToDevice));
+    HIP_CHECK(copy_h2d(p, v.data(), v.size() * 4));
     return p;
   };
   auto w16_transposed = [&](const std::string& k) {  // [D][E] -> [E][D]
@@ -1818,7 +1819,9 @@ void destroy_comms(clipgpu_engine& e) {
 
 void destroy_replica(Replica& r) {
   (void)hipSetDevice(r.device);
-  if (r.stream) (void)hipStreamSynchronize(r.stream);
+  // every stream of the replica (lanes, copy streams: a device-path call's forks may still run) is idle
+  // before its memory goes
+  (void)hipDeviceSynchronize();
   if (r.arena) (void)hipFree(r.arena);
   if (r.work) (void)hipFree(r.work);
   if (r.pin_in) (void)hipHostFree(r.pin_in);
@@ -2124,6 +2127,16 @@ int clipgpu_host_unregister(void* ptr) {
     std::lock_guard<std::mutex> lk(h.mu);
     for (size_t i = 0; i < h.r.size(); ++i)
       if (h.r[i].first == (uintptr_t)ptr) {
+        // no transfer of any device may still reference the range
+        int ndev = 0;
+        HIP_CHECK(hipGetDeviceCount(&ndev));
+        int cur = 0;
+        HIP_CHECK(hipGetDevice(&cur));
+        for (int d = 0; d < ndev; ++d) {
+          HIP_CHECK(hipSetDevice(d));
+          HIP_CHECK(hipDeviceSynchronize());
+        }
+        HIP_CHECK(hipSetDevice(cur));
         HIP_CHECK(hipHostUnregister(ptr));
         h.r.erase(h.r.begin() + (long)i);
         return;
@@ -2274,12 +2287,12 @@ int clipgpu_similarity(int device, const float* img, int64_t n_img, const float*
     char* d = nullptr;
     HIP_CHECK(hipMalloc((void**)&d, align256(bi) + align256(bt) + bo));
     float *di = (float*)d, *dt = (float*)(d + align256(bi)), *dO = (float*)(d + align256(bi) + align256(bt));
-    hipError_t err = hipMemcpy(di, img, bi, hipMemcpyHostToDevice);
-    if (err == hipSuccess) err = hipMemcpy(dt, txt, bt, hipMemcpyHostToDevice);
+    hipError_t err = copy_h2d(di, img, bi);
+    if (err == hipSuccess) err = copy_h2d(dt, txt, bt);
     if (err == hipSuccess)
       err = launch_similarity(di, (int)n_img, dt, (int)n_txt, (int)E, logit_scale, logit_bias, activation, axis, dO,
                               nullptr);
-    if (err == hipSuccess) err = hipMemcpy(out, dO, bo, hipMemcpyDeviceToHost);
+    if (err == hipSuccess) err = copy_d2h(out, dO, bo);
     (void)hipFree(d);
     check(err, "similarity");
   });
@@ -2384,11 +2397,11 @@ int clipgpu_test_resize_rgb8_gpu(const uint8_t* const* images, const int* widths
     HIP_CHECK(hipMalloc((void**)&dev, host.size()));
     HIP_CHECK(hipMalloc((void**)&tmp, std::max<size_t>(b.tmp_bytes, 16)));
     HIP_CHECK(hipMalloc((void**)&dout, out_bytes));
-    HIP_CHECK(hipMemcpy(dev, host.data(), host.size(), hipMemcpyHostToDevice));
+    HIP_CHECK(copy_h2d(dev, host.data(), host.size()));
     const hipError_t err = launch_resize((const uint8_t*)dev + desc_bytes + ints_bytes, tmp,
                                          (const int*)(dev + desc_bytes), (const ResizeImage*)dev, (int)n, b.max_th,
                                          size, dout, nullptr);
-    const hipError_t err2 = hipMemcpy(out, dout, out_bytes, hipMemcpyDeviceToHost);
+    const hipError_t err2 = copy_d2h(out, dout, out_bytes);
     (void)hipFree(dev);
     (void)hipFree(tmp);
     (void)hipFree(dout);

@@ -9,6 +9,7 @@
 
 #include "../../include/clipgpu.h"
 #include "../../include/clipgpu_testing.h"
+#include "bounce.hpp"
 #include "host/api_util.hpp"
 #include "kernels/common.hpp"
 #include "kernels/kernels.hpp"
@@ -64,8 +65,8 @@ __global__ void clock_probe_kernel(unsigned long long* out, unsigned long long t
   if (lane < 2) out[lane] = lane == 0 ? t1 - t0 : r - r0;
 }
 
-void up(void* d, const void* h, size_t n) { TCHECK(hipMemcpy(d, h, n, hipMemcpyHostToDevice)); }
-void down(void* h, const void* d, size_t n) { TCHECK(hipMemcpy(h, d, n, hipMemcpyDeviceToHost)); }
+void up(void* d, const void* h, size_t n) { TCHECK(copy_h2d(d, h, n)); }
+void down(void* h, const void* d, size_t n) { TCHECK(copy_d2h(h, d, n)); }
 
 // f32 host -> 16-bit device
 void up16(DType dt, void* d16, const float* h, size_t n) {
