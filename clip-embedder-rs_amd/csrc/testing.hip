@@ -313,7 +313,8 @@ int clipgpu_test_gemm_bench_ld(int dtype, int epi, int act, int64_t M, int64_t N
     g.A = dA.p; g.lda = lda; g.W = dW.p; g.ldw = ldw; g.bias = dB.as<float>();
     g.out = dO.p; g.ldo = N; g.M = (int)M; g.N = (int)N; g.K = (int)K; g.tile = tile;
     if (tile != 0 && tile != TILE_SKINNY && !gemm_tile_built(tile)) throw ClipErr(CLIPGPU_ERR_INVALID, "not a built tile");
-    const int e = epi == 1 ? EPI_RESID : (epi == 2 ? EPI_STORE32 : EPI_STORE16);
+    const int e = (epi == 1 || epi == 3) ? EPI_RESID : (epi == 2 ? EPI_STORE32 : EPI_STORE16);
+    g.x16 = epi == 3;  // the f16 residual stream (its random f32 fill read as f16: timing only)
     for (int i = 0; i < 3; ++i) TCHECK(launch_gemm(dt, A_ROWS, e, epi == 0 ? act : 0, g, nullptr));
     hipEvent_t a, b;
     TCHECK(hipEventCreate(&a));

@@ -65,7 +65,7 @@ int clipgpu_test_patch_rows(int dtype, int mode, int64_t B, int64_t S, int64_t P
                             const float mean[3], const float std[3], float* rows_out);
 
 /* Device-resident GEMM timing (random operands): `iters` back-to-back launches of the same
- * GEMM as the engine issues it (epi: 0 store16 (+act), 1 residual f32, 2 store32), tile: a GemmTile
+ * GEMM as the engine issues it (epi: 0 store16 (+act), 1 residual f32, 2 store32, 3 residual f16), tile: a GemmTile
  * id (kernels.hpp; 0 auto).  Returns the mean µs per launch (HIP events). */
 int clipgpu_test_gemm_bench(int dtype, int epi, int act, int64_t M, int64_t N, int64_t K, int tile, int iters,
                             double* us_per_launch);

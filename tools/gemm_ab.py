@@ -2,7 +2,7 @@
 """Interleaved A/B of GEMM tiles at one shape, in one process (cdna_hip_programming.md §5.4
 rule 24): ROUNDS rounds, every tile once per round, median and min µs per tile.
 usage: gemm_ab.py M N K epi act tile[,tile...] [rounds] [iters]
-epi: 0 store16 (+act), 1 residual f32, 2 store32; tiles: kernels.hpp GemmTile ids."""
+epi: 0 store16 (+act), 1 residual f32, 2 store32, 3 residual f16; tiles: kernels.hpp GemmTile ids."""
 import ctypes
 import os
 import statistics
