@@ -1537,10 +1537,17 @@ void run_host(clipgpu_engine& e, InKind kind, const HostRows& src, int64_t B, co
 // pixels) pipelined over the lane slots as run_host_shard does.
 constexpr size_t kChunkRawBytes = 256u << 20;
 
+// The staged source of an image is only the window its resize reads (round 6): the horizontal pass reads
+// source rows [yfirst, yfirst + th) and, over all its outputs, columns [x0, x1) -- a 640x480 image cropped
+// to its centre square needs 486 of its 640 columns; a vertical-only plan (width already S) reads rows
+// [y0, y1).  The descriptor and the tap bounds are shifted to the window, so every output reads the same
+// pixels with the same coefficients (bit-identical to the host resize).
 struct ResizeBatch {
   std::vector<ResizeImage> d;
   std::vector<int> ints;
   std::vector<size_t> raw_off;  // per image, in the raw region
+  struct Window { int y0, rows, x0, cols; };
+  std::vector<Window> win;      // per image: the source window staged
   size_t raw_bytes = 0, tmp_bytes = 0;
   int max_th = 0;
 };
@@ -1552,6 +1559,7 @@ ResizeBatch plan_resize_batch(int S, const std::string& interp, const std::strin
   ResizeBatch b;
   b.d.resize(n);
   b.raw_off.resize(n);
+  b.win.resize(n);
   for (int i = 0; i < n; ++i) {
     const ResizePlan p = make_resize_plan(W[i0 + i], H[i0 + i], S, interp, mode);
     ResizeImage& d = b.d[i];
@@ -1569,18 +1577,46 @@ ResizeBatch plan_resize_batch(int S, const std::string& interp, const std::strin
       b.ints.insert(b.ints.end(), v.begin(), v.end());
       return off;
     };
-    d.h_bounds = put(p.h.bounds);
+    ResizeBatch::Window w{0, p.H, 0, p.W};
+    std::vector<int> hb = p.h.bounds, vb = p.v.bounds;
+    if (p.need_h && p.th > 0 && !hb.empty()) {  // rows [yfirst, yfirst + th), the columns the taps read
+      int x0 = hb[0], x1 = hb[0] + hb[1];
+      for (size_t o = 0; o + 1 < hb.size(); o += 2) {
+        x0 = std::min(x0, hb[o]);
+        x1 = std::max(x1, hb[o] + hb[o + 1]);
+      }
+      for (size_t o = 0; o < hb.size(); o += 2) hb[o] -= x0;
+      w = {p.yfirst, p.th, x0, x1 - x0};
+      d.W = w.cols;
+      d.yfirst = 0;
+    } else if (!p.need_h && p.need_v && !vb.empty()) {  // the rows the vertical taps read, all S columns
+      int y0 = vb[0], y1 = vb[0] + vb[1];
+      for (size_t o = 0; o + 1 < vb.size(); o += 2) {
+        y0 = std::min(y0, vb[o]);
+        y1 = std::max(y1, vb[o] + vb[o + 1]);
+      }
+      for (size_t o = 0; o < vb.size(); o += 2) vb[o] -= y0;
+      w = {y0, y1 - y0, 0, p.W};
+    }
+    b.win[i] = w;
+    d.h_bounds = put(hb);
     d.h_coef = put(std::vector<int>(p.h.k.begin(), p.h.k.end()));
-    d.v_bounds = put(p.v.bounds);
+    d.v_bounds = put(vb);
     d.v_coef = put(std::vector<int>(p.v.k.begin(), p.v.k.end()));
     b.raw_off[i] = b.raw_bytes;
     d.src = (long)b.raw_bytes;  // relative to the raw region
-    b.raw_bytes = align16(b.raw_bytes + (size_t)p.W * p.H * 3);
+    b.raw_bytes = align16(b.raw_bytes + (size_t)w.rows * w.cols * 3);
     d.tmp = (long)b.tmp_bytes;
     if (p.need_h) b.tmp_bytes = align16(b.tmp_bytes + (size_t)p.th * S * 3);
     b.max_th = std::max(b.max_th, d.th);
   }
   return b;
+}
+
+// Copy tasks that stage image i's window (src: its full [H][W][3] pixels, W its width) at dst.
+void add_window_tasks(std::vector<CopyTask>& t, const ResizeBatch& b, int i, char* dst, const uint8_t* src, int W) {
+  const ResizeBatch::Window& w = b.win[i];
+  add_copy_tasks_2d(t, dst, src + ((size_t)w.y0 * W + w.x0) * 3, (size_t)w.cols * 3, (size_t)w.rows, (size_t)W * 3);
 }
 
 void grow_pinned(char*& p, size_t& cap, size_t need) {
@@ -1649,14 +1685,9 @@ void run_images_shard(clipgpu_engine& e, Replica& r, const uint8_t* const* image
       int i1 = i0 + 1;
       while (i1 < n && b.raw_off[i1] - b.raw_off[i0] < kStagePiece) ++i1;
       const size_t p0 = b.raw_off[i0], p1 = i1 < n ? b.raw_off[i1] : b.raw_bytes;
-      if (i1 - i0 == 1) {
-        pool_memcpy(raw_pin + p0, images[c0 + i0], (size_t)W[c0 + i0] * H[c0 + i0] * 3);
-      } else {
-        CopyPool::instance().run(i1 - i0, [&](int t) {
-          const int i = i0 + t;
-          std::memcpy(raw_pin + b.raw_off[i], images[c0 + i], (size_t)W[c0 + i] * H[c0 + i] * 3);
-        });
-      }
+      std::vector<CopyTask> tasks;
+      for (int i = i0; i < i1; ++i) add_window_tasks(tasks, b, i, raw_pin + b.raw_off[i], images[c0 + i], W[c0 + i]);
+      pool_copy(tasks);
       HIP_CHECK(hipMemcpyAsync(sl.dev + head + p0, raw_pin + p0, p1 - p0, hipMemcpyHostToDevice, r.copy));
       i0 = i1;
     }
@@ -2390,7 +2421,11 @@ int clipgpu_test_resize_rgb8_gpu(const uint8_t* const* images, const int* widths
     std::memcpy(host.data(), b.d.data(), b.d.size() * sizeof(ResizeImage));
     std::memcpy(host.data() + desc_bytes, b.ints.data(), b.ints.size() * sizeof(int));
     for (int64_t i = 0; i < n; ++i)
-      std::memcpy(host.data() + desc_bytes + ints_bytes + b.raw_off[i], images[i], (size_t)widths[i] * heights[i] * 3);
+    {
+      std::vector<CopyTask> tasks;
+      add_window_tasks(tasks, b, (int)i, host.data() + desc_bytes + ints_bytes + b.raw_off[i], images[i], widths[i]);
+      pool_copy(tasks);
+    }
     char* dev = nullptr;
     uint8_t *tmp = nullptr, *dout = nullptr;
     const size_t out_bytes = (size_t)n * size * size * 3;

@@ -72,25 +72,45 @@ void CopyPool::run(int n, const std::function<void(int)>& f) {
   cur_ = nullptr;
 }
 
-void pool_memcpy(void* dst, const void* src, size_t n) {
-  constexpr size_t kPiece = 1u << 20;
-  if (n < 2 * kPiece) {
-    std::memcpy(dst, src, n);
+void add_copy_tasks(std::vector<CopyTask>& t, void* dst, const void* src, size_t n) {
+  for (size_t o = 0; o < n; o += kCopyTask)
+    t.push_back({(char*)dst + o, (const char*)src + o, std::min(kCopyTask, n - o), 1, 0});
+}
+
+void add_copy_tasks_2d(std::vector<CopyTask>& t, void* dst, const void* src, size_t row_bytes, size_t rows,
+                       size_t sstride) {
+  if (sstride == row_bytes) {
+    add_copy_tasks(t, dst, src, row_bytes * rows);
     return;
   }
-  const int pieces = (int)((n + kPiece - 1) / kPiece);
-  CopyPool::instance().run(pieces, [&](int i) {
-    const size_t o = (size_t)i * kPiece;
-    std::memcpy((char*)dst + o, (const char*)src + o, std::min(kPiece, n - o));
+  const size_t per = std::max<size_t>(1, kCopyTask / std::max<size_t>(row_bytes, 1));
+  for (size_t r = 0; r < rows; r += per)
+    t.push_back({(char*)dst + r * row_bytes, (const char*)src + r * sstride, row_bytes, std::min(per, rows - r),
+                 sstride});
+}
+
+void pool_copy(const std::vector<CopyTask>& t) {
+  CopyPool::instance().run((int)t.size(), [&](int i) {
+    const CopyTask& c = t[i];
+    for (size_t r = 0; r < c.rows; ++r)
+      std::memcpy((char*)c.dst + r * c.n, (const char*)c.src + r * c.sstride, c.n);
   });
 }
 
-void pool_gather(void* dst, const void* const* rows, size_t row, int n) {
-  if ((size_t)n * row < (2u << 20)) {
-    for (int i = 0; i < n; ++i) std::memcpy((char*)dst + (size_t)i * row, rows[i], row);
+void pool_memcpy(void* dst, const void* src, size_t n) {
+  if (n < 2 * kCopyTask) {
+    std::memcpy(dst, src, n);
     return;
   }
-  CopyPool::instance().run(n, [&](int i) { std::memcpy((char*)dst + (size_t)i * row, rows[i], row); });
+  std::vector<CopyTask> t;
+  add_copy_tasks(t, dst, src, n);
+  pool_copy(t);
+}
+
+void pool_gather(void* dst, const void* const* rows, size_t row, int n) {
+  std::vector<CopyTask> t;
+  for (int i = 0; i < n; ++i) add_copy_tasks(t, (char*)dst + (size_t)i * row, rows[i], row);
+  pool_copy(t);
 }
 
 }  // namespace clipgpu

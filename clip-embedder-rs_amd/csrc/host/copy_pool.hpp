@@ -42,7 +42,25 @@ class CopyPool {
   std::vector<std::thread> th_;
 };
 
-// memcpy split into 1 MiB pieces over the pool (a plain memcpy below 2 MiB).
+// Copies are cut into tasks of at most kCopyTask bytes (enough tasks to keep every worker busy on a
+// 4 MiB staging piece; round 6 first used 1 MiB tasks, which left 12 of 16 workers idle there).
+constexpr size_t kCopyTask = 256u << 10;
+// `rows` rows of n bytes: source rows `sstride` bytes apart, destination rows packed (n apart).
+struct CopyTask {
+  void* dst;
+  const void* src;
+  size_t n;
+  size_t rows = 1, sstride = 0;
+};
+// Appends dst[0 .. n) = src[0 .. n) as tasks of <= kCopyTask bytes.
+void add_copy_tasks(std::vector<CopyTask>& t, void* dst, const void* src, size_t n);
+// Appends a 2-D copy (rows of row_bytes, source rows sstride bytes apart, packed destination) as tasks
+// of whole rows, <= kCopyTask bytes each where a row allows.
+void add_copy_tasks_2d(std::vector<CopyTask>& t, void* dst, const void* src, size_t row_bytes, size_t rows,
+                       size_t sstride);
+// Runs the tasks over the pool (inline when there is only one).
+void pool_copy(const std::vector<CopyTask>& t);
+// memcpy over the pool (a plain memcpy below 2 tasks' worth).
 void pool_memcpy(void* dst, const void* src, size_t n);
 // dst[i * row .. +row) = rows[i][0 .. row) for i < n, over the pool.
 void pool_gather(void* dst, const void* const* rows, size_t row, int n);

@@ -318,9 +318,10 @@ def lnf_case(M, N, K, seed):
                                        (6400, 3072, 768, 1), (12801, 1536, 512, 0), (1000, 2048, 512, 2)])
 def test_layernorm_folded_gemm(M, N, K, act):
     """EPI_LNF (ln_1 / ln_2 folded into QKV / c_fc): every tile -- and the skinny kernel at M <= 256 --
-    gives the same bits (the row statistics are accumulated from the MFMA A fragments in the same
-    K order everywhere), and the result matches LayerNorm-then-Linear in fp64 within the bf16
-    output rounding plus the f16 rounding of W diag(gamma) (|err| <= 2^-7 |ref| + 0.01 rms(ref))."""
+    gives the same bits (each row's (mean, rstd) come from the statistics pass, launch_ln_stats, and
+    every tile runs the same K-ordered MFMA chain and epilogue ops), and the result matches
+    LayerNorm-then-Linear in fp64 within the bf16 output rounding plus the f16 rounding of
+    W diag(gamma) (|err| <= 2^-7 |ref| + 0.01 rms(ref))."""
     x, w, gamma, beta, b, wf, cs, bp = lnf_case(M, N, K, M + N + act)
     eps = 1e-5
     tiles = [0] + BUILT_TILES + ([100] if M <= 256 else [])
