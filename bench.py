@@ -669,8 +669,9 @@ def main():
         text["lanes"] = t_lanes.value
         tout_host = tout.cpu().numpy()
         if world == 1 and not args.no_e2e:
-            text_e2e = {"text_ids_host": host_leg(te, "tokens", ids.cpu().numpy(), max(3, args.steps // 4)),
-                        "text_ids_host_registered": host_leg(te, "tokens", ids.cpu().numpy(), max(3, args.steps // 4),
+            ids_host = np.array(ids.cpu().numpy())  # a numpy-owned caller array, as a Rust caller's Vec
+            text_e2e = {"text_ids_host": host_leg(te, "tokens", ids_host, max(3, args.steps // 4)),
+                        "text_ids_host_registered": host_leg(te, "tokens", ids_host, max(3, args.steps // 4),
                                                              registered=True)}
         te.close()
 
@@ -680,12 +681,14 @@ def main():
     e2e = None
     if world == 1 and not args.no_e2e:
         g = torch.Generator(device="cpu").manual_seed(1000 + rank)
-        u8_host = torch.randint(0, 256, (B_VISION, 224, 224, 3), dtype=torch.uint8, generator=g).numpy()
+        # numpy-owned caller arrays (copies out of torch's CPU allocator), as a Rust caller's buffers
+        u8_host = np.array(torch.randint(0, 256, (B_VISION, 224, 224, 3), dtype=torch.uint8, generator=g).numpy())
+        px_host = np.array(px.cpu().numpy())
         n_e2e = max(3, args.steps // 4)
         e2e = {"vision_u8_host": host_leg(ve, "u8", u8_host, n_e2e),
                "vision_u8_host_registered": host_leg(ve, "u8", u8_host, n_e2e, registered=True),
-               "vision_f32_host": host_leg(ve, "f32", px.cpu().numpy(), n_e2e),
-               "vision_f32_host_registered": host_leg(ve, "f32", px.cpu().numpy(), n_e2e, registered=True)}
+               "vision_f32_host": host_leg(ve, "f32", px_host, n_e2e),
+               "vision_f32_host_registered": host_leg(ve, "f32", px_host, n_e2e, registered=True)}
         # four consecutive 256-image batches in one call: the engine alternates two staging sets, so
         # batch i + 1's host copy and H2D run under batch i's forward (engine.hip run_host_shard)
         u8_4x = np.concatenate([u8_host, np.roll(u8_host, 1, axis=0), np.roll(u8_host, 2, axis=0),

@@ -2,6 +2,7 @@
 // device 0 over host f32 buffers so tests/ can check it against numpy.
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <exception>
@@ -10,6 +11,7 @@
 #include "../../include/clipgpu.h"
 #include "../../include/clipgpu_testing.h"
 #include "bounce.hpp"
+#include "host/copy_pool.hpp"
 #include "host/api_util.hpp"
 #include "kernels/common.hpp"
 #include "kernels/kernels.hpp"
@@ -461,6 +463,34 @@ int clipgpu_test_gemm_mx_bench(int epi, int act, int64_t M, int64_t N, int64_t K
     (void)hipEventDestroy(ea);
     (void)hipEventDestroy(eb);
     *us_per_launch = (double)ms * 1000.0 / iters;
+  });
+}
+
+int clipgpu_test_host_copy(int64_t bytes, int mode, int iters, double* us_per_copy) {
+  return guarded([&]() {
+    if (bytes <= 0 || iters <= 0 || !us_per_copy || mode < 0 || mode > 3)
+      throw ClipErr(CLIPGPU_ERR_INVALID, "bad host copy arguments");
+    // source: page-aligned malloc'd memory; destination: malloc'd (mode 0 / 1) or pinned hipHostMalloc
+    // memory (mode 2 / 3, the host path's staging); one thread (0 / 2) or the copy pool (1 / 3)
+    void* src = nullptr;
+    if (posix_memalign(&src, 4096, (size_t)bytes) != 0) throw ClipErr(CLIPGPU_ERR_INVALID, "host alloc");
+    std::memset(src, 3, (size_t)bytes);
+    void* dst = nullptr;
+    if (mode >= 2) TCHECK(hipHostMalloc(&dst, (size_t)bytes, hipHostMallocDefault));
+    else if (posix_memalign(&dst, 4096, (size_t)bytes) != 0) throw ClipErr(CLIPGPU_ERR_INVALID, "host alloc");
+    std::memset(dst, 0, (size_t)bytes);
+    auto once = [&]() {
+      if (mode & 1) pool_memcpy(dst, src, (size_t)bytes);
+      else std::memcpy(dst, src, (size_t)bytes);
+    };
+    once();
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int i = 0; i < iters; ++i) once();
+    const auto t1 = std::chrono::steady_clock::now();
+    *us_per_copy = std::chrono::duration<double, std::micro>(t1 - t0).count() / iters;
+    if (mode >= 2) (void)hipHostFree(dst);
+    else std::free(dst);
+    std::free(src);
   });
 }
 

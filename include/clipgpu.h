@@ -116,13 +116,17 @@ typedef struct clipgpu_options {
   int32_t residual;     /* storage of the residual stream x: 1 = f32; 2 = f16 (half the bytes of x's two
                            read-modify-writes and two LayerNorm reads per layer; every add into x and every
                            LayerNorm statistic stays f32; CLIP-family engines of every dtype, SigLIP
-                           CLIPGPU_ERR_INVALID); 0 = the default: f16 where it applies, else f32 */
+                           CLIPGPU_ERR_INVALID); 0 = the default: f16 where it applies, else f32.  f16 holds
+                           |x| <= 65504 (a larger value is stored as inf); CLIP / DFN residual streams stay in
+                           the hundreds (tests/test_gpu_parity.py test_massive_residual_channels_parity):
+                           choose 1 for a checkpoint whose stream exceeds that range */
   int32_t ln_fold;      /* ln_1 / ln_2 folded into the QKV / c_fc GEMMs (f16 residual stream only): the GEMM
                            reads x itself with W' = W diag(gamma) in f16 and applies each row's mean / rstd
-                           (accumulated from its MFMA operands) and bias + W beta in its epilogue -- no
-                           LayerNorm kernels in the trunk.  0 = the default: on where it applies (bf16 / f16
-                           engines, residual f16, QuickGELU / GELU MLP); 1 = on (CLIPGPU_ERR_INVALID where it
-                           does not apply); -1 = off (LayerNorm kernels + bf16 / f16 GEMMs) */
+                           and bias + W beta in its epilogue; the rows' (mean, rstd) come from a statistics-only
+                           pass (8 bytes per row) instead of a normalised copy of x.  0 = the default: on where
+                           it applies (bf16 / f16 engines, residual f16, QuickGELU / GELU MLP); 1 = on
+                           (CLIPGPU_ERR_INVALID where it does not apply); -1 = off (LayerNorm kernels + bf16 /
+                           f16 GEMMs) */
 } clipgpu_options;
 /* Fills *opts with the defaults. */
 int clipgpu_options_init(clipgpu_options* opts);
