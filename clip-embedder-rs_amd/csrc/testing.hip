@@ -3,6 +3,11 @@
 #include <hip/hip_runtime.h>
 
 #include <chrono>
+#include <csignal>
+#include <cstdio>
+#include <dlfcn.h>
+#include <execinfo.h>
+#include <unistd.h>
 #include <cstdlib>
 #include <cstring>
 #include <exception>
@@ -464,6 +469,43 @@ int clipgpu_test_gemm_mx_bench(int epi, int act, int64_t M, int64_t N, int64_t K
     (void)hipEventDestroy(eb);
     *us_per_launch = (double)ms * 1000.0 / iters;
   });
+}
+
+// Crash diagnostics for GPU-box runs (no debugger there): a SIGSEGV / SIGABRT handler that prints each
+// frame's object file and offset (map offsets to functions with addr2line -f -C -e <object> <offset>),
+// then re-raises with the default action.
+static void crash_handler(int sig) {
+  void* frames[64];
+  const int n = backtrace(frames, 64);
+  char line[512];
+  int len = snprintf(line, sizeof(line), "clipgpu crash handler: signal %d, %d frames\n", sig, n);
+  if (write(2, line, (size_t)len) < 0) {}
+  for (int i = 0; i < n; ++i) {
+    Dl_info info{};
+    if (dladdr(frames[i], &info) && info.dli_fname) {
+      len = snprintf(line, sizeof(line), "  #%d %s +0x%lx (%s)\n", i, info.dli_fname,
+                     (unsigned long)((char*)frames[i] - (char*)info.dli_fbase), info.dli_sname ? info.dli_sname : "?");
+    } else {
+      len = snprintf(line, sizeof(line), "  #%d %p\n", i, frames[i]);
+    }
+    if (write(2, line, (size_t)len) < 0) {}
+  }
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+
+int clipgpu_test_install_crash_handler(void) {
+  static char alt[1 << 16];  // the handler runs on its own stack, so a stack overflow is reported too
+  stack_t ss{};
+  ss.ss_sp = alt;
+  ss.ss_size = sizeof(alt);
+  sigaltstack(&ss, nullptr);
+  struct sigaction sa{};
+  sa.sa_handler = crash_handler;
+  sa.sa_flags = SA_ONSTACK;
+  sigaction(SIGSEGV, &sa, nullptr);
+  sigaction(SIGABRT, &sa, nullptr);
+  return 0;
 }
 
 int clipgpu_test_host_copy(int64_t bytes, int mode, int iters, double* us_per_copy) {

@@ -75,6 +75,8 @@ _PROTOS = [
     ("clipgpu_test_gemm_grid", c_int, [c_int, c_int64, c_int64, c_int64, POINTER(c_int)]),
     ("clipgpu_test_gemm_bench", c_int, [c_int, c_int, c_int, c_int64, c_int64, c_int64, c_int, c_int, POINTER(c_double)]),
     ("clipgpu_test_h2d_bench", c_int, [c_int64, c_int, c_int, POINTER(c_double)]),
+    ("clipgpu_test_host_copy", c_int, [c_int64, c_int, c_int, POINTER(c_double)]),
+    ("clipgpu_test_install_crash_handler", c_int, []),
     ("clipgpu_test_gemm_bench_ld", c_int, [c_int, c_int, c_int, c_int64, c_int64, c_int64, c_int64, c_int64, c_int, c_int,
                                            POINTER(c_double)]),
     ("clipgpu_test_engine_tiles", c_int, [c_void_p, POINTER(c_int)]),

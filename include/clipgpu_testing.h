@@ -81,6 +81,9 @@ int clipgpu_test_gemm_bench_ld(int dtype, int epi, int act, int64_t M, int64_t N
  * mode 0: std::memcpy into malloc'd memory; 1: the copy pool (pool_memcpy) into it; 2 / 3: the same
  * into pinned hipHostMalloc memory (the host path's staging). */
 int clipgpu_test_host_copy(int64_t bytes, int mode, int iters, double* us_per_copy);
+/* Installs a SIGSEGV / SIGABRT handler that prints the faulting thread's frames as object + offset
+ * (diagnostics for GPU-box runs), then re-raises. */
+int clipgpu_test_install_crash_handler(void);
 /* Shader-clock probe (bench.py's per-window clock): launches ONE wave on `stream` (a hipStream_t, NULL =
  * the legacy default stream) that sleeps for duration_us of wall time (s_memrealtime, 100 MHz) and writes
  * d_out[0] = shader-clock ticks (s_memtime) and d_out[1] = 100 MHz ticks elapsed over that span (device
