@@ -626,7 +626,8 @@ int clipgpu_diag_gemm_stamps(int dtype, int epi, int act, int64_t M, int64_t N, 
     GemmParams g{};
     g.A = dA.p; g.lda = K; g.W = dW.p; g.ldw = K; g.bias = dB.as<float>();
     g.out = dO.p; g.ldo = N; g.M = (int)M; g.N = (int)N; g.K = (int)K; g.tile = tile; g.diag = diag;
-    const int e = epi == 1 ? EPI_RESID : (epi == 2 ? EPI_STORE32 : EPI_STORE16);
+    const int e = (epi == 1 || epi == 3) ? EPI_RESID : (epi == 2 ? EPI_STORE32 : EPI_STORE16);
+    g.x16 = epi == 3;  // the f16 residual stream (timing only)
     for (int i = 0; i < 20; ++i) TCHECK(launch_gemm(dt, A_ROWS, e, epi == 0 ? act : 0, g, nullptr));
     TCHECK(hipDeviceSynchronize());
     TCHECK(read_gemm_stamps(nullptr, nblocks, true));

@@ -8,6 +8,8 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
+# steps: tests, tests_sel (PYTEST_SEL), smoke, bench, bench_quick, bench_pin (PIN_TILES), breakdown, prof,
+# vtrace, pmc, sweep, ab (AB_SPECS), ablate, timeline, host, stamps_gemm (STAMP_SPEC)
 STEPS=${STEPS:-tests bench prof}
 run() {  # name, limit, cmd...
   local name=$1 lim=$2; shift 2
@@ -26,7 +28,7 @@ for s in $STEPS; do
     tests_sel)  # PYTEST_SEL: test files / node ids
       run pytest_sel 900 python -u -m pytest ${PYTEST_SEL} -m gpu -v -s -rf -p no:cacheprovider --timeout 300 --timeout-method thread
       rc=$?; [ $rc -le 1 ] || exit $rc ;;
-    host)  # host facts the CPU baseline reads (num_cpus rule: affinity capped by the cgroup quota)
+    hostinfo)  # host facts the CPU baseline reads (num_cpus rule: affinity capped by the cgroup quota)
       { nproc; cat /sys/fs/cgroup/cpu.max 2>&1; cat /sys/fs/cgroup/cpu/cpu.cfs_quota_us 2>&1; echo "OMP=$OMP_NUM_THREADS"; } > gpurun_out/host.txt; cat gpurun_out/host.txt ;;
     sweep)
       run gemm_sweep 600 python tools/gemm_sweep.py || exit $? ;;
@@ -45,6 +47,15 @@ for s in $STEPS; do
       cp gpurun_out/ablate.log gpurun_out/ablate.jsonl ;;
     bench_quick)  # the bench without the CPU leg
       run bench_quick 400 python bench.py --steps 20 --warmup 5 --no-cpu-baseline || exit $? ;;
+    timeline)  # per-launch start / end of every trunk op with the lanes concurrent (tools/timeline.py)
+      for spec in "vision 5 0" "vision 5 1" "text 3 0"; do
+        run tl_$(echo $spec | tr ' ' _) 200 python tools/timeline.py $spec || exit $?
+      done ;;
+    host)  # host-side rates: copy pool, decoded-image entry point, u8 host path (tools/host_probe.py)
+      run host_probe 300 python tools/host_probe.py || exit $? ;;
+    stamps_gemm)  # K-step / epilogue cycles of one GEMM (needs lib/libclipgpu_stamps.so: make stamps;
+                  # STAMP_SPEC "M N K epi act tile")
+      CLIPGPU_LIB=$PWD/clip-embedder-rs_amd/lib/libclipgpu_stamps.so run stamps 300 python tools/gemm_stamps.py ${STAMP_SPEC} || exit $? ;;
     smoke)
       run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
     bench)
