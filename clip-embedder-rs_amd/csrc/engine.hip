@@ -1406,7 +1406,7 @@ void ensure_host_set2(const clipgpu_engine& e, Replica& r) {
 // so a lane's next forward starts right behind its last one.  Each round runs the same forward on the
 // same rows as a call of its own: the outputs are bit-identical.
 // (Round 6 removed the schedules measured and not kept -- lockstep, joined and device-path rounds, D2H
-// on the copy or lane streams, split and pulled H2Ds; DESIGN.md §6 keeps their numbers.)
+// on the copy or lane streams, split and pulled H2Ds; DESIGN.md §10 keeps their numbers.)
 constexpr size_t kStagePiece = 4u << 20;
 
 void run_host_shard(clipgpu_engine& e, Replica& r, InKind kind, const HostRows& src, int64_t b0, int64_t b1,

@@ -698,7 +698,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
     // the epilogue's stores (3 stages: all but the youngest step's pieces), so that the counted
     // wait after a full epilogue never relies on a store retiring after an older LDS-DMA (the
     // compiler's own wait insertion treats mixed pending VMEM reads and writes as unordered).
-    // DESIGN.md §5 "The 224x256 race-check failure" records what this was and was not.
+    // DESIGN.md §3 (race check) and §10 (round 3) record what this was and was not.
 #if CLIPGPU_GEMM_EPI_DMA_WAIT
     if constexpr (NS == 3) vm_wait_step(std::integral_constant<int, 0>{});
     else vm_wait<0>();
@@ -793,7 +793,7 @@ hipError_t launch_pipe_224(const GemmParams& p, hipStream_t s) {
 // (one K-step), 16-bit outputs whose row pitch is not a multiple of 8 elements -- at any M, with N
 // tails (clamped W rows, masked stores) and element stores where a row is not 4-aligned.  Round 6
 // removed the 128x128 "bt" kernel that used to take these shapes: its run-to-run wrong outputs
-// (one accumulator register of one lane quarter, DESIGN.md §5) were never root-caused, and this
+// (one accumulator register of one lane quarter, DESIGN.md §10) were never root-caused, and this
 // form gives the pipelined tiles' bits by construction (test_general_gemm_is_bit_exact).
 constexpr int SKINNY_MAX_M = 256;
 constexpr int SKINNY_U = 8;

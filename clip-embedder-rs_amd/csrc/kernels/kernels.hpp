@@ -57,12 +57,12 @@ struct GemmParams {
 };
 
 // Tile configurations of the MFMA GEMM.  Ids are stable across rounds; the ones not listed were
-// experiment tiles that never won a site (round 4 removed them from the library: DESIGN.md §5 keeps
+// experiment tiles that never won a site (round 4 removed them from the library: DESIGN.md §10 keeps
 // their measurements): 4-12 and 16 (4- / 8-wave 128-192-row variants), 19-20 (ping-pong schedule),
 // 21-25 (32x32x16 MFMA), 27 (spread-DMA 224x192).
 enum GemmTile {
   TILE_AUTO = 0,
-  // (1: the 128x128 "bt" kernel, removed in round 6 -- run-to-run wrong outputs, DESIGN.md §5; its
+  // (1: the 128x128 "bt" kernel, removed in round 6 -- run-to-run wrong outputs, DESIGN.md §10; its
   // shapes, K < 128 and unaligned 16-bit rows, run the skinny kernel's general form)
   TILE_256x128 = 2,       // gemm_pipe_kernel: 8 waves (4x2, 64x64 each), 96 KiB LDS (shape heuristic)
   TILE_256x256 = 3,       // gemm_pipe_kernel: 8 waves (2x4, 128x64 each), 128 KiB LDS (shape heuristic)

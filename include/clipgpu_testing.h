@@ -142,7 +142,7 @@ int clipgpu_test_engine_residual(const struct clipgpu_engine* e, int* residual, 
 /* The host-buffer vision path's chunk plan (tools/host_plan_ab.py): n_chunks (1..4) chunks of a
  * max_batch round cut at bounds[0 .. n_chunks - 2]; n_chunks = 0 restores the default
  * (engine.hip host_chunks).  copy_stream must be 0 or 1 (round 6 removed the schedule variants it
- * used to select; DESIGN.md §6 keeps their measurements).  Speed only, never the bits. */
+ * used to select; DESIGN.md §10 keeps their measurements).  Speed only, never the bits. */
 int clipgpu_test_host_plan(struct clipgpu_engine* e, int n_chunks, const int* bounds, int copy_stream);
 /* on != 0: clipgpu_embed_images_rgb8 sends batches of image_size x image_size images through the GPU
  * resize path too (by default they take the u8 host path: their resize plan is the identity).  The

@@ -143,7 +143,7 @@ def test_torch_cpu_port_matches_oracle(cfg_name):
 
 
 def test_layernorm_fold_identity():
-    """The algebra behind the engine's LayerNorm fold (EPI_LNF, DESIGN.md §5 round 5): for a Linear
+    """The algebra behind the engine's LayerNorm fold (EPI_LNF, DESIGN.md §8): for a Linear
     W, b behind LayerNorm (gamma, beta), LN(x) W^T + b = rstd (x W'^T - mean cs) + (b + W beta) with
     W' = W diag(gamma), cs = W' 1, mean / rstd of each row of x.  Checked in fp64 on the oracle's
     own LayerNorm (`clip_ref.layer_norm`) and on residual-stream-like rows (per-row offsets, a few

@@ -5,7 +5,7 @@ inline-asm lgkmcnt wait; nothing stops the register allocator from touching a de
 (a spill store, a copy) between the two, which reads the register before the LDS data arrives.
 tools/check_lds_waits.py scans every kernel's control-flow graph for such a use.  Round 3 found
 exactly this in the race-check build of a dropped 224x256 tile (its extra instrumentation pushed
-the kernel to 224 spilled registers, DESIGN.md §5), so the check runs on the product library AND
+the kernel to 224 spilled registers, DESIGN.md §3), so the check runs on the product library AND
 on the race-check library whose verdicts the GPU tests trust.
 """
 import os

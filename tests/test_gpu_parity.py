@@ -361,7 +361,7 @@ def test_chunked_gemm_launches_are_bit_exact(tower):
 
 
 def test_removed_bt_tile_pin_is_refused():
-    """Tile 1 (the 128x128 bt kernel, removed in round 6: run-to-run wrong outputs, DESIGN.md §5) is no
+    """Tile 1 (the 128x128 bt kernel, removed in round 6: run-to-run wrong outputs, DESIGN.md §10) is no
     longer a built tile: a pin of it fails at creation instead of running a kernel that is gone."""
     from open_clip_inference.error import ClipError
     with pytest.raises(ClipError):
@@ -610,7 +610,7 @@ def test_massive_residual_channels_parity(cfg, tower, B):
     """The f16 residual stream + LayerNorm fold (the CLIP-family default, round 5) on real-like
     activations: three channels carry 300 + 12 per layer in every token (up to
     ~690 in ViT-H/14's 32 layers).  Both storages against the fp64 oracle at the north-star 0.9999,
-    and the f16 default within 2e-5 of the f32 stream's cosine; the cosines are in DESIGN.md §8."""
+    and the f16 default within 2e-5 of the f32 stream's cosine; the cosines are in DESIGN.md §3."""
     from open_clip_inference.engine import Engine
     v, t = specs(cfg)
     w = _massive_weights(cfg, tower)

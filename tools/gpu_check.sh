@@ -55,7 +55,7 @@ for s in $STEPS; do
       run host_probe 300 python tools/host_probe.py || exit $? ;;
     stamps_gemm)  # K-step / epilogue cycles of one GEMM (needs lib/libclipgpu_stamps.so: make stamps;
                   # STAMP_SPEC "M N K epi act tile")
-      CLIPGPU_LIB=$PWD/clip-embedder-rs_amd/lib/libclipgpu_stamps.so run stamps 300 python tools/gemm_stamps.py ${STAMP_SPEC} || exit $? ;;
+      CLIPGPU_LIB=$PWD/clip-embedder-rs_amd/lib/libclipgpu_stamps.so run stamps 300 python tools/gemm_stamps.py ${STAMP_SPEC:-} || exit $? ;;
     smoke)
       run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
     bench)
