@@ -166,7 +166,9 @@ def test_gemm_pipelines_never_read_a_stage_before_its_dma_lands(M, N, K, mode, a
 
 
 @pytest.mark.parametrize("M,N,K,mode", [(12800, 768, 3072, 1), (12800, 768, 768, 1), (12801, 776, 3072, 1),
-                                        (1000, 768, 128, 1), (6400, 768, 3072, 2), (12800, 3072, 768, 0)])
+                                        (1000, 768, 128, 1), (6400, 768, 3072, 2), (12800, 3072, 768, 0),
+                                        (6400, 768, 3072, 3), (6400, 768, 768, 3), (20000, 768, 768, 3),
+                                        (12801, 776, 3072, 3), (1000, 768, 320, 3), (1000, 768, 256, 3)])
 def test_224x192_residual_tile_is_bit_exact(M, N, K, mode, monkeypatch):
     """TILE_224x192_W8 (26: 3 LDS stages with an uneven DMA piece split, 52 pieces over 8 waves, so
     per-wave counted waits) with the NI = 3 column permutation and W swizzle
@@ -174,12 +176,14 @@ def test_224x192_residual_tile_is_bit_exact(M, N, K, mode, monkeypatch):
     to the table's 160x128 tile 17 at the ViT-B/32 residual shapes (one round of 232 tiles), with M / N
     tails, 2 K-steps (the 2-stage fallback), and a persistent multi-tile walk through the 3-stage
     pipeline with the 16-bit QuickGELU epilogue (12800 x 3072: 928 tiles over 256 blocks); the race-check
-    build gives the same bits."""
+    build gives the same bits.  Mode 3: the f16 residual stream (the engines' default) at the lane shapes
+    of out_proj / c_proj (one tile per block), a persistent walk (20000 rows: 360 tiles over 256 blocks),
+    M / N tails and short K."""
     rng = np.random.default_rng(M + N + K + mode)
     A = np.ascontiguousarray(round16(rng.standard_normal((M, K)), BF16))
     W = np.ascontiguousarray(round16(rng.standard_normal((N, K)) / np.sqrt(K), BF16))
     bias = rng.standard_normal(N).astype(np.float32)
-    resid = rng.standard_normal((M, N)).astype(np.float32) if mode == 1 else None
+    resid = rng.standard_normal((M, N)).astype(np.float32) if mode in (1, 3) else None
     act = 1 if mode == 0 else 0
     monkeypatch.setenv("CLIPGPU_TEST_TILE", "17")
     want = run_gemm(BF16, mode, act, A, W, bias, resid)
