@@ -106,6 +106,8 @@ constexpr int BK = 64;
 
 template <typename T>
 __device__ __forceinline__ T to16(float v) { return (T)v; }
+__device__ __forceinline__ float4 widen4(float4 v) { return v; }
+__device__ __forceinline__ float4 widen4(f16x4 h) { return make_float4((float)h[0], (float)h[1], (float)h[2], (float)h[3]); }
 
 // ---------------------------------------------------------------------------
 // Software-pipelined GEMM for row-major A (the trunk GEMMs; K >= 128).
@@ -296,18 +298,27 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
     d_n0 = n0;
     d_m0 = m0;
   }
+  // A piece's issue is branch-free scalar work the compiler shares across the step's pieces: the stage
+  // base (d_stage, rotated instead of d_g % NS), the K-step's source bases, a wave-uniform per-piece
+  // LDS offset.  Only piece NP - 1 can fall past the PT pieces (uneven splits: waves >= PT % NW skip
+  // it).  (Round 6: the per-piece branches and modulos cost ~15 scalar instructions a piece, ~105 per
+  // K-step and wave on the 224x192 tile -- as many issue slots as its 42 MFMAs.)
+  const bool last_piece = EVEN || wave < PT % NW;
+  int d_stage = 0;  // d_g % NS
   auto dma_piece = [&](auto ic) {
     constexpr int i = decltype(ic)::value;
-    const int q = wave + NW * i;
-    if (!EVEN && q >= PT) return;
+    if constexpr (!EVEN && i == NP - 1) {
+      if (!last_piece) return;
+    }
 #ifdef CLIPGPU_GEMM_STAMPS
     if (p.diag & 4) return;  // timing experiment: no operand DMA in the loop (stale LDS tiles)
 #endif
-    char* const st = smem + (d_g % NS) * STAGE;
-    char* const dst = piece_is_w(i, q) ? st + A_BYTES + q * 1024 : st + (q - PW) * 1024;
+    const int q = wave + NW * i;
+    const bool w = piece_is_w(i, q);
+    char* const dst = smem + d_stage * STAGE + (w ? A_BYTES + q * 1024 : (q - PW) * 1024);
+    const char* const src = (w ? Wb : Ab) + (size_t)d_kt * (BK * 2);
     GEMM_POISON(dst);
-    if (piece_is_w(i, q)) glds16(Wb + (size_t)d_kt * (BK * 2) + poff[i], dst);
-    else glds16(Ab + (size_t)d_kt * (BK * 2) + poff[i], dst);
+    glds16(src + poff[i], dst);
   };
   auto dma_bias = [&]() {  // the tile's bias slice, with its first K-step (tile-parity buffer)
     if (bias_p != nullptr && wave == 0 && d_kt == 0) {
@@ -328,6 +339,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
   };
   auto dma_advance = [&]() {
     ++d_g;
+    if (++d_stage == NS) d_stage = 0;
     if (++d_kt == nk) {
       d_kt = 0;
       d_t += t_stride;
@@ -519,13 +531,15 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
     constexpr bool XALL = MI * NI <= (NW == 8 ? (OCC >= 2 ? 4 : 12) : 20);
     constexpr int XRING = (NW == 8 && OCC < 2 && MI * NI <= 24) ? 3 : 2;
     constexpr int XR = XALL ? MI : (XRING < MI ? XRING : MI);
-    float4 xr[XR][NI];
-    auto load_x = [&](int mi, float4(&dst)[NI]) {
+    // (the f16 residual rows stay f16 in the ring, 2 registers per 4 columns, widened at the add)
+    typedef typename std::conditional<EPI == EPI_RESID16, f16x4, float4>::type XV;
+    XV xr[XR][NI];
+    auto load_x = [&](int mi, XV(&dst)[NI]) {
       const int m = m0 + wm_cur + mi * 16 + fr;
       if (m < p.M && nfull && (!HM || mi < mi_lim)) {
         const auto src = add_src(m);
 #pragma unroll
-        for (int ni = 0; ni < NI; ++ni) dst[ni] = ldx4(src + ni * 4);
+        for (int ni = 0; ni < NI; ++ni) dst[ni] = *(const XV*)(src + ni * 4);
       }
     };
     if constexpr (ADDX) {
@@ -604,7 +618,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
           for (int ni = 0; ni < NI; ++ni) {
             float4 w = make_float4(v[ni][0], v[ni][1], v[ni][2], v[ni][3]);
             if constexpr (ADDX) {
-              const float4 x = xr[XALL ? mi : mi % XR][ni];
+              const float4 x = widen4(xr[XALL ? mi : mi % XR][ni]);
               w.x += x.x; w.y += x.y; w.z += x.z; w.w += x.w;
             }
             stx4(o + ni * 4, w);
@@ -658,6 +672,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
   GEMM_STAMP(1);
 
   int g = 0;
+  int gs = 0;  // g % NS
   bool after_full_epi = false;
   int ti = 0;
   for (int t = t_first; t < t_end; t += t_stride, ++ti) {
@@ -666,7 +681,8 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
     GEMM_STAMP(2 + ti * 4);
     for (int kt = 0; kt < nk; ++kt, ++g) {
       if (kt + 1 == nk) GEMM_STAMP(3 + ti * 4);
-      const uint32_t buf = lds0 + (g % NS) * STAGE;
+      const int gs1 = gs + 1 == NS ? 0 : gs + 1;
+      const uint32_t buf = lds0 + gs * STAGE;
       if (kt == 0) phase0(std::true_type{}, buf);
       else phase0(std::false_type{}, buf);
       // the DMA of step g+1 has landed once at most the later ops are outstanding: the
@@ -690,7 +706,8 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
 #else
       __builtin_amdgcn_s_barrier();
 #endif
-      phase1(kt + 1 < nk, lds0 + ((g + 1) % NS) * STAGE);
+      phase1(kt + 1 < nk, lds0 + gs1 * STAGE);
+      gs = gs1;
       if (ti == 0 && kt + 1 < nk && 34 + kt < 61) GEMM_STAMP(34 + kt);  // (slots 61-63: HW_ID, realtime)
     }
     GEMM_STAMP(4 + ti * 4);
@@ -708,7 +725,7 @@ __global__ __launch_bounds__(WGM* WGN * 64, (PipeBounds<WGM * WGN, OCC>::waves_p
     after_full_epi = m0 + BM <= p.M && n0 + BN <= p.N && (!HM || t < hm_F);
     if (!after_full_epi) vm_wait<0>();
     if (t + t_stride < t_end) {  // the next tile's step 0 landed at the last barrier
-      const uint32_t buf = lds0 + (g % NS) * STAGE;
+      const uint32_t buf = lds0 + gs * STAGE;
       set_layout(t + t_stride);
       read_b(b0, buf, 0);
       read_a(a0, buf, 0);

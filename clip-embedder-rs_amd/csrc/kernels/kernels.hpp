@@ -59,7 +59,8 @@ struct GemmParams {
 // Tile configurations of the MFMA GEMM.  Ids are stable across rounds; the ones not listed were
 // experiment tiles that never won a site (round 4 removed them from the library: DESIGN.md §10 keeps
 // their measurements): 4-12 and 16 (4- / 8-wave 128-192-row variants), 19-20 (ping-pong schedule),
-// 21-25 (32x32x16 MFMA), 27 (spread-DMA 224x192).
+// 21-25 (32x32x16 MFMA), 27 (spread-DMA 224x192), 28 (224x192 at 4 waves of 112x96, one per SIMD: the
+// same speed as 26, round 6).
 enum GemmTile {
   TILE_AUTO = 0,
   // (1: the 128x128 "bt" kernel, removed in round 6 -- run-to-run wrong outputs; its
