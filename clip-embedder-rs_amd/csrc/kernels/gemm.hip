@@ -100,6 +100,9 @@ constexpr int BK = 64;
 #ifndef CLIPGPU_GEMM_SPREAD_ALL
 #define CLIPGPU_GEMM_SPREAD_ALL 0
 #endif
+#ifndef CLIPGPU_GEMM_NONPERSIST
+#define CLIPGPU_GEMM_NONPERSIST 0
+#endif
 #ifndef CLIPGPU_GEMM_EPI_DMA_WAIT
 #define CLIPGPU_GEMM_EPI_DMA_WAIT 1
 #endif
@@ -747,6 +750,7 @@ inline int pipe_grid(int BM, int BN, int NW, int OCC, int M, int N) {
   const int lds = 2 * (BM + BN) * BK * 2 + 2048;
   const int per_cu = std::max(1, std::min(NW == 8 ? pipe_kocc(NW, OCC) : OCC, (160 * 1024) / lds));
   const int resident = device_cus() * per_cu;
+  if (CLIPGPU_GEMM_NONPERSIST) return ntiles;  // (A/B build: one tile per block)
   return ntiles <= resident ? ntiles : resident;
 }
 // Half-tile last round for the 256x256 RS tile: applies when every XCD has >= 1 whole round and at
