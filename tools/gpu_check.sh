@@ -84,7 +84,7 @@ for s in $STEPS; do
       for SITE in c_fc c_proj out_proj; do  # every site with a record; the bench reads its roofline kernel's
         ROWS=$(python3 -c "import json;print([json.loads(l) for l in open('gpurun_out/bench.log') if l.startswith('{')][-1]['gemm_sites']['$SITE']['rows_per_launch'])") || exit 1
         python3 tools/pmc_traffic.py gpurun_out/pmc_bench/FETCH_SIZE gpurun_out/pmc_bench/WRITE_SIZE \
-            gpurun_out/pmc_c_fc.json $ROWS "${PMC_LABEL:-round-4 run}: --pmc FETCH_SIZE and --pmc WRITE_SIZE passes of bench.py --no-text, tiles $TILES" \
+            gpurun_out/pmc_c_fc.json $ROWS "${PMC_LABEL:-pmc run}: --pmc FETCH_SIZE and --pmc WRITE_SIZE passes of bench.py --no-text, tiles $TILES" \
             "$TILES" $SITE || exit $?
       done ;;
   esac
