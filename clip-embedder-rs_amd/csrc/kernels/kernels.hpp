@@ -71,7 +71,8 @@ enum GemmTile {
   // the spread fragment-read schedule (gemm_pipe_kernel RS = 1: a phase's reads for the next phase go
   // out over its first MI - 2 MFMA groups); bit-identical to the others, speed only
   TILE_256x256_RS = 14,
-  TILE_160x128_RS = 15,     // 4 waves of 80x64, 74 KiB LDS, 2 blocks / CU (small M; the table's large-text c_proj)
+  TILE_160x128_RS = 15,     // 4 waves of 80x64, 74 KiB LDS, 2 blocks / CU (small M; the table's vision c_fc / c_proj /
+                            // patch and large-text c_proj)
   TILE_160x128_W8_RS = 17,  // 2x4 waves of 80x32, 74 KiB LDS, 2 blocks / CU (the table's N = width sites)
   TILE_256x256_HALF = 18,   // 256x256 RS with the partial last round as half tiles (HM = 1; the table's
                             // qkv / c_fc)
