@@ -915,14 +915,15 @@ void table_tiles(clipgpu_engine& e) {
   const int G = e.spec.grid();
   const int prow = e.spec.tower == TOWER_VISION ? rows / e.spec.tokens() * G * G : 0;
   e.tile_patch = prow >= 2048 ? TILE_160x128_W8_RS : TILE_AUTO;
-  // the two-lane vision regime (table_lanes): c_fc, c_proj and the patch GEMM (c_proj's shape class) on
-  // the 4-wave 160x128 RS tile (two blocks per CU), out_proj on the 8-wave 224x192 tile (one round of
-  // 116 tiles per 6400-row lane).  Round 4 put c_proj on 224x192 too (+0.4-0.9 %, f32 stream,
+  // the two-lane vision regime (table_lanes): qkv, c_fc, c_proj and the patch GEMM (c_proj's shape class)
+  // on the 4-wave 160x128 RS tile (two blocks per CU), out_proj on the 8-wave 224x192 tile (one round of
+  // 116 tiles per 6400-row lane).  qkv moved off the 256x256 half tile in round 6: the same 26 us alone,
+  // 94.2k vs 92.9k img/s in the forward (profiles/r06_qkv_tile_ab.txt).  Round 4 put c_proj on 224x192 too (+0.4-0.9 %, f32 stream,
   // profiles/r04_residual26_two_lanes_ab.jsonl); with the f16 stream and the round-6 DMA issue,
   // c_proj alone takes 41.4 us on 160x128 against 57.1 us on 224x192 and the step is as fast or faster
   // (93.1k vs 92.3k img/s, profiles/r06_residual_tiles_ab.txt); c_fc on 224x192 loses 3 %
   if (vision_two_lanes(e) && e.dev_lanes == 2 && rows >= 2048) {
-    e.tile[GS_FC] = e.tile[GS_PROJ] = TILE_160x128_RS;
+    e.tile[GS_QKV] = e.tile[GS_FC] = e.tile[GS_PROJ] = TILE_160x128_RS;
     e.tile[GS_OUT] = TILE_224x192_W8;
     if (prow >= 2048) e.tile_patch = TILE_160x128_RS;
   }

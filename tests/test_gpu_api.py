@@ -441,7 +441,7 @@ def test_one_device_clique_runs_the_multi_device_comm_path():
 def test_tile_table_is_deterministic_and_bit_invisible():
     """The default tile choice is the committed table (engine.hip table_tiles): two engines of
     the bench's configuration pick the same tiles and lanes on any box (vision at 256 images: two
-    lanes, c_fc / c_proj on the 4-wave 160x128 RS tile, out_proj on the 8-wave 224x192); a timing tuner
+    lanes, qkv / c_fc / c_proj on the 4-wave 160x128 RS tile, out_proj on the 8-wave 224x192); a timing tuner
     (clipgpu_options.tuning) may pick others, with the same output bits."""
     from oracle.model_spec import VIT_B_32_CFG
     from open_clip_inference.engine import Engine
@@ -449,7 +449,7 @@ def test_tile_table_is_deterministic_and_bit_invisible():
     d = make_model_dir(VIT_B_32_CFG, seed=1234)
     a = Engine(d, 0, [0], "bf16", 256)
     b = Engine(d, 0, [0], "bf16", 256)
-    assert a.info() == b.info() == ([18, 26, 15, 15], 2, [])
+    assert a.info() == b.info() == ([15, 26, 15, 15], 2, [])
     t = Engine(d, 0, [0], "bf16", 256, tuning=True)
     v = vision_spec_from_cfg(VIT_B_32_CFG["model_cfg"])
     x = normalized_pixels(weights.synth_images_u8(31, 64, v.image_size), OPENAI_MEAN, OPENAI_STD)

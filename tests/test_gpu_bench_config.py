@@ -3,8 +3,8 @@
 `bench.py`'s headline (BASELINE.json configs[1]) and its text leg (configs[2]) run engines
 built exactly as the bench builds them: the bench's own model folder and seeded inputs,
 max_batch 256 / 1024, the committed tile table (engine.hip table_tiles / table_lanes: vision two
-lanes of 128 images with tiles 18,26,15,15 -- 256x256 half-tile qkv, 224x192 8-wave out_proj /
-patch GEMM, 160x128 4-wave RS c_fc / c_proj; text two lanes of 512 sequences with 18,17,18,15),
+lanes of 128 images with tiles 15,26,15,15 -- 224x192 8-wave out_proj, 160x128 4-wave RS qkv / c_fc /
+c_proj / patch GEMM; text two lanes of 512 sequences with 18,17,18,15),
 the hipGraph-replayed device entry point on the caller's stream.  Sampled rows spread over the
 batch: the first and last rows, the rows around the 128 / 512 midpoints (where the two lanes of
 each tower cut) and rows whose tokens
