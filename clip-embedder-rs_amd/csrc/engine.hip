@@ -926,6 +926,12 @@ void table_tiles(clipgpu_engine& e) {
     e.tile[GS_QKV] = e.tile[GS_FC] = e.tile[GS_PROJ] = TILE_160x128_RS;
     e.tile[GS_OUT] = TILE_224x192_W8;
     if (prow >= 2048) e.tile_patch = TILE_160x128_RS;
+    if (e.mx) {  // fp8 engines: the timing tuner's picks in this regime, 105.0k vs 102.6k img/s over the MX
+                 // shape heuristic (profiles/r06_fp8_tiles_probe.jsonl)
+      e.mxtile[GS_QKV] = MX_TILE_256x128;
+      e.mxtile[GS_FC] = e.mxtile[GS_PROJ] = MX_TILE_128x128;
+      e.tile[GS_OUT] = TILE_160x128_RS;
+    }
   }
 }
 

@@ -454,6 +454,11 @@ def test_tile_table_is_deterministic_and_bit_invisible():
     v = vision_spec_from_cfg(VIT_B_32_CFG["model_cfg"])
     x = normalized_pixels(weights.synth_images_u8(31, 64, v.image_size), OPENAI_MEAN, OPENAI_STD)
     assert np.array_equal(a.embed_pixels(x), t.embed_pixels(x))
+    # fp8 engines of the same configuration: the MX sites on the tuner's MX tiles (qkv 256x128, c_fc /
+    # c_proj 128x128), out_proj on 160x128 RS
+    f = Engine(d, 0, [0], "fp8", 256)
+    assert f.info() == ([2, 15, 3, 3], 2, ["qkv", "fc", "proj"])
+    f.close()
     small = Engine(d, 0, [0], "bf16", 8)  # rows < 2048: the shape heuristic
     assert small.info()[0] == [0, 0, 0, 0]
     # the text tower at the bench's 1024 x 77 batch: two lanes, c_proj on the 4-wave 160x128 RS
